@@ -1,0 +1,118 @@
+"""ctypes binding of libfedagg.so (the C ABI in include/fedagg.h).
+
+The library is built in-tree (``make -C fedml_amd/csrc`` or ``__graft_entry__.build()``) and
+loaded from ``fedml_amd/libfedagg.so``.  There is no fallback: if the library is missing or fails
+to load, every entry point raises ``FedAggNativeError`` -- the product path never silently
+computes on the CPU.
+
+torch is imported first so that the HIP runtime torch ships (soname ``libamdhip64.so.7``) is the
+one the library binds to; both then share devices, streams and the caching allocator's memory.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch  # noqa: F401  (load torch's HIP runtime before libfedagg.so)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libfedagg.so")
+ABI_VERSION = 1
+
+F32, BF16, F16, F64, I64 = 0, 1, 2, 3, 4
+MUL_W, MUL_N_DIV_N, SUM = 0, 1, 2
+
+FA_OK, FA_ERR_INVALID, FA_ERR_DTYPE, FA_ERR_HIP, FA_ERR_NOMEM = 0, -1, -2, -3, -4
+
+EXPORTED_SYMBOLS = (
+    "fa_abi_version", "fa_ctx_create", "fa_ctx_destroy", "fa_weighted_sum",
+    "fa_weighted_sum_multi", "fa_mix", "fa_ctx_set_variant", "fa_strerror", "fa_last_error",
+)
+
+
+class FedAggNativeError(RuntimeError):
+    """The HIP library is unavailable or a native call failed."""
+
+
+_lib = None
+_lock = threading.Lock()
+
+_vp = ctypes.c_void_p
+_P_vp = ctypes.POINTER(ctypes.c_void_p)
+_P_d = ctypes.POINTER(ctypes.c_double)
+_P_i64 = ctypes.POINTER(ctypes.c_int64)
+_P_i32 = ctypes.POINTER(ctypes.c_int32)
+
+
+def _declare(L):
+    L.fa_abi_version.restype = ctypes.c_int
+    L.fa_abi_version.argtypes = []
+    L.fa_ctx_create.restype = ctypes.c_int
+    L.fa_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    L.fa_ctx_destroy.restype = ctypes.c_int
+    L.fa_ctx_destroy.argtypes = [_vp]
+    L.fa_ctx_set_variant.restype = ctypes.c_int
+    L.fa_ctx_set_variant.argtypes = [_vp, ctypes.c_int]
+    L.fa_weighted_sum.restype = ctypes.c_int
+    L.fa_weighted_sum.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int32,
+                                  _P_vp, _P_d, ctypes.c_double, _vp, _vp]
+    L.fa_weighted_sum_multi.restype = ctypes.c_int
+    L.fa_weighted_sum_multi.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int32, _P_i64,
+                                        ctypes.c_int32, _P_vp, _P_d, ctypes.c_double, _P_vp, _vp]
+    L.fa_mix.restype = ctypes.c_int
+    L.fa_mix.argtypes = [_vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int32, _P_i32, _P_i32, _P_d,
+                         ctypes.c_int32, _P_vp, _P_vp, _P_d, _P_vp, _vp]
+    L.fa_strerror.restype = ctypes.c_char_p
+    L.fa_strerror.argtypes = [ctypes.c_int]
+    L.fa_last_error.restype = ctypes.c_char_p
+    L.fa_last_error.argtypes = []
+
+
+def lib():
+    """Load (once) and return the native library, or raise FedAggNativeError."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise FedAggNativeError(
+                f"{LIB_PATH} not found: build it with `make -C fedml_amd/csrc` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        try:
+            L = ctypes.CDLL(LIB_PATH)
+        except OSError as e:
+            raise FedAggNativeError(f"cannot load {LIB_PATH}: {e}") from e
+        missing = [s for s in EXPORTED_SYMBOLS if not hasattr(L, s)]
+        if missing:
+            raise FedAggNativeError(f"{LIB_PATH} lacks symbols {missing}")
+        _declare(L)
+        if L.fa_abi_version() != ABI_VERSION:
+            raise FedAggNativeError(f"ABI version {L.fa_abi_version()} != {ABI_VERSION}")
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != FA_OK:
+        L = lib()
+        raise FedAggNativeError(
+            f"{what} failed: {L.fa_strerror(rc).decode()} ({L.fa_last_error().decode()})")
+
+
+def ptr_array(ptrs):
+    return (ctypes.c_void_p * len(ptrs))(*ptrs)
+
+
+def f64_array(vals):
+    return (ctypes.c_double * len(vals))(*[float(v) for v in vals])
+
+
+def i64_array(vals):
+    return (ctypes.c_int64 * len(vals))(*[int(v) for v in vals])
+
+
+def i32_array(vals):
+    return (ctypes.c_int32 * len(vals))(*[int(v) for v in vals])

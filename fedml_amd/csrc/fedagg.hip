@@ -1,0 +1,752 @@
+// fedagg.hip -- MI355X (gfx950 / CDNA4) kernels and C ABI of the FedAvg-family aggregation engine.
+//
+// Public contract: include/fedagg.h (which reference loop each entry replaces, exact arithmetic).
+//
+// Design (DESIGN.md has the numbers):
+//  * The path is an HBM-bound ordered reduction over K client streams: per output element it reads
+//    K inputs and writes one.  No MFMA (0.5 flop/B) and no LDS staging (no data reuse): every lane
+//    owns V consecutive elements (one 16-byte vector) of one tile and walks the K clients IN ORDER,
+//    which is what makes the result bit-identical to the reference's client-ordered CPU loop.
+//  * Bandwidth comes from memory-level parallelism: the client loop is unrolled by U with all U
+//    16-byte loads issued before any is consumed (U KiB in flight per wave), so a CU with ~8-20
+//    resident waves keeps >= 64 KiB of HBM reads in flight.  Out-of-range clients in the last group
+//    are loaded from a clamped (valid) index and skipped on the uniform accumulate branch, so no
+//    load sits behind a branch (hipcc would otherwise wait vmcnt(0) per load).
+//  * Inputs are read exactly once -> non-temporal loads; the output is written once -> non-temporal
+//    stores.  (Mixing re-reads neighbours, so fa_mix keeps the default cache policy.)
+//  * A whole state_dict (many tensors of one dtype) is one launch: a device-resident segment table
+//    maps each 256-thread tile to (segment, offset) by a wave-uniform binary search (scalar loads).
+//  * Arithmetic: op(.) = IEEE op in float/double, rounded once to the storage type, never fused
+//    (compiled with -ffp-contract=off, __f*_rn intrinsics).  The accumulator starts at -0.0, which
+//    is the exact identity of IEEE addition (-0 + t == t bitwise for every t, incl. +-0, NaN, Inf),
+//    so "acc = t_0" needs no select.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <type_traits>
+
+#include "fedagg.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kSlots = 8;
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// --------------------------------------------------------------------------------------------
+// Device-resident descriptors (staged per call from pinned host memory).
+struct Seg {                // one state_dict tensor
+  int64_t numel;
+  int64_t tile_start;     // first tile (workgroup) of this segment
+  void* out;
+  int32_t ptr_base;       // index of client 0's pointer for this segment in the pointer table
+  int32_t aligned;        // every input and the output are 16-byte aligned
+};
+static_assert(sizeof(Seg) == 32, "Seg layout");
+
+struct MixRow {             // one output row of a mixing matrix
+  int32_t begin, end;     // CSR entry range
+  void* out;
+  void* out2;             // PushSum z output (or null)
+  double scale;           // PushSum post-scale (1/omega)
+};
+static_assert(sizeof(MixRow) == 32, "MixRow layout");
+
+// --------------------------------------------------------------------------------------------
+// Exact per-op arithmetic.
+__device__ __forceinline__ float op_mul(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float op_add(float a, float b) { return __fadd_rn(a, b); }
+__device__ __forceinline__ float op_div(float a, float b) { return __fdiv_rn(a, b); }
+__device__ __forceinline__ double op_mul(double a, double b) { return __dmul_rn(a, b); }
+__device__ __forceinline__ double op_add(double a, double b) { return __dadd_rn(a, b); }
+__device__ __forceinline__ double op_div(double a, double b) { return __ddiv_rn(a, b); }
+
+__device__ __forceinline__ float bf16_round(float x) { return (float)(__bf16)x; }
+__device__ __forceinline__ unsigned bf16_bits(float x) {
+  return (unsigned)__builtin_bit_cast(unsigned short, (__bf16)x);
+}
+__device__ __forceinline__ float f16_round(float x) { return (float)(_Float16)x; }
+__device__ __forceinline__ unsigned f16_bits(float x) {
+  return (unsigned)__builtin_bit_cast(unsigned short, (_Float16)x);
+}
+__device__ __forceinline__ float f16_from_bits(unsigned b) {
+  return (float)__builtin_bit_cast(_Float16, (unsigned short)b);
+}
+
+// --------------------------------------------------------------------------------------------
+// Element traits per (input dtype, mode):
+//   R     raw element value after unpacking (exact widening: float for f32/bf16/f16)
+//   A     accumulator / op type;  C coefficient type;  D divisor type
+//   V     elements per 16-byte input vector;  IN_BYTES / OUT_BYTES element sizes
+//   term  t_i of the contract;  acc   op(acc + t);  zero  the exact additive identity
+template <int DT, int MODE> struct Tr;
+
+template <int MODE> struct TrFloatBase {
+  using A = float; using C = float; using D = float; using R = float;
+  __device__ static C coef(double c) { return (float)c; }
+  __device__ static D div(double d) { return (float)d; }
+  __device__ static A zero() { return -0.0f; }
+};
+
+template <int MODE> struct Tr<FA_DTYPE_F32, MODE> : TrFloatBase<MODE> {
+  static constexpr int V = 4, IN_BYTES = 4, OUT_BYTES = 4;
+  __device__ static float rnd(float x) { return x; }
+  __device__ static void unpack(u32x4 r, float (&x)[V]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) x[j] = __uint_as_float(r[j]);
+  }
+  __device__ static float ld1(const void* p, int64_t e) { return ((const float*)p)[e]; }
+  __device__ static void st1(void* p, int64_t e, float v) { ((float*)p)[e] = v; }
+  __device__ static void stv(void* p, const float (&a)[V]) {
+    u32x4 w = {__float_as_uint(a[0]), __float_as_uint(a[1]), __float_as_uint(a[2]), __float_as_uint(a[3])};
+    __builtin_nontemporal_store(w, (__attribute__((address_space(1))) u32x4*)p);
+  }
+};
+
+template <int MODE> struct Tr<FA_DTYPE_BF16, MODE> : TrFloatBase<MODE> {
+  static constexpr int V = 8, IN_BYTES = 2, OUT_BYTES = 2;
+  __device__ static float rnd(float x) { return bf16_round(x); }
+  __device__ static void unpack(u32x4 r, float (&x)[V]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x[2 * j] = __uint_as_float(r[j] << 16);
+      x[2 * j + 1] = __uint_as_float(r[j] & 0xFFFF0000u);
+    }
+  }
+  __device__ static float ld1(const void* p, int64_t e) {
+    return __uint_as_float((unsigned)((const unsigned short*)p)[e] << 16);
+  }
+  __device__ static void st1(void* p, int64_t e, float v) { ((unsigned short*)p)[e] = (unsigned short)bf16_bits(v); }
+  __device__ static void stv(void* p, const float (&a)[V]) {
+    u32x4 w;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = bf16_bits(a[2 * j]) | (bf16_bits(a[2 * j + 1]) << 16);
+    __builtin_nontemporal_store(w, (__attribute__((address_space(1))) u32x4*)p);
+  }
+};
+
+template <int MODE> struct Tr<FA_DTYPE_F16, MODE> : TrFloatBase<MODE> {
+  static constexpr int V = 8, IN_BYTES = 2, OUT_BYTES = 2;
+  __device__ static float rnd(float x) { return f16_round(x); }
+  __device__ static void unpack(u32x4 r, float (&x)[V]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      x[2 * j] = f16_from_bits(r[j] & 0xFFFFu);
+      x[2 * j + 1] = f16_from_bits(r[j] >> 16);
+    }
+  }
+  __device__ static float ld1(const void* p, int64_t e) { return f16_from_bits(((const unsigned short*)p)[e]); }
+  __device__ static void st1(void* p, int64_t e, float v) { ((unsigned short*)p)[e] = (unsigned short)f16_bits(v); }
+  __device__ static void stv(void* p, const float (&a)[V]) {
+    u32x4 w;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) w[j] = f16_bits(a[2 * j]) | (f16_bits(a[2 * j + 1]) << 16);
+    __builtin_nontemporal_store(w, (__attribute__((address_space(1))) u32x4*)p);
+  }
+};
+
+template <int MODE> struct Tr<FA_DTYPE_F64, MODE> {
+  using A = double; using C = double; using D = double; using R = double;
+  static constexpr int V = 2, IN_BYTES = 8, OUT_BYTES = 8;
+  __device__ static C coef(double c) { return c; }
+  __device__ static D div(double d) { return d; }
+  __device__ static A zero() { return -0.0; }
+  __device__ static double rnd(double x) { return x; }
+  __device__ static void unpack(u32x4 r, double (&x)[V]) {
+    x[0] = __builtin_bit_cast(double, u32x2{r[0], r[1]});
+    x[1] = __builtin_bit_cast(double, u32x2{r[2], r[3]});
+  }
+  __device__ static double ld1(const void* p, int64_t e) { return ((const double*)p)[e]; }
+  __device__ static void st1(void* p, int64_t e, double v) { ((double*)p)[e] = v; }
+  __device__ static void stv(void* p, const double (&a)[V]) {
+    u32x2 lo = __builtin_bit_cast(u32x2, a[0]), hi = __builtin_bit_cast(u32x2, a[1]);
+    u32x4 w = {lo[0], lo[1], hi[0], hi[1]};
+    __builtin_nontemporal_store(w, (__attribute__((address_space(1))) u32x4*)p);
+  }
+};
+
+// int64 inputs, weighted modes: float32 output (PyTorch type promotion int64 (*) float -> float32)
+template <int MODE> struct Tr<FA_DTYPE_I64, MODE> {
+  using A = float; using R = long long; using D = float;
+  using C = typename std::conditional<MODE == FA_MODE_MUL_N_DIV_N, long long, float>::type;
+  static constexpr int V = 2, IN_BYTES = 8, OUT_BYTES = 4;
+  __device__ static C coef(double c) { return (C)c; }
+  __device__ static D div(double d) { return (float)d; }
+  __device__ static A zero() { return -0.0f; }
+  __device__ static float rnd(float x) { return x; }
+  __device__ static void unpack(u32x4 r, long long (&x)[V]) {
+    x[0] = __builtin_bit_cast(long long, u32x2{r[0], r[1]});
+    x[1] = __builtin_bit_cast(long long, u32x2{r[2], r[3]});
+  }
+  __device__ static long long ld1(const void* p, int64_t e) { return ((const long long*)p)[e]; }
+  __device__ static void st1(void* p, int64_t e, float v) { ((float*)p)[e] = v; }
+  __device__ static void stv(void* p, const float (&a)[V]) {
+    u32x2 w = {__float_as_uint(a[0]), __float_as_uint(a[1])};
+    __builtin_nontemporal_store(w, (__attribute__((address_space(1))) u32x2*)p);
+  }
+};
+
+// int64 inputs, plain sum: int64 output, two's-complement wrap
+template <> struct Tr<FA_DTYPE_I64, FA_MODE_SUM> {
+  using A = unsigned long long; using R = long long; using C = float; using D = float;
+  static constexpr int V = 2, IN_BYTES = 8, OUT_BYTES = 8;
+  __device__ static C coef(double) { return 0.f; }
+  __device__ static D div(double) { return 0.f; }
+  __device__ static A zero() { return 0ull; }
+  __device__ static A rnd(A x) { return x; }
+  __device__ static void unpack(u32x4 r, long long (&x)[V]) {
+    x[0] = __builtin_bit_cast(long long, u32x2{r[0], r[1]});
+    x[1] = __builtin_bit_cast(long long, u32x2{r[2], r[3]});
+  }
+  __device__ static long long ld1(const void* p, int64_t e) { return ((const long long*)p)[e]; }
+  __device__ static void st1(void* p, int64_t e, A v) { ((unsigned long long*)p)[e] = v; }
+  __device__ static void stv(void* p, const A (&a)[V]) {
+    u32x2 lo = __builtin_bit_cast(u32x2, a[0]), hi = __builtin_bit_cast(u32x2, a[1]);
+    u32x4 w = {lo[0], lo[1], hi[0], hi[1]};
+    __builtin_nontemporal_store(w, (__attribute__((address_space(1))) u32x4*)p);
+  }
+};
+
+// t_i of the contract
+template <int DT, int MODE>
+__device__ __forceinline__ typename Tr<DT, MODE>::A term(typename Tr<DT, MODE>::R x,
+                                                         typename Tr<DT, MODE>::C c,
+                                                         typename Tr<DT, MODE>::D d) {
+  using T = Tr<DT, MODE>;
+  if constexpr (DT == FA_DTYPE_I64) {
+    if constexpr (MODE == FA_MODE_SUM) {
+      return (unsigned long long)x;
+    } else if constexpr (MODE == FA_MODE_MUL_W) {
+      return op_mul((float)x, c);
+    } else {  // int64 * int64 (wrapping), then true_divide in float32
+      return op_div((float)(long long)((unsigned long long)x * (unsigned long long)c), d);
+    }
+  } else {
+    if constexpr (MODE == FA_MODE_SUM) {
+      return x;
+    } else if constexpr (MODE == FA_MODE_MUL_W) {
+      return T::rnd(op_mul(x, c));
+    } else {
+      return T::rnd(op_div(T::rnd(op_mul(x, c)), d));
+    }
+  }
+}
+
+template <int DT, int MODE>
+__device__ __forceinline__ typename Tr<DT, MODE>::A accum(typename Tr<DT, MODE>::A acc,
+                                                          typename Tr<DT, MODE>::A t) {
+  if constexpr (DT == FA_DTYPE_I64 && MODE == FA_MODE_SUM) {
+    return acc + t;
+  } else {
+    return Tr<DT, MODE>::rnd(op_add(acc, t));
+  }
+}
+
+// Client tensors are plain device allocations: load through the GLOBAL address space so hipcc
+// emits global_load_dwordx4 (in-order vmcnt accounting) instead of flat_load_dwordx4.
+typedef const __attribute__((address_space(1))) u32x4* gp_u32x4;
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const void* p) {
+  gp_u32x4 g = (gp_u32x4)p;
+  if constexpr (NT) return __builtin_nontemporal_load(g);
+  else return *g;
+}
+
+// Wave-uniform lookup of the segment that owns `tile` (segments sorted by tile_start).
+__device__ __forceinline__ int find_seg(const Seg* __restrict__ segs, int nseg, int64_t tile) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (segs[mid].tile_start <= tile) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// --------------------------------------------------------------------------------------------
+// The ordered weighted-sum kernel.  One workgroup = one tile of kBlock*V elements of one segment.
+template <int DT, int MODE, int U, bool NT>
+__global__ void __launch_bounds__(kBlock)
+k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
+       const void* const* __restrict__ ptrs, int k, double divisor) {
+  using T = Tr<DT, MODE>;
+  using A = typename T::A;
+  using R = typename T::R;
+  constexpr int V = T::V;
+  constexpr int64_t TILE = (int64_t)kBlock * V;
+
+  const int64_t tile = blockIdx.x;
+  const Seg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
+  const int64_t base = (tile - sg.tile_start) * TILE;
+  const void* const* in = ptrs + sg.ptr_base;
+  const typename T::D d = T::div(divisor);
+
+  if (sg.aligned && base + TILE <= sg.numel) {
+    const int64_t e0 = base + (int64_t)threadIdx.x * V;
+    const int64_t boff = e0 * T::IN_BYTES;
+    A acc[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[v] = T::zero();
+    for (int i0 = 0; i0 < k; i0 += U) {
+      u32x4 r[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = min(i0 + u, k - 1);  // clamped: every load unconditional
+        r[u] = ld16<NT>((const char*)in[i] + boff);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (i0 + u < k) {  // wave-uniform
+          const typename T::C c = T::coef(coef[i0 + u]);
+          R x[V];
+          T::unpack(r[u], x);
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[v] = accum<DT, MODE>(acc[v], term<DT, MODE>(x[v], c, d));
+        }
+      }
+    }
+    T::stv((char*)sg.out + e0 * T::OUT_BYTES, acc);
+  } else {
+    // tail tile or unaligned segment: coalesced scalar loads, same arithmetic
+    const int64_t end = min(base + TILE, sg.numel);
+    for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
+      A acc = T::zero();
+      for (int i = 0; i < k; ++i)
+        acc = accum<DT, MODE>(acc, term<DT, MODE>(T::ld1(in[i], e), T::coef(coef[i]), d));
+      T::st1(sg.out, e, acc);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// Mixing / gossip kernel: one workgroup = one element tile, looping over every output row so that
+// an input shared by neighbouring rows is re-read from L2 / Infinity Cache, not HBM.
+template <int DT, int U, bool POST>
+__global__ void __launch_bounds__(kBlock)
+k_mix(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict__ cols,
+      const double* __restrict__ vals, const void* const* __restrict__ in, int64_t n, int aligned) {
+  using T = Tr<DT, FA_MODE_MUL_W>;
+  constexpr int V = T::V;
+  constexpr int64_t TILE = (int64_t)kBlock * V;
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const float dz = 0.f;
+
+  if (aligned && base + TILE <= n) {
+    const int64_t e0 = base + (int64_t)threadIdx.x * V;
+    const int64_t boff = e0 * T::IN_BYTES;
+    for (int r = 0; r < nrows; ++r) {
+      const MixRow row = rows[r];
+      float acc[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[v] = -0.0f;
+      for (int j0 = row.begin; j0 < row.end; j0 += U) {
+        u32x4 x4[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int j = min(j0 + u, row.end - 1);
+          x4[u] = ld16<false>((const char*)in[cols[j]] + boff);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (j0 + u < row.end) {
+            const float c = (float)vals[j0 + u];
+            float x[V];
+            T::unpack(x4[u], x);
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+              acc[v] = accum<DT, FA_MODE_MUL_W>(acc[v], term<DT, FA_MODE_MUL_W>(x[v], c, dz));
+          }
+        }
+      }
+      T::stv((char*)row.out + e0 * T::OUT_BYTES, acc);
+      if constexpr (POST) {
+        const float s = (float)row.scale;
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] = T::rnd(op_mul(acc[v], s));
+        T::stv((char*)row.out2 + e0 * T::OUT_BYTES, acc);
+      }
+    }
+  } else {
+    const int64_t end = min(base + TILE, n);
+    for (int r = 0; r < nrows; ++r) {
+      const MixRow row = rows[r];
+      for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
+        float acc = -0.0f;
+        for (int j = row.begin; j < row.end; ++j)
+          acc = accum<DT, FA_MODE_MUL_W>(
+              acc, term<DT, FA_MODE_MUL_W>(T::ld1(in[cols[j]], e), (float)vals[j], dz));
+        T::st1(row.out, e, acc);
+        if constexpr (POST) T::st1(row.out2, e, T::rnd(op_mul(acc, (float)row.scale)));
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------------
+// Host side: error reporting, context, staging.
+thread_local char g_last_error[512] = "";
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+#define FA_HIP(call)                                                                     \
+  do {                                                                                   \
+    hipError_t e_ = (call);                                                              \
+    if (e_ != hipSuccess) return fail(FA_ERR_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) { prev = -1; }
+    if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+}  // namespace
+
+struct fa_ctx {
+  int device = 0;
+  int variant = 0;  // kernel tuning variant (results identical for every variant)
+  struct Slot {
+    void* host = nullptr;
+    void* dev = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+  } slots[kSlots];
+  int next = 0;
+};
+
+namespace {
+
+// Take the next staging slot with >= bytes of room; waits only if that slot's previous call is
+// still in flight (kSlots calls ago).
+int acquire_slot(fa_ctx* ctx, size_t bytes, fa_ctx::Slot** out) {
+  fa_ctx::Slot& s = ctx->slots[ctx->next];
+  ctx->next = (ctx->next + 1) % kSlots;
+  if (s.pending) {
+    FA_HIP(hipEventSynchronize(s.ev));
+    s.pending = false;
+  }
+  if (s.cap < bytes) {
+    size_t cap = std::max(bytes, std::max<size_t>(2 * s.cap, 16384));
+    if (s.host) FA_HIP(hipHostFree(s.host));
+    if (s.dev) FA_HIP(hipFree(s.dev));
+    s.host = s.dev = nullptr;
+    s.cap = 0;
+    if (hipHostMalloc(&s.host, cap, hipHostMallocDefault) != hipSuccess)
+      return fail(FA_ERR_NOMEM, "hipHostMalloc(%zu) failed", cap);
+    if (hipMalloc(&s.dev, cap) != hipSuccess) return fail(FA_ERR_NOMEM, "hipMalloc(%zu) failed", cap);
+    s.cap = cap;
+  }
+  *out = &s;
+  return FA_OK;
+}
+
+int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st) {
+  FA_HIP(hipMemcpyAsync(s->dev, s->host, bytes, hipMemcpyHostToDevice, st));
+  return FA_OK;
+}
+
+int release(fa_ctx::Slot* s, hipStream_t st) {
+  FA_HIP(hipEventRecord(s->ev, st));
+  s->pending = true;
+  return FA_OK;
+}
+
+template <int DT, int MODE, int U, bool NT>
+void launch_wsum(int64_t tiles, hipStream_t st, const Seg* segs, int nseg, const double* coef,
+                 const void* const* ptrs, int k, double divisor) {
+  hipLaunchKernelGGL((k_wsum<DT, MODE, U, NT>), dim3((unsigned)tiles), dim3(kBlock), 0, st, segs, nseg,
+                     coef, ptrs, k, divisor);
+}
+
+// variant: 0 = default (U=8, nt); 1 = U=4 nt; 2 = U=16 nt; 3 = U=8 plain loads
+template <int DT, int MODE>
+void dispatch_variant(int variant, int64_t tiles, hipStream_t st, const Seg* segs, int nseg,
+                      const double* coef, const void* const* ptrs, int k, double divisor) {
+  switch (variant) {
+    case 1: launch_wsum<DT, MODE, 4, true>(tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
+    case 2: launch_wsum<DT, MODE, 16, true>(tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
+    case 3: launch_wsum<DT, MODE, 8, false>(tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
+    default: launch_wsum<DT, MODE, 8, true>(tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
+  }
+}
+
+template <int DT>
+int dispatch_mode(int mode, int variant, int64_t tiles, hipStream_t st, const Seg* segs, int nseg,
+                  const double* coef, const void* const* ptrs, int k, double divisor) {
+  switch (mode) {
+    case FA_MODE_MUL_W: dispatch_variant<DT, FA_MODE_MUL_W>(variant, tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
+    case FA_MODE_MUL_N_DIV_N: dispatch_variant<DT, FA_MODE_MUL_N_DIV_N>(variant, tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
+    case FA_MODE_SUM: dispatch_variant<DT, FA_MODE_SUM>(variant, tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
+    default: return fail(FA_ERR_DTYPE, "unknown mode %d", mode);
+  }
+  return FA_OK;
+}
+
+int elems_per_vec(int dtype) {
+  switch (dtype) {
+    case FA_DTYPE_F32: return 4;
+    case FA_DTYPE_BF16: case FA_DTYPE_F16: return 8;
+    case FA_DTYPE_F64: case FA_DTYPE_I64: return 2;
+    default: return 0;
+  }
+}
+size_t in_bytes(int dtype) {
+  switch (dtype) {
+    case FA_DTYPE_F32: return 4;
+    case FA_DTYPE_BF16: case FA_DTYPE_F16: return 2;
+    default: return 8;
+  }
+}
+size_t out_bytes(int dtype, int mode) {
+  if (dtype == FA_DTYPE_I64) return mode == FA_MODE_SUM ? 8 : 4;
+  return in_bytes(dtype);
+}
+
+inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace
+
+// ============================================================================================ ABI
+extern "C" {
+
+int fa_abi_version(void) { return FA_ABI_VERSION; }
+
+const char* fa_strerror(int code) {
+  switch (code) {
+    case FA_OK: return "FA_OK";
+    case FA_ERR_INVALID: return "FA_ERR_INVALID";
+    case FA_ERR_DTYPE: return "FA_ERR_DTYPE";
+    case FA_ERR_HIP: return "FA_ERR_HIP";
+    case FA_ERR_NOMEM: return "FA_ERR_NOMEM";
+    default: return "FA_ERR_UNKNOWN";
+  }
+}
+
+const char* fa_last_error(void) { return g_last_error; }
+
+int fa_ctx_create(int hip_device, fa_ctx** out) {
+  if (!out) return fail(FA_ERR_INVALID, "fa_ctx_create: out is NULL");
+  *out = nullptr;
+  int ndev = 0;
+  FA_HIP(hipGetDeviceCount(&ndev));
+  if (hip_device < 0 || hip_device >= ndev)
+    return fail(FA_ERR_INVALID, "fa_ctx_create: device %d out of range [0,%d)", hip_device, ndev);
+  DeviceGuard g(hip_device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", hip_device);
+  fa_ctx* c = new (std::nothrow) fa_ctx();
+  if (!c) return fail(FA_ERR_NOMEM, "fa_ctx_create: out of host memory");
+  c->device = hip_device;
+  for (auto& s : c->slots) {
+    if (hipEventCreateWithFlags(&s.ev, hipEventDisableTiming) != hipSuccess) {
+      fa_ctx_destroy(c);
+      return fail(FA_ERR_HIP, "hipEventCreate failed");
+    }
+  }
+  *out = c;
+  return FA_OK;
+}
+
+int fa_ctx_destroy(fa_ctx* c) {
+  if (!c) return FA_OK;
+  DeviceGuard g(c->device);
+  for (auto& s : c->slots) {
+    if (s.pending && s.ev) (void)hipEventSynchronize(s.ev);
+    if (s.ev) (void)hipEventDestroy(s.ev);
+    if (s.host) (void)hipHostFree(s.host);
+    if (s.dev) (void)hipFree(s.dev);
+  }
+  delete c;
+  return FA_OK;
+}
+
+// Tuning knob (not part of the arithmetic contract): kernel variant for the weighted sum.
+int fa_ctx_set_variant(fa_ctx* c, int variant) {
+  if (!c || variant < 0 || variant > 3) return fail(FA_ERR_INVALID, "fa_ctx_set_variant: bad args");
+  c->variant = variant;
+  return FA_OK;
+}
+
+int fa_weighted_sum_multi(fa_ctx* ctx, int dtype, int mode, int32_t num_segments,
+                          const int64_t* seg_numel, int32_t k, const void* const* d_in,
+                          const double* coef, double divisor, void* const* d_out, void* hip_stream) {
+  if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (k <= 0) return fail(FA_ERR_INVALID, "k must be > 0 (got %d)", k);
+  if (num_segments <= 0 || !seg_numel || !d_in || !d_out)
+    return fail(FA_ERR_INVALID, "num_segments/seg_numel/d_in/d_out invalid");
+  if (mode < FA_MODE_MUL_W || mode > FA_MODE_SUM) return fail(FA_ERR_DTYPE, "unknown mode %d", mode);
+  const int V = elems_per_vec(dtype);
+  if (V == 0) return fail(FA_ERR_DTYPE, "unknown dtype %d", dtype);
+  if (mode != FA_MODE_SUM && !coef) return fail(FA_ERR_INVALID, "coef is NULL for a weighted mode");
+
+  // count non-empty segments and tiles
+  const int64_t tile_elems = (int64_t)kBlock * V;
+  int nseg = 0;
+  int64_t tiles = 0;
+  for (int s = 0; s < num_segments; ++s) {
+    if (seg_numel[s] < 0) return fail(FA_ERR_INVALID, "segment %d has negative numel", s);
+    if (seg_numel[s] == 0) continue;
+    if (!d_out[s]) return fail(FA_ERR_INVALID, "segment %d: output is NULL", s);
+    for (int i = 0; i < k; ++i)
+      if (!d_in[(int64_t)s * k + i]) return fail(FA_ERR_INVALID, "segment %d client %d: input NULL", s, i);
+    ++nseg;
+    tiles += (seg_numel[s] + tile_elems - 1) / tile_elems;
+  }
+  if (nseg == 0) return FA_OK;
+  if (tiles > 0x7FFFFFFFll) return fail(FA_ERR_INVALID, "too many tiles (%lld)", (long long)tiles);
+
+  const size_t seg_bytes = align16(sizeof(Seg) * nseg);
+  const size_t coef_bytes = align16(sizeof(double) * k);
+  const size_t ptr_bytes = sizeof(void*) * (size_t)nseg * k;
+  const size_t bytes = seg_bytes + coef_bytes + ptr_bytes;
+
+  DeviceGuard g(ctx->device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
+  hipStream_t st = (hipStream_t)hip_stream;
+  fa_ctx::Slot* slot = nullptr;
+  int rc = acquire_slot(ctx, bytes, &slot);
+  if (rc) return rc;
+
+  char* h = (char*)slot->host;
+  Seg* hs = (Seg*)h;
+  double* hc = (double*)(h + seg_bytes);
+  const void** hp = (const void**)(h + seg_bytes + coef_bytes);
+  for (int i = 0; i < k; ++i) hc[i] = coef ? coef[i] : 0.0;
+  int j = 0;
+  int64_t t0 = 0;
+  const size_t ib = in_bytes(dtype), ob = out_bytes(dtype, mode);
+  for (int s = 0; s < num_segments; ++s) {
+    const int64_t n = seg_numel[s];
+    if (n == 0) continue;
+    bool aligned = al16(d_out[s]);
+    for (int i = 0; i < k; ++i) {
+      const void* p = d_in[(int64_t)s * k + i];
+      hp[(int64_t)j * k + i] = p;
+      aligned = aligned && al16(p);
+    }
+    (void)ib; (void)ob;
+    hs[j] = Seg{n, t0, d_out[s], j * k, aligned ? 1 : 0};
+    t0 += (n + tile_elems - 1) / tile_elems;
+    ++j;
+  }
+  rc = stage(slot, bytes, st);
+  if (rc) return rc;
+  char* d = (char*)slot->dev;
+  const Seg* ds = (const Seg*)d;
+  const double* dc = (const double*)(d + seg_bytes);
+  const void* const* dp = (const void* const*)(d + seg_bytes + coef_bytes);
+
+  switch (dtype) {
+    case FA_DTYPE_F32: rc = dispatch_mode<FA_DTYPE_F32>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor); break;
+    case FA_DTYPE_BF16: rc = dispatch_mode<FA_DTYPE_BF16>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor); break;
+    case FA_DTYPE_F16: rc = dispatch_mode<FA_DTYPE_F16>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor); break;
+    case FA_DTYPE_F64: rc = dispatch_mode<FA_DTYPE_F64>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor); break;
+    case FA_DTYPE_I64: rc = dispatch_mode<FA_DTYPE_I64>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor); break;
+  }
+  if (rc) return rc;
+  FA_HIP(hipGetLastError());
+  return release(slot, st);
+}
+
+int fa_weighted_sum(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t k, const void* const* d_in,
+                    const double* coef, double divisor, void* d_out, void* hip_stream) {
+  if (n < 0) return fail(FA_ERR_INVALID, "n must be >= 0");
+  void* outs[1] = {d_out};
+  return fa_weighted_sum_multi(ctx, dtype, mode, 1, &n, k, d_in, coef, divisor, outs, hip_stream);
+}
+
+int fa_mix(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_ptr,
+           const int32_t* cols, const double* vals, int32_t num_in, const void* const* d_in,
+           void* const* d_out, const double* post_scale, void* const* d_out2, void* hip_stream) {
+  if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (rows <= 0 || n < 0 || !row_ptr || !cols || !vals || !d_in || !d_out || num_in <= 0)
+    return fail(FA_ERR_INVALID, "fa_mix: invalid arguments");
+  if (dtype != FA_DTYPE_F32 && dtype != FA_DTYPE_BF16 && dtype != FA_DTYPE_F16)
+    return fail(FA_ERR_DTYPE, "fa_mix: dtype %d not supported (F32, BF16, F16)", dtype);
+  if (post_scale && !d_out2) return fail(FA_ERR_INVALID, "fa_mix: post_scale without d_out2");
+  if (row_ptr[0] != 0) return fail(FA_ERR_INVALID, "fa_mix: row_ptr[0] must be 0");
+  bool aligned = true;
+  for (int r = 0; r < rows; ++r) {
+    if (row_ptr[r + 1] <= row_ptr[r]) return fail(FA_ERR_INVALID, "fa_mix: row %d is empty", r);
+    if (!d_out[r] || (post_scale && !d_out2[r])) return fail(FA_ERR_INVALID, "fa_mix: row %d output NULL", r);
+    aligned = aligned && al16(d_out[r]) && (!post_scale || al16(d_out2[r]));
+  }
+  const int32_t nnz = row_ptr[rows];
+  for (int j = 0; j < nnz; ++j)
+    if (cols[j] < 0 || cols[j] >= num_in) return fail(FA_ERR_INVALID, "fa_mix: col %d out of range", cols[j]);
+  for (int i = 0; i < num_in; ++i) {
+    if (!d_in[i]) return fail(FA_ERR_INVALID, "fa_mix: input %d NULL", i);
+    aligned = aligned && al16(d_in[i]);
+  }
+  if (n == 0) return FA_OK;
+  const int V = elems_per_vec(dtype);
+  const int64_t tiles = (n + (int64_t)kBlock * V - 1) / ((int64_t)kBlock * V);
+  if (tiles > 0x7FFFFFFFll) return fail(FA_ERR_INVALID, "too many tiles");
+
+  const size_t row_bytes = align16(sizeof(MixRow) * rows);
+  const size_t col_bytes = align16(sizeof(int32_t) * nnz);
+  const size_t val_bytes = align16(sizeof(double) * nnz);
+  const size_t ptr_bytes = sizeof(void*) * num_in;
+  const size_t bytes = row_bytes + col_bytes + val_bytes + ptr_bytes;
+
+  DeviceGuard g(ctx->device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
+  hipStream_t st = (hipStream_t)hip_stream;
+  fa_ctx::Slot* slot = nullptr;
+  int rc = acquire_slot(ctx, bytes, &slot);
+  if (rc) return rc;
+  char* h = (char*)slot->host;
+  MixRow* hr = (MixRow*)h;
+  for (int r = 0; r < rows; ++r)
+    hr[r] = MixRow{row_ptr[r], row_ptr[r + 1], d_out[r], post_scale ? d_out2[r] : nullptr,
+                   post_scale ? post_scale[r] : 1.0};
+  memcpy(h + row_bytes, cols, sizeof(int32_t) * nnz);
+  memcpy(h + row_bytes + col_bytes, vals, sizeof(double) * nnz);
+  memcpy(h + row_bytes + col_bytes + val_bytes, d_in, ptr_bytes);
+  rc = stage(slot, bytes, st);
+  if (rc) return rc;
+  char* d = (char*)slot->dev;
+  const MixRow* drw = (const MixRow*)d;
+  const int32_t* dcol = (const int32_t*)(d + row_bytes);
+  const double* dval = (const double*)(d + row_bytes + col_bytes);
+  const void* const* dptr = (const void* const*)(d + row_bytes + col_bytes + val_bytes);
+  const dim3 grid((unsigned)tiles), blk(kBlock);
+  const int al = aligned ? 1 : 0;
+#define FA_MIX_LAUNCH(DT)                                                                        \
+  if (post_scale)                                                                                \
+    hipLaunchKernelGGL((k_mix<DT, 4, true>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, n, al); \
+  else                                                                                           \
+    hipLaunchKernelGGL((k_mix<DT, 4, false>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, n, al);
+  switch (dtype) {
+    case FA_DTYPE_F32: FA_MIX_LAUNCH(FA_DTYPE_F32); break;
+    case FA_DTYPE_BF16: FA_MIX_LAUNCH(FA_DTYPE_BF16); break;
+    case FA_DTYPE_F16: FA_MIX_LAUNCH(FA_DTYPE_F16); break;
+  }
+#undef FA_MIX_LAUNCH
+  FA_HIP(hipGetLastError());
+  return release(slot, st);
+}
+
+}  // extern "C"

@@ -1,0 +1,171 @@
+"""AggEngine: the device-side aggregation engine over torch tensors (one per HIP device).
+
+Thin host layer over libfedagg.so: validates tensors, builds the pointer tables the C ABI takes,
+and launches on the current torch stream.  All arithmetic happens in the HIP kernels
+(fedml_amd/csrc/fedagg.hip); this module never computes results on the CPU.
+"""
+from __future__ import annotations
+
+import threading
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from . import _native as N
+
+MUL_W, MUL_N_DIV_N, SUM = N.MUL_W, N.MUL_N_DIV_N, N.SUM
+
+DTYPE_CODE = {
+    torch.float32: N.F32,
+    torch.bfloat16: N.BF16,
+    torch.float16: N.F16,
+    torch.float64: N.F64,
+    torch.int64: N.I64,
+}
+
+
+def out_dtype(dtype: torch.dtype, mode: int) -> torch.dtype:
+    """Result dtype of the reference's op sequence for an input dtype (PyTorch promotion)."""
+    if dtype == torch.int64 and mode != SUM:
+        return torch.float32
+    return dtype
+
+
+def _require_device(t: torch.Tensor, dev: torch.device, what: str):
+    if t.device != dev:
+        raise ValueError(f"{what}: tensor on {t.device}, engine on {dev}")
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: tensor must be contiguous")
+
+
+class AggEngine:
+    """One native context bound to one HIP device."""
+
+    _engines: Dict[int, "AggEngine"] = {}
+    _elock = threading.Lock()
+
+    def __init__(self, device: Optional[int] = None):
+        if not torch.cuda.is_available():
+            raise N.FedAggNativeError("no HIP device visible: the aggregation engine runs on MI355X only")
+        self.device_index = torch.cuda.current_device() if device is None else int(device)
+        self.device = torch.device("cuda", self.device_index)
+        L = N.lib()
+        h = N.ctypes.c_void_p()
+        N.check(L.fa_ctx_create(self.device_index, N.ctypes.byref(h)), "fa_ctx_create")
+        self._ctx = h
+        self._lib = L
+
+    @classmethod
+    def get(cls, device: Optional[int] = None) -> "AggEngine":
+        idx = torch.cuda.current_device() if device is None else int(device)
+        with cls._elock:
+            eng = cls._engines.get(idx)
+            if eng is None:
+                eng = cls._engines[idx] = AggEngine(idx)
+            return eng
+
+    def close(self):
+        if getattr(self, "_ctx", None) is not None and self._ctx.value:
+            self._lib.fa_ctx_destroy(self._ctx)
+            self._ctx = N.ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_variant(self, variant: int):
+        N.check(self._lib.fa_ctx_set_variant(self._ctx, int(variant)), "fa_ctx_set_variant")
+
+    def _stream(self, stream=None):
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        return N.ctypes.c_void_p(s.cuda_stream)
+
+    # ------------------------------------------------------------------ weighted sums
+    def weighted_sum(self, xs: Sequence[torch.Tensor], mode: int, coef: Optional[Sequence[float]] = None,
+                     divisor: float = 1.0, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """Ordered reduction over clients of same-shape device tensors (include/fedagg.h)."""
+        return self.weighted_sum_multi([list(xs)], mode, coef, divisor,
+                                       outs=None if out is None else [out], stream=stream)[0]
+
+    def weighted_sum_multi(self, segments: Sequence[Sequence[torch.Tensor]], mode: int,
+                           coef: Optional[Sequence[float]] = None, divisor: float = 1.0,
+                           outs: Optional[Sequence[torch.Tensor]] = None, stream=None) -> List[torch.Tensor]:
+        """segments[s][i] = client i's tensor for key s (one dtype for all); one launch."""
+        if len(segments) == 0:
+            return []
+        k = len(segments[0])
+        if k == 0:
+            raise ValueError("weighted_sum: no client tensors")
+        dt = segments[0][0].dtype
+        if dt not in DTYPE_CODE:
+            raise TypeError(f"weighted_sum: unsupported dtype {dt}")
+        if mode != SUM and (coef is None or len(coef) != k):
+            raise ValueError("weighted_sum: need one coefficient per client")
+        odt = out_dtype(dt, mode)
+        numels, in_ptrs, out_ptrs, results = [], [], [], []
+        for s, seg in enumerate(segments):
+            if len(seg) != k:
+                raise ValueError(f"segment {s}: {len(seg)} clients, expected {k}")
+            shape = seg[0].shape
+            for i, t in enumerate(seg):
+                if t.dtype != dt:
+                    raise TypeError(f"segment {s} client {i}: dtype {t.dtype} != {dt}")
+                if t.shape != shape:
+                    raise RuntimeError(f"segment {s} client {i}: shape {tuple(t.shape)} != {tuple(shape)}")
+                _require_device(t, self.device, f"segment {s} client {i}")
+                in_ptrs.append(t.data_ptr())
+            if outs is not None:
+                o = outs[s]
+                if o.dtype != odt or o.numel() != seg[0].numel():
+                    raise ValueError(f"segment {s}: output must be {odt} with {seg[0].numel()} elements")
+                _require_device(o, self.device, f"segment {s} output")
+            else:
+                o = torch.empty(shape, dtype=odt, device=self.device)
+            results.append(o)
+            out_ptrs.append(o.data_ptr())
+            numels.append(seg[0].numel())
+        c = N.f64_array(coef if coef is not None else [0.0] * k)
+        rc = self._lib.fa_weighted_sum_multi(
+            self._ctx, DTYPE_CODE[dt], int(mode), len(segments), N.i64_array(numels), k,
+            N.ptr_array(in_ptrs), c, float(divisor), N.ptr_array(out_ptrs), self._stream(stream))
+        N.check(rc, "fa_weighted_sum_multi")
+        return results
+
+    # ------------------------------------------------------------------ mixing / gossip
+    def mix(self, xs: Sequence[torch.Tensor], row_ptr: Sequence[int], cols: Sequence[int],
+            vals: Sequence[float], post_scale: Optional[Sequence[float]] = None,
+            outs: Optional[Sequence[torch.Tensor]] = None, outs2: Optional[Sequence[torch.Tensor]] = None,
+            stream=None) -> Tuple[List[torch.Tensor], Optional[List[torch.Tensor]]]:
+        """CSR-ordered mixing rows over same-shape device tensors (fa_mix)."""
+        if len(xs) == 0:
+            raise ValueError("mix: no inputs")
+        dt, shape = xs[0].dtype, xs[0].shape
+        for i, t in enumerate(xs):
+            if t.dtype != dt or t.shape != shape:
+                raise ValueError(f"mix: input {i} dtype/shape mismatch")
+            _require_device(t, self.device, f"mix input {i}")
+        rows = len(row_ptr) - 1
+        if outs is None:
+            outs = [torch.empty(shape, dtype=dt, device=self.device) for _ in range(rows)]
+        if post_scale is not None and outs2 is None:
+            outs2 = [torch.empty(shape, dtype=dt, device=self.device) for _ in range(rows)]
+        in_set = {t.data_ptr() for t in xs}
+        for o in list(outs) + list(outs2 or []):
+            _require_device(o, self.device, "mix output")
+            if o.data_ptr() in in_set:
+                raise ValueError("mix: outputs must not alias inputs")
+        rc = self._lib.fa_mix(
+            self._ctx, DTYPE_CODE.get(dt, -1), xs[0].numel(), rows, N.i32_array(row_ptr), N.i32_array(cols),
+            N.f64_array(vals), len(xs), N.ptr_array([t.data_ptr() for t in xs]),
+            N.ptr_array([o.data_ptr() for o in outs]),
+            N.f64_array(post_scale) if post_scale is not None else None,
+            N.ptr_array([o.data_ptr() for o in outs2]) if outs2 is not None else None,
+            self._stream(stream))
+        N.check(rc, "fa_mix")
+        return list(outs), (list(outs2) if outs2 is not None else None)
+
+
+def get_engine(device: Optional[int] = None) -> AggEngine:
+    return AggEngine.get(device)

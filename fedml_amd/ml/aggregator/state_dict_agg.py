@@ -1,0 +1,104 @@
+"""state_dict-level aggregation on the HIP engine.
+
+`aggregate(dicts, mode, coef, divisor)` reproduces, for every key of client 0's dict (in that
+key order), the reference's per-key client loop -- e.g. python/fedml/ml/aggregator/
+agg_operator.py:37-44 -- with the dtype semantics of the PyTorch ops it issues:
+
+* float32 / bfloat16 / float16 / float64 keys aggregate in their own type (per-op rounding);
+* integer keys: weighted modes promote to float32 (``int_tensor * python_float``); SUM keeps the
+  integer type with wrap-around (``int_tensor += int_tensor``); bool SUM is a logical OR;
+* every key of one dtype goes to the device in ONE launch (fa_weighted_sum_multi).
+
+Device placement: tensors already on a HIP device are aggregated in place on that device; CPU
+tensors (what the reference's transports deliver) are staged to the engine's device, aggregated
+there, and the result is returned on the CPU, matching the reference's output placement.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from ...engine import MUL_N_DIV_N, MUL_W, SUM, AggEngine, get_engine
+
+_NATIVE = (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64)
+_SMALL_INT = (torch.int32, torch.int16, torch.int8, torch.uint8)
+
+
+def _engine_for(tensors) -> AggEngine:
+    for t in tensors:
+        if t.is_cuda:
+            return get_engine(t.device.index)
+    return get_engine(None)
+
+
+def _to_engine(t: torch.Tensor, eng: AggEngine) -> torch.Tensor:
+    if t.device != eng.device:
+        t = t.to(eng.device, non_blocking=False)
+    return t if t.is_contiguous() else t.contiguous()
+
+
+def aggregate(dicts: Sequence[Dict[str, torch.Tensor]], mode: int, coef: Optional[Sequence[float]] = None,
+              divisor: float = 1.0, engine: Optional[AggEngine] = None) -> "OrderedDict[str, torch.Tensor]":
+    """Ordered per-key reduction over client state_dicts (see module docstring)."""
+    if len(dicts) == 0:
+        raise IndexError("list index out of range")  # the reference indexes raw_grad_list[0]
+    keys = list(dicts[0].keys())
+    first = [dicts[0][k] for k in keys]
+    eng = engine or _engine_for(first)
+    on_cpu = not any(t.is_cuda for t in first)
+    out: "OrderedDict[str, torch.Tensor]" = OrderedDict()
+    groups: Dict[torch.dtype, List[str]] = {}
+    post: Dict[str, torch.dtype] = {}
+    staged: Dict[str, List[torch.Tensor]] = {}
+    for k in keys:
+        col = [d[k] for d in dicts]  # KeyError on a missing key, like the reference
+        dt = col[0].dtype
+        for i, t in enumerate(col):
+            if t.dtype != dt:
+                raise TypeError(f"key {k!r}: client {i} has dtype {t.dtype}, client 0 has {dt} "
+                                "(mixed-dtype promotion is not part of the supported contract)")
+            if t.shape != col[0].shape:
+                raise RuntimeError(f"key {k!r}: client {i} shape {tuple(t.shape)} != {tuple(col[0].shape)}")
+        col = [_to_engine(t, eng) for t in col]
+        if dt in _SMALL_INT or dt == torch.bool:
+            # exact widening: int64 arithmetic gives the same low bits (SUM) and the same fp32
+            # conversion (weighted modes) as the narrower integer type
+            col = [t.to(torch.int64) for t in col]
+            if mode == SUM:
+                post[k] = dt
+        elif dt not in _NATIVE:
+            raise TypeError(f"key {k!r}: dtype {dt} is not supported")
+        staged[k] = col
+        groups.setdefault(col[0].dtype, []).append(k)
+    results: Dict[str, torch.Tensor] = {}
+    for dt, ks in groups.items():
+        outs = eng.weighted_sum_multi([staged[k] for k in ks], mode, coef, divisor)
+        for k, o in zip(ks, outs):
+            results[k] = o
+    for k in keys:
+        r = results[k]
+        if k in post:
+            tgt = post[k]
+            r = (r != 0) if tgt == torch.bool else r.to(tgt)
+        if on_cpu:
+            r = r.cpu()
+        out[k] = r
+    return out
+
+
+def fedavg(dicts, counts, engine=None):
+    """avg[k] = sum_i x_i[k] * (n_i / N), client order (agg_operator.py:35-44)."""
+    N = sum(counts)
+    return aggregate(dicts, MUL_W, [n / N for n in counts], engine=engine)
+
+
+def fedavg_xn_div_n(dicts, counts, engine=None):
+    """avg[k] = sum_i (x_i[k] * n_i) / N (simulation/mpi/fedavg/FedAVGAggregator.py:99-116)."""
+    return aggregate(dicts, MUL_N_DIV_N, list(counts), float(sum(counts)), engine=engine)
+
+
+def plain_sum(dicts, engine=None):
+    """avg[k] = sum_i x_i[k] (agg_operator.py:55-63 FedAvg_seq, :68-77 FedDyn)."""
+    return aggregate(dicts, SUM, engine=engine)

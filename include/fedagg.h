@@ -1,0 +1,140 @@
+/*
+ * fedagg.h -- C ABI of the MI355X-native FedAvg-family aggregation engine (libfedagg.so).
+ *
+ * This is the drop-in boundary under the reference's server-side aggregation operator
+ * (liuliuliu0605/FedML, python/fedml/; paths below are relative to that directory).  The
+ * reference has no native code on this path: every entry point here replaces a Python loop of
+ * PyTorch-CPU tensor ops.  Which loop each entry replaces:
+ *
+ *   fa_weighted_sum / fa_weighted_sum_multi
+ *     FA_MODE_MUL_W        ml/aggregator/agg_operator.py:35-54   torch_aggregator, FedAvg/FedProx
+ *                          ml/aggregator/agg_operator.py:100-133 SCAFFOLD / Mime (per dict)
+ *                          simulation/sp/fedavg/fedavg_api.py:144-159 FedAvgAPI._aggregate
+ *                          simulation/mpi/fedavg_seq/FedAvgClientManager.py:67-73 add_client_model
+ *                          simulation/nccl/base_framework/LocalAggregator.py:69-83 + params.py:73-82
+ *     FA_MODE_MUL_N_DIV_N  simulation/mpi/fedavg/FedAVGAggregator.py:99-116 _fedavg_aggregation_
+ *                          simulation/mpi/hierarchical_fl/HierFedAvgCloudAggregator.py:140-172
+ *     FA_MODE_SUM          ml/aggregator/agg_operator.py:55-63, 68-77 FedAvg_seq / FedDyn
+ *                          simulation/mpi/fedavg_seq/FedAVGAggregator.py:201-236 aggregate
+ *   fa_mix
+ *                          HierFedAvgCloudAggregator.py:174-195 _pfedavg_mixing_ (dense CSR)
+ *                          simulation/sp/decentralized/client_dsgd.py:104-122 (gossip step)
+ *                          simulation/sp/decentralized/client_pushsum.py:127-156 (+ post_scale)
+ *
+ * Arithmetic contract (bit-exact to the reference on the same inputs; pinned by the golden
+ * fixtures in tests/golden/): for every element e, clients i = 0..k-1 IN ORDER,
+ *   MUL_W:       t_i = op(x_i[e] * c_i)
+ *   MUL_N_DIV_N: t_i = op(op(x_i[e] * c_i) / divisor)
+ *   SUM:         t_i = x_i[e]
+ *   out[e] = t_0;  out[e] = op(out[e] + t_i) for i >= 1
+ * op(.) computes in float (FA_DTYPE_F32/BF16/F16/I64-promoted) or double (F64), rounds once to
+ * the storage type, and never fuses a multiply with an add.  Coefficients arrive as double
+ * (w_i = n_i / N is a Python float) and are cast to the op type, as PyTorch casts a Python
+ * scalar operand.  FA_DTYPE_I64 inputs: MUL_W -> float32 output (fp32(x) * fp32(w));
+ * MUL_N_DIV_N -> float32 output (fp32((int64)(x * (int64)c)) / fp32(divisor)); SUM -> int64
+ * output (two's-complement wrap).
+ *
+ * Memory: every data pointer is a DEVICE pointer on the context's HIP device, caller-owned
+ * (e.g. torch tensors).  Outputs must not alias inputs.  Pointer tables, coefficients and
+ * sizes are HOST arrays; the library stages them to the device itself.  Nothing in the hot call
+ * allocates once the context's staging slots are warm.  Calls are asynchronous on `hip_stream`
+ * (NULL = the null stream); host arrays may be reused as soon as a call returns.
+ *
+ * Errors: every entry returns FA_OK (0) or a negative fa_status; the library never aborts.
+ * fa_strerror(code) names the code; fa_last_error() gives the detail of the calling thread's
+ * last failure.  A context is not thread-safe: use one per thread or lock externally.
+ */
+#ifndef FEDAGG_H
+#define FEDAGG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct fa_ctx fa_ctx;
+
+enum fa_dtype {
+    FA_DTYPE_F32 = 0,
+    FA_DTYPE_BF16 = 1,
+    FA_DTYPE_F16 = 2,
+    FA_DTYPE_F64 = 3,
+    FA_DTYPE_I64 = 4
+};
+
+enum fa_mode {
+    FA_MODE_MUL_W = 0,
+    FA_MODE_MUL_N_DIV_N = 1,
+    FA_MODE_SUM = 2
+};
+
+enum fa_status {
+    FA_OK = 0,
+    FA_ERR_INVALID = -1,  /* null pointer, k <= 0, n < 0, bad CSR, ...   */
+    FA_ERR_DTYPE = -2,    /* dtype/mode combination not supported          */
+    FA_ERR_HIP = -3,      /* a HIP runtime call failed (see fa_last_error) */
+    FA_ERR_NOMEM = -4     /* staging allocation failed                     */
+};
+
+#define FA_ABI_VERSION 1
+
+/* ABI version of the loaded library (== FA_ABI_VERSION of the header it was built with). */
+int fa_abi_version(void);
+
+/* Create a context bound to HIP device `hip_device` (owns pinned + device staging slots). */
+int fa_ctx_create(int hip_device, fa_ctx **out);
+/* Destroy a context; waits for the calls still using its staging slots. */
+int fa_ctx_destroy(fa_ctx *ctx);
+
+/*
+ * One flat parameter vector per client:
+ *   d_in[i] (i < k): device pointer to n elements of `dtype`; coef[i]: w_i (MUL_W) or n_i
+ *   (MUL_N_DIV_N), ignored for SUM (may be NULL then); divisor: N (MUL_N_DIV_N only).
+ *   d_out: n elements of the output type (see the contract above).
+ * Replaces the per-key inner loop `for i in range(K)` of agg_operator.py:37-44 and its kin.
+ */
+int fa_weighted_sum(fa_ctx *ctx, int dtype, int mode, int64_t n, int32_t k,
+                     const void *const *d_in, const double *coef, double divisor,
+                     void *d_out, void *hip_stream);
+
+/*
+ * A whole state_dict in ONE launch: `num_segments` tensors (keys) of one dtype.
+ *   seg_numel[s]            elements of key s;
+ *   d_in[s * k + i]         client i's tensor for key s (device pointer);
+ *   d_out[s]                output tensor for key s.
+ * Same arithmetic per element as fa_weighted_sum; coef/divisor shared by all keys.
+ * Replaces the outer `for k in avg_params.keys()` loop of agg_operator.py:37.
+ */
+int fa_weighted_sum_multi(fa_ctx *ctx, int dtype, int mode, int32_t num_segments,
+                           const int64_t *seg_numel, int32_t k, const void *const *d_in,
+                           const double *coef, double divisor, void *const *d_out,
+                           void *hip_stream);
+
+/*
+ * Mixing / gossip: for every row r < rows, with CSR entries j in [row_ptr[r], row_ptr[r+1]):
+ *   d_out[r][e] = ordered MUL_W reduction of d_in[cols[j]][e] * vals[j]   (entry order = CSR order)
+ *   if post_scale: d_out2[r][e] = op(d_out[r][e] * post_scale[r])         (PushSum z = x / omega)
+ * Dense rows (every column, zeros included, ascending) reproduce _pfedavg_mixing_ exactly, incl.
+ * NaN from 0 * Inf; the DSGD row is [self, in-neighbours ascending].  dtype: F32, BF16 or F16.
+ * num_in: number of input pointers (cols must be < num_in).  Outputs must not alias inputs.
+ */
+int fa_mix(fa_ctx *ctx, int dtype, int64_t n, int32_t rows, const int32_t *row_ptr,
+           const int32_t *cols, const double *vals, int32_t num_in, const void *const *d_in,
+           void *const *d_out, const double *post_scale, void *const *d_out2, void *hip_stream);
+
+/* Performance tuning only (results are identical for every variant): selects the weighted-sum
+ * kernel's client unroll / cache policy.  0 = default (U=8, non-temporal loads), 1 = U=4,
+ * 2 = U=16, 3 = U=8 with default-policy loads. */
+int fa_ctx_set_variant(fa_ctx *ctx, int variant);
+
+/* Static name of a status code. */
+const char *fa_strerror(int code);
+/* Detail of the calling thread's last error ("" if none). */
+const char *fa_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FEDAGG_H */

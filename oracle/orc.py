@@ -1,0 +1,92 @@
+"""ctypes wrapper over the C oracle (``fedagg_oracle.c``) -- TEST INFRASTRUCTURE ONLY.
+
+Operates on CPU torch tensors.  Codes follow include/fedagg.h (F32=0, BF16=1, F16=2, F64=3,
+I64=4; MUL_W=0, MUL_N_DIV_N=1, SUM=2).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liborc.so")
+
+F32, BF16, F16, F64, I64 = 0, 1, 2, 3, 4
+MUL_W, MUL_N_DIV_N, SUM = 0, 1, 2
+
+_DT = {torch.float32: F32, torch.bfloat16: BF16, torch.float16: F16, torch.float64: F64,
+       torch.int64: I64}
+
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.orc_weighted_sum.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int32,
+                                       ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_double),
+                                       ctypes.c_double, ctypes.c_void_p]
+        L.orc_weighted_sum.restype = ctypes.c_int
+        L.orc_mix.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int32,
+                              ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32),
+                              ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_void_p),
+                              ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_double),
+                              ctypes.POINTER(ctypes.c_void_p)]
+        L.orc_mix.restype = ctypes.c_int
+        L.orc_f32_to_bf16.argtypes = [ctypes.c_float]
+        L.orc_f32_to_bf16.restype = ctypes.c_uint16
+        L.orc_f32_to_f16.argtypes = [ctypes.c_float]
+        L.orc_f32_to_f16.restype = ctypes.c_uint16
+        _lib = L
+    return _lib
+
+
+def out_dtype(dtype: torch.dtype, mode: int) -> torch.dtype:
+    if dtype == torch.int64 and mode != SUM:
+        return torch.float32
+    return dtype
+
+
+def weighted_sum(xs, mode: int, coef=None, divisor: float = 1.0) -> torch.Tensor:
+    """Ordered reduction over the list of same-shape CPU tensors ``xs``."""
+    xs = [x.contiguous() for x in xs]
+    dt = xs[0].dtype
+    assert all(x.dtype == dt and x.shape == xs[0].shape for x in xs)
+    k = len(xs)
+    out = torch.empty(xs[0].shape, dtype=out_dtype(dt, mode))
+    ptrs = (ctypes.c_void_p * k)(*[x.data_ptr() for x in xs])
+    c = (ctypes.c_double * k)(*([float(v) for v in coef] if coef is not None else [0.0] * k))
+    rc = lib().orc_weighted_sum(_DT[dt], mode, xs[0].numel(), k, ptrs, c, float(divisor), out.data_ptr())
+    if rc != 0:
+        raise RuntimeError(f"orc_weighted_sum failed: {rc}")
+    return out
+
+
+def mix(xs, row_ptr, cols, vals, post_scale=None):
+    """CSR-ordered mixing rows (see orc_mix); returns (outs, outs2 or None)."""
+    xs = [x.contiguous() for x in xs]
+    rows = len(row_ptr) - 1
+    outs = [torch.empty_like(xs[0]) for _ in range(rows)]
+    outs2 = [torch.empty_like(xs[0]) for _ in range(rows)] if post_scale is not None else None
+    P = ctypes.c_void_p
+    rc = lib().orc_mix(
+        _DT[xs[0].dtype], xs[0].numel(), rows,
+        (ctypes.c_int32 * len(row_ptr))(*row_ptr), (ctypes.c_int32 * len(cols))(*cols),
+        (ctypes.c_double * len(vals))(*[float(v) for v in vals]),
+        (P * len(xs))(*[x.data_ptr() for x in xs]), (P * rows)(*[o.data_ptr() for o in outs]),
+        (ctypes.c_double * rows)(*post_scale) if post_scale is not None else None,
+        (P * rows)(*[o.data_ptr() for o in outs2]) if outs2 is not None else None)
+    if rc != 0:
+        raise RuntimeError(f"orc_mix failed: {rc}")
+    return outs, outs2

@@ -1,0 +1,93 @@
+"""Read/write the committed golden fixtures (data only: inputs + expected outputs).
+
+Fixture format (one ``.npz`` per case, ``allow_pickle=False``):
+
+* ``meta``            -- uint8 array holding UTF-8 JSON: case name, kind, sample counts,
+                          key order, dtypes, extra parameters.
+* ``x{i}__{key}``     -- client ``i``'s tensor for ``key`` (bf16 stored as its uint16 bits).
+* ``y{j}__{key}``     -- expected output ``j`` (most cases have a single output, ``j = 0``).
+* any other array     -- case-specific extras named in ``meta`` (e.g. a mixing matrix ``W``).
+
+The fixtures were produced by ``make_golden.py`` from the reference implementation
+(``/root/reference``) inside the build container; nothing here reads the reference.
+"""
+from __future__ import annotations
+
+import json
+import os
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+GOLDEN_DIR = os.path.dirname(os.path.abspath(__file__))
+
+_TORCH_TO_NAME = {
+    torch.float32: "float32",
+    torch.float64: "float64",
+    torch.float16: "float16",
+    torch.bfloat16: "bfloat16",
+    torch.int64: "int64",
+    torch.int32: "int32",
+    torch.uint8: "uint8",
+    torch.bool: "bool",
+}
+_NAME_TO_TORCH = {v: k for k, v in _TORCH_TO_NAME.items()}
+
+
+def tensor_to_np(t: torch.Tensor) -> np.ndarray:
+    t = t.detach().cpu().contiguous()
+    if t.dtype == torch.bfloat16:
+        return t.view(torch.int16).numpy().view(np.uint16).copy()
+    return t.numpy().copy()
+
+
+def np_to_tensor(a: np.ndarray, dtype_name: str) -> torch.Tensor:
+    if dtype_name == "bfloat16":
+        return torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16)
+    t = torch.from_numpy(np.ascontiguousarray(a).copy())
+    assert t.dtype == _NAME_TO_TORCH[dtype_name], (t.dtype, dtype_name)
+    return t
+
+
+def dtype_name(t: torch.Tensor) -> str:
+    return _TORCH_TO_NAME[t.dtype]
+
+
+def save_case(path: str, meta: dict, arrays: dict) -> None:
+    blob = np.frombuffer(json.dumps(meta, sort_keys=True).encode("utf-8"), dtype=np.uint8)
+    np.savez_compressed(path, meta=blob, **arrays)
+
+
+def load_case(path: str):
+    with np.load(path, allow_pickle=False) as z:
+        meta = json.loads(bytes(z["meta"]).decode("utf-8"))
+        arrays = {k: z[k] for k in z.files if k != "meta"}
+    return meta, arrays
+
+
+def client_dicts(meta: dict, arrays: dict):
+    """Rebuild the list of client state_dicts (OrderedDicts in the fixture's key order)."""
+    out = []
+    for i in range(meta["num_clients"]):
+        d = OrderedDict()
+        for key, dt in zip(meta["keys"], meta["in_dtypes"]):
+            d[key] = np_to_tensor(arrays[f"x{i}__{key}"], dt)
+        out.append(d)
+    return out
+
+
+def expected_dicts(meta: dict, arrays: dict):
+    out = []
+    for j in range(meta.get("num_outputs", 1)):
+        d = OrderedDict()
+        for key, dt in zip(meta["keys"], meta["out_dtypes"]):
+            d[key] = np_to_tensor(arrays[f"y{j}__{key}"], dt)
+        out.append(d)
+    return out
+
+
+def list_cases():
+    return sorted(
+        os.path.join(GOLDEN_DIR, f) for f in os.listdir(GOLDEN_DIR) if f.endswith(".npz")
+    )

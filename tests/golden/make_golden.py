@@ -1,0 +1,591 @@
+"""Generate the golden fixtures under tests/golden/ from the REFERENCE implementation.
+
+Runs only in the build container, where the read-only reference is mounted at
+/root/reference (it never travels to the GPU box; the fixtures it writes do).
+Nothing from the reference is copied: this script imports the reference's own
+functions, feeds them seeded synthetic client updates, and stores inputs and
+outputs as plain arrays (see golden_io.py for the format).
+
+Loading recipe:
+  * ``fedml.ml.aggregator.agg_operator`` is imported behind stub parent packages
+    (``import fedml`` itself needs torchvision, which is absent).
+  * Methods that live in modules importing wandb / mpi4py / torchvision are
+    extracted with ``ast`` (only the named FunctionDef) and executed with a stub
+    ``self``.
+  * The topology managers need ``nx.to_numpy_matrix`` (removed in networkx 3);
+    ``nx.to_numpy_array`` yields the same values once cast to float32.
+
+Usage:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import ast
+import copy
+import functools
+import importlib
+import json
+import logging
+import os
+import random
+import sys
+import time
+import types
+from collections import OrderedDict
+
+sys.dont_write_bytecode = True  # never write __pycache__ into the read-only reference
+
+import networkx as nx
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from golden_io import dtype_name, save_case, tensor_to_np  # noqa: E402
+
+REF_PY = "/root/reference/python"
+REF = REF_PY + "/fedml"
+
+
+# ----------------------------------------------------------------------------- loading
+def _stub_pkg(name: str, path: str) -> None:
+    if name in sys.modules:
+        return
+    m = types.ModuleType(name)
+    m.__path__ = [path]
+    sys.modules[name] = m
+
+
+def load_agg_operator():
+    for name, sub in [
+        ("fedml", ""),
+        ("fedml.core", "/core"),
+        ("fedml.core.common", "/core/common"),
+        ("fedml.ml", "/ml"),
+        ("fedml.ml.aggregator", "/ml/aggregator"),
+    ]:
+        _stub_pkg(name, REF + sub)
+    return importlib.import_module("fedml.ml.aggregator.agg_operator")
+
+
+def load_topology():
+    if not hasattr(nx, "to_numpy_matrix"):
+        nx.to_numpy_matrix = nx.to_numpy_array
+    for name, sub in [
+        ("fedml", ""),
+        ("fedml.core", "/core"),
+        ("fedml.core.distributed", "/core/distributed"),
+        ("fedml.core.distributed.topology", "/core/distributed/topology"),
+    ]:
+        _stub_pkg(name, REF + sub)
+    stm = importlib.import_module("fedml.core.distributed.topology.symmetric_topology_manager")
+    tu = importlib.import_module("fedml.core.distributed.topology.topo_utils")
+    return stm, tu
+
+
+def extract_method(relpath: str, class_name: str, func_name: str, extra_globals=None):
+    """Compile ONLY `class_name.func_name` from a reference file and return it as a function."""
+    path = os.path.join(REF, relpath)
+    with open(path) as f:
+        tree = ast.parse(f.read(), filename=path)
+    for node in tree.body:
+        if isinstance(node, ast.ClassDef) and node.name == class_name:
+            for item in node.body:
+                if isinstance(item, ast.FunctionDef) and item.name == func_name:
+                    mod = ast.Module(body=[item], type_ignores=[])
+                    g = {"copy": copy, "torch": torch, "np": np, "logging": logging, "time": time}
+                    if extra_globals:
+                        g.update(extra_globals)
+                    exec(compile(mod, path, "exec"), g)
+                    return g[func_name]
+    raise KeyError(f"{relpath}:{class_name}.{func_name}")
+
+
+class _Off:
+    """Stub for FedMLAttacker / FedMLDefender singletons: every feature disabled."""
+
+    @classmethod
+    def get_instance(cls):
+        return cls()
+
+    def is_model_attack(self):
+        return False
+
+    def is_defense_enabled(self):
+        return False
+
+
+# ----------------------------------------------------------------------------- data
+def gen_clients(seed, K, layout, kind="normal"):
+    """K client state_dicts with the given [(key, shape, dtype)] layout."""
+    g = torch.Generator().manual_seed(seed)
+    clients = []
+    for i in range(K):
+        d = OrderedDict()
+        for key, shape, dt in layout:
+            if dt in (torch.int64, torch.int32):
+                d[key] = torch.randint(0, 50, shape, generator=g, dtype=dt)
+            else:
+                if kind == "normal":
+                    v = torch.randn(shape, generator=g, dtype=torch.float64)
+                elif kind == "cancel":
+                    # near-cancelling values: large common magnitude, alternating sign per client
+                    base = torch.randn(shape, generator=g, dtype=torch.float64) * 1e3
+                    v = base * (1 if i % 2 == 0 else -1) + torch.randn(shape, generator=g, dtype=torch.float64) * 1e-3
+                elif kind == "wide":
+                    v = torch.randn(shape, generator=g, dtype=torch.float64) * torch.exp2(
+                        torch.randint(-30, 30, shape, generator=g).double())
+                else:
+                    raise ValueError(kind)
+                d[key] = v.to(dt)
+        clients.append(d)
+    return clients
+
+
+def gen_counts(seed, K, lo=50, hi=600):
+    rng = np.random.RandomState(seed)
+    return [int(v) for v in rng.randint(lo, hi + 1, size=K)]
+
+
+def pack(clients, outputs, meta):
+    arrays = {}
+    keys = list(clients[0].keys())
+    for i, c in enumerate(clients):
+        for k in keys:
+            arrays[f"x{i}__{k}"] = tensor_to_np(c[k])
+    for j, o in enumerate(outputs):
+        for k in keys:
+            arrays[f"y{j}__{k}"] = tensor_to_np(o[k])
+    meta = dict(meta)
+    meta.update(
+        num_clients=len(clients),
+        num_outputs=len(outputs),
+        keys=keys,
+        in_dtypes=[dtype_name(clients[0][k]) for k in keys],
+        out_dtypes=[dtype_name(outputs[0][k]) for k in keys],
+        shapes=[list(clients[0][k].shape) for k in keys],
+    )
+    return meta, arrays
+
+
+WRITTEN = []
+
+
+def write(name, clients, outputs, meta, extra=None):
+    meta, arrays = pack(clients, outputs, meta)
+    meta["name"] = name
+    if extra:
+        arrays.update(extra)
+    path = os.path.join(HERE, name + ".npz")
+    save_case(path, meta, arrays)
+    WRITTEN.append((name, os.path.getsize(path)))
+
+
+def dc(x):
+    return copy.deepcopy(x)
+
+
+class Args(types.SimpleNamespace):
+    pass
+
+
+LR_LAYOUT = [("linear.weight", (10, 784), torch.float32), ("linear.bias", (10,), torch.float32)]
+
+
+# ----------------------------------------------------------------------------- cases
+def cases_agg_operator(ao):
+    """G1/G2/G3/G5/G9 through FedMLAggOperator.agg (agg_operator.py:9-134)."""
+    agg = ao.FedMLAggOperator.agg
+    seed = 100
+    # G1: fp32 FedAvg, flat parameter vectors
+    for K in (1, 2, 3, 7, 32):
+        for P in (1, 3, 1000, 4099):
+            seed += 1
+            clients = gen_clients(seed, K, [("w", (P,), torch.float32)])
+            n = gen_counts(seed, K)
+            out = agg(Args(federated_optimizer="FedAvg"), list(zip(n, dc(clients))))
+            write(f"g1_fedavg_f32_K{K}_P{P}", clients, [out],
+                  dict(kind="agg", optimizer="FedAvg", n=n, ref="agg_operator.py:35-44"))
+    # G1: FedProx branch (agg_operator.py:45-54), LR layout (config 1 shape)
+    clients = gen_clients(7, 2, LR_LAYOUT)
+    n = gen_counts(7, 2)
+    for opt in ("FedAvg", "FedProx"):
+        out = agg(Args(federated_optimizer=opt), list(zip(n, dc(clients))))
+        write(f"g1_{opt.lower()}_lr_K2", clients, [out],
+              dict(kind="agg", optimizer=opt, n=n, ref="agg_operator.py:35-54"))
+    # G1: cancellation-heavy and wide-exponent values
+    for kind in ("cancel", "wide"):
+        clients = gen_clients(11, 16, [("w", (2053,), torch.float32)], kind=kind)
+        n = gen_counts(11, 16)
+        out = agg(Args(federated_optimizer="FedAvg"), list(zip(n, dc(clients))))
+        write(f"g1_fedavg_f32_{kind}_K16", clients, [out],
+              dict(kind="agg", optimizer="FedAvg", n=n, ref="agg_operator.py:35-44"))
+    # G2: bf16 FedAvg (per-op bf16 rounding, fp32 weight)
+    for K, P in ((7, 4099), (32, 1000), (3, 5)):
+        clients = gen_clients(200 + K, K, [("w", (P,), torch.bfloat16), ("b", (17,), torch.bfloat16)])
+        n = gen_counts(200 + K, K)
+        out = agg(Args(federated_optimizer="FedAvg"), list(zip(n, dc(clients))))
+        write(f"g2_fedavg_bf16_K{K}_P{P}", clients, [out],
+              dict(kind="agg", optimizer="FedAvg", n=n, ref="agg_operator.py:35-44"))
+    # fp16 and fp64 FedAvg (same operator, other storage types)
+    for dt, tag in ((torch.float16, "f16"), (torch.float64, "f64")):
+        clients = gen_clients(300, 5, [("w", (999,), dt)])
+        n = gen_counts(300, 5)
+        out = agg(Args(federated_optimizer="FedAvg"), list(zip(n, dc(clients))))
+        write(f"g2_fedavg_{tag}_K5", clients, [out],
+              dict(kind="agg", optimizer="FedAvg", n=n, ref="agg_operator.py:35-44"))
+    # G3: mixed-dtype state_dict (fp32 params + int64 num_batches_tracked-style scalars)
+    layout = [
+        ("conv1.weight", (8, 3, 3, 3), torch.float32),
+        ("bn1.weight", (8,), torch.float32),
+        ("bn1.bias", (8,), torch.float32),
+        ("bn1.num_batches_tracked", (), torch.int64),
+        ("fc.weight", (10, 72), torch.float32),
+        ("fc.bias", (10,), torch.float32),
+        ("layer.num_batches_tracked", (), torch.int64),
+    ]
+    for K in (2, 5):
+        clients = gen_clients(400 + K, K, layout)
+        n = gen_counts(400 + K, K)
+        out = agg(Args(federated_optimizer="FedAvg"), list(zip(n, dc(clients))))
+        write(f"g3_fedavg_mixed_K{K}", clients, [out],
+              dict(kind="agg", optimizer="FedAvg", n=n, ref="agg_operator.py:35-44"))
+    # G5: plain sum branches FedAvg_seq / FedDyn (agg_operator.py:55-63, 68-77), incl. int64 sums
+    layout = [("w", (1001,), torch.float32), ("steps", (), torch.int64), ("h", (33,), torch.bfloat16)]
+    for opt in ("FedAvg_seq", "FedDyn"):
+        clients = gen_clients(500, 6, layout)
+        n = gen_counts(500, 6)
+        out = agg(Args(federated_optimizer=opt), list(zip(n, dc(clients))))
+        write(f"g5_{opt.lower()}_sum_K6", clients, [out],
+              dict(kind="agg", optimizer=opt, n=n, ref="agg_operator.py:55-77"))
+    # G9: edge values -- +-0, subnormals, inf/nan, huge counts
+    K = 4
+    vals = torch.tensor([0.0, -0.0, 1e-45, -1e-45, 1.17e-38, 3.4e38, -3.4e38, float("inf"),
+                         float("-inf"), float("nan"), 1.0, -1.0, 1e-30, 7.0, 0.1, -0.0],
+                        dtype=torch.float32)
+    clients = []
+    for i in range(K):
+        g = torch.Generator().manual_seed(900 + i)
+        perm = torch.randperm(vals.numel(), generator=g)
+        clients.append(OrderedDict(w=vals[perm].clone()))
+    for name, n in (("g9_edge_values_K4", [3, 5, 7, 11]),
+                    ("g9_edge_bigcounts_K4", [2 ** 24 + 1, 3, 2 ** 30 + 7, 99991])):
+        out = agg(Args(federated_optimizer="FedAvg"), list(zip(n, dc(clients))))
+        write(name, clients, [out], dict(kind="agg", optimizer="FedAvg", n=n, ref="agg_operator.py:35-44"))
+    # G9: inexact n_i/N (N = 3 * 7 * 13), normal data
+    clients = gen_clients(950, 3, [("w", (4099,), torch.float32)])
+    n = [7, 13, 273 - 20]
+    out = agg(Args(federated_optimizer="FedAvg"), list(zip(n, dc(clients))))
+    write("g9_inexact_weights_K3", clients, [out], dict(kind="agg", optimizer="FedAvg", n=n,
+                                                        ref="agg_operator.py:35-44"))
+    # SCAFFOLD / Mime (agg_operator.py:100-133) -- two-dict outputs, with SCAFFOLD's overwrite defect
+    K = 4
+    lay = [("w", (257,), torch.float32), ("b", (9,), torch.float32)]
+    xs = gen_clients(960, K, lay)
+    cs = gen_clients(961, K, lay)
+    n = gen_counts(960, K)
+    out = agg(Args(federated_optimizer="SCAFFOLD", client_num_in_total=10),
+              [(n[i], dc(xs[i]), dc(cs[i])) for i in range(K)])
+    extra = {}
+    for i in range(K):
+        for k in ("w", "b"):
+            extra[f"c{i}__{k}"] = tensor_to_np(cs[i][k])
+    write("g5_scaffold_K4", xs, [out[0], out[1]],
+          dict(kind="agg", optimizer="SCAFFOLD", n=n, client_num_in_total=10,
+               ref="agg_operator.py:100-118"), extra)
+    out = agg(Args(federated_optimizer="Mime", client_num_per_round=K),
+              [(n[i], dc(xs[i]), dc(cs[i])) for i in range(K)])
+    write("g5_mime_K4", xs, [out[0], out[1]],
+          dict(kind="agg", optimizer="Mime", n=n, client_num_per_round=K,
+               ref="agg_operator.py:120-133"), extra)
+
+
+def cases_call_sites():
+    """a6 / a7 / a8 / a12: the inline re-implementations of the same loop."""
+    sp_aggregate = extract_method("simulation/sp/fedavg/fedavg_api.py", "FedAvgAPI", "_aggregate")
+    mpi_agg = extract_method("simulation/mpi/fedavg/FedAVGAggregator.py", "FedAVGAggregator",
+                             "_fedavg_aggregation_")
+    stub = types.SimpleNamespace()
+    # a6: SP FedAvgAPI._aggregate (fedavg_api.py:144-159)
+    clients = gen_clients(600, 9, [("w", (3001,), torch.float32), ("b", (10,), torch.float32)])
+    n = gen_counts(600, 9)
+    out = sp_aggregate(stub, list(zip(n, dc(clients))))
+    write("g1_sp_aggregate_K9", clients, [out], dict(kind="sp_aggregate", n=n, ref="fedavg_api.py:144-159"))
+    # a7: MPI (x*n)/N (FedAVGAggregator.py:99-116) -- G4, incl. config-1 LR layout, K=2
+    for K, lay, tag in ((3, [("w", (4099,), torch.float32)], "K3"),
+                        (32, [("w", (1000,), torch.float32)], "K32"),
+                        (2, LR_LAYOUT, "lr_K2")):
+        clients = gen_clients(610 + K, K, lay)
+        n = gen_counts(610 + K, K)
+        out = mpi_agg(stub, list(zip(n, dc(clients))))
+        write(f"g4_mpi_xn_div_N_{tag}", clients, [out],
+              dict(kind="mpi_fedavg", n=n, ref="simulation/mpi/fedavg/FedAVGAggregator.py:99-116"))
+    # a7 with bf16 and with counts >= 2^24
+    clients = gen_clients(620, 4, [("w", (777,), torch.bfloat16)])
+    n = gen_counts(620, 4)
+    out = mpi_agg(stub, list(zip(n, dc(clients))))
+    write("g4_mpi_xn_div_N_bf16_K4", clients, [out], dict(kind="mpi_fedavg", n=n,
+                                                          ref="FedAVGAggregator.py:99-116"))
+    clients = gen_clients(621, 3, [("w", (501,), torch.float32)])
+    n = [2 ** 24 + 3, 2 ** 25 + 1, 5]
+    out = mpi_agg(stub, list(zip(n, dc(clients))))
+    write("g4_mpi_xn_div_N_bigcounts_K3", clients, [out], dict(kind="mpi_fedavg", n=n,
+                                                               ref="FedAVGAggregator.py:99-116"))
+    # a7 with int64 buffers: (x * n) is an int64 op, then true_divide -> float32
+    lay = [("w", (301,), torch.float32), ("bn.num_batches_tracked", (), torch.int64),
+           ("cnt", (7,), torch.int64)]
+    clients = gen_clients(622, 5, lay)
+    clients[2]["cnt"][3] = 2 ** 40 + 12345
+    n = gen_counts(622, 5)
+    out = mpi_agg(stub, list(zip(n, dc(clients))))
+    write("g4_mpi_xn_div_N_int64_K5", clients, [out], dict(kind="mpi_fedavg", n=n,
+                                                           ref="FedAVGAggregator.py:99-116"))
+
+    # a12: fedavg_seq two-level reduce (FedAvgClientManager.py:67-73 + FedAVGAggregator.py:189-236)
+    add_client_model = extract_method("simulation/mpi/fedavg_seq/FedAvgClientManager.py",
+                                      "FedAVGClientManager", "add_client_model")
+    get_average_weight = extract_method("simulation/mpi/fedavg_seq/FedAVGAggregator.py",
+                                        "FedAVGAggregator", "get_average_weight")
+    seq_aggregate = extract_method("simulation/mpi/fedavg_seq/FedAVGAggregator.py",
+                                   "FedAVGAggregator", "aggregate")
+    K = 10
+    clients = gen_clients(630, K, [("w", (2049,), torch.float32), ("b", (10,), torch.float32)])
+    n = gen_counts(630, K)
+    server = types.SimpleNamespace(train_data_local_num_dict={i: n[i] for i in range(K)})
+    wdict = get_average_weight(server, list(range(K)))
+    schedule = [[0, 1, 2, 3], [4, 5, 6], [7, 8, 9]]
+    partials = []
+    for wk in schedule:
+        acc = {}
+        for ci in wk:
+            add_client_model(None, acc, dc(clients[ci]), weight=wdict[ci])
+        partials.append(acc)
+    seq_server = types.SimpleNamespace(
+        worker_num=len(schedule), model_dict={i: partials[i] for i in range(len(schedule))},
+        set_global_model_params=lambda p: None)
+    out = seq_aggregate(seq_server)
+    write("g6_fedavg_seq_two_level_K10", clients, [out],
+          dict(kind="fedavg_seq", n=n, schedule=schedule,
+               ref="fedavg_seq/FedAvgClientManager.py:67-73; fedavg_seq/FedAVGAggregator.py:189-236"))
+
+    # a6 hierarchical SP: group _aggregate then global _aggregate weighted by group sample counts
+    K = 12
+    groups = [[0, 1, 2, 3, 4], [5, 6], [7, 8, 9, 10, 11]]
+    clients = gen_clients(640, K, [("w", (1537,), torch.float32), ("b", (10,), torch.float32)])
+    n = gen_counts(640, K)
+    w_groups = []
+    for grp in groups:
+        gw = sp_aggregate(stub, [(n[i], dc(clients[i])) for i in grp])
+        w_groups.append((sum(n[i] for i in grp), gw))
+    out = sp_aggregate(stub, w_groups)
+    write("g7_hier_sp_K12_G3", clients, [out],
+          dict(kind="hier_sp", n=n, groups=groups,
+               ref="sp/hierarchical_fl/group.py:43-66; trainer.py:100-110; fedavg_api.py:144-159"))
+
+    # a8 MPI cloud aggregate() with its double application (HierFedAvgCloudAggregator.py:67-103)
+    cloud_fedavg = extract_method("simulation/mpi/hierarchical_fl/HierFedAvgCloudAggregator.py",
+                                  "HierFedAVGCloudAggregator", "_fedavg_aggregation_")
+    cloud_aggregate = extract_method("simulation/mpi/hierarchical_fl/HierFedAvgCloudAggregator.py",
+                                     "HierFedAVGCloudAggregator", "aggregate",
+                                     {"FedMLAttacker": _Off, "FedMLDefender": _Off})
+    E, R = 3, 2  # edges (workers) x group_comm_round
+    edge_models = gen_clients(650, E * R, [("w", (1025,), torch.float32), ("b", (10,), torch.float32)])
+    ne = [gen_counts(650 + e, R) for e in range(E)]
+    cloud = types.SimpleNamespace(
+        worker_num=E,
+        sample_num_dict={e: list(ne[e]) for e in range(E)},
+        model_dict={e: [(r, dc(edge_models[e * R + r])) for r in range(R)] for e in range(E)},
+    )
+    cloud._fedavg_aggregation_ = functools.partial(cloud_fedavg, cloud)
+    cloud.set_global_model_params = lambda p: None
+    cloud.test_on_cloud_for_all_clients = lambda r: None
+    cloud.get_global_model_params = lambda: None
+    out = cloud_aggregate(cloud)
+    write("g7_hier_cloud_aggregate_E3_R2", edge_models, [out],
+          dict(kind="hier_cloud", edges=E, group_comm_round=R, edge_counts=ne,
+               note="client index = e*R + r",
+               ref="mpi/hierarchical_fl/HierFedAvgCloudAggregator.py:67-103,140-157"))
+    return cloud_fedavg
+
+
+def cases_topology_and_mixing(stm, tu):
+    """a9 / a10 / a11: mixing matrices, _pfedavg_mixing_, mix(), DSGD / PushSum gossip steps."""
+    # a10: topologies
+    extra = {}
+    meta_topos = []
+    for n in (8, 256):
+        m = stm.SymmetricTopologyManager(n, 2)
+        m.generate_custom_topology(Args(topo_name="ring"))
+        extra[f"W_ring_{n}"] = np.asarray(m.topology, dtype=np.float32)
+        meta_topos.append(f"W_ring_{n}")
+    for name, fn in (("complete", tu.get_complete_overlay), ("star", tu.get_star_overlay),
+                     ("isolated", tu.get_isolated_overlay)):
+        for n in (8, 9):
+            extra[f"W_{name}_{n}"] = np.asarray(fn(n), dtype=np.float32)
+            meta_topos.append(f"W_{name}_{n}")
+    for n in (9, 16):
+        extra[f"W_2d_torus_{n}"] = np.asarray(tu.get_2d_torus_overlay(n), dtype=np.float32)
+        meta_topos.append(f"W_2d_torus_{n}")
+    for n in (7, 8):
+        extra[f"W_balanced_tree_{n}"] = np.asarray(tu.get_balanced_tree_overlay(n, 2), dtype=np.float32)
+        meta_topos.append(f"W_balanced_tree_{n}")
+    m = stm.SymmetricTopologyManager(10, 4)
+    m.generate_topology()
+    extra["W_symmetric_10_4"] = np.asarray(m.topology, dtype=np.float32)
+    meta_topos.append("W_symmetric_10_4")
+    for n, p, s in ((8, 0.5, 3), (12, 0.3, 4)):
+        random.seed(s)
+        extra[f"W_random_{n}_seed{s}"] = np.asarray(tu.get_random_overlay(n, p), dtype=np.float32)
+        meta_topos.append(f"W_random_{n}_seed{s}")
+    blob = np.frombuffer(json.dumps({"name": "topologies", "matrices": meta_topos,
+                                     "ref": "symmetric_topology_manager.py:22-78; topo_utils.py:6-94",
+                                     "random_seed_note": "python `random.seed(s)` before get_random_overlay"}
+                                    ).encode(), dtype=np.uint8)
+    np.savez_compressed(os.path.join(HERE, "topologies.npz"), meta=blob, **extra)
+    WRITTEN.append(("topologies", os.path.getsize(os.path.join(HERE, "topologies.npz"))))
+
+    # a9: _pfedavg_mixing_ rows + mix() (return value incl. edge-0 overwrite) + _pfedavg_aggregation_
+    mixing = extract_method("simulation/mpi/hierarchical_fl/HierFedAvgCloudAggregator.py",
+                            "HierFedAVGCloudAggregator", "_pfedavg_mixing_")
+    pagg = extract_method("simulation/mpi/hierarchical_fl/HierFedAvgCloudAggregator.py",
+                          "HierFedAVGCloudAggregator", "_pfedavg_aggregation_")
+
+    def consensus_speed(W, r, args):  # wandb-free stand-in for utils.cal_mixing_consensus_speed
+        A = np.array(W) - 1 / np.shape(W)[0]
+        return 1 - np.linalg.norm(A, ord=2) ** 2
+
+    mix = extract_method("simulation/mpi/hierarchical_fl/HierFedAvgCloudAggregator.py",
+                         "HierFedAVGCloudAggregator", "mix",
+                         {"cal_mixing_consensus_speed": consensus_speed})
+    for topo in ("ring", "complete"):
+        E = 8
+        W = extra[f"W_{topo}_{E}"]
+        edges = gen_clients(700, E, [("w", (1531,), torch.float32), ("b", (10,), torch.float32)])
+        ne = gen_counts(700, E)
+        stub = types.SimpleNamespace()
+        rows = [mixing(stub, [(ne[j], dc(edges[j])) for j in range(E)], W[i]) for i in range(E)]
+        write(f"g8_pfedavg_mixing_{topo}_E{E}", edges, rows,
+              dict(kind="mix_rows", n=ne, topology=f"W_{topo}_{E}",
+                   ref="HierFedAvgCloudAggregator.py:174-195"), {"W": W})
+    # mix() with group_comm_round = 2 (the returned list has edge 0 replaced by the average)
+    E, R = 8, 2
+    W = extra["W_ring_8"]
+    edge_models = gen_clients(710, E * R, [("w", (515,), torch.float32), ("b", (10,), torch.float32)])
+    ne = [gen_counts(710 + e, R) for e in range(E)]
+    cloud = types.SimpleNamespace(
+        worker_num=E, args=Args(enable_wandb=False),
+        sample_num_dict={e: list(ne[e]) for e in range(E)},
+        model_dict={e: [(r, dc(edge_models[e * R + r])) for r in range(R)] for e in range(E)},
+    )
+    cloud._pfedavg_mixing_ = functools.partial(mixing, cloud)
+    cloud._pfedavg_aggregation_ = functools.partial(pagg, cloud)
+    cloud.set_global_model_params = lambda p: None
+    cloud.test_on_cloud_for_all_clients = lambda r: None
+    topo_mgr = types.SimpleNamespace(topology=W, get_in_neighbor_weights=lambda i: W[i])
+    outs = mix(cloud, topo_mgr)
+    write("g8_cloud_mix_ring_E8_R2", edge_models, outs,
+          dict(kind="hier_mix", edges=E, group_comm_round=R, edge_counts=ne, topology="W_ring_8",
+               note="client index = e*R + r",
+               ref="HierFedAvgCloudAggregator.py:105-138,159-195"), {"W": W})
+    # mixing with Inf / NaN in a zero-weight neighbour (0*inf = nan propagates in the dense loop)
+    edges = gen_clients(720, 8, [("w", (64,), torch.float32)])
+    edges[4]["w"][3] = float("inf")
+    edges[5]["w"][7] = float("nan")
+    edges[6]["w"][9] = -0.0
+    W = extra["W_ring_8"]
+    rows = [mixing(types.SimpleNamespace(), [(1, dc(edges[j])) for j in range(8)], W[i]) for i in range(8)]
+    write("g9_mixing_nonfinite_ring_E8", edges, rows,
+          dict(kind="mix_rows", n=[1] * 8, topology="W_ring_8", ref="HierFedAvgCloudAggregator.py:174-195"),
+          {"W": W})
+
+    # a11: DSGD / PushSum update_local_parameters at the function level (distinct model objects)
+    dsgd = extract_method("simulation/sp/decentralized/client_dsgd.py", "ClientDSGD", "update_local_parameters")
+    pushsum = extract_method("simulation/sp/decentralized/client_pushsum.py", "ClientPushsum",
+                             "update_local_parameters")
+
+    class _M:
+        def __init__(self, tensors):
+            self.ps = [torch.nn.Parameter(t.clone(), requires_grad=False) for t in tensors]
+
+        def parameters(self):
+            return iter(self.ps)
+
+    n_nodes = 8
+    W = extra["W_ring_8"]
+    lay = [("w", (10, 97), torch.float32), ("b", (10,), torch.float32)]
+    xs = gen_clients(730, n_nodes, lay)
+    outs, outs_ps = [], []
+    omegas = [1.0 + 0.125 * i for i in range(n_nodes)]
+    omega_out = []
+    for i in range(n_nodes):
+        for fn, sink in ((dsgd, outs), (pushsum, outs_ps)):
+            me = types.SimpleNamespace(
+                id=i, topology=W[i], model_x=_M(list(xs[i].values())), model=_M(list(xs[i].values())),
+                neighbors_weight_dict=OrderedDict(), neighbors_topo_weight_dict=OrderedDict(),
+                neighbors_omega_dict=OrderedDict(), omega=omegas[i])
+            # receive order = ascending sender id (decentralized_fl_api.py:115-120)
+            for j in range(n_nodes):
+                if W[j][i] != 0 and j != i:
+                    me.neighbors_weight_dict[j] = _M(list(xs[j].values()))
+                    me.neighbors_topo_weight_dict[j] = W[j][i]
+                    me.neighbors_omega_dict[j] = omegas[j] * W[j][i]
+            fn(me)
+            sink.append(OrderedDict((k, p.data.clone()) for k, p in zip(xs[i].keys(), me.model.ps)))
+            if fn is pushsum:
+                omega_out.append(float(me.omega))
+    write("g8_dsgd_ring_N8", xs, outs,
+          dict(kind="dsgd", topology="W_ring_8", ref="sp/decentralized/client_dsgd.py:92-122"), {"W": W})
+    write("g8_pushsum_ring_N8", xs, outs_ps,
+          dict(kind="pushsum", topology="W_ring_8", omegas_in=omegas, omegas_out=omega_out,
+               ref="sp/decentralized/client_pushsum.py:111-156"), {"W": W})
+
+
+def layouts(ao):
+    """Model layouts used by the configs: names/shapes/dtypes only (no weights)."""
+    for name, sub in [("fedml.model", "/model"), ("fedml.model.cv", "/model/cv")]:
+        _stub_pkg(name, REF + sub)
+    import contextlib
+    import io
+    with contextlib.redirect_stdout(io.StringIO()):
+        rn = importlib.import_module("fedml.model.cv.resnet_gn").resnet18()
+    sd = rn.state_dict()
+    out = {"resnet18_gn": [[k, list(v.shape), dtype_name(v)] for k, v in sd.items()]}
+    # ViT-B/16 (synthetic: the reference has no ViT) in torchvision's state_dict order
+    D, L, M, C = 768, 12, 3072, 1000
+    vit = [["class_token", [1, 1, D], "bfloat16"], ["conv_proj.weight", [D, 3, 16, 16], "bfloat16"],
+           ["conv_proj.bias", [D], "bfloat16"], ["encoder.pos_embedding", [1, 197, D], "bfloat16"]]
+    for i in range(L):
+        p = f"encoder.layers.encoder_layer_{i}."
+        vit += [[p + "ln_1.weight", [D], "bfloat16"], [p + "ln_1.bias", [D], "bfloat16"],
+                [p + "self_attention.in_proj_weight", [3 * D, D], "bfloat16"],
+                [p + "self_attention.in_proj_bias", [3 * D], "bfloat16"],
+                [p + "self_attention.out_proj.weight", [D, D], "bfloat16"],
+                [p + "self_attention.out_proj.bias", [D], "bfloat16"],
+                [p + "ln_2.weight", [D], "bfloat16"], [p + "ln_2.bias", [D], "bfloat16"],
+                [p + "mlp.0.weight", [M, D], "bfloat16"], [p + "mlp.0.bias", [M], "bfloat16"],
+                [p + "mlp.3.weight", [D, M], "bfloat16"], [p + "mlp.3.bias", [D], "bfloat16"]]
+    vit += [["encoder.ln.weight", [D], "bfloat16"], ["encoder.ln.bias", [D], "bfloat16"],
+            ["heads.head.weight", [C, D], "bfloat16"], ["heads.head.bias", [C], "bfloat16"]]
+    out["vit_b16_bf16"] = vit
+    out["lr_mnist"] = [["linear.weight", [10, 784], "float32"], ["linear.bias", [10], "float32"]]
+    with open(os.path.join(HERE, "layouts.json"), "w") as f:
+        json.dump(out, f, indent=0)
+    for k, v in out.items():
+        numel = sum(int(np.prod(s)) for _, s, _ in v)
+        print(f"layout {k}: {len(v)} tensors, {numel} elements")
+
+
+def main():
+    ao = load_agg_operator()
+    stm, tu = load_topology()
+    cases_agg_operator(ao)
+    cases_call_sites()
+    cases_topology_and_mixing(stm, tu)
+    layouts(ao)
+    total = sum(s for _, s in WRITTEN)
+    for name, s in WRITTEN:
+        print(f"{name:45s} {s:9d} B")
+    print(f"total {total / 1e6:.2f} MB in {len(WRITTEN)} files")
+
+
+if __name__ == "__main__":
+    main()
