@@ -72,9 +72,17 @@ __device__ __forceinline__ float bf16_round(float x) { return (float)(__bf16)x; 
 __device__ __forceinline__ unsigned bf16_bits(float x) {
   return (unsigned)__builtin_bit_cast(unsigned short, (__bf16)x);
 }
-__device__ __forceinline__ float f16_round(float x) { return (float)(_Float16)x; }
+// The f32 -> f16 rounding must see a MATERIALISED f32 value: otherwise the gfx950 backend folds
+// fptrunc(fmul(fpext(h), c)) into v_fma_mixlo_f16, which rounds the exact product to f16 ONCE,
+// while the reference (PyTorch CPU) rounds it to f32 first and then to f16 (double rounding).
+// The empty asm pins the f32 intermediate in a VGPR (no instruction is emitted).
+__device__ __forceinline__ float pin_f32(float x) {
+  asm("" : "+v"(x));
+  return x;
+}
+__device__ __forceinline__ float f16_round(float x) { return (float)(_Float16)pin_f32(x); }
 __device__ __forceinline__ unsigned f16_bits(float x) {
-  return (unsigned)__builtin_bit_cast(unsigned short, (_Float16)x);
+  return (unsigned)__builtin_bit_cast(unsigned short, (_Float16)pin_f32(x));
 }
 __device__ __forceinline__ float f16_from_bits(unsigned b) {
   return (float)__builtin_bit_cast(_Float16, (unsigned short)b);

@@ -1,0 +1,40 @@
+#!/usr/bin/env python
+"""Practical HBM ceilings on this MI355X (read-only stream, copy), for DESIGN.md's roofline table."""
+import ctypes, json, os, subprocess, sys
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(HERE, "libhbmprobe.so")
+if not os.path.exists(SO):
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-o", SO,
+                    os.path.join(HERE, "hbm_probe.hip")], check=True)
+L = ctypes.CDLL(SO)
+L.hbm_probe_read.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+L.hbm_probe_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_void_p]
+
+def timeit(fn, reps=10):
+    fn(); torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        fn()
+    b.record(); torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps * 1e-3
+
+GB = int(float(sys.argv[1]) * 2**30) if len(sys.argv) > 1 else 16 * 2**30
+src = torch.empty(GB // 4, dtype=torch.float32, device="cuda").normal_()
+s = torch.cuda.current_stream().cuda_stream
+res = {"bytes": GB}
+for blocks in (2048, 4096, 8192, 16384):
+    out = torch.empty(blocks * 256, dtype=torch.int32, device="cuda")
+    for u in (4, 8, 16):
+        t = timeit(lambda: L.hbm_probe_read(src.data_ptr(), GB, out.data_ptr(), blocks, u, s))
+        res[f"read_b{blocks}_u{u}_GBs"] = round(GB / t / 1e9, 1)
+half = GB // 2
+dst = torch.empty(half // 4, dtype=torch.float32, device="cuda")
+for blocks in (2048, 8192):
+    t = timeit(lambda: L.hbm_probe_copy(src.data_ptr(), dst.data_ptr(), half, blocks, s))
+    res[f"copy_b{blocks}_GBs"] = round(2 * half / t / 1e9, 1)
+res["read_best_GBs"] = max(v for k, v in res.items() if k.startswith("read_"))
+res["copy_best_GBs"] = max(v for k, v in res.items() if k.startswith("copy_"))
+print(json.dumps(res))
