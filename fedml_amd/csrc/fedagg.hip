@@ -279,16 +279,56 @@ __device__ __forceinline__ int find_seg(const Seg* __restrict__ segs, int nseg, 
 }
 
 // --------------------------------------------------------------------------------------------
-// The ordered weighted-sum kernel.  One workgroup = one tile of kBlock*V elements of one segment.
-template <int DT, int MODE, int U, bool NT>
-__global__ void __launch_bounds__(kBlock)
-k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
-       const void* const* __restrict__ ptrs, int k, double divisor) {
+// The ordered weighted-sum kernel.  One workgroup = one tile of kBlock*V*S elements of one segment:
+// lane l owns the S vectors at e0 + s*kBlock*V (each slot coalesced across the wave).  Clients are
+// consumed in groups of U; with PF (prefetch) the next group's U*S loads are issued before the
+// current group is consumed, so a wave keeps up to 2*U*S KiB in flight.
+template <int DT, int MODE, int U, int S, bool NT>
+struct WsumBody {
   using T = Tr<DT, MODE>;
   using A = typename T::A;
   using R = typename T::R;
+  static constexpr int V = T::V;
+  static constexpr int64_t SLOT_BYTES = (int64_t)kBlock * V * T::IN_BYTES;
+
+  __device__ static void load(u32x4 (&r)[U][S], const void* const* __restrict__ in, int i0, int k,
+                              int64_t boff) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = min(i0 + u, k - 1);  // clamped: every load unconditional
+      const char* p = (const char*)in[i] + boff;
+#pragma unroll
+      for (int s = 0; s < S; ++s) r[u][s] = ld16<NT>(p + s * SLOT_BYTES);
+    }
+  }
+  template <bool GUARD>
+  __device__ static void consume(A (&acc)[S][V], const u32x4 (&r)[U][S], const double* __restrict__ coef,
+                                 int i0, int k, typename T::D d) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (!GUARD || i0 + u < k) {  // wave-uniform
+        const typename T::C c = T::coef(coef[i0 + u]);
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+          R x[V];
+          T::unpack(r[u][s], x);
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[s][v] = accum<DT, MODE>(acc[s][v], term<DT, MODE>(x[v], c, d));
+        }
+      }
+    }
+  }
+};
+
+template <int DT, int MODE, int U, int S, bool NT, bool PF>
+__global__ void __launch_bounds__(kBlock)
+k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
+       const void* const* __restrict__ ptrs, int k, double divisor) {
+  using B = WsumBody<DT, MODE, U, S, NT>;
+  using T = typename B::T;
+  using A = typename B::A;
   constexpr int V = T::V;
-  constexpr int64_t TILE = (int64_t)kBlock * V;
+  constexpr int64_t TILE = (int64_t)kBlock * V * S;
 
   const int64_t tile = blockIdx.x;
   const Seg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
@@ -299,28 +339,38 @@ k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
   if (sg.aligned && base + TILE <= sg.numel) {
     const int64_t e0 = base + (int64_t)threadIdx.x * V;
     const int64_t boff = e0 * T::IN_BYTES;
-    A acc[V];
+    A acc[S][V];
 #pragma unroll
-    for (int v = 0; v < V; ++v) acc[v] = T::zero();
-    for (int i0 = 0; i0 < k; i0 += U) {
-      u32x4 r[U];
+    for (int s = 0; s < S; ++s)
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int i = min(i0 + u, k - 1);  // clamped: every load unconditional
-        r[u] = ld16<NT>((const char*)in[i] + boff);
+      for (int v = 0; v < V; ++v) acc[s][v] = T::zero();
+    if constexpr (PF) {
+      u32x4 ra[U][S], rb[U][S];
+      B::load(ra, in, 0, k, boff);
+      int i0 = 0;
+      // two groups per trip so the ping-pong buffers keep fixed registers
+      for (; i0 + 2 * U < k; i0 += 2 * U) {
+        B::load(rb, in, i0 + U, k, boff);
+        B::template consume<false>(acc, ra, coef, i0, k, d);
+        B::load(ra, in, i0 + 2 * U, k, boff);
+        B::template consume<false>(acc, rb, coef, i0 + U, k, d);
       }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (i0 + u < k) {  // wave-uniform
-          const typename T::C c = T::coef(coef[i0 + u]);
-          R x[V];
-          T::unpack(r[u], x);
-#pragma unroll
-          for (int v = 0; v < V; ++v) acc[v] = accum<DT, MODE>(acc[v], term<DT, MODE>(x[v], c, d));
-        }
+      if (i0 + U < k) {
+        B::load(rb, in, i0 + U, k, boff);
+        B::template consume<false>(acc, ra, coef, i0, k, d);
+        B::template consume<true>(acc, rb, coef, i0 + U, k, d);
+      } else {
+        B::template consume<true>(acc, ra, coef, i0, k, d);
+      }
+    } else {
+      for (int i0 = 0; i0 < k; i0 += U) {
+        u32x4 r[U][S];
+        B::load(r, in, i0, k, boff);
+        B::template consume<true>(acc, r, coef, i0, k, d);
       }
     }
-    T::stv((char*)sg.out + e0 * T::OUT_BYTES, acc);
+#pragma unroll
+    for (int s = 0; s < S; ++s) T::stv((char*)sg.out + (e0 + (int64_t)s * kBlock * V) * T::OUT_BYTES, acc[s]);
   } else {
     // tail tile or unaligned segment: coalesced scalar loads, same arithmetic
     const int64_t end = min(base + TILE, sg.numel);
@@ -482,23 +532,45 @@ int release(fa_ctx::Slot* s, hipStream_t st) {
   return FA_OK;
 }
 
-template <int DT, int MODE, int U, bool NT>
+// Kernel variants (performance only; every variant computes the identical result).
+struct Variant { int U, S; bool NT, PF; };
+constexpr Variant kVariants[] = {
+    {8, 1, true, false},   // 0: default
+    {4, 1, true, false},   // 1
+    {16, 1, true, false},  // 2
+    {8, 1, false, false},  // 3: default-policy loads
+    {4, 2, true, false},   // 4
+    {8, 2, true, false},   // 5
+    {4, 4, true, false},   // 6
+    {8, 1, true, true},    // 7: double-buffered prefetch
+    {4, 2, true, true},    // 8
+};
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+template <int DT, int MODE, int U, int S, bool NT, bool PF>
 void launch_wsum(int64_t tiles, hipStream_t st, const Seg* segs, int nseg, const double* coef,
                  const void* const* ptrs, int k, double divisor) {
-  hipLaunchKernelGGL((k_wsum<DT, MODE, U, NT>), dim3((unsigned)tiles), dim3(kBlock), 0, st, segs, nseg,
-                     coef, ptrs, k, divisor);
+  hipLaunchKernelGGL((k_wsum<DT, MODE, U, S, NT, PF>), dim3((unsigned)tiles), dim3(kBlock), 0, st, segs,
+                     nseg, coef, ptrs, k, divisor);
 }
 
-// variant: 0 = default (U=8, nt); 1 = U=4 nt; 2 = U=16 nt; 3 = U=8 plain loads
 template <int DT, int MODE>
 void dispatch_variant(int variant, int64_t tiles, hipStream_t st, const Seg* segs, int nseg,
                       const double* coef, const void* const* ptrs, int k, double divisor) {
+#define FA_V(ID, U, S, NT, PF) \
+  case ID: launch_wsum<DT, MODE, U, S, NT, PF>(tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
   switch (variant) {
-    case 1: launch_wsum<DT, MODE, 4, true>(tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
-    case 2: launch_wsum<DT, MODE, 16, true>(tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
-    case 3: launch_wsum<DT, MODE, 8, false>(tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
-    default: launch_wsum<DT, MODE, 8, true>(tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
+    FA_V(1, 4, 1, true, false)
+    FA_V(2, 16, 1, true, false)
+    FA_V(3, 8, 1, false, false)
+    FA_V(4, 4, 2, true, false)
+    FA_V(5, 8, 2, true, false)
+    FA_V(6, 4, 4, true, false)
+    FA_V(7, 8, 1, true, true)
+    FA_V(8, 4, 2, true, true)
+    default: launch_wsum<DT, MODE, 8, 1, true, false>(tiles, st, segs, nseg, coef, ptrs, k, divisor);
   }
+#undef FA_V
 }
 
 template <int DT>
@@ -592,7 +664,8 @@ int fa_ctx_destroy(fa_ctx* c) {
 
 // Tuning knob (not part of the arithmetic contract): kernel variant for the weighted sum.
 int fa_ctx_set_variant(fa_ctx* c, int variant) {
-  if (!c || variant < 0 || variant > 3) return fail(FA_ERR_INVALID, "fa_ctx_set_variant: bad args");
+  if (!c || variant < 0 || variant >= kNumVariants)
+    return fail(FA_ERR_INVALID, "fa_ctx_set_variant: variant must be in [0, %d)", kNumVariants);
   c->variant = variant;
   return FA_OK;
 }
@@ -610,7 +683,7 @@ int fa_weighted_sum_multi(fa_ctx* ctx, int dtype, int mode, int32_t num_segments
   if (mode != FA_MODE_SUM && !coef) return fail(FA_ERR_INVALID, "coef is NULL for a weighted mode");
 
   // count non-empty segments and tiles
-  const int64_t tile_elems = (int64_t)kBlock * V;
+  const int64_t tile_elems = (int64_t)kBlock * V * kVariants[ctx->variant].S;
   int nseg = 0;
   int64_t tiles = 0;
   for (int s = 0; s < num_segments; ++s) {

@@ -124,8 +124,8 @@ int fa_mix(fa_ctx *ctx, int dtype, int64_t n, int32_t rows, const int32_t *row_p
            void *const *d_out, const double *post_scale, void *const *d_out2, void *hip_stream);
 
 /* Performance tuning only (results are identical for every variant): selects the weighted-sum
- * kernel's client unroll / cache policy.  0 = default (U=8, non-temporal loads), 1 = U=4,
- * 2 = U=16, 3 = U=8 with default-policy loads. */
+ * kernel's shape -- U clients per load group, S 16-byte vectors per lane, load cache policy,
+ * double-buffered group prefetch.  0 = default; valid range [0, 9). */
 int fa_ctx_set_variant(fa_ctx *ctx, int variant);
 
 /* Static name of a status code. */

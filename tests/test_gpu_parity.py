@@ -175,3 +175,27 @@ def test_mix_vs_oracle_ring(eng, dtype):
         go, go2 = eng.mix([x.cuda() for x in xs], *csr, post_scale=scale)
         for a, b in zip(go + go2, eo + eo2):
             assert bits_equal(a.cpu(), b)
+
+
+@pytest.mark.parametrize("variant", list(range(9)))
+@pytest.mark.parametrize("dtype,mode", [(torch.float32, MUL_W), (torch.bfloat16, MUL_W), (torch.float16, MUL_N_DIV_N),
+                                        (torch.float64, MUL_W), (torch.int64, SUM), (torch.int64, MUL_N_DIV_N)],
+                         ids=str)
+def test_all_kernel_variants_identical(variant, dtype, mode):
+    """Every tuning variant computes the same bits (incl. ragged tails and K not a multiple of U)."""
+    from oracle import orc
+    from fedml_amd.engine import AggEngine
+    eng = AggEngine(0)
+    try:
+        eng.set_variant(variant)
+        g = torch.Generator().manual_seed(variant)
+        for K, P in ((1, 70_001), (13, 262_144 + 77), (37, 33_333)):
+            xs = [_rand((P,), dtype, g) for _ in range(K)]
+            counts = [int(v) for v in torch.randint(50, 601, (K,), generator=g)]
+            N = sum(counts)
+            coef = [c / N for c in counts] if mode == MUL_W else counts
+            exp = orc.weighted_sum(xs, mode, coef, float(N))
+            got = eng.weighted_sum([x.cuda() for x in xs], mode, coef, float(N)).cpu()
+            assert bits_equal(got, exp), (variant, dtype, mode, K, P)
+    finally:
+        eng.close()
