@@ -1,20 +1,25 @@
 #!/usr/bin/env python
 """Benchmark: device-resident FedAvg aggregation GB/s (BASELINE.json metric) on MI355X.
 
-Default workload (the metric's configuration): K = 128 synthetic client updates x P = 125,000,000
-fp32 parameters, all resident in HBM; one step = one FedAvg aggregation (ordered weighted sum over
-the 128 clients, reference formula of python/fedml/ml/aggregator/agg_operator.py:35-44).
+Default workload (the metric's configuration, BASELINE.json configs / SURVEY.md §8(d)):
+K = 128 synthetic client updates x P = 125,000,000 fp32 parameters, all resident in HBM; one
+step = one FedAvg aggregation (ordered weighted sum over the 128 clients, the reference formula
+of python/fedml/ml/aggregator/agg_operator.py:35-44), value = algorithmic bytes / step time with
+B = K*P*4 (reads) + P*4 (write) = 64.5 GB.
 
-  python bench.py [--gpus N --steps K --warmup W] [--config metric|resnet18|vit_bf16]
+  python bench.py [--gpus N --steps K --warmup W] [--config metric|resnet18|vit_bf16|hier|gossip]
 
-N > 1 (launched by torch.distributed.run, one rank per GPU, RCCL): the SAME total problem is
-split by client groups -- rank r holds clients [r*K/N, (r+1)*K/N) -- each rank forms its ordered
-local partial with the global weights (the group step), then the partials are SUM-reduced over
-xGMI to rank 0 (the global step; the reference's pattern in simulation/nccl/base_framework/
-params.py:98-105 + common.py:196-210).  The reduce is pipelined in chunks behind the local
-kernels.  That is strong scaling of a fixed workload.
+N > 1 (torch.distributed.run, one rank per GPU, RCCL over xGMI): the SAME total problem split by
+client group -- rank r holds clients [r*K/N, (r+1)*K/N) -- each rank forms its ordered local
+partial with the global weights (group step, HIP kernel), and the partials are SUM-reduced to
+rank 0 (global step, the reference's pattern in simulation/nccl/base_framework/params.py:98-105),
+pipelined in chunks behind the local kernels (fedml_amd/distributed/group_reduce.py).  Total work
+is fixed, so scaling is "strong".
 
-Output: ONE JSON line on rank 0 (see DESIGN.md for the roofline / traffic definitions).
+Other configs (one JSON line each, same fields): resnet18 = cfg2 (ResNet-18-GN state_dict, 122
+tensors incl. 20 int64, K=32); vit_bf16 = cfg3 (ViT-B/16 layout, bf16, K=128); hier = cfg4 (8
+groups x 64 clients of ResNet-18 size, group FedAvg then the cloud step); gossip = cfg5 (256 ranks,
+ring W, one DSGD step over ResNet-18-size models).
 """
 from __future__ import annotations
 
@@ -32,6 +37,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 METRIC = "device-resident aggregate GB/s, K=128 × 125M fp32 params; 1/2/4/8 GPU"
+RESNET18_P = 11_699_132
 
 
 def parse():
@@ -39,12 +45,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", default="metric", choices=["metric", "resnet18", "vit_bf16"])
-    p.add_argument("--clients", type=int, default=128)
-    p.add_argument("--params", type=int, default=125_000_000)
+    p.add_argument("--config", default="metric", choices=["metric", "resnet18", "vit_bf16", "hier", "gossip"])
+    p.add_argument("--clients", type=int, default=None)
+    p.add_argument("--params", type=int, default=None)
     p.add_argument("--variant", type=int, default=0, help="kernel variant (fa_ctx_set_variant)")
     p.add_argument("--chunks", type=int, default=8, help="pipeline chunks of the cross-GPU reduce")
-    p.add_argument("--collective", default="reduce", choices=["reduce", "reduce_scatter", "all_reduce"])
+    p.add_argument("--collective", default="reduce", choices=["reduce", "reduce_scatter", "all_reduce", "ordered"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     p.add_argument("--check-samples", type=int, default=65536)
@@ -56,9 +62,8 @@ def init_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    if world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
@@ -82,7 +87,7 @@ def max_over_ranks(x, world):
     return float(t.item())
 
 
-# ----------------------------------------------------------------------------- workloads
+# ----------------------------------------------------------------------------- synthetic inputs
 def client_counts(K):
     rng = np.random.RandomState(7)  # n_i ~ U{50..600}, seed 7
     return [int(v) for v in rng.randint(50, 601, size=K)]
@@ -116,6 +121,198 @@ def make_layout_clients(idx, layout):
     return dicts
 
 
+def split(K, rank, world):
+    per = K // world
+    return list(range(rank * per, (rank + 1) * per if rank < world - 1 else K))
+
+
+class Timed:
+    """HIP-event timing of the dominant kernel launches, on the stream they are issued on."""
+
+    def __init__(self):
+        self.pairs = []
+        self.on = False
+
+    def __enter__(self):
+        if self.on:
+            self.a = torch.cuda.Event(enable_timing=True)
+            self.a.record(torch.cuda.current_stream())
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            b = torch.cuda.Event(enable_timing=True)
+            b.record(torch.cuda.current_stream())
+            self.pairs.append((self.a, b))
+
+    def avg_ms(self):
+        d = [a.elapsed_time(b) for a, b in self.pairs]
+        return float(np.mean(d)) if d else None
+
+
+# ----------------------------------------------------------------------------- workloads
+def wl_metric(args, eng, rank, world, timer):
+    """Flat FedAvg K x P fp32 (the metric).  Returns a workload dict."""
+    from fedml_amd.engine import MUL_W
+    K = args.clients or 128
+    P = args.params or 125_000_000
+    counts = client_counts(K)
+    N = sum(counts)
+    mine = split(K, rank, world)
+    w = [counts[i] / N for i in mine]
+    xs = make_flat_clients(mine, P)
+    out = torch.empty(P, device="cuda")
+    if world > 1:
+        from fedml_amd.distributed.group_reduce import GroupReducer
+
+        def timed_sum(xs_, mode, coef, div, o):
+            with timer:
+                return eng.weighted_sum(xs_, mode, coef, div, out=o)
+        red = GroupReducer(collective=args.collective, chunks=args.chunks, local_sum=timed_sum)
+
+        def step():
+            red.fedavg(xs, w, out=out)
+        launches = args.chunks
+    else:
+        def step():
+            with timer:
+                eng.weighted_sum(xs, MUL_W, w, out=out)
+        launches = 1
+
+    def parity():
+        if world > 1 or args.check_samples <= 0:
+            return None
+        from oracle import orc
+        gi = torch.Generator(device="cuda").manual_seed(99)
+        idx = torch.randint(0, P, (args.check_samples,), generator=gi, device="cuda")
+        exp = orc.weighted_sum([x.index_select(0, idx).cpu() for x in xs], MUL_W, w)
+        ok = torch.equal(out.index_select(0, idx).cpu().view(torch.int32), exp.view(torch.int32))
+        return f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on {args.check_samples} sampled elements"
+
+    return dict(name=f"fedavg_flat_K{K}_P{P}_fp32", dtype="fp32", step=step, parity=parity,
+                bytes_total=K * P * 4 + P * 4, launch_bytes=(len(mine) * P * 4 + P * 4) / launches,
+                clients=K, params=P, cpu_K=K)
+
+
+def wl_layout(args, eng, rank, world, timer):
+    """cfg2 / cfg3: a real state_dict layout, all keys of one dtype in one launch."""
+    from fedml_amd.ml.aggregator.state_dict_agg import MUL_W, aggregate
+    resnet = args.config == "resnet18"
+    layout = load_layout("resnet18_gn" if resnet else "vit_b16_bf16")
+    K = args.clients or (32 if resnet else 128)
+    counts = client_counts(K)
+    N = sum(counts)
+    mine = split(K, rank, world)
+    w = [counts[i] / N for i in mine]
+    dicts = make_layout_clients(mine, layout)
+    P = sum(int(np.prod(s)) for _, s, _ in layout)
+    size = {"int64": 8, "bfloat16": 2, "float32": 4}
+    in_b = sum(int(np.prod(s)) * size[dt] for _, s, dt in layout)
+    out_b = sum(int(np.prod(s)) * (2 if dt == "bfloat16" else 4) for _, s, dt in layout)
+    res = {}
+
+    def step():
+        with timer:
+            res["out"] = aggregate(dicts, MUL_W, w)
+        if world > 1:
+            import torch.distributed as dist
+            for t in res["out"].values():
+                dist.reduce(t, dst=0)
+
+    def parity():
+        if world > 1:
+            return None
+        from oracle import orc
+        bad = 0
+        for name, shape, dt in layout:
+            n = int(np.prod(shape))
+            idx = torch.arange(0, n, max(1, n // 512), device="cuda")
+            exp = orc.weighted_sum([d[name].reshape(-1).index_select(0, idx).cpu() for d in dicts], MUL_W, w)
+            got = res["out"][name].reshape(-1).index_select(0, idx).cpu()
+            ib = {torch.float32: torch.int32, torch.bfloat16: torch.int16}[got.dtype]
+            bad += int((got.view(ib) != exp.view(ib)).sum())
+        return f"{'bit-exact' if bad == 0 else f'{bad} MISMATCHES'} vs oracle on a strided sample of every key"
+
+    tag = "resnet18gn" if resnet else "vitb16_bf16"
+    return dict(name=f"fedavg_{tag}_K{K}_P{P}", dtype="fp32" if resnet else "bf16", step=step, parity=parity,
+                bytes_total=K * in_b + out_b, launch_bytes=None, clients=K, params=P, cpu_K=None)
+
+
+def wl_hier(args, eng, rank, world, timer):
+    """cfg4: G groups x M clients (ResNet-18 size, flat fp32): group FedAvg (weights n_i/N_g), cloud
+    term (G_g * N_g) / N, then the global sum over groups (rank order = group order)."""
+    from fedml_amd.engine import MUL_N_DIV_N, MUL_W, SUM
+    G, M = 8, (args.clients or 512) // 8
+    P = args.params or RESNET18_P
+    counts = client_counts(G * M)
+    N = sum(counts)
+    my_groups = split(G, rank, world)
+    xs = {g: make_flat_clients(range(g * M, (g + 1) * M), P) for g in my_groups}
+    gsum = {g: sum(counts[g * M:(g + 1) * M]) for g in range(G)}
+    terms = {g: torch.empty(P, device="cuda") for g in my_groups}
+    scratch = torch.empty(P, device="cuda")
+    out = torch.empty(P, device="cuda")
+    red = None
+    if world > 1:
+        from fedml_amd.distributed.group_reduce import GroupReducer
+
+        def timed_sum(xs_, mode, coef, div, o):
+            with timer:
+                return eng.weighted_sum(xs_, mode, coef, div, out=o)
+        red = GroupReducer(collective=args.collective if args.collective != "reduce" else "ordered",
+                           chunks=args.chunks, local_sum=timed_sum)
+
+    def step():
+        if red is not None:
+            (g,) = my_groups
+            red.hierarchical(xs[g], counts[g * M:(g + 1) * M], N, out=out)
+            return
+        for g in my_groups:
+            with timer:
+                eng.weighted_sum(xs[g], MUL_W, [c / gsum[g] for c in counts[g * M:(g + 1) * M]], out=scratch)
+            eng.weighted_sum([scratch], MUL_N_DIV_N, [gsum[g]], float(N), out=terms[g])
+        eng.weighted_sum([terms[g] for g in my_groups], SUM, out=out)
+
+    return dict(name=f"hier_fedavg_G{G}x{M}_P{P}_fp32", dtype="fp32", step=step, parity=lambda: None,
+                bytes_total=G * M * P * 4 + P * 4, launch_bytes=M * P * 4 + P * 4, clients=G * M, params=P,
+                cpu_K=None)
+
+
+def wl_gossip(args, eng, rank, world, timer):
+    """cfg5: n = 256 nodes on a ring (W = 1/3), one synchronous DSGD step, models of ResNet-18 size."""
+    from fedml_amd.core.distributed.topology.topology_manager import SymmetricTopologyManager, gossip_rows
+    n = args.clients or 256
+    P = args.params or RESNET18_P
+    m = SymmetricTopologyManager(n, 2)
+    m.generate_topology()
+    W = m.topology
+    if world > 1:
+        from fedml_amd.distributed.gossip import DistributedGossip
+
+        def timed_mix(xs_, rp, cs, vs, ps, outs, outs2):
+            with timer:
+                return eng.mix(xs_, rp, cs, vs, ps, outs, outs2)
+        dg = DistributedGossip(W, local_mix=timed_mix)
+        xs = make_flat_clients(dg.mine, P)
+
+        def step():
+            dg.step(xs)
+        rows = len(dg.mine)
+    else:
+        xs = make_flat_clients(range(n), P)
+        rp, cs, vs = gossip_rows(W)
+        outs = [torch.empty(P, device="cuda") for _ in range(n)]
+
+        def step():
+            with timer:
+                eng.mix(xs, rp, cs, vs, outs=outs)
+        rows = n
+    # survey §8(d): B = sum_i (deg_i + 1) * P * s + n * P * s  (ring: 4 n P s); compulsory = 2 n P s
+    return dict(name=f"gossip_ring_n{n}_P{P}_fp32", dtype="fp32", step=step, parity=lambda: None,
+                bytes_total=4 * n * P * 4, launch_bytes=2 * rows * P * 4, clients=n, params=P, cpu_K=None,
+                roofline_note="achieved uses compulsory bytes 2*rows*P*4 (each model read once, written once)")
+
+
 # ----------------------------------------------------------------------------- CPU baseline
 def cpu_baseline(K, budget_s):
     """The reference's CPU cost: oracle/torch_port.py (op-for-op restatement of agg_operator.py's
@@ -138,16 +335,15 @@ def cpu_baseline(K, budget_s):
         runs += 1
     gbs = (K * P * 4 + P * 4) / best / 1e9
     return {"value": round(gbs, 2), "unit": "GB/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"K={K} x P={P} fp32 host-resident, best of {runs} runs of oracle/torch_port.agg('FedAvg')"}
+            "sample": f"K={K} x P={P} fp32 host-resident, best of {runs} runs of oracle/torch_port.agg('FedAvg') "
+                      f"(op-for-op restatement of agg_operator.py:35-44)"}
 
 
 def pmc_traffic(workload):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py), if any."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
-        with open(path) as f:
-            d = json.load(f)
-        return d.get(workload, {}).get("hbm_bytes_per_launch")
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            return json.load(f).get(workload, {}).get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None
 
@@ -156,148 +352,44 @@ def pmc_traffic(workload):
 def main():
     args = parse()
     rank, world, local = init_dist(args)
-    from fedml_amd.engine import MUL_W, get_engine
+    from fedml_amd.engine import get_engine
     eng = get_engine(local)
     if args.variant:
         eng.set_variant(args.variant)
+    timer = Timed()
+    wl = {"metric": wl_metric, "resnet18": wl_layout, "vit_bf16": wl_layout, "hier": wl_hier,
+          "gossip": wl_gossip}[args.config](args, eng, rank, world, timer)
 
-    K, P = args.clients, args.params
-    counts = client_counts(K)
-    N_tot = sum(counts)
-    w_all = [c / N_tot for c in counts]
-    per = K // world
-    mine = list(range(rank * per, (rank + 1) * per if rank < world - 1 else K))
-    w_mine = [w_all[i] for i in mine]
-
-    if args.config == "metric":
-        workload = f"fedavg_flat_K{K}_P{P}_fp32"
-        xs = make_flat_clients(mine, P)
-        out = torch.empty(P, device="cuda")
-        bytes_total = K * P * 4 + P * 4
-        dtype = "fp32"
-        segs = None
-    else:
-        layout = load_layout("resnet18_gn" if args.config == "resnet18" else "vit_b16_bf16")
-        if args.config == "resnet18":
-            K = args.clients if args.clients != 128 else 32
-        counts = client_counts(K)
-        N_tot = sum(counts)
-        w_all = [c / N_tot for c in counts]
-        per = K // world
-        mine = list(range(rank * per, (rank + 1) * per if rank < world - 1 else K))
-        w_mine = [w_all[i] for i in mine]
-        dicts = make_layout_clients(mine, layout)
-        P = sum(int(np.prod(s)) for _, s, _ in layout)
-        in_b = sum(int(np.prod(s)) * (8 if dt == "int64" else (2 if dt == "bfloat16" else 4)) for _, s, dt in layout)
-        out_b = sum(int(np.prod(s)) * (2 if dt == "bfloat16" else 4) for _, s, dt in layout)
-        bytes_total = K * in_b + out_b
-        workload = f"fedavg_{args.config}_K{K}_P{P}"
-        dtype = "bf16" if args.config == "vit_bf16" else "fp32"
-        from fedml_amd.ml.aggregator.state_dict_agg import aggregate
-        segs = (dicts, aggregate)
-
-    stream = torch.cuda.current_stream()
-    kernel_ms = []
-
-    def local_step(record):
-        if segs is None:
-            if world == 1:
-                ev0 = torch.cuda.Event(enable_timing=True) if record else None
-                if record:
-                    ev0.record(stream)
-                eng.weighted_sum(xs, MUL_W, w_mine, out=out)
-                if record:
-                    ev1 = torch.cuda.Event(enable_timing=True)
-                    ev1.record(stream)
-                    kernel_ms.append((ev0, ev1))
-                return out
-            # pipelined group -> global: local partial per chunk, then the collective on that chunk
-            import torch.distributed as dist
-            C = max(1, args.chunks)
-            bounds = [(P * c // C, P * (c + 1) // C) for c in range(C)]
-            works = []
-            for (a, b) in bounds:
-                ev0 = torch.cuda.Event(enable_timing=True) if record else None
-                if record:
-                    ev0.record(stream)
-                eng.weighted_sum([x[a:b] for x in xs], MUL_W, w_mine, out=out[a:b])
-                if record:
-                    ev1 = torch.cuda.Event(enable_timing=True)
-                    ev1.record(stream)
-                    kernel_ms.append((ev0, ev1))
-                if args.collective == "reduce":
-                    works.append(dist.reduce(out[a:b], dst=0, op=dist.ReduceOp.SUM, async_op=True))
-                elif args.collective == "all_reduce":
-                    works.append(dist.all_reduce(out[a:b], op=dist.ReduceOp.SUM, async_op=True))
-                else:
-                    n = b - a
-                    sh = n // world
-                    works.append(dist.reduce_scatter_tensor(shard[a // world:a // world + sh], out[a:a + sh * world],
-                                                            op=dist.ReduceOp.SUM, async_op=True))
-            for wk in works:
-                wk.wait()
-            return out
-        dicts_, agg = segs
-        ev0 = torch.cuda.Event(enable_timing=True) if record else None
-        if record:
-            ev0.record(stream)
-        r = agg(dicts_, MUL_W, w_mine)
-        if record:
-            ev1 = torch.cuda.Event(enable_timing=True)
-            ev1.record(stream)
-            kernel_ms.append((ev0, ev1))
-        if world > 1:
-            import torch.distributed as dist
-            for t in r.values():
-                dist.reduce(t, dst=0)
-        return r
-
-    shard = torch.empty(P // world + 1, device="cuda") if world > 1 else None
     for _ in range(args.warmup):
-        local_step(False)
+        wl["step"]()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
+    timer.on = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        local_step(True)
+        wl["step"]()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    timer.on = False
     ms_per_step = elapsed / args.steps * 1e3
-    value = bytes_total * args.steps / elapsed / 1e9
+    value = wl["bytes_total"] * args.steps / elapsed / 1e9
 
-    # dominant kernel: average launch duration (HIP events on the launch stream)
-    durs = [a.elapsed_time(b) for a, b in kernel_ms]
-    launches_per_step = len(durs) // max(1, args.steps)
-    kernel_avg_ms = float(np.mean(durs)) if durs else None
-    if segs is None:
-        per_launch_bytes = (len(mine) * P * 4 + P * 4) / max(1, launches_per_step)
-    else:
-        per_launch_bytes = bytes_total * len(mine) / K
-    achieved = per_launch_bytes / (kernel_avg_ms * 1e-3) / 1e9 if kernel_avg_ms else None
-
-    # parity spot-check at full size: sampled elements vs the C oracle (exact for N = 1)
-    parity = None
-    if segs is None and world == 1 and args.check_samples > 0:
-        from oracle import orc
-        torch.cuda.synchronize()
-        gi = torch.Generator(device="cuda").manual_seed(99)
-        idx = torch.randint(0, P, (args.check_samples,), generator=gi, device="cuda")
-        sample = [x.index_select(0, idx).cpu() for x in xs]
-        exp = orc.weighted_sum(sample, MUL_W, w_mine)
-        got = out.index_select(0, idx).cpu()
-        ok = torch.equal(got.view(torch.int32), exp.view(torch.int32))
-        parity = f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on {args.check_samples} sampled elements"
-
+    kernel_ms = timer.avg_ms()
+    launch_bytes = wl["launch_bytes"]
+    if launch_bytes is None and kernel_ms:  # layout configs: the whole aggregate() call per step
+        launch_bytes = wl["bytes_total"] / world
+    achieved = launch_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms else None
+    parity = wl["parity"]()
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(K if segs is None else K, args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and wl.get("cpu_K"):
+        cpu = cpu_baseline(wl["cpu_K"], args.cpu_seconds)
 
     if rank == 0:
         line = {
-            "metric": METRIC if args.config == "metric" else f"device-resident aggregate GB/s, {workload}",
+            "metric": METRIC if args.config == "metric" else f"device-resident aggregate GB/s, {wl['name']}",
             "value": round(value, 2),
             "unit": "GB/s",
             "n_gpus": world,
@@ -307,20 +399,23 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": dtype,
-            "data": "synthetic (N(0,1) client updates, seeds 1000+i; n_i ~ U{50..600}, seed 7), resident in HBM",
-            "config": {"workload": workload, "clients": K, "params_per_client": P,
-                       "parallelism": f"client-groups x{world}" + (f" + {args.collective} over RCCL, {args.chunks} chunks" if world > 1 else ""),
+            "dtype": wl["dtype"],
+            "data": "synthetic N(0,1) client updates (seeds 1000+i), n_i ~ U{50..600} (seed 7); resident in HBM",
+            "config": {"workload": wl["name"], "clients": wl["clients"], "params_per_client": wl["params"],
+                       "parallelism": f"client-groups x{world}" +
+                                      (f", {args.collective} over RCCL in {args.chunks} chunks" if world > 1 else ""),
                        "kernel_variant": args.variant},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": pmc_traffic(workload),
-                         "kernel_avg_ms": round(kernel_avg_ms, 4) if kernel_avg_ms else None,
-                         "algorithmic_bytes_per_launch": int(per_launch_bytes)},
+                         "traffic": pmc_traffic(wl["name"]),
+                         "kernel_avg_ms": round(kernel_ms, 4) if kernel_ms else None,
+                         "algorithmic_bytes_per_launch": int(launch_bytes) if launch_bytes else None},
             "cpu_baseline": cpu,
             "parity": parity,
         }
+        if wl.get("roofline_note"):
+            line["roofline"]["note"] = wl["roofline_note"]
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -1,0 +1,144 @@
+"""Multi-GPU group -> global aggregation: one client group per GPU, RCCL over xGMI for the exchange.
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL).  Rank r holds client group r.
+
+* Group step (local, the HIP kernel): the ordered weighted partial of the rank's clients,
+  ``S_r = sum_{i in r} x_i * w_i`` (flat FedAvg with GLOBAL weights w_i = n_i / N), or, for the
+  hierarchical formula, the group FedAvg ``G_r`` (weights n_i / N_r) pre-scaled to the cloud
+  formula's term ``(G_r * N_r) / N`` (HierFedAvgCloudAggregator.py:146-156) -- the exact per-element
+  ops the reference applies before its cloud-side accumulation.
+* Global step (the exchange), ``collective``:
+    "reduce"          SUM-reduce to ``dst`` -- the reference's NCCL simulator pattern
+                      (simulation/nccl/base_framework/params.py:98-105, common.py:196-210); the
+                      cross-rank summation order is RCCL's, so the result matches the sequential
+                      reference normwise (~1e-7), not bit-for-bit;
+    "all_reduce"      the same, result on every rank;
+    "reduce_scatter"  the same, result sharded (rank r owns elements [r*P/G, (r+1)*P/G));
+    "ordered"         gather the G partials to ``dst`` and sum them there IN RANK ORDER with the
+                      engine's SUM mode: bit-identical to the reference's two-level reduces --
+                      fedavg_seq (worker partials, then an ordered sum; FedAVGAggregator.py:201-236)
+                      and the hierarchical cloud step (ordered sum of the pre-scaled group terms).
+* Pipelining: P is cut into ``chunks``; chunk c's collective is issued (async, stream-ordered
+  behind chunk c's kernel) while chunk c+1's partial is computed, so the xGMI transfer hides
+  behind HBM streaming.
+
+The local reduction is injectable (``local_sum``) so the exchange logic can be tested with the
+gloo backend on CPU; in the product it is the HIP engine and there is no CPU path.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from ..engine import MUL_N_DIV_N, MUL_W, SUM
+
+LocalSum = Callable[..., torch.Tensor]  # (xs, mode, coef, divisor, out) -> out
+
+
+def _engine_local_sum(xs, mode, coef, divisor, out):
+    from ..engine import get_engine
+    return get_engine(out.device.index).weighted_sum(xs, mode, coef, divisor, out=out)
+
+
+def chunk_bounds(n: int, chunks: int) -> List[tuple]:
+    chunks = max(1, min(chunks, n)) if n > 0 else 1
+    return [(n * c // chunks, n * (c + 1) // chunks) for c in range(chunks)]
+
+
+class GroupReducer:
+    """Group -> global reduction of flat parameter vectors over a process group."""
+
+    def __init__(self, group=None, collective: str = "reduce", dst: int = 0, chunks: int = 8,
+                 local_sum: Optional[LocalSum] = None):
+        if collective not in ("reduce", "all_reduce", "reduce_scatter", "ordered"):
+            raise ValueError(f"unknown collective {collective!r}")
+        self.group = group
+        self.collective = collective
+        self.dst = dst
+        self.chunks = chunks
+        self.local_sum = local_sum or _engine_local_sum
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+
+    # -------------------------------------------------------------- public entry points
+    def fedavg(self, xs: Sequence[torch.Tensor], weights: Sequence[float], out: Optional[torch.Tensor] = None):
+        """Global FedAvg of all ranks' clients; ``weights`` = this rank's GLOBAL w_i = n_i / N."""
+        return self._run(xs, MUL_W, list(weights), 1.0, out)
+
+    def hierarchical(self, xs: Sequence[torch.Tensor], counts: Sequence[int], total: int,
+                     out: Optional[torch.Tensor] = None):
+        """Hierarchical round: group FedAvg (weights n_i / N_r, sp/fedavg_api.py:144-159), then the
+        cloud term (G_r * N_r) / N (MPI cloud formula), then the global sum over groups."""
+        n_r = sum(counts)
+        return self._run(xs, MUL_W, [c / n_r for c in counts], 1.0, out, post=(n_r, float(total)))
+
+    def sum(self, xs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None):
+        """Plain global sum (FedAvg_seq / FedDyn branches)."""
+        return self._run(xs, SUM, None, 1.0, out)
+
+    # -------------------------------------------------------------- implementation
+    def _run(self, xs, mode, coef, divisor, out, post=None):
+        n = xs[0].numel()
+        dev = xs[0].device
+        if out is None:
+            out = torch.empty(n, dtype=torch.float32 if xs[0].dtype == torch.int64 and mode != SUM else xs[0].dtype,
+                              device=dev)
+        flat = [x.reshape(-1) for x in xs]
+        bounds = chunk_bounds(n, self.chunks)
+        works = []
+        gathered = []
+        shard = None
+        if self.collective == "reduce_scatter":
+            if n % self.world:
+                raise ValueError("reduce_scatter needs P divisible by the world size")
+            S = n // self.world
+            shard = torch.empty(S, dtype=out.dtype, device=dev)
+            # chunk-major staging: chunk [a, b) of every rank's shard is laid out contiguously
+            # (rank-major inside the chunk), which is what reduce_scatter_tensor consumes
+            for a, b in chunk_bounds(S, self.chunks):
+                L = b - a
+                base = self.world * a
+                for r in range(self.world):
+                    lo = r * S + a
+                    self._local(flat, mode, coef, divisor, out[base + r * L: base + (r + 1) * L], lo, lo + L, post)
+                if self.world > 1:
+                    works.append(dist.reduce_scatter_tensor(shard[a:b], out[base: base + self.world * L],
+                                                            op=dist.ReduceOp.SUM, group=self.group,
+                                                            async_op=True))
+                else:
+                    shard[a:b].copy_(out[base: base + L])
+            for w in works:
+                w.wait()
+            return shard
+        for a, b in bounds:
+            part = out[a:b]
+            self._local(flat, mode, coef, divisor, part, a, b, post)
+            if self.world == 1:
+                continue
+            if self.collective == "reduce":
+                works.append(dist.reduce(part, dst=self.dst, op=dist.ReduceOp.SUM, group=self.group,
+                                         async_op=True))
+            elif self.collective == "all_reduce":
+                works.append(dist.all_reduce(part, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+            else:  # ordered
+                bufs = [torch.empty_like(part) for _ in range(self.world)] if self.rank == self.dst else None
+                works.append(dist.gather(part, bufs, dst=self.dst, group=self.group, async_op=True))
+                gathered.append((a, b, bufs))
+        for w in works:
+            w.wait()
+        if self.collective == "ordered" and self.rank == self.dst and self.world > 1:
+            for a, b, bufs in gathered:
+                self.local_sum(bufs, SUM, None, 1.0, out[a:b])
+        return out
+
+    def _local(self, flat, mode, coef, divisor, part, a, b, post):
+        if post is None:
+            self.local_sum([x[a:b] for x in flat], mode, coef, divisor, part)
+            return
+        # hierarchical: group FedAvg G into scratch, then the cloud term (G * N_r) / N into part
+        n_r, total = post
+        g = torch.empty_like(part)
+        self.local_sum([x[a:b] for x in flat], mode, coef, divisor, g)
+        self.local_sum([g], MUL_N_DIV_N, [n_r], total, part)

@@ -102,3 +102,36 @@ def fedavg_xn_div_n(dicts, counts, engine=None):
 def plain_sum(dicts, engine=None):
     """avg[k] = sum_i x_i[k] (agg_operator.py:55-63 FedAvg_seq, :68-77 FedDyn)."""
     return aggregate(dicts, SUM, engine=engine)
+
+
+def mix(dicts: Sequence[Dict[str, torch.Tensor]], row_ptr, cols, vals, post_scale=None,
+        engine: Optional[AggEngine] = None):
+    """Per-key CSR mixing of model dicts (fa_mix): returns (rows, rows2) lists of OrderedDicts.
+
+    rows[r][k] = ordered sum over the row's entries j of dicts[cols[j]][k] * vals[j]
+    (HierFedAvgCloudAggregator.py:174-195 with a dense row; client_dsgd.py:104-122 with a gossip
+    row); rows2[r][k] = rows[r][k] * post_scale[r] when post_scale is given (client_pushsum.py:150-156).
+    """
+    keys = list(dicts[0].keys())
+    eng = engine or _engine_for([dicts[0][k] for k in keys])
+    on_cpu = not any(dicts[0][k].is_cuda for k in keys)
+    nrows = len(row_ptr) - 1
+    rows = [OrderedDict() for _ in range(nrows)]
+    rows2 = [OrderedDict() for _ in range(nrows)] if post_scale is not None else None
+    for k in keys:
+        col = [_to_engine(d[k], eng) for d in dicts]
+        dt = col[0].dtype
+        if dt in _SMALL_INT or dt in (torch.int64, torch.bool):
+            # int tensor * float32 weight -> float32 (PyTorch promotion): exact int -> fp32 cast first
+            col = [t.to(torch.float32) for t in col]
+        elif dt not in (torch.float32, torch.bfloat16, torch.float16):
+            raise TypeError(f"mix: key {k!r} has dtype {dt} (float32/bfloat16/float16/integer only)")
+        shape = col[0].shape
+        outs, outs2 = eng.mix([t.reshape(-1) for t in col], row_ptr, cols, vals, post_scale)
+        for r in range(nrows):
+            o = outs[r].reshape(shape)
+            rows[r][k] = o.cpu() if on_cpu else o
+            if rows2 is not None:
+                o2 = outs2[r].reshape(shape)
+                rows2[r][k] = o2.cpu() if on_cpu else o2
+    return rows, rows2

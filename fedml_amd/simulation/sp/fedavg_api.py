@@ -1,0 +1,47 @@
+"""Single-process FedAvg round driver (reference: python/fedml/simulation/sp/fedavg/fedavg_api.py).
+
+``FedAvgAPI._aggregate(w_locals)`` is the reference's inline FedAvg loop (fedavg_api.py:144-159,
+bit-identical to FedMLAggOperator.agg's FedAvg branch), run on the MI355X engine.  ``train`` is a
+compact version of the reference's round loop (:66-125): every round, each sampled client gets
+the global weights, trains with its ClientTrainer, and the updates are averaged on the GPU.
+"""
+from __future__ import annotations
+
+import copy
+import logging
+from collections import OrderedDict
+from typing import Callable, List, Optional, Sequence, Tuple
+
+from ...ml.aggregator.state_dict_agg import fedavg
+
+
+class FedAvgAPI:
+    def __init__(self, args, device, model, client_trainers: Sequence = (), train_data: Sequence = (),
+                 sample_nums: Sequence[int] = (), sampler: Optional[Callable[[int], List[int]]] = None):
+        self.args = args
+        self.device = device
+        self.model = model
+        self.client_trainers = list(client_trainers)
+        self.train_data = list(train_data)
+        self.sample_nums = list(sample_nums)
+        self.sampler = sampler
+
+    def _aggregate(self, w_locals: List[Tuple[int, "OrderedDict"]]):
+        """Reference fedavg_api.py:144-159: avg[k] = sum_i x_i[k] * (n_i / N), client order."""
+        return fedavg([params for _, params in w_locals], [n for n, _ in w_locals])
+
+    def train(self, rounds: Optional[int] = None):
+        rounds = rounds if rounds is not None else int(getattr(self.args, "comm_round", 1))
+        w_global = self.model.state_dict()
+        for r in range(rounds):
+            idx = self.sampler(r) if self.sampler else list(range(len(self.client_trainers)))
+            w_locals = []
+            for i in idx:
+                trainer = self.client_trainers[i]
+                trainer.set_model_params(copy.deepcopy(w_global))
+                trainer.train(self.train_data[i], self.device, self.args)
+                w_locals.append((self.sample_nums[i], trainer.get_model_params()))
+            w_global = self._aggregate(w_locals)
+            self.model.load_state_dict(w_global)
+            logging.info("round %d aggregated %d clients", r, len(w_locals))
+        return w_global

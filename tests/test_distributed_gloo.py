@@ -1,0 +1,162 @@
+"""N > 1 exchange logic on CPU: world_size-2 gloo runs of the group -> global reducer and the
+distributed gossip step, with the C oracle injected as the local reduction (the product path uses
+the HIP kernels; these tests check the orchestration: chunking, collectives, ordering, halos)."""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+import traceback
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_sum(xs, mode, coef, divisor, out):
+    from oracle import orc
+    out.copy_(orc.weighted_sum([x.contiguous() for x in xs], mode, coef, divisor).reshape(out.shape))
+    return out
+
+
+def _oracle_mix(xs, row_ptr, cols, vals, post_scale, outs, outs2):
+    from oracle import orc
+    o, o2 = orc.mix(xs, row_ptr, cols, vals, post_scale)
+    for a, b in zip(outs, o):
+        a.copy_(b)
+    if outs2 is not None:
+        for a, b in zip(outs2, o2):
+            a.copy_(b)
+
+
+def _clients(K, P, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    xs = [torch.randn(P, generator=g) for _ in range(K)]
+    counts = [int(v) for v in torch.randint(50, 601, (K,), generator=g)]
+    return xs, counts
+
+
+def _bits(a, b):
+    return torch.equal(a.view(torch.int32), b.view(torch.int32))
+
+
+def _worker(rank, world, port, fn, errq):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        fn(rank, world)
+    except Exception:  # noqa: BLE001
+        errq.put(f"rank {rank}: {traceback.format_exc()}")
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(fn, world=2):
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, errq)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, "\n".join(errs)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+# ------------------------------------------------------------------------------ group reduce
+def _case_group_reduce(rank, world):
+    from oracle import orc
+    from fedml_amd.distributed.group_reduce import GroupReducer
+    K, P = 6, 10_001
+    xs, counts = _clients(K, P)
+    N = sum(counts)
+    per = K // world
+    mine = list(range(rank * per, (rank + 1) * per))
+    w = [counts[i] / N for i in mine]
+    # expected: ordered partial per rank, then rank-ordered sum (two ranks: any order is exact)
+    parts = [orc.weighted_sum([xs[i] for i in range(r * per, (r + 1) * per)], 0,
+                              [counts[i] / N for i in range(r * per, (r + 1) * per)]) for r in range(world)]
+    exp = orc.weighted_sum(parts, 2)
+    for coll in ("reduce", "all_reduce", "ordered"):
+        for chunks in (1, 3, 8):
+            red = GroupReducer(collective=coll, chunks=chunks, local_sum=_oracle_sum)
+            got = red.fedavg([xs[i] for i in mine], w)
+            if rank == 0 or coll == "all_reduce":
+                assert _bits(got, exp), (coll, chunks)
+    # hierarchical: group FedAvg, cloud term (G*N_r)/N, ordered sum over groups
+    red = GroupReducer(collective="ordered", chunks=4, local_sum=_oracle_sum)
+    got = red.hierarchical([xs[i] for i in mine], [counts[i] for i in mine], N)
+    terms = []
+    for r in range(world):
+        idx = list(range(r * per, (r + 1) * per))
+        nr = sum(counts[i] for i in idx)
+        G = orc.weighted_sum([xs[i] for i in idx], 0, [counts[i] / nr for i in idx])
+        terms.append(orc.weighted_sum([G], 1, [nr], float(N)))
+    if rank == 0:
+        assert _bits(got, orc.weighted_sum(terms, 2))
+
+
+def test_group_reduce_gloo_world2():
+    _spawn(_case_group_reduce)
+
+
+def _case_reduce_scatter(rank, world):
+    from oracle import orc
+    from fedml_amd.distributed.group_reduce import GroupReducer
+    K, P = 4, 4000
+    xs, counts = _clients(K, P, seed=5)
+    N = sum(counts)
+    mine = [rank * 2, rank * 2 + 1]
+    parts = [orc.weighted_sum([xs[2 * r], xs[2 * r + 1]], 0, [counts[2 * r] / N, counts[2 * r + 1] / N])
+             for r in range(world)]
+    exp = orc.weighted_sum(parts, 2)
+    red = GroupReducer(collective="reduce_scatter", chunks=3, local_sum=_oracle_sum)
+    shard = red.fedavg([xs[i] for i in mine], [counts[i] / N for i in mine])
+    S = P // world
+    assert _bits(shard, exp[rank * S:(rank + 1) * S])
+
+
+def test_reduce_scatter_gloo_world2():
+    _spawn(_case_reduce_scatter)
+
+
+# ------------------------------------------------------------------------------ gossip
+def _case_gossip(rank, world):
+    from oracle import orc
+    from fedml_amd.core.distributed.topology.topology_manager import SymmetricTopologyManager, gossip_rows
+    from fedml_amd.distributed.gossip import DistributedGossip
+    n, P = 8, 3001
+    m = SymmetricTopologyManager(n, 4)
+    m.generate_topology()
+    W = m.topology
+    xs, _ = _clients(n, P, seed=9)
+    exp_rows, exp2 = orc.mix(xs, *gossip_rows(W), post_scale=[1.0 / (1 + i) for i in range(n)])
+    dg = DistributedGossip(W, local_mix=_oracle_mix)
+    mine = dg.mine
+    assert mine == list(range(rank * 4, rank * 4 + 4))
+    outs, outs2 = dg.step([xs[i] for i in mine], post_scale=[1.0 / (1 + i) for i in mine])
+    for k, i in enumerate(mine):
+        assert _bits(outs[k], exp_rows[i]), i
+        assert _bits(outs2[k], exp2[i]), i
+    assert dg.halo_in and dg.boundary
+
+
+def test_gossip_gloo_world2():
+    _spawn(_case_gossip)

@@ -1,0 +1,201 @@
+"""The round drivers (callers of the engine) reproduce the reference functions they mirror,
+bit-for-bit, on the golden fixtures generated from those very functions."""
+from __future__ import annotations
+
+import os
+import types
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+import torch
+
+from golden_io import GOLDEN_DIR, client_dicts, expected_dicts, load_case
+from refcases import assert_dict_bits
+
+pytestmark = pytest.mark.gpu
+
+
+def case(name):
+    return load_case(os.path.join(GOLDEN_DIR, name + ".npz"))
+
+
+def on_gpu(d):
+    return OrderedDict((k, v.cuda()) for k, v in d.items())
+
+
+def cpu(d):
+    return OrderedDict((k, v.cpu()) for k, v in d.items())
+
+
+@pytest.mark.parametrize("where", ["cpu", "cuda"])
+def test_sp_fedavg_aggregate(where):
+    from fedml_amd.simulation.sp.fedavg_api import FedAvgAPI
+    meta, arr = case("g1_sp_aggregate_K9")
+    cl = client_dicts(meta, arr)
+    if where == "cuda":
+        cl = [on_gpu(c) for c in cl]
+    api = FedAvgAPI(types.SimpleNamespace(), "cuda:0", None)
+    got = api._aggregate(list(zip(meta["n"], cl)))
+    assert_dict_bits(cpu(got), expected_dicts(meta, arr)[0], "sp")
+
+
+@pytest.mark.parametrize("name", ["g4_mpi_xn_div_N_K3", "g4_mpi_xn_div_N_K32", "g4_mpi_xn_div_N_lr_K2",
+                                  "g4_mpi_xn_div_N_bf16_K4", "g4_mpi_xn_div_N_bigcounts_K3",
+                                  "g4_mpi_xn_div_N_int64_K5"])
+def test_mpi_fedavg_aggregator(name):
+    from fedml_amd.simulation.mpi.fedavg_aggregator import FedAVGAggregator
+    meta, arr = case(name)
+    cl = client_dicts(meta, arr)
+    agg = FedAVGAggregator(worker_num=len(cl))
+    for i in reversed(range(len(cl))):  # arrival order must not matter
+        assert not agg.check_whether_all_receive()
+        agg.add_local_trained_result(i, cl[i], meta["n"][i])
+    assert agg.check_whether_all_receive()
+    got = agg.aggregate()
+    assert_dict_bits(cpu(got), expected_dicts(meta, arr)[0], name)
+
+
+def test_fedavg_seq_two_level():
+    from fedml_amd.simulation.mpi import fedavg_seq as fs
+    meta, arr = case("g6_fedavg_seq_two_level_K10")
+    cl = [on_gpu(c) for c in client_dicts(meta, arr)]
+    n = meta["n"]
+    w = fs.get_average_weight({i: n[i] for i in range(len(n))}, list(range(len(n))))
+    # batched worker partials
+    partials = [fs.worker_partial([cl[i] for i in wk], [w[i] for i in wk]) for wk in meta["schedule"]]
+    got = fs.server_aggregate(partials)
+    exp = expected_dicts(meta, arr)[0]
+    assert_dict_bits(cpu(got), exp, "fedavg_seq batched")
+    # incremental add_client_model, clients arriving one by one
+    partials = []
+    for wk in meta["schedule"]:
+        acc = {}
+        for i in wk:
+            fs.add_client_model(acc, cl[i], w[i])
+        partials.append(acc)
+    assert_dict_bits(cpu(fs.server_aggregate(partials)), exp, "fedavg_seq incremental")
+
+
+def test_add_client_model_int_buffers():
+    """int64 buffers are promoted by the first p*w and keep the reference's arithmetic after."""
+    from fedml_amd.simulation.mpi import fedavg_seq as fs
+    from oracle import torch_port
+    g = torch.Generator().manual_seed(3)
+    cl = [OrderedDict(w=torch.randn(1000, generator=g), steps=torch.randint(0, 99, (), generator=g))
+          for _ in range(4)]
+    ws = [0.1, 0.2, 0.3, 0.4]
+    exp, acc = {}, {}
+    for c, w in zip(cl, ws):
+        torch_port.fedavg_seq_worker(exp, c, w)
+        fs.add_client_model(acc, on_gpu(c), w)
+    assert_dict_bits(cpu(acc), OrderedDict(exp), "int buffers")
+
+
+def test_hierarchical_sp():
+    from fedml_amd.simulation.sp.hierarchical import hierarchical_round
+    meta, arr = case("g7_hier_sp_K12_G3")
+    cl = [on_gpu(c) for c in client_dicts(meta, arr)]
+    n = meta["n"]
+    groups = {g: [(n[i], cl[i]) for i in members] for g, members in enumerate(meta["groups"])}
+    assert_dict_bits(cpu(hierarchical_round(groups)), expected_dicts(meta, arr)[0], "hier sp")
+
+
+def _cloud(meta, cl):
+    from fedml_amd.simulation.mpi.hier_cloud_aggregator import HierFedAVGCloudAggregator
+    E, R = meta["edges"], meta["group_comm_round"]
+    agg = HierFedAVGCloudAggregator(worker_num=E)
+    for e in range(E):
+        agg.add_local_trained_result(e, [(r, on_gpu(cl[e * R + r])) for r in range(R)], meta["edge_counts"][e])
+    assert agg.check_whether_all_receive()
+    return agg
+
+
+def test_hier_cloud_aggregate_with_reference_double_pass():
+    meta, arr = case("g7_hier_cloud_aggregate_E3_R2")
+    agg = _cloud(meta, client_dicts(meta, arr))
+    assert_dict_bits(cpu(agg.aggregate()), expected_dicts(meta, arr)[0], "cloud aggregate")
+
+
+def test_hier_cloud_mix():
+    meta, arr = case("g8_cloud_mix_ring_E8_R2")
+    agg = _cloud(meta, client_dicts(meta, arr))
+    topo = types.SimpleNamespace(topology=arr["W"])
+    got = agg.mix(topo)
+    exp = expected_dicts(meta, arr)
+    assert len(got) == len(exp)
+    for j, (g, e) in enumerate(zip(got, exp)):
+        assert_dict_bits(cpu(g), e, f"mix[{j}]")
+
+
+@pytest.mark.parametrize("name", ["g8_pfedavg_mixing_ring_E8", "g8_pfedavg_mixing_complete_E8",
+                                  "g9_mixing_nonfinite_ring_E8"])
+def test_pfedavg_mixing_rows(name):
+    from fedml_amd.simulation.mpi.hier_cloud_aggregator import HierFedAVGCloudAggregator
+    meta, arr = case(name)
+    cl = [on_gpu(c) for c in client_dicts(meta, arr)]
+    W = arr["W"]
+    exp = expected_dicts(meta, arr)
+    for i in range(W.shape[0]):
+        got = HierFedAVGCloudAggregator._pfedavg_mixing_([(meta["n"][j], cl[j]) for j in range(len(cl))], W[i])
+        assert_dict_bits(cpu(got), exp[i], f"{name} row {i}")
+
+
+def test_dsgd_and_pushsum_steps():
+    from fedml_amd.simulation.sp.decentralized import dsgd_step, pushsum_step
+    meta, arr = case("g8_dsgd_ring_N8")
+    cl = [on_gpu(c) for c in client_dicts(meta, arr)]
+    for g, e in zip(dsgd_step(cl, arr["W"]), expected_dicts(meta, arr)):
+        assert_dict_bits(cpu(g), e, "dsgd")
+    meta, arr = case("g8_pushsum_ring_N8")
+    cl = [on_gpu(c) for c in client_dicts(meta, arr)]
+    _, z, om = pushsum_step(cl, arr["W"], meta["omegas_in"])
+    assert om == meta["omegas_out"]
+    for g, e in zip(z, expected_dicts(meta, arr)):
+        assert_dict_bits(cpu(g), e, "pushsum")
+
+
+def test_cross_silo_round_with_user_server_aggregator():
+    """A user-defined ServerAggregator subclass drives a full cross-silo aggregation round."""
+    from fedml_amd.core.alg_frame.server_aggregator import ServerAggregator
+    from fedml_amd.cross_silo.server.fedml_aggregator import FedMLAggregator
+
+    class MyServerAggregator(ServerAggregator):
+        def get_model_params(self):
+            return self.model.state_dict()
+
+        def set_model_params(self, p):
+            self.model.load_state_dict(p)
+
+        def test(self, test_data, device, args):
+            return None
+
+    meta, arr = case("g1_fedavg_lr_K2")
+    cl = client_dicts(meta, arr)
+    model = torch.nn.Linear(784, 10)
+    args = types.SimpleNamespace(federated_optimizer="FedAvg")
+    srv = FedMLAggregator(client_num=2, device="cuda:0", args=args, server_aggregator=MyServerAggregator(model, args))
+    srv.add_local_trained_result(1, cl[1], meta["n"][1])
+    assert not srv.check_whether_all_receive()
+    srv.add_local_trained_result(0, cl[0], meta["n"][0])
+    assert srv.check_whether_all_receive()
+    avg, _, idx = srv.aggregate()
+    exp = expected_dicts(meta, arr)[0]
+    assert_dict_bits(cpu(avg), exp, "cross-silo")
+    assert idx == [0, 1]
+    assert torch.equal(model.weight.detach().cpu(), exp["linear.weight"])
+
+
+def test_default_server_aggregator_round():
+    from fedml_amd.ml.aggregator.default_aggregator import create_server_aggregator
+    model = torch.nn.Sequential(torch.nn.Linear(8, 4))
+    args = types.SimpleNamespace(federated_optimizer="FedAvg", dataset="synthetic")
+    agg = create_server_aggregator(model, args)
+    g = torch.Generator().manual_seed(0)
+    ups = [(10 * (i + 1), OrderedDict((k, torch.randn(v.shape, generator=g)) for k, v in model.state_dict().items()))
+           for i in range(3)]
+    avg = agg.aggregate(agg.on_before_aggregation(ups)[0])
+    agg.set_model_params(agg.on_after_aggregation(avg))
+    data = [(torch.randn(16, 8, generator=g), torch.randint(0, 4, (16,), generator=g))]
+    acc, loss, _, _ = agg.test(data, "cuda:0", args)
+    assert 0.0 <= acc <= 1.0 and loss > 0

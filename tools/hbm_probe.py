@@ -30,6 +30,23 @@ for blocks in (2048, 4096, 8192, 16384):
     for u in (4, 8, 16):
         t = timeit(lambda: L.hbm_probe_read(src.data_ptr(), GB, out.data_ptr(), blocks, u, s))
         res[f"read_b{blocks}_u{u}_GBs"] = round(GB / t / 1e9, 1)
+L.hbm_probe_multi.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+for k in (8, 32, 128):
+    per = (GB // k) // 4096 * 4096
+    views = [src[i * per // 4:(i + 1) * per // 4] for i in range(k)]
+    ptrs = torch.tensor([v.data_ptr() for v in views], dtype=torch.int64, device="cuda")
+    out = torch.empty(per // 16, dtype=torch.int32, device="cuda")
+    for u in (8, 16):
+        t = timeit(lambda: L.hbm_probe_multi(ptrs.data_ptr(), k, per, out.data_ptr(), u, s))
+        res[f"multi_k{k}_u{u}_GBs"] = round(k * per / t / 1e9, 1)
+# 128 SEPARATE allocations (how bench.py lays out the clients)
+k, per = 128, (GB // 2 // 128) // 4096 * 4096
+sep = [torch.empty(per // 4, dtype=torch.float32, device="cuda").normal_() for _ in range(k)]
+ptrs = torch.tensor([v.data_ptr() for v in sep], dtype=torch.int64, device="cuda")
+out = torch.empty(per // 16, dtype=torch.int32, device="cuda")
+t = timeit(lambda: L.hbm_probe_multi(ptrs.data_ptr(), k, per, out.data_ptr(), 8, s))
+res["multi_sep_k128_u8_GBs"] = round(k * per / t / 1e9, 1)
+del sep
 half = GB // 2
 dst = torch.empty(half // 4, dtype=torch.float32, device="cuda")
 for blocks in (2048, 8192):
