@@ -263,7 +263,7 @@ def wl_hier(args, eng, rank, world, timer):
                            chunks=args.chunks, local_sum=timed_sum)
 
     def step():
-        if red is not None:
+        if red is not None and len(my_groups) == 1:
             (g,) = my_groups
             red.hierarchical(xs[g], counts[g * M:(g + 1) * M], N, out=out)
             return
@@ -271,7 +271,10 @@ def wl_hier(args, eng, rank, world, timer):
             with timer:
                 eng.weighted_sum(xs[g], MUL_W, [c / gsum[g] for c in counts[g * M:(g + 1) * M]], out=scratch)
             eng.weighted_sum([scratch], MUL_N_DIV_N, [gsum[g]], float(N), out=terms[g])
-        eng.weighted_sum([terms[g] for g in my_groups], SUM, out=out)
+        if red is not None:  # several groups per rank: local ordered sum of the terms, then RCCL
+            red.sum([terms[g] for g in my_groups], out=out)
+        else:
+            eng.weighted_sum([terms[g] for g in my_groups], SUM, out=out)
 
     return dict(name=f"hier_fedavg_G{G}x{M}_P{P}_fp32", dtype="fp32", step=step, parity=lambda: None,
                 bytes_total=G * M * P * 4 + P * 4, launch_bytes=M * P * 4 + P * 4, clients=G * M, params=P,
