@@ -385,8 +385,12 @@ k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
 
 // --------------------------------------------------------------------------------------------
 // Mixing / gossip kernel: one workgroup = one element tile, looping over every output row so that
-// an input shared by neighbouring rows is re-read from L2 / Infinity Cache, not HBM.
-template <int DT, int U, bool POST>
+// an input shared by neighbouring rows is re-read from L2 / Infinity Cache, not HBM.  Rows go in
+// groups of RG: the loads of all RG rows (up to MAXD entries each, clamped like k_wsum) are issued
+// before any is consumed, so a wave keeps RG*MAXD KiB in flight -- RG-1 of every RG rows' new
+// neighbour is an L2 hit for a ring, so without the grouping a wave would hold only ~1 HBM miss.
+// Rows with more than MAXD entries take ceil(deg / MAXD) passes (dense rows, e.g. 8x8 mixing).
+template <int DT, int RG, int MAXD, bool POST>
 __global__ void __launch_bounds__(kBlock)
 k_mix(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict__ cols,
       const double* __restrict__ vals, const void* const* __restrict__ in, int64_t n, int aligned) {
@@ -399,36 +403,57 @@ k_mix(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict__ co
   if (aligned && base + TILE <= n) {
     const int64_t e0 = base + (int64_t)threadIdx.x * V;
     const int64_t boff = e0 * T::IN_BYTES;
-    for (int r = 0; r < nrows; ++r) {
-      const MixRow row = rows[r];
-      float acc[V];
+    for (int r0 = 0; r0 < nrows; r0 += RG) {
+      int beg[RG], end[RG];
+      int maxd = 0;
 #pragma unroll
-      for (int v = 0; v < V; ++v) acc[v] = -0.0f;
-      for (int j0 = row.begin; j0 < row.end; j0 += U) {
-        u32x4 x4[U];
+      for (int g = 0; g < RG; ++g) {
+        const int r = min(r0 + g, nrows - 1);
+        beg[g] = rows[r].begin;
+        end[g] = rows[r].end;
+        maxd = max(maxd, end[g] - beg[g]);
+      }
+      float acc[RG][V];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int j = min(j0 + u, row.end - 1);
-          x4[u] = ld16<false>((const char*)in[cols[j]] + boff);
-        }
+      for (int g = 0; g < RG; ++g)
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (j0 + u < row.end) {
-            const float c = (float)vals[j0 + u];
-            float x[V];
-            T::unpack(x4[u], x);
+        for (int v = 0; v < V; ++v) acc[g][v] = -0.0f;
+      for (int p = 0; p < maxd; p += MAXD) {
+        u32x4 x4[RG][MAXD];
 #pragma unroll
-            for (int v = 0; v < V; ++v)
-              acc[v] = accum<DT, FA_MODE_MUL_W>(acc[v], term<DT, FA_MODE_MUL_W>(x[v], c, dz));
+        for (int g = 0; g < RG; ++g)
+#pragma unroll
+          for (int u = 0; u < MAXD; ++u) {
+            const int j = min(beg[g] + p + u, end[g] - 1);
+            x4[g][u] = ld16<false>((const char*)in[cols[j]] + boff);
+          }
+#pragma unroll
+        for (int g = 0; g < RG; ++g)
+#pragma unroll
+          for (int u = 0; u < MAXD; ++u) {
+            if (beg[g] + p + u < end[g]) {  // wave-uniform
+              const float c = (float)vals[beg[g] + p + u];
+              float x[V];
+              T::unpack(x4[g][u], x);
+#pragma unroll
+              for (int v = 0; v < V; ++v)
+                acc[g][v] = accum<DT, FA_MODE_MUL_W>(acc[g][v], term<DT, FA_MODE_MUL_W>(x[v], c, dz));
+            }
+          }
+      }
+#pragma unroll
+      for (int g = 0; g < RG; ++g) {
+        if (r0 + g < nrows) {
+          const MixRow& row = rows[r0 + g];
+          T::stv((char*)row.out + e0 * T::OUT_BYTES, acc[g]);
+          if constexpr (POST) {
+            const float s = (float)row.scale;
+            float z[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) z[v] = T::rnd(op_mul(acc[g][v], s));
+            T::stv((char*)row.out2 + e0 * T::OUT_BYTES, z);
           }
         }
-      }
-      T::stv((char*)row.out + e0 * T::OUT_BYTES, acc);
-      if constexpr (POST) {
-        const float s = (float)row.scale;
-#pragma unroll
-        for (int v = 0; v < V; ++v) acc[v] = T::rnd(op_mul(acc[v], s));
-        T::stv((char*)row.out2 + e0 * T::OUT_BYTES, acc);
       }
     }
   } else {
@@ -815,17 +840,25 @@ int fa_mix(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_p
   const void* const* dptr = (const void* const*)(d + row_bytes + col_bytes + val_bytes);
   const dim3 grid((unsigned)tiles), blk(kBlock);
   const int al = aligned ? 1 : 0;
-#define FA_MIX_LAUNCH(DT)                                                                        \
-  if (post_scale)                                                                                \
-    hipLaunchKernelGGL((k_mix<DT, 4, true>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, n, al); \
-  else                                                                                           \
-    hipLaunchKernelGGL((k_mix<DT, 4, false>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, n, al);
+  int maxdeg = 0;
+  for (int r = 0; r < rows; ++r) maxdeg = std::max(maxdeg, row_ptr[r + 1] - row_ptr[r]);
+  // shape by row degree: ring-like (<= 3 entries), up to 4, or dense rows in passes of 8
+#define FA_MIX_SHAPE(DT, RG, MAXD)                                                                     \
+  if (post_scale)                                                                                      \
+    hipLaunchKernelGGL((k_mix<DT, RG, MAXD, true>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, n, al); \
+  else                                                                                                 \
+    hipLaunchKernelGGL((k_mix<DT, RG, MAXD, false>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, n, al);
+#define FA_MIX_LAUNCH(DT)                        \
+  if (maxdeg <= 3) { FA_MIX_SHAPE(DT, 4, 3) }    \
+  else if (maxdeg <= 4) { FA_MIX_SHAPE(DT, 4, 4) } \
+  else { FA_MIX_SHAPE(DT, 2, 8) }
   switch (dtype) {
     case FA_DTYPE_F32: FA_MIX_LAUNCH(FA_DTYPE_F32); break;
     case FA_DTYPE_BF16: FA_MIX_LAUNCH(FA_DTYPE_BF16); break;
     case FA_DTYPE_F16: FA_MIX_LAUNCH(FA_DTYPE_F16); break;
   }
 #undef FA_MIX_LAUNCH
+#undef FA_MIX_SHAPE
   FA_HIP(hipGetLastError());
   return release(slot, st);
 }

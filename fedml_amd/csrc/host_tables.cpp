@@ -1,0 +1,124 @@
+// host_tables.cpp -- host-side helper of the aggregation engine's Python binding (CPU code only).
+//
+// A state_dict round hands the engine K client dicts x T keys = K*T tensors (ViT-B/16 at K=128:
+// 19,456).  Walking them in Python to validate and collect data pointers costs ~1 us per tensor,
+// i.e. longer than the GPU takes to aggregate them.  This helper does the walk in C++ (tens of ns
+// per tensor) and also carves the outputs out of one device allocation.  It never touches tensor
+// DATA: all arithmetic stays in the HIP kernels behind the C ABI (include/fedagg.h).
+#include <torch/extension.h>
+
+#include <string>
+#include <vector>
+
+namespace py = pybind11;
+
+namespace {
+
+int fa_dtype_code(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return 0;
+    case at::kBFloat16: return 1;
+    case at::kHalf: return 2;
+    case at::kDouble: return 3;
+    case at::kLong: return 4;
+    default: return -1;
+  }
+}
+
+}  // namespace
+
+// gather(dicts, keys) -> (ptrs int64[T*K] key-major, numel int64[T], codes int64[T], shapes, device)
+//  * KeyError if a client lacks a key (as the reference's `local_model_params[k]`);
+//  * TypeError if clients disagree on a key's dtype, RuntimeError on a shape mismatch;
+//  * every tensor must be contiguous and on the device of client 0's first tensor;
+//  * code -1 marks dtypes the C ABI does not take natively (the caller widens those).
+py::tuple gather(py::list dicts, py::list keys) {
+  const int64_t K = (int64_t)py::len(dicts);
+  const int64_t T = (int64_t)py::len(keys);
+  if (K == 0) throw py::index_error("list index out of range");
+  auto ptrs = torch::empty({T * K}, torch::kInt64);
+  auto numel = torch::empty({T}, torch::kInt64);
+  auto codes = torch::empty({T}, torch::kInt64);
+  int64_t* P = ptrs.data_ptr<int64_t>();
+  int64_t* Nn = numel.data_ptr<int64_t>();
+  int64_t* C = codes.data_ptr<int64_t>();
+  py::list shapes;
+  std::vector<py::dict> ds;
+  ds.reserve(K);
+  for (auto d : dicts) ds.push_back(py::reinterpret_borrow<py::dict>(d));
+  c10::optional<at::Device> dev;
+  int64_t t = 0;
+  for (auto kobj : keys) {
+    at::ScalarType st = at::kFloat;
+    std::vector<int64_t> shape;
+    for (int64_t i = 0; i < K; ++i) {
+      PyObject* item = PyDict_GetItemWithError(ds[i].ptr(), kobj.ptr());
+      if (!item) {
+        if (PyErr_Occurred()) throw py::error_already_set();
+        throw py::key_error(py::str(kobj).cast<std::string>());
+      }
+      if (!THPVariable_Check(item)) throw py::type_error("state_dict values must be tensors");
+      const at::Tensor& x = THPVariable_Unpack(item);
+      if (i == 0) {
+        st = x.scalar_type();
+        shape = x.sizes().vec();
+        if (!dev) dev = x.device();
+        Nn[t] = x.numel();
+        C[t] = fa_dtype_code(st);
+        shapes.append(py::cast(shape));
+      } else {
+        if (x.scalar_type() != st)
+          throw py::type_error("key " + py::str(kobj).cast<std::string>() + ": client " + std::to_string(i) +
+                               " has a different dtype than client 0");
+        if (x.sizes() != c10::IntArrayRef(shape))
+          throw std::runtime_error("key " + py::str(kobj).cast<std::string>() + ": client " +
+                                   std::to_string(i) + " shape differs from client 0");
+      }
+      if (x.device() != *dev)
+        throw std::invalid_argument("key " + py::str(kobj).cast<std::string>() + ": client " + std::to_string(i) +
+                                    " is on another device than client 0");
+      if (!x.is_contiguous())
+        throw std::invalid_argument("key " + py::str(kobj).cast<std::string>() + ": client " + std::to_string(i) +
+                                    " is not contiguous");
+      P[t * K + i] = (int64_t)x.data_ptr();
+    }
+    ++t;
+  }
+  std::string devs = dev ? dev->str() : std::string("cpu");
+  return py::make_tuple(ptrs, numel, codes, shapes, devs);
+}
+
+// alloc_outputs(shapes, dtypes, device) -> (arena, views, ptrs int64[T])
+// One device allocation; every output starts on a 256-byte boundary (vector path of the kernel).
+py::tuple alloc_outputs(py::list shapes, py::list dtypes, const std::string& device) {
+  const int64_t T = (int64_t)py::len(shapes);
+  std::vector<int64_t> off(T), nbytes(T);
+  std::vector<at::ScalarType> sts(T);
+  std::vector<std::vector<int64_t>> shp(T);
+  int64_t total = 0;
+  for (int64_t t = 0; t < T; ++t) {
+    shp[t] = shapes[t].cast<std::vector<int64_t>>();
+    sts[t] = torch::python::detail::py_object_to_dtype(dtypes[t]);
+    int64_t n = 1;
+    for (auto s : shp[t]) n *= s;
+    nbytes[t] = n * (int64_t)c10::elementSize(sts[t]);
+    off[t] = total;
+    total += (nbytes[t] + 255) / 256 * 256;
+  }
+  auto arena = torch::empty({std::max<int64_t>(total, 256)}, torch::TensorOptions().dtype(torch::kUInt8).device(device));
+  py::list views;
+  auto ptrs = torch::empty({T}, torch::kInt64);
+  int64_t* P = ptrs.data_ptr<int64_t>();
+  for (int64_t t = 0; t < T; ++t) {
+    at::Tensor v = arena.narrow(0, off[t], nbytes[t]).view(sts[t]).view(shp[t]);
+    P[t] = (int64_t)v.data_ptr();
+    views.append(py::cast(v));
+  }
+  return py::make_tuple(arena, views, ptrs);
+}
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "host-side table builder of the fedml_amd aggregation engine (no tensor data access)";
+  m.def("gather", &gather, "validate K client dicts x T keys, return the device pointer table");
+  m.def("alloc_outputs", &alloc_outputs, "carve T aligned outputs out of one device allocation");
+}

@@ -133,6 +133,26 @@ class AggEngine:
         N.check(rc, "fa_weighted_sum_multi")
         return results
 
+    def weighted_sum_table(self, dtype_code: int, mode: int, seg_numel: torch.Tensor, k: int,
+                           in_ptrs: torch.Tensor, out_ptrs: torch.Tensor, coef: Optional[Sequence[float]] = None,
+                           divisor: float = 1.0, stream=None) -> None:
+        """Raw multi-segment launch from prebuilt host tables (int64 CPU tensors):
+        seg_numel[T], in_ptrs[T*k] (key-major device pointers), out_ptrs[T].  Used by the
+        state_dict path, whose tables are built and validated by fedml_amd._host."""
+        T = seg_numel.numel()
+        assert in_ptrs.dtype == torch.int64 and in_ptrs.numel() == T * k and in_ptrs.is_contiguous()
+        assert out_ptrs.dtype == torch.int64 and out_ptrs.numel() == T and out_ptrs.is_contiguous()
+        assert seg_numel.dtype == torch.int64 and seg_numel.is_contiguous()
+        if mode != SUM and (coef is None or len(coef) != k):
+            raise ValueError("weighted_sum: need one coefficient per client")
+        c = N.f64_array(coef if coef is not None else [0.0] * k)
+        rc = self._lib.fa_weighted_sum_multi(
+            self._ctx, int(dtype_code), int(mode), T,
+            N.ctypes.cast(seg_numel.data_ptr(), N._P_i64), k,
+            N.ctypes.cast(in_ptrs.data_ptr(), N._P_vp), c, float(divisor),
+            N.ctypes.cast(out_ptrs.data_ptr(), N._P_vp), self._stream(stream))
+        N.check(rc, "fa_weighted_sum_multi")
+
     # ------------------------------------------------------------------ mixing / gossip
     def mix(self, xs: Sequence[torch.Tensor], row_ptr: Sequence[int], cols: Sequence[int],
             vals: Sequence[float], post_scale: Optional[Sequence[float]] = None,

@@ -20,7 +20,8 @@ from typing import Dict, List, Optional, Sequence
 
 import torch
 
-from ...engine import MUL_N_DIV_N, MUL_W, SUM, AggEngine, get_engine
+from ... import _host
+from ...engine import MUL_N_DIV_N, MUL_W, SUM, AggEngine, get_engine, out_dtype
 
 _NATIVE = (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64)
 _SMALL_INT = (torch.int32, torch.int16, torch.int8, torch.uint8)
@@ -39,12 +40,50 @@ def _to_engine(t: torch.Tensor, eng: AggEngine) -> torch.Tensor:
     return t if t.is_contiguous() else t.contiguous()
 
 
+_CODE_DTYPE = {0: torch.float32, 1: torch.bfloat16, 2: torch.float16, 3: torch.float64, 4: torch.int64}
+
+
 def aggregate(dicts: Sequence[Dict[str, torch.Tensor]], mode: int, coef: Optional[Sequence[float]] = None,
               divisor: float = 1.0, engine: Optional[AggEngine] = None) -> "OrderedDict[str, torch.Tensor]":
     """Ordered per-key reduction over client state_dicts (see module docstring)."""
     if len(dicts) == 0:
         raise IndexError("list index out of range")  # the reference indexes raw_grad_list[0]
     keys = list(dicts[0].keys())
+    if not keys:
+        return OrderedDict()
+    try:
+        ptrs, numel, codes, shapes, dev = _host.gather(list(dicts), keys)
+    except ValueError:  # mixed devices / non-contiguous: the staging path below normalises them
+        ptrs = None
+    if ptrs is not None and dev.startswith("cuda") and int(codes.min()) >= 0:
+        return _aggregate_device(keys, ptrs, numel, codes, shapes, dev, len(dicts), mode, coef, divisor, engine)
+    return _aggregate_staged(dicts, keys, mode, coef, divisor, engine)
+
+
+def _aggregate_device(keys, ptrs, numel, codes, shapes, dev, k, mode, coef, divisor, engine):
+    """Fast path: every tensor already on one HIP device, native dtypes; one launch per dtype."""
+    eng = engine or get_engine(torch.device(dev).index)
+    code_list = codes.tolist()
+    out_dt = [out_dtype(_CODE_DTYPE[c], mode) for c in code_list]
+    _, views, optrs = _host.alloc_outputs(shapes, out_dt, dev)
+    groups: Dict[int, List[int]] = {}
+    for t, c in enumerate(code_list):
+        groups.setdefault(c, []).append(t)
+    table = ptrs.view(len(keys), k)
+    for c, idx in groups.items():
+        if len(idx) == len(keys):
+            eng.weighted_sum_table(c, mode, numel, k, ptrs, optrs, coef, divisor)
+        else:
+            sel = torch.tensor(idx, dtype=torch.int64)
+            eng.weighted_sum_table(c, mode, numel.index_select(0, sel).contiguous(), k,
+                                   table.index_select(0, sel).reshape(-1).contiguous(),
+                                   optrs.index_select(0, sel).contiguous(), coef, divisor)
+    return OrderedDict(zip(keys, views))
+
+
+def _aggregate_staged(dicts, keys, mode, coef, divisor, engine):
+    """General path: host (CPU) tensors are staged to the engine's device; narrow integer types are
+    widened exactly to int64 first.  Arithmetic is still the HIP kernels'."""
     first = [dicts[0][k] for k in keys]
     eng = engine or _engine_for(first)
     on_cpu = not any(t.is_cuda for t in first)

@@ -172,7 +172,8 @@ def test_cross_silo_round_with_user_server_aggregator():
 
     meta, arr = case("g1_fedavg_lr_K2")
     cl = client_dicts(meta, arr)
-    model = torch.nn.Linear(784, 10)
+    model = torch.nn.Module()
+    model.linear = torch.nn.Linear(784, 10)
     args = types.SimpleNamespace(federated_optimizer="FedAvg")
     srv = FedMLAggregator(client_num=2, device="cuda:0", args=args, server_aggregator=MyServerAggregator(model, args))
     srv.add_local_trained_result(1, cl[1], meta["n"][1])
@@ -183,7 +184,7 @@ def test_cross_silo_round_with_user_server_aggregator():
     exp = expected_dicts(meta, arr)[0]
     assert_dict_bits(cpu(avg), exp, "cross-silo")
     assert idx == [0, 1]
-    assert torch.equal(model.weight.detach().cpu(), exp["linear.weight"])
+    assert torch.equal(model.linear.weight.detach().cpu(), exp["linear.weight"])
 
 
 def test_default_server_aggregator_round():
