@@ -54,6 +54,9 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     p.add_argument("--check-samples", type=int, default=65536)
+    p.add_argument("--layout", default="arena", choices=["arena", "tensors"],
+                   help="arena: client updates in one ClientArena allocation (fedml_amd/arena.py); "
+                        "tensors: one allocation per client tensor")
     return p.parse_args()
 
 
@@ -99,6 +102,19 @@ def make_flat_clients(idx, P, dtype=torch.float32):
         g = torch.Generator(device="cuda").manual_seed(1000 + i)
         out.append(torch.randn(P, generator=g, device="cuda", dtype=torch.float32).to(dtype))
     return out
+
+
+def make_arena_rows(idx, P, dtype=torch.float32):
+    """Client updates as rows of ONE ClientArena allocation (same values as make_flat_clients)."""
+    from fedml_amd.arena import ArenaLayout, ClientArena
+    arena = ClientArena(ArenaLayout([("w", (P,), dtype)]), capacity=len(idx), zero=False)
+    rows = []
+    for j, i in enumerate(idx):
+        g = torch.Generator(device="cuda").manual_seed(1000 + i)
+        row = arena.bufs[dtype][j][:P]
+        row.copy_(torch.randn(P, generator=g, device="cuda", dtype=torch.float32).to(dtype))
+        rows.append(row)
+    return rows
 
 
 def load_layout(name):
@@ -160,7 +176,7 @@ def wl_metric(args, eng, rank, world, timer):
     N = sum(counts)
     mine = split(K, rank, world)
     w = [counts[i] / N for i in mine]
-    xs = make_flat_clients(mine, P)
+    xs = make_arena_rows(mine, P) if args.layout == "arena" else make_flat_clients(mine, P)
     out = torch.empty(P, device="cuda")
     if world > 1:
         from fedml_amd.distributed.group_reduce import GroupReducer
@@ -189,7 +205,8 @@ def wl_metric(args, eng, rank, world, timer):
         ok = torch.equal(out.index_select(0, idx).cpu().view(torch.int32), exp.view(torch.int32))
         return f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on {args.check_samples} sampled elements"
 
-    return dict(name=f"fedavg_flat_K{K}_P{P}_fp32", dtype="fp32", step=step, parity=parity,
+    return dict(name=f"fedavg_flat_K{K}_P{P}_fp32" + ("" if args.layout == "arena" else "_tensors"),
+                dtype="fp32", step=step, parity=parity,
                 bytes_total=K * P * 4 + P * 4, launch_bytes=(len(mine) * P * 4 + P * 4) / launches,
                 clients=K, params=P, cpu_K=K)
 
@@ -205,6 +222,15 @@ def wl_layout(args, eng, rank, world, timer):
     mine = split(K, rank, world)
     w = [counts[i] / N for i in mine]
     dicts = make_layout_clients(mine, layout)
+    arena = None
+    if args.layout == "arena":
+        from fedml_amd.arena import ArenaLayout, ClientArena
+        arena = ClientArena(ArenaLayout([(n, tuple(s), getattr(torch, dt)) for n, s, dt in layout]),
+                            capacity=len(mine))
+        for j, d in enumerate(dicts):
+            arena.write(j, d)
+        dicts = [arena.slot(j) for j in range(len(mine))]
+        torch.cuda.synchronize()
     P = sum(int(np.prod(s)) for _, s, _ in layout)
     size = {"int64": 8, "bfloat16": 2, "float32": 4}
     in_b = sum(int(np.prod(s)) * size[dt] for _, s, dt in layout)
@@ -213,7 +239,7 @@ def wl_layout(args, eng, rank, world, timer):
 
     def step():
         with timer:
-            res["out"] = aggregate(dicts, MUL_W, w)
+            res["out"] = arena.aggregate(MUL_W, w) if arena is not None else aggregate(dicts, MUL_W, w)
         if world > 1:
             import torch.distributed as dist
             for t in res["out"].values():
@@ -233,7 +259,7 @@ def wl_layout(args, eng, rank, world, timer):
             bad += int((got.view(ib) != exp.view(ib)).sum())
         return f"{'bit-exact' if bad == 0 else f'{bad} MISMATCHES'} vs oracle on a strided sample of every key"
 
-    tag = "resnet18gn" if resnet else "vitb16_bf16"
+    tag = ("resnet18gn" if resnet else "vitb16_bf16") + ("" if args.layout == "arena" else "_tensors")
     return dict(name=f"fedavg_{tag}_K{K}_P{P}", dtype="fp32" if resnet else "bf16", step=step, parity=parity,
                 bytes_total=K * in_b + out_b, launch_bytes=None, clients=K, params=P, cpu_K=None)
 
@@ -247,7 +273,8 @@ def wl_hier(args, eng, rank, world, timer):
     counts = client_counts(G * M)
     N = sum(counts)
     my_groups = split(G, rank, world)
-    xs = {g: make_flat_clients(range(g * M, (g + 1) * M), P) for g in my_groups}
+    mk = make_arena_rows if args.layout == "arena" else make_flat_clients
+    xs = {g: mk(range(g * M, (g + 1) * M), P) for g in my_groups}
     gsum = {g: sum(counts[g * M:(g + 1) * M]) for g in range(G)}
     terms = {g: torch.empty(P, device="cuda") for g in my_groups}
     scratch = torch.empty(P, device="cuda")
@@ -296,13 +323,13 @@ def wl_gossip(args, eng, rank, world, timer):
             with timer:
                 return eng.mix(xs_, rp, cs, vs, ps, outs, outs2)
         dg = DistributedGossip(W, local_mix=timed_mix)
-        xs = make_flat_clients(dg.mine, P)
+        xs = (make_arena_rows if args.layout == "arena" else make_flat_clients)(dg.mine, P)
 
         def step():
             dg.step(xs)
         rows = len(dg.mine)
     else:
-        xs = make_flat_clients(range(n), P)
+        xs = (make_arena_rows if args.layout == "arena" else make_flat_clients)(range(n), P)
         rp, cs, vs = gossip_rows(W)
         outs = [torch.empty(P, device="cuda") for _ in range(n)]
 
@@ -407,7 +434,7 @@ def main():
             "config": {"workload": wl["name"], "clients": wl["clients"], "params_per_client": wl["params"],
                        "parallelism": f"client-groups x{world}" +
                                       (f", {args.collective} over RCCL in {args.chunks} chunks" if world > 1 else ""),
-                       "kernel_variant": args.variant},
+                       "kernel_variant": args.variant, "layout": args.layout},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,

@@ -1,0 +1,171 @@
+"""ClientArena: device-resident, client-major storage for one round of client updates.
+
+Why: the aggregation is a pure HBM stream, and how the K client updates sit in HBM matters.
+K separately allocated buffers read at ~5.9 TB/s on MI355X, the same bytes as K rows of ONE
+allocation at ~6.8 TB/s (tools/hbm_probe.py, profiles/r01_hbm_probe*.json: address translation
+over many independent allocations costs ~13 %).  A state_dict round also costs one pointer per
+(client, key) -- 19,456 for ViT-B/16 at K = 128 -- where an arena needs one per client.
+
+Layout: the model's keys are grouped by storage dtype; for each dtype group the arena holds one
+tensor ``[capacity, P_group]`` in which client i's row carries that group's keys at fixed offsets,
+each key padded to a 64-element (256-byte for fp32) boundary so every key and every row starts
+16-byte aligned (the kernel's vector path).  Aggregating the round is then ONE flat launch per
+dtype group over K row pointers (fa_weighted_sum with n = P_group), and the result lives in an
+output arena with the same offsets, exposed as per-key views in the model's key order.
+
+Ingest: ``write(i, state_dict)`` copies a client's tensors into row i (device -> device, or host
+-> device).  Host updates (what the reference's transports deliver, e.g. mpi_receive_thread.py:25)
+go through a pinned staging ring: the client's tensors are packed into pinned memory, one async
+H2D per dtype group is issued on a copy stream, and the aggregation stream waits on its event.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from .engine import MUL_W, AggEngine, get_engine, out_dtype
+
+_ALIGN_ELEMS = 64
+_SUPPORTED = (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64)
+
+
+def _pad(n: int) -> int:
+    return (n + _ALIGN_ELEMS - 1) // _ALIGN_ELEMS * _ALIGN_ELEMS
+
+
+class ArenaLayout:
+    """Key -> (dtype group, offset, shape) map of a model state_dict."""
+
+    def __init__(self, spec: Sequence[Tuple[str, Sequence[int], torch.dtype]]):
+        self.keys: List[str] = []
+        self.where: Dict[str, Tuple[torch.dtype, int, Tuple[int, ...], int]] = {}
+        self.group_numel: Dict[torch.dtype, int] = {}
+        for name, shape, dt in spec:
+            if dt not in _SUPPORTED:
+                raise TypeError(f"arena: key {name!r} has unsupported dtype {dt}")
+            n = 1
+            for s in shape:
+                n *= int(s)
+            off = self.group_numel.get(dt, 0)
+            self.where[name] = (dt, off, tuple(int(s) for s in shape), n)
+            self.group_numel[dt] = off + _pad(max(n, 1))
+            self.keys.append(name)
+
+    @classmethod
+    def from_state_dict(cls, sd) -> "ArenaLayout":
+        return cls([(k, tuple(v.shape), v.dtype) for k, v in sd.items()])
+
+    def views(self, bufs: Dict[torch.dtype, torch.Tensor], row: Optional[int]) -> "OrderedDict[str, torch.Tensor]":
+        out = OrderedDict()
+        for k in self.keys:
+            dt, off, shape, n = self.where[k]
+            b = bufs[dt] if row is None else bufs[dt][row]
+            out[k] = b[off:off + n].view(shape)
+        return out
+
+
+class ClientArena:
+    def __init__(self, layout: ArenaLayout, capacity: int, device=None, engine: Optional[AggEngine] = None,
+                 zero: bool = True):
+        self.layout = layout
+        self.capacity = int(capacity)
+        self.engine = engine or get_engine(None if device is None else torch.device(device).index)
+        self.device = self.engine.device
+        alloc = torch.zeros if zero else torch.empty  # zeroed padding keeps padded outputs finite
+        self.bufs: Dict[torch.dtype, torch.Tensor] = {
+            dt: alloc((self.capacity, n), dtype=dt, device=self.device) for dt, n in layout.group_numel.items()}
+        self._copy_stream = None
+        self._staging: List[Tuple[Dict[torch.dtype, torch.Tensor], Optional[torch.cuda.Event]]] = []
+        self._next_stage = 0
+        self._pending: List[torch.cuda.Event] = []
+
+    @classmethod
+    def for_model(cls, template_state_dict, capacity: int, device=None, **kw) -> "ClientArena":
+        return cls(ArenaLayout.from_state_dict(template_state_dict), capacity, device, **kw)
+
+    def slot(self, i: int) -> "OrderedDict[str, torch.Tensor]":
+        """Client i's tensors (views into the arena), in the model's key order."""
+        return self.layout.views(self.bufs, i)
+
+    def rows(self, dt: torch.dtype, clients: Sequence[int]) -> List[torch.Tensor]:
+        return [self.bufs[dt][i] for i in clients]
+
+    # ------------------------------------------------------------------ ingest
+    def write(self, i: int, state_dict) -> None:
+        """Copy one client's update into row i (device tensors: D2D on the current stream; host
+        tensors: packed into pinned staging and sent with one H2D per dtype group)."""
+        if not 0 <= i < self.capacity:
+            raise IndexError(f"arena row {i} out of range [0, {self.capacity})")
+        slot = self.slot(i)
+        for k, v in slot.items():
+            t = state_dict[k]  # KeyError on a missing key, like the reference's per-key access
+            if t.dtype != v.dtype or tuple(t.shape) != tuple(v.shape):
+                raise TypeError(f"arena: key {k!r} is {t.dtype}{tuple(t.shape)}, layout says {v.dtype}{tuple(v.shape)}")
+        first = state_dict[self.layout.keys[0]]
+        if first.is_cuda:
+            for k, v in slot.items():
+                v.copy_(state_dict[k])
+            return
+        self._write_host(i, state_dict)
+
+    def _stage_slot(self):
+        if len(self._staging) < 2:
+            bufs = {dt: torch.zeros(n, dtype=dt, pin_memory=True) for dt, n in self.layout.group_numel.items()}
+            self._staging.append((bufs, None))
+        idx = self._next_stage % len(self._staging)
+        self._next_stage += 1
+        bufs, ev = self._staging[idx]
+        if ev is not None:
+            ev.synchronize()  # the H2D that last used this pinned slot has finished
+        return idx, bufs
+
+    def _write_host(self, i: int, state_dict) -> None:
+        if self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(self.device)
+        idx, pinned = self._stage_slot()
+        views = self.layout.views(pinned, None)
+        for k, v in views.items():
+            v.copy_(state_dict[k])
+        with torch.cuda.stream(self._copy_stream):
+            for dt, buf in pinned.items():
+                self.bufs[dt][i].copy_(buf, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._copy_stream)
+        self._staging[idx] = (pinned, ev)
+        self._pending.append(ev)
+
+    def _wait_ingest(self):
+        cur = torch.cuda.current_stream(self.device)
+        for ev in self._pending:
+            cur.wait_event(ev)
+        self._pending.clear()
+
+    # ------------------------------------------------------------------ aggregation
+    def aggregate(self, mode: int, coef: Optional[Sequence[float]] = None, divisor: float = 1.0,
+                  clients: Optional[Sequence[int]] = None,
+                  out: Optional[Dict[torch.dtype, torch.Tensor]] = None) -> "OrderedDict[str, torch.Tensor]":
+        """Ordered reduction over the given client rows (default: all), one launch per dtype group.
+        ``out`` (optional): preallocated flat output per INPUT dtype group (reused across rounds).
+        Returns per-key views of the result in the model's key order."""
+        clients = list(range(self.capacity)) if clients is None else list(clients)
+        if not clients:
+            raise IndexError("list index out of range")
+        self._wait_ingest()
+        outs: Dict[torch.dtype, torch.Tensor] = {}
+        for dt, buf in self.bufs.items():
+            odt = out_dtype(dt, mode)
+            o = out[dt] if out is not None else torch.empty(buf.shape[1], dtype=odt, device=self.device)
+            self.engine.weighted_sum([buf[i] for i in clients], mode, coef, divisor, out=o)
+            outs[dt] = o
+        res = OrderedDict()
+        for k in self.layout.keys:
+            dt, off, shape, n = self.layout.where[k]
+            res[k] = outs[dt][off:off + n].view(shape)
+        return res
+
+    def fedavg(self, counts: Sequence[int], clients: Optional[Sequence[int]] = None):
+        """FedMLAggOperator.agg FedAvg branch (agg_operator.py:35-44) over the arena rows."""
+        N = sum(counts)
+        return self.aggregate(MUL_W, [c / N for c in counts], clients=clients)

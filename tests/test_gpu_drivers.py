@@ -200,3 +200,29 @@ def test_default_server_aggregator_round():
     data = [(torch.randn(16, 8, generator=g), torch.randint(0, 4, (16,), generator=g))]
     acc, loss, _, _ = agg.test(data, "cuda:0", args)
     assert 0.0 <= acc <= 1.0 and loss > 0
+
+
+@pytest.mark.parametrize("name", ["g3_fedavg_mixed_K5", "g2_fedavg_bf16_K7_P4099", "g1_fedavg_lr_K2",
+                                  "g2_fedavg_f64_K5", "g9_edge_values_K4"])
+@pytest.mark.parametrize("src", ["cpu", "cuda"])
+def test_client_arena_fedavg(name, src):
+    """Updates ingested into a ClientArena (host via pinned staging, or device) aggregate to the
+    reference's FedAvg result."""
+    from fedml_amd.arena import ClientArena
+    meta, arr = case(name)
+    cl = client_dicts(meta, arr)
+    arena = ClientArena.for_model(cl[0], capacity=len(cl) + 1, device="cuda:0")
+    for i, c in enumerate(cl):
+        arena.write(i, on_gpu(c) if src == "cuda" else c)
+    got = arena.fedavg(meta["n"], clients=list(range(len(cl))))
+    assert_dict_bits(cpu(got), expected_dicts(meta, arr)[0], f"arena:{name}")
+
+
+def test_client_arena_rejects_wrong_dtype():
+    from fedml_amd.arena import ClientArena
+    tmpl = OrderedDict(w=torch.zeros(10), b=torch.zeros(3, dtype=torch.bfloat16))
+    arena = ClientArena.for_model(tmpl, capacity=2, device="cuda:0")
+    with pytest.raises(TypeError):
+        arena.write(0, OrderedDict(w=torch.zeros(10, dtype=torch.float64), b=torch.zeros(3, dtype=torch.bfloat16)))
+    with pytest.raises(KeyError):
+        arena.write(0, OrderedDict(w=torch.zeros(10)))
