@@ -45,7 +45,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", default="metric", choices=["metric", "resnet18", "vit_bf16", "hier", "gossip"])
+    p.add_argument("--config", default="metric", choices=["metric", "resnet18", "vit_bf16", "hier", "gossip", "host"])
     p.add_argument("--clients", type=int, default=None)
     p.add_argument("--params", type=int, default=None)
     p.add_argument("--variant", type=int, default=0, help="kernel variant (fa_ctx_set_variant)")
@@ -54,6 +54,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     p.add_argument("--check-samples", type=int, default=65536)
+    p.add_argument("--pinned", action="store_true", help="host config: client updates already in pinned memory")
     p.add_argument("--layout", default="arena", choices=["arena", "tensors"],
                    help="arena: client updates in one ClientArena allocation (fedml_amd/arena.py); "
                         "tensors: one allocation per client tensor")
@@ -343,6 +344,37 @@ def wl_gossip(args, eng, rank, world, timer):
                 roofline_note="achieved uses compulsory bytes 2*rows*P*4 (each model read once, written once)")
 
 
+def wl_host(args, eng, rank, world, timer):
+    """Host path (SURVEY.md §8(d) 'Host path'): client updates start in pageable host memory (as
+    unpickled from MPI / socket receive buffers), are packed into pinned staging and copied H2D into
+    the ClientArena (copy stream, overlapped with packing the next client), aggregated, and the
+    averaged model is copied back D2H for broadcast.  Step = ingest K clients + FedAvg + D2H."""
+    from fedml_amd.arena import ArenaLayout, ClientArena
+    from fedml_amd.engine import MUL_W
+    K = args.clients or 128
+    P = args.params or 16_000_000
+    counts = client_counts(K)
+    N = sum(counts)
+    w = [c / N for c in counts]
+    g = torch.Generator().manual_seed(0)
+    host = [{"w": torch.randn(P, generator=g)} for _ in range(K)]
+    if args.pinned:
+        host = [{"w": h["w"].pin_memory()} for h in host]
+    arena = ClientArena(ArenaLayout([("w", (P,), torch.float32)]), capacity=K)
+    result = torch.empty(P, pin_memory=True)
+
+    def step():
+        for i in range(K):
+            arena.write(i, host[i])
+        with timer:
+            avg = arena.aggregate(MUL_W, w)
+        result.copy_(avg["w"], non_blocking=True)
+
+    return dict(name=f"fedavg_host_ingest_{'pinned' if args.pinned else 'pageable'}_K{K}_P{P}_fp32", dtype="fp32", step=step, parity=lambda: None,
+                bytes_total=K * P * 4 + P * 4, launch_bytes=K * P * 4 + P * 4, clients=K, params=P, cpu_K=None,
+                roofline_note="value includes pageable->pinned packing, H2D over PCIe and the D2H of the result")
+
+
 # ----------------------------------------------------------------------------- CPU baseline
 def cpu_baseline(K, budget_s):
     """The reference's CPU cost: oracle/torch_port.py (op-for-op restatement of agg_operator.py's
@@ -388,7 +420,7 @@ def main():
         eng.set_variant(args.variant)
     timer = Timed()
     wl = {"metric": wl_metric, "resnet18": wl_layout, "vit_bf16": wl_layout, "hier": wl_hier,
-          "gossip": wl_gossip}[args.config](args, eng, rank, world, timer)
+          "gossip": wl_gossip, "host": wl_host}[args.config](args, eng, rank, world, timer)
 
     for _ in range(args.warmup):
         wl["step"]()

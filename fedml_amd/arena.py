@@ -124,6 +124,16 @@ class ClientArena:
     def _write_host(self, i: int, state_dict) -> None:
         if self._copy_stream is None:
             self._copy_stream = torch.cuda.Stream(self.device)
+        if all(state_dict[k].is_pinned() for k in self.layout.keys):
+            # already page-locked (e.g. a transport that receives into pinned buffers): DMA directly
+            slot = self.slot(i)
+            with torch.cuda.stream(self._copy_stream):
+                for k, v in slot.items():
+                    v.copy_(state_dict[k], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self._copy_stream)
+            self._pending.append(ev)
+            return
         idx, pinned = self._stage_slot()
         views = self.layout.views(pinned, None)
         for k, v in views.items():
