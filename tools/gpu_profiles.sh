@@ -1,0 +1,13 @@
+# rocprofv3 evidence for the configs (summaries only are kept under gpurun_out/summary).
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out/summary
+fault() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
+for cfg in ${CONFIGS:-metric resnet18 vit_bf16 gossip hier}; do
+  tag=${ROUND:-r01}_$cfg
+  BENCH_ARGS="--config $cfg --steps 5 --warmup 2 --no-cpu-baseline --check-samples 0" KERNEL=${KERNEL:-k_} timeout -k 10 900 bash tools/profile.sh $tag > gpurun_out/summary/$tag.log 2>&1; rc=$?
+  echo "== $cfg rc=$rc"; tail -22 gpurun_out/summary/$tag.log
+  fault $rc && exit $rc
+  rm -rf gpurun_out/prof_$tag
+done
+exit 0

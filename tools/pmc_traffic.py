@@ -25,32 +25,33 @@ def find(d, pattern):
     return sorted(glob.glob(os.path.join(d, "**", pattern), recursive=True))
 
 
-def counter_values(d, counter):
+def counter_values(d, counter, name):
+    """Counter values of every dispatch of the kernel `name` (exact match)."""
     vals = []
     for f in find(d, "*counter_collection.csv"):
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                if KERNEL in row.get("Kernel_Name", "") and row.get("Counter_Name") == counter:
+                if row.get("Kernel_Name", "") == name and row.get("Counter_Name") == counter:
                     vals.append(float(row["Counter_Value"]))
     return vals
 
 
-def main(out_dir, tag):
-    prof = os.path.join(ROOT, "profiles")
+def main(out_dir, tag, dest=None):
+    prof = dest or os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     summary = {"tag": tag, "kernel_filter": KERNEL}
     stats = find(os.path.join(out_dir, "trace"), "*kernel_stats.csv")
     if stats:
         shutil.copy(stats[0], os.path.join(prof, f"{tag}_kernel_stats.csv"))
         with open(stats[0]) as fh:
-            for row in csv.DictReader(fh):
-                if KERNEL in row["Name"]:
-                    summary["kernel"] = row["Name"]
-                    summary["calls"] = int(row["Calls"])
-                    summary["avg_ns"] = float(row["AverageNs"])
-                    summary["min_ns"] = float(row["MinNs"])
-                    summary["max_ns"] = float(row["MaxNs"])
-                    break
+            rows = [r for r in csv.DictReader(fh) if KERNEL in r["Name"]]
+        if rows:  # the dominant kernel = largest total duration among the engine's kernels
+            row = max(rows, key=lambda r: float(r["TotalDurationNs"]))
+            summary["kernel"] = row["Name"]
+            summary["calls"] = int(row["Calls"])
+            summary["avg_ns"] = float(row["AverageNs"])
+            summary["min_ns"] = float(row["MinNs"])
+            summary["max_ns"] = float(row["MaxNs"])
     try:
         with open(os.path.join(out_dir, "trace_bench.json")) as fh:
             bench = json.loads(fh.read().strip().splitlines()[-1])
@@ -60,8 +61,9 @@ def main(out_dir, tag):
     except Exception as e:  # noqa: BLE001
         print("no bench line:", e)
         workload, algo = "unknown", None
-    fetch = counter_values(os.path.join(out_dir, "fetch"), "FETCH_SIZE")
-    write = counter_values(os.path.join(out_dir, "write"), "WRITE_SIZE")
+    name = summary.get("kernel", "")
+    fetch = counter_values(os.path.join(out_dir, "fetch"), "FETCH_SIZE", name)
+    write = counter_values(os.path.join(out_dir, "write"), "WRITE_SIZE", name)
     if fetch:
         summary["fetch_size_kb_median"] = statistics.median(fetch)
         summary["fetch_dispatches"] = len(fetch)
@@ -88,11 +90,13 @@ def main(out_dir, tag):
         allw = {}
     if "hbm_bytes_per_launch" in summary:
         allw[workload] = {"hbm_bytes_per_launch": int(summary["hbm_bytes_per_launch"]),
-                          "source": f"profiles/{tag}_pmc_summary.json"}
+                          "source": f"profiles/{tag}_pmc_summary.json",
+                          "avg_kernel_ns": summary.get("avg_ns"),
+                          "traffic_over_algorithmic": summary.get("traffic_over_algorithmic")}
         with open(tp, "w") as fh:
             json.dump(allw, fh, indent=1)
     print(json.dumps({k: v for k, v in summary.items() if k != "bench_line"}, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "r01")
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "r01", sys.argv[3] if len(sys.argv) > 3 else None)

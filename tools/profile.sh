@@ -17,5 +17,7 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -
 echo "fetch rc=$rc"; fault $rc && exit $rc
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- python3 bench.py $BENCH_ARGS > $OUT/write_bench.json 2> $OUT/write.err; rc=$?
 echo "write rc=$rc"; fault $rc && exit $rc
-find $OUT -name "*.csv" | head -20
-python3 tools/pmc_traffic.py $OUT $TAG || true
+mkdir -p gpurun_out/summary
+python3 tools/pmc_traffic.py $OUT $TAG gpurun_out/summary || true
+# keep gpurun_out small (it is copied back only if < 64 MiB): drop the raw traces
+rm -rf $OUT/trace $OUT/fetch $OUT/write
