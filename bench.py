@@ -267,46 +267,57 @@ def wl_layout(args, eng, rank, world, timer):
 
 def wl_hier(args, eng, rank, world, timer):
     """cfg4: G groups x M clients (ResNet-18 size, flat fp32): group FedAvg (weights n_i/N_g), cloud
-    term (G_g * N_g) / N, then the global sum over groups (rank order = group order)."""
-    from fedml_amd.engine import MUL_N_DIV_N, MUL_W, SUM
+    term (G_g * N_g) / N (HierFedAvgCloudAggregator.py:140-157), ordered global sum over groups --
+    one fused two-level kernel pass over this rank's clients (fa_weighted_sum_grouped); across
+    ranks (one or more groups each) the partials are SUM-reduced over RCCL."""
+    from fedml_amd.engine import MUL_N_DIV_N, MUL_W
     G, M = 8, (args.clients or 512) // 8
     P = args.params or RESNET18_P
     counts = client_counts(G * M)
     N = sum(counts)
     my_groups = split(G, rank, world)
-    mk = make_arena_rows if args.layout == "arena" else make_flat_clients
-    xs = {g: mk(range(g * M, (g + 1) * M), P) for g in my_groups}
-    gsum = {g: sum(counts[g * M:(g + 1) * M]) for g in range(G)}
-    terms = {g: torch.empty(P, device="cuda") for g in my_groups}
-    scratch = torch.empty(P, device="cuda")
+    clients = [i for g in my_groups for i in range(g * M, (g + 1) * M)]
+    xs = (make_arena_rows if args.layout == "arena" else make_flat_clients)(clients, P)
+    gcounts = [counts[g * M:(g + 1) * M] for g in my_groups]
+    gn = [sum(c) for c in gcounts]
+    w = [c / gn[j] for j, cs in enumerate(gcounts) for c in cs]
+    gptr = [j * M for j in range(len(my_groups) + 1)]
     out = torch.empty(P, device="cuda")
-    red = None
+
+    def timed_grouped(xs_, mode, coef, div, gp, gm, gc, gd, o):
+        with timer:
+            return eng.weighted_sum_grouped(xs_, mode, coef, div, gp, gm, gc, gd, out=o)
+
     if world > 1:
         from fedml_amd.distributed.group_reduce import GroupReducer
+        red = GroupReducer(collective=args.collective, chunks=args.chunks, local_grouped=timed_grouped)
 
-        def timed_sum(xs_, mode, coef, div, o):
-            with timer:
-                return eng.weighted_sum(xs_, mode, coef, div, out=o)
-        red = GroupReducer(collective=args.collective if args.collective != "reduce" else "ordered",
-                           chunks=args.chunks, local_sum=timed_sum)
+        def step():
+            red.hierarchical_groups(xs, gcounts, N, out=out)
+        launches = args.chunks
+    else:
+        def step():
+            timed_grouped(xs, MUL_W, w, 1.0, gptr, MUL_N_DIV_N, gn, [float(N)] * len(gn), out)
+        launches = 1
 
-    def step():
-        if red is not None and len(my_groups) == 1:
-            (g,) = my_groups
-            red.hierarchical(xs[g], counts[g * M:(g + 1) * M], N, out=out)
-            return
-        for g in my_groups:
-            with timer:
-                eng.weighted_sum(xs[g], MUL_W, [c / gsum[g] for c in counts[g * M:(g + 1) * M]], out=scratch)
-            eng.weighted_sum([scratch], MUL_N_DIV_N, [gsum[g]], float(N), out=terms[g])
-        if red is not None:  # several groups per rank: local ordered sum of the terms, then RCCL
-            red.sum([terms[g] for g in my_groups], out=out)
-        else:
-            eng.weighted_sum([terms[g] for g in my_groups], SUM, out=out)
+    def parity():
+        if world > 1 or args.check_samples <= 0:
+            return None
+        from oracle import orc
+        gi = torch.Generator(device="cuda").manual_seed(98)
+        idx = torch.randint(0, P, (min(args.check_samples, 8192),), generator=gi, device="cuda")
+        sample = [x.index_select(0, idx).cpu() for x in xs]
+        terms = []
+        for j in range(len(my_groups)):
+            Gj = orc.weighted_sum(sample[gptr[j]:gptr[j + 1]], 0, w[gptr[j]:gptr[j + 1]])
+            terms.append(orc.weighted_sum([Gj], 1, [gn[j]], float(N)))
+        exp = orc.weighted_sum(terms, 2)
+        ok = torch.equal(out.index_select(0, idx).cpu().view(torch.int32), exp.view(torch.int32))
+        return f"{'bit-exact' if ok else 'MISMATCH'} vs oracle (group FedAvg -> cloud term -> ordered sum) on {idx.numel()} sampled elements"
 
-    return dict(name=f"hier_fedavg_G{G}x{M}_P{P}_fp32", dtype="fp32", step=step, parity=lambda: None,
-                bytes_total=G * M * P * 4 + P * 4, launch_bytes=M * P * 4 + P * 4, clients=G * M, params=P,
-                cpu_K=None)
+    return dict(name=f"hier_fedavg_G{G}x{M}_P{P}_fp32", dtype="fp32", step=step, parity=parity,
+                bytes_total=G * M * P * 4 + P * 4, launch_bytes=(len(clients) * P * 4 + P * 4) / launches,
+                clients=G * M, params=P, cpu_K=None)
 
 
 def wl_gossip(args, eng, rank, world, timer):

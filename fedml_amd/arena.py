@@ -25,7 +25,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from .engine import MUL_W, AggEngine, get_engine, out_dtype
+from .engine import MUL_N_DIV_N, MUL_W, SUM, AggEngine, get_engine, out_dtype
 
 _ALIGN_ELEMS = 64
 _SUPPORTED = (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64)
@@ -174,6 +174,40 @@ class ClientArena:
             dt, off, shape, n = self.layout.where[k]
             res[k] = outs[dt][off:off + n].view(shape)
         return res
+
+    def aggregate_grouped(self, groups: Sequence[Sequence[int]], mode: int, coef: Optional[Sequence[float]],
+                          divisor: float, group_mode: int, group_coef: Optional[Sequence[float]] = None,
+                          group_divisor: Optional[Sequence[float]] = None) -> "OrderedDict[str, torch.Tensor]":
+        """Two-level reduction over client groups in ONE pass per dtype group (fa_weighted_sum_grouped).
+        ``coef`` is indexed like the concatenation of ``groups``.  Float dtype groups only."""
+        self._wait_ingest()
+        order = [i for g in groups for i in g]
+        gptr = [0]
+        for g in groups:
+            gptr.append(gptr[-1] + len(g))
+        outs: Dict[torch.dtype, torch.Tensor] = {}
+        for dt, buf in self.bufs.items():
+            outs[dt] = self.engine.weighted_sum_grouped([buf[i] for i in order], mode, coef, divisor, gptr,
+                                                        group_mode, group_coef, group_divisor)
+        res = OrderedDict()
+        for k in self.layout.keys:
+            dt, off, shape, n = self.layout.where[k]
+            res[k] = outs[dt][off:off + n].view(shape)
+        return res
+
+    def hierarchical(self, groups: Sequence[Sequence[int]], counts: Sequence[int], formula: str = "sp"):
+        """Hierarchical FedAvg of a round in one pass: group FedAvg (weights n_i / N_g), then
+        formula "sp": global = sum_g G_g * (N_g / N)       (sp/hierarchical_fl/trainer.py:108-110)
+        formula "cloud": global = sum_g (G_g * N_g) / N   (HierFedAvgCloudAggregator.py:140-157)."""
+        w, gn = [], []
+        for g in groups:
+            Ng = sum(counts[i] for i in g)
+            gn.append(Ng)
+            w += [counts[i] / Ng for i in g]
+        N = sum(gn)
+        if formula == "sp":
+            return self.aggregate_grouped(groups, MUL_W, w, 1.0, MUL_W, [n / N for n in gn])
+        return self.aggregate_grouped(groups, MUL_W, w, 1.0, MUL_N_DIV_N, gn, [float(N)] * len(gn))
 
     def fedavg(self, counts: Sequence[int], clients: Optional[Sequence[int]] = None):
         """FedMLAggOperator.agg FedAvg branch (agg_operator.py:35-44) over the arena rows."""

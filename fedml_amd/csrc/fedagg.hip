@@ -384,6 +384,80 @@ k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
 }
 
 // --------------------------------------------------------------------------------------------
+// Two-level (grouped) ordered reduction in ONE pass over the clients: for every group g (a
+// contiguous client range), the group partial G_g = ordered reduction of its clients (MODE), then
+// the group epilogue t_g (none / op(G_g * c_g) / op(op(G_g * c_g) / d_g)), then out = ordered sum
+// of t_g.  This is the reference's two-level arithmetic -- hierarchical FL (group FedAvg, then the
+// cloud's (G*n)/N or the SP trainer's G*(N_g/N)), fedavg_seq (worker partials, then a plain sum) --
+// with every intermediate kept in registers: bit-identical to running the levels as separate
+// launches, minus the intermediate HBM round trips.
+struct GroupDesc {
+  int32_t begin, end;  // client range
+  double mul;          // epilogue coefficient c_g
+  double div;          // epilogue divisor d_g
+  int64_t pad;
+};
+static_assert(sizeof(GroupDesc) == 32, "GroupDesc layout");
+
+template <int DT, int MODE, int U, bool NT>
+__global__ void __launch_bounds__(kBlock)
+k_wsum_grouped(const Seg* __restrict__ segs, const double* __restrict__ coef,
+               const void* const* __restrict__ ptrs, double divisor,
+               const GroupDesc* __restrict__ groups, int ngroups, int gmode) {
+  using B = WsumBody<DT, MODE, U, 1, NT>;
+  using T = typename B::T;
+  using A = typename B::A;
+  constexpr int V = T::V;
+  constexpr int64_t TILE = (int64_t)kBlock * V;
+  const int64_t tile = blockIdx.x;
+  const Seg sg = segs[0];
+  const int64_t base = tile * TILE;
+  const void* const* in = ptrs;
+  const typename T::D d = T::div(divisor);
+
+  auto epilogue = [&](A g, const GroupDesc& gd) -> A {
+    if (gmode == FA_MODE_MUL_W) return T::rnd(op_mul(g, (A)gd.mul));
+    if (gmode == FA_MODE_MUL_N_DIV_N) return T::rnd(op_div(T::rnd(op_mul(g, (A)gd.mul)), (A)gd.div));
+    return g;
+  };
+
+  if (sg.aligned && base + TILE <= sg.numel) {
+    const int64_t e0 = base + (int64_t)threadIdx.x * V;
+    const int64_t boff = e0 * T::IN_BYTES;
+    A out[V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) out[v] = T::zero();
+    for (int g = 0; g < ngroups; ++g) {
+      const GroupDesc gd = groups[g];
+      A acc[1][V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[0][v] = T::zero();
+      for (int i0 = gd.begin; i0 < gd.end; i0 += U) {
+        u32x4 r[U][1];
+        B::load(r, in, i0, gd.end, boff);
+        B::template consume<true>(acc, r, coef, i0, gd.end, d);
+      }
+#pragma unroll
+      for (int v = 0; v < V; ++v) out[v] = accum<DT, MODE>(out[v], epilogue(acc[0][v], gd));
+    }
+    T::stv((char*)sg.out + e0 * T::OUT_BYTES, out);
+  } else {
+    const int64_t end = min(base + TILE, sg.numel);
+    for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
+      A out = T::zero();
+      for (int g = 0; g < ngroups; ++g) {
+        const GroupDesc gd = groups[g];
+        A acc = T::zero();
+        for (int i = gd.begin; i < gd.end; ++i)
+          acc = accum<DT, MODE>(acc, term<DT, MODE>(T::ld1(in[i], e), T::coef(coef[i]), d));
+        out = accum<DT, MODE>(out, epilogue(acc, gd));
+      }
+      T::st1(sg.out, e, out);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------------
 // Mixing / gossip kernel: one workgroup = one element tile, looping over every output row so that
 // an input shared by neighbouring rows is re-read from L2 / Infinity Cache, not HBM.  Rows go in
 // groups of RG: the loads of all RG rows (up to MAXD entries each, clamped like k_wsum) are issued
@@ -781,6 +855,81 @@ int fa_weighted_sum(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t k, cons
   if (n < 0) return fail(FA_ERR_INVALID, "n must be >= 0");
   void* outs[1] = {d_out};
   return fa_weighted_sum_multi(ctx, dtype, mode, 1, &n, k, d_in, coef, divisor, outs, hip_stream);
+}
+
+int fa_weighted_sum_grouped(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t k, const void* const* d_in,
+                            const double* coef, double divisor, int32_t num_groups, const int32_t* group_ptr,
+                            int group_mode, const double* group_coef, const double* group_divisor,
+                            void* d_out, void* hip_stream) {
+  if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (k <= 0 || n < 0 || !d_in || !d_out || num_groups <= 0 || !group_ptr)
+    return fail(FA_ERR_INVALID, "fa_weighted_sum_grouped: invalid arguments");
+  if (dtype != FA_DTYPE_F32 && dtype != FA_DTYPE_BF16 && dtype != FA_DTYPE_F16 && dtype != FA_DTYPE_F64)
+    return fail(FA_ERR_DTYPE, "fa_weighted_sum_grouped: dtype %d not supported (F32, BF16, F16, F64)", dtype);
+  if (mode < FA_MODE_MUL_W || mode > FA_MODE_SUM || group_mode < FA_MODE_MUL_W || group_mode > FA_MODE_SUM)
+    return fail(FA_ERR_DTYPE, "fa_weighted_sum_grouped: unknown mode");
+  if (mode != FA_MODE_SUM && !coef) return fail(FA_ERR_INVALID, "coef is NULL for a weighted mode");
+  if (group_mode != FA_MODE_SUM && !group_coef) return fail(FA_ERR_INVALID, "group_coef is NULL");
+  if (group_mode == FA_MODE_MUL_N_DIV_N && !group_divisor) return fail(FA_ERR_INVALID, "group_divisor is NULL");
+  if (group_ptr[0] != 0 || group_ptr[num_groups] != k)
+    return fail(FA_ERR_INVALID, "group_ptr must start at 0 and end at k");
+  for (int g = 0; g < num_groups; ++g)
+    if (group_ptr[g + 1] <= group_ptr[g]) return fail(FA_ERR_INVALID, "group %d is empty", g);
+  bool aligned = al16(d_out);
+  for (int i = 0; i < k; ++i) {
+    if (!d_in[i]) return fail(FA_ERR_INVALID, "client %d: input NULL", i);
+    aligned = aligned && al16(d_in[i]);
+  }
+  if (n == 0) return FA_OK;
+  const int64_t tile_elems = (int64_t)kBlock * elems_per_vec(dtype);
+  const int64_t tiles = (n + tile_elems - 1) / tile_elems;
+  if (tiles > 0x7FFFFFFFll) return fail(FA_ERR_INVALID, "too many tiles");
+  const size_t seg_bytes = align16(sizeof(Seg));
+  const size_t coef_bytes = align16(sizeof(double) * k);
+  const size_t grp_bytes = sizeof(GroupDesc) * num_groups;
+  const size_t ptr_bytes = sizeof(void*) * k;
+  const size_t bytes = seg_bytes + coef_bytes + grp_bytes + ptr_bytes;
+  DeviceGuard g(ctx->device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
+  hipStream_t st = (hipStream_t)hip_stream;
+  fa_ctx::Slot* slot = nullptr;
+  int rc = acquire_slot(ctx, bytes, &slot);
+  if (rc) return rc;
+  char* h = (char*)slot->host;
+  *(Seg*)h = Seg{n, 0, d_out, 0, aligned ? 1 : 0};
+  double* hc = (double*)(h + seg_bytes);
+  for (int i = 0; i < k; ++i) hc[i] = coef ? coef[i] : 0.0;
+  GroupDesc* hg = (GroupDesc*)(h + seg_bytes + coef_bytes);
+  for (int gi = 0; gi < num_groups; ++gi)
+    hg[gi] = GroupDesc{group_ptr[gi], group_ptr[gi + 1], group_coef ? group_coef[gi] : 1.0,
+                       group_divisor ? group_divisor[gi] : 1.0, 0};
+  memcpy(h + seg_bytes + coef_bytes + grp_bytes, d_in, ptr_bytes);
+  rc = stage(slot, bytes, st);
+  if (rc) return rc;
+  char* dv = (char*)slot->dev;
+  const Seg* ds = (const Seg*)dv;
+  const double* dc = (const double*)(dv + seg_bytes);
+  const GroupDesc* dg = (const GroupDesc*)(dv + seg_bytes + coef_bytes);
+  const void* const* dp = (const void* const*)(dv + seg_bytes + coef_bytes + grp_bytes);
+  const dim3 grid((unsigned)tiles), blk(kBlock);
+#define FA_G(DT, MODE) \
+  hipLaunchKernelGGL((k_wsum_grouped<DT, MODE, 8, true>), grid, blk, 0, st, ds, dc, dp, divisor, dg, num_groups, group_mode)
+#define FA_G_MODES(DT)                                   \
+  switch (mode) {                                        \
+    case FA_MODE_MUL_W: FA_G(DT, FA_MODE_MUL_W); break;  \
+    case FA_MODE_MUL_N_DIV_N: FA_G(DT, FA_MODE_MUL_N_DIV_N); break; \
+    default: FA_G(DT, FA_MODE_SUM); break;               \
+  }
+  switch (dtype) {
+    case FA_DTYPE_F32: FA_G_MODES(FA_DTYPE_F32); break;
+    case FA_DTYPE_BF16: FA_G_MODES(FA_DTYPE_BF16); break;
+    case FA_DTYPE_F16: FA_G_MODES(FA_DTYPE_F16); break;
+    case FA_DTYPE_F64: FA_G_MODES(FA_DTYPE_F64); break;
+  }
+#undef FA_G_MODES
+#undef FA_G
+  FA_HIP(hipGetLastError());
+  return release(slot, st);
 }
 
 int fa_mix(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_ptr,

@@ -42,6 +42,12 @@ def _engine_local_sum(xs, mode, coef, divisor, out):
     return get_engine(out.device.index).weighted_sum(xs, mode, coef, divisor, out=out)
 
 
+def _engine_local_grouped(xs, mode, coef, divisor, gptr, gmode, gcoef, gdiv, out):
+    from ..engine import get_engine
+    return get_engine(out.device.index).weighted_sum_grouped(xs, mode, coef, divisor, gptr, gmode, gcoef,
+                                                             gdiv, out=out)
+
+
 def chunk_bounds(n: int, chunks: int) -> List[tuple]:
     chunks = max(1, min(chunks, n)) if n > 0 else 1
     return [(n * c // chunks, n * (c + 1) // chunks) for c in range(chunks)]
@@ -51,7 +57,7 @@ class GroupReducer:
     """Group -> global reduction of flat parameter vectors over a process group."""
 
     def __init__(self, group=None, collective: str = "reduce", dst: int = 0, chunks: int = 8,
-                 local_sum: Optional[LocalSum] = None):
+                 local_sum: Optional[LocalSum] = None, local_grouped: Optional[Callable] = None):
         if collective not in ("reduce", "all_reduce", "reduce_scatter", "ordered"):
             raise ValueError(f"unknown collective {collective!r}")
         self.group = group
@@ -59,37 +65,75 @@ class GroupReducer:
         self.dst = dst
         self.chunks = chunks
         self.local_sum = local_sum or _engine_local_sum
+        # fused two-level local step (group partial + epilogue in one kernel pass); with an injected
+        # local_sum and no local_grouped the levels run as separate passes (same arithmetic)
+        self.local_grouped = local_grouped if local_grouped is not None else (
+            _engine_local_grouped if local_sum is None else None)
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
 
     # -------------------------------------------------------------- public entry points
     def fedavg(self, xs: Sequence[torch.Tensor], weights: Sequence[float], out: Optional[torch.Tensor] = None):
         """Global FedAvg of all ranks' clients; ``weights`` = this rank's GLOBAL w_i = n_i / N."""
-        return self._run(xs, MUL_W, list(weights), 1.0, out)
+        flat = [x.reshape(-1) for x in xs]
+        w = list(weights)
+        return self._run(flat, lambda part, a, b: self.local_sum([x[a:b] for x in flat], MUL_W, w, 1.0, part),
+                         out, mode=MUL_W)
 
     def hierarchical(self, xs: Sequence[torch.Tensor], counts: Sequence[int], total: int,
                      out: Optional[torch.Tensor] = None):
-        """Hierarchical round: group FedAvg (weights n_i / N_r, sp/fedavg_api.py:144-159), then the
-        cloud term (G_r * N_r) / N (MPI cloud formula), then the global sum over groups."""
-        n_r = sum(counts)
-        return self._run(xs, MUL_W, [c / n_r for c in counts], 1.0, out, post=(n_r, float(total)))
+        """This rank's clients form ONE group: group FedAvg (weights n_i / N_r,
+        sp/fedavg_api.py:144-159), cloud term (G_r * N_r) / N (MPI cloud formula), global sum."""
+        return self.hierarchical_groups(xs, [list(counts)], total, out)
+
+    def hierarchical_groups(self, xs: Sequence[torch.Tensor], group_counts: Sequence[Sequence[int]], total: int,
+                            out: Optional[torch.Tensor] = None):
+        """This rank holds several consecutive groups (xs concatenated in group order): per group the
+        group FedAvg and cloud term, the ordered sum over this rank's groups, then the global sum."""
+        flat = [x.reshape(-1) for x in xs]
+        w, gn, gptr = [], [], [0]
+        for cnts in group_counts:
+            ng = sum(cnts)
+            gn.append(ng)
+            w += [c / ng for c in cnts]
+            gptr.append(gptr[-1] + len(cnts))
+        if len(flat) != gptr[-1]:
+            raise ValueError("hierarchical_groups: client count does not match the groups")
+        T = float(total)
+
+        def local(part, a, b):
+            sl = [x[a:b] for x in flat]
+            if self.local_grouped is not None:
+                self.local_grouped(sl, MUL_W, w, 1.0, gptr, MUL_N_DIV_N, gn, [T] * len(gn), part)
+                return
+            terms = []
+            for g in range(len(gn)):  # two-pass form (injected local_sum): same arithmetic
+                G = torch.empty_like(part)
+                self.local_sum(sl[gptr[g]:gptr[g + 1]], MUL_W, w[gptr[g]:gptr[g + 1]], 1.0, G)
+                t = torch.empty_like(part)
+                self.local_sum([G], MUL_N_DIV_N, [gn[g]], T, t)
+                terms.append(t)
+            if len(terms) == 1:
+                part.copy_(terms[0])
+            else:
+                self.local_sum(terms, SUM, None, 1.0, part)
+        return self._run(flat, local, out, mode=MUL_W)
 
     def sum(self, xs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None):
         """Plain global sum (FedAvg_seq / FedDyn branches)."""
-        return self._run(xs, SUM, None, 1.0, out)
+        flat = [x.reshape(-1) for x in xs]
+        return self._run(flat, lambda part, a, b: self.local_sum([x[a:b] for x in flat], SUM, None, 1.0, part),
+                         out, mode=SUM)
 
     # -------------------------------------------------------------- implementation
-    def _run(self, xs, mode, coef, divisor, out, post=None):
-        n = xs[0].numel()
-        dev = xs[0].device
+    def _run(self, flat, local, out, mode):
+        n = flat[0].numel()
+        dev = flat[0].device
         if out is None:
-            out = torch.empty(n, dtype=torch.float32 if xs[0].dtype == torch.int64 and mode != SUM else xs[0].dtype,
-                              device=dev)
-        flat = [x.reshape(-1) for x in xs]
-        bounds = chunk_bounds(n, self.chunks)
+            out = torch.empty(n, dtype=torch.float32 if flat[0].dtype == torch.int64 and mode != SUM
+                              else flat[0].dtype, device=dev)
         works = []
         gathered = []
-        shard = None
         if self.collective == "reduce_scatter":
             if n % self.world:
                 raise ValueError("reduce_scatter needs P divisible by the world size")
@@ -102,7 +146,7 @@ class GroupReducer:
                 base = self.world * a
                 for r in range(self.world):
                     lo = r * S + a
-                    self._local(flat, mode, coef, divisor, out[base + r * L: base + (r + 1) * L], lo, lo + L, post)
+                    local(out[base + r * L: base + (r + 1) * L], lo, lo + L)
                 if self.world > 1:
                     works.append(dist.reduce_scatter_tensor(shard[a:b], out[base: base + self.world * L],
                                                             op=dist.ReduceOp.SUM, group=self.group,
@@ -112,9 +156,9 @@ class GroupReducer:
             for w in works:
                 w.wait()
             return shard
-        for a, b in bounds:
+        for a, b in chunk_bounds(n, self.chunks):
             part = out[a:b]
-            self._local(flat, mode, coef, divisor, part, a, b, post)
+            local(part, a, b)
             if self.world == 1:
                 continue
             if self.collective == "reduce":
@@ -132,13 +176,3 @@ class GroupReducer:
             for a, b, bufs in gathered:
                 self.local_sum(bufs, SUM, None, 1.0, out[a:b])
         return out
-
-    def _local(self, flat, mode, coef, divisor, part, a, b, post):
-        if post is None:
-            self.local_sum([x[a:b] for x in flat], mode, coef, divisor, part)
-            return
-        # hierarchical: group FedAvg G into scratch, then the cloud term (G * N_r) / N into part
-        n_r, total = post
-        g = torch.empty_like(part)
-        self.local_sum([x[a:b] for x in flat], mode, coef, divisor, g)
-        self.local_sum([g], MUL_N_DIV_N, [n_r], total, part)

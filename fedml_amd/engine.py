@@ -133,6 +133,36 @@ class AggEngine:
         N.check(rc, "fa_weighted_sum_multi")
         return results
 
+    def weighted_sum_grouped(self, xs: Sequence[torch.Tensor], mode: int, coef: Optional[Sequence[float]],
+                             divisor: float, group_ptr: Sequence[int], group_mode: int,
+                             group_coef: Optional[Sequence[float]] = None,
+                             group_divisor: Optional[Sequence[float]] = None,
+                             out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """Two-level ordered reduction in one pass (fa_weighted_sum_grouped): groups of clients
+        [group_ptr[g], group_ptr[g+1]), group epilogue `group_mode`, ordered sum over groups."""
+        k = len(xs)
+        if k == 0:
+            raise ValueError("weighted_sum_grouped: no client tensors")
+        dt, shape = xs[0].dtype, xs[0].shape
+        if dt not in (torch.float32, torch.bfloat16, torch.float16, torch.float64):
+            raise TypeError(f"weighted_sum_grouped: unsupported dtype {dt}")
+        for i, t in enumerate(xs):
+            if t.dtype != dt or t.shape != shape:
+                raise ValueError(f"client {i}: dtype/shape mismatch")
+            _require_device(t, self.device, f"client {i}")
+        G = len(group_ptr) - 1
+        if out is None:
+            out = torch.empty(shape, dtype=dt, device=self.device)
+        _require_device(out, self.device, "output")
+        rc = self._lib.fa_weighted_sum_grouped(
+            self._ctx, DTYPE_CODE[dt], int(mode), xs[0].numel(), k, N.ptr_array([t.data_ptr() for t in xs]),
+            N.f64_array(coef) if coef is not None else None, float(divisor), G, N.i32_array(group_ptr),
+            int(group_mode), N.f64_array(group_coef) if group_coef is not None else None,
+            N.f64_array(group_divisor) if group_divisor is not None else None, out.data_ptr(),
+            self._stream(stream))
+        N.check(rc, "fa_weighted_sum_grouped")
+        return out
+
     def weighted_sum_table(self, dtype_code: int, mode: int, seg_numel: torch.Tensor, k: int,
                            in_ptrs: torch.Tensor, out_ptrs: torch.Tensor, coef: Optional[Sequence[float]] = None,
                            divisor: float = 1.0, stream=None) -> None:

@@ -112,6 +112,24 @@ int fa_weighted_sum_multi(fa_ctx *ctx, int dtype, int mode, int32_t num_segments
                            void *hip_stream);
 
 /*
+ * Two-level (grouped) reduction in one pass, one flat vector per client:
+ *   clients [group_ptr[g], group_ptr[g+1]) form group g (group_ptr[0] = 0, group_ptr[G] = k,
+ *   groups non-empty); G_g = the ordered `mode` reduction of the group's clients (coef[i],
+ *   divisor as in fa_weighted_sum); t_g = G_g (group_mode SUM), op(G_g * group_coef[g]) (MUL_W)
+ *   or op(op(G_g * group_coef[g]) / group_divisor[g]) (MUL_N_DIV_N); out = ordered sum of t_g.
+ * Bit-identical to the separate launches of each level.  Replaces the reference's two-level
+ * loops: hierarchical FL (sp/hierarchical_fl/group.py:60-62 + trainer.py:108-110; the MPI cloud
+ * HierFedAvgCloudAggregator.py:140-157 over HierGroup.py:76 edge models) and FedAvg_seq
+ * (fedavg_seq/FedAvgClientManager.py:67-73 + FedAVGAggregator.py:201-236).  dtype: F32, BF16,
+ * F16, F64.
+ */
+int fa_weighted_sum_grouped(fa_ctx *ctx, int dtype, int mode, int64_t n, int32_t k,
+                            const void *const *d_in, const double *coef, double divisor,
+                            int32_t num_groups, const int32_t *group_ptr, int group_mode,
+                            const double *group_coef, const double *group_divisor, void *d_out,
+                            void *hip_stream);
+
+/*
  * Mixing / gossip: for every row r < rows, with CSR entries j in [row_ptr[r], row_ptr[r+1]):
  *   d_out[r][e] = ordered MUL_W reduction of d_in[cols[j]][e] * vals[j]   (entry order = CSR order)
  *   if post_scale: d_out2[r][e] = op(d_out[r][e] * post_scale[r])         (PushSum z = x / omega)

@@ -226,3 +226,31 @@ def test_client_arena_rejects_wrong_dtype():
         arena.write(0, OrderedDict(w=torch.zeros(10, dtype=torch.float64), b=torch.zeros(3, dtype=torch.bfloat16)))
     with pytest.raises(KeyError):
         arena.write(0, OrderedDict(w=torch.zeros(10)))
+
+
+def test_arena_fused_hierarchical_sp_golden():
+    """SP hierarchical round (group FedAvg then global FedAvg over groups) in ONE kernel pass."""
+    from fedml_amd.arena import ClientArena
+    meta, arr = case("g7_hier_sp_K12_G3")
+    cl = client_dicts(meta, arr)
+    arena = ClientArena.for_model(cl[0], capacity=len(cl), device="cuda:0")
+    for i, c in enumerate(cl):
+        arena.write(i, c)
+    got = arena.hierarchical(meta["groups"], meta["n"], formula="sp")
+    assert_dict_bits(cpu(got), expected_dicts(meta, arr)[0], "fused hier sp")
+
+
+def test_arena_fused_fedavg_seq_golden():
+    """fedavg_seq two-level reduce (worker partials with global weights, then the plain sum), fused."""
+    from fedml_amd.arena import ClientArena
+    from fedml_amd.engine import MUL_W, SUM
+    meta, arr = case("g6_fedavg_seq_two_level_K10")
+    cl = client_dicts(meta, arr)
+    arena = ClientArena.for_model(cl[0], capacity=len(cl), device="cuda:0")
+    for i, c in enumerate(cl):
+        arena.write(i, c)
+    n = meta["n"]
+    sched = meta["schedule"]
+    w = [n[i] / sum(n) for wk in sched for i in wk]
+    got = arena.aggregate_grouped(sched, MUL_W, w, 1.0, SUM)
+    assert_dict_bits(cpu(got), expected_dicts(meta, arr)[0], "fused fedavg_seq")

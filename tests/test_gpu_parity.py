@@ -199,3 +199,34 @@ def test_all_kernel_variants_identical(variant, dtype, mode):
             assert bits_equal(got, exp), (variant, dtype, mode, K, P)
     finally:
         eng.close()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64], ids=str)
+@pytest.mark.parametrize("mode,gmode", [(MUL_W, MUL_W), (MUL_W, MUL_N_DIV_N), (MUL_W, SUM), (SUM, SUM),
+                                        (MUL_N_DIV_N, MUL_N_DIV_N)])
+@pytest.mark.parametrize("P", [1, 2049, 300_001])
+def test_grouped_two_level_vs_oracle(eng, dtype, mode, gmode, P):
+    """fa_weighted_sum_grouped == the levels run as separate ordered reductions (C oracle)."""
+    from oracle import orc
+    g = torch.Generator().manual_seed(P + mode * 10 + gmode)
+    gptr = [0, 4, 5, 13, 20]
+    K = gptr[-1]
+    xs = [_rand((P,), dtype, g) for _ in range(K)]
+    counts = [int(v) for v in torch.randint(50, 601, (K,), generator=g)]
+    coef = [c / sum(counts) for c in counts] if mode == MUL_W else counts
+    div = float(sum(counts))
+    gcoef = [0.3, 1.7, 2.0, 0.01] if gmode == MUL_W else [11, 7, 3, 5]
+    gdiv = [26.0, 26.0, 13.0, 7.0]
+    terms = []
+    for j in range(len(gptr) - 1):
+        Gj = orc.weighted_sum(xs[gptr[j]:gptr[j + 1]], mode, coef[gptr[j]:gptr[j + 1]], div)
+        if gmode == SUM:
+            terms.append(Gj)
+        elif gmode == MUL_W:
+            terms.append(orc.weighted_sum([Gj], MUL_W, [gcoef[j]]))
+        else:
+            terms.append(orc.weighted_sum([Gj], MUL_N_DIV_N, [gcoef[j]], gdiv[j]))
+    exp = orc.weighted_sum(terms, SUM)
+    got = eng.weighted_sum_grouped([x.cuda() for x in xs], mode, coef, div, gptr, gmode,
+                                   gcoef if gmode != SUM else None, gdiv if gmode == MUL_N_DIV_N else None)
+    assert bits_equal(got.cpu(), exp)
