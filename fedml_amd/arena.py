@@ -166,9 +166,8 @@ class ClientArena:
         outs: Dict[torch.dtype, torch.Tensor] = {}
         for dt, buf in self.bufs.items():
             odt = out_dtype(dt, mode)
-            o = out[dt] if out is not None else torch.empty(buf.shape[1], dtype=odt, device=self.device)
-            self.engine.weighted_sum([buf[i] for i in clients], mode, coef, divisor, out=o)
-            outs[dt] = o
+            o = out[dt] if out is not None else None
+            outs[dt] = self.engine.weighted_sum_rows(buf, clients, mode, coef, divisor, out=o)
         res = OrderedDict()
         for k in self.layout.keys:
             dt, off, shape, n = self.layout.where[k]

@@ -133,6 +133,38 @@ class AggEngine:
         N.check(rc, "fa_weighted_sum_multi")
         return results
 
+    def weighted_sum_rows(self, buf: torch.Tensor, rows: Sequence[int], mode: int,
+                          coef: Optional[Sequence[float]] = None, divisor: float = 1.0,
+                          out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """Ordered reduction over rows of ONE 2-D device tensor (a ClientArena dtype group):
+        pointers are computed from the base address, so the host cost is O(1) tensor checks."""
+        if buf.dim() != 2 or not buf.is_contiguous():
+            raise ValueError("weighted_sum_rows: buf must be a contiguous 2-D tensor")
+        _require_device(buf, self.device, "arena")
+        dt = buf.dtype
+        if dt not in DTYPE_CODE:
+            raise TypeError(f"weighted_sum_rows: unsupported dtype {dt}")
+        k = len(rows)
+        if k == 0:
+            raise ValueError("weighted_sum_rows: no rows")
+        nrow, ncol = buf.shape
+        if min(rows) < 0 or max(rows) >= nrow:
+            raise IndexError("weighted_sum_rows: row out of range")
+        if mode != SUM and (coef is None or len(coef) != k):
+            raise ValueError("weighted_sum_rows: need one coefficient per row")
+        odt = out_dtype(dt, mode)
+        if out is None:
+            out = torch.empty(ncol, dtype=odt, device=self.device)
+        elif out.dtype != odt or out.numel() != ncol:
+            raise ValueError(f"weighted_sum_rows: output must be {odt} with {ncol} elements")
+        _require_device(out, self.device, "output")
+        base, stride = buf.data_ptr(), ncol * buf.element_size()
+        rc = self._lib.fa_weighted_sum(
+            self._ctx, DTYPE_CODE[dt], int(mode), ncol, k, N.ptr_array([base + r * stride for r in rows]),
+            N.f64_array(coef) if coef is not None else None, float(divisor), out.data_ptr(), self._stream(stream))
+        N.check(rc, "fa_weighted_sum")
+        return out
+
     def weighted_sum_grouped(self, xs: Sequence[torch.Tensor], mode: int, coef: Optional[Sequence[float]],
                              divisor: float, group_ptr: Sequence[int], group_mode: int,
                              group_coef: Optional[Sequence[float]] = None,

@@ -32,24 +32,28 @@ __global__ void __launch_bounds__(256) probe_copy(const u32x4* __restrict__ src,
 
 // K separate streams, one 4-KiB tile of each per workgroup (the aggregation kernel's access
 // pattern with the arithmetic removed): isolates the cost of reading 128 streams at once.
-template <int U>
+template <int U, bool WIDE_OUT>
 __global__ void __launch_bounds__(256) probe_multi(const u32x4* const* __restrict__ ptrs, int k, unsigned* out) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  unsigned acc = 0;
+  u32x4 acc = {0, 0, 0, 0};
   for (int i0 = 0; i0 < k; i0 += U) {
     u32x4 r[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) r[u] = __builtin_nontemporal_load((gp)(ptrs[min(i0 + u, k - 1)] + e));
 #pragma unroll
-    for (int u = 0; u < U; ++u) acc ^= r[u][0] ^ r[u][1] ^ r[u][2] ^ r[u][3];
+    for (int u = 0; u < U; ++u) acc ^= r[u];
   }
-  out[e] = acc;
+  if constexpr (WIDE_OUT)  // one 16-B output vector per lane, like the aggregation kernel
+    __builtin_nontemporal_store(acc, (__attribute__((address_space(1))) u32x4*)((u32x4*)out + e));
+  else
+    out[e] = acc[0] ^ acc[1] ^ acc[2] ^ acc[3];
 }
 
 extern "C" int hbm_probe_multi(const void* dptrs, int k, int64_t bytes_per_stream, void* out, int unroll, void* stream) {
   const int64_t tiles = bytes_per_stream / (16 * 256);
-  if (unroll == 16) hipLaunchKernelGGL(probe_multi<16>, dim3(tiles), dim3(256), 0, (hipStream_t)stream, (const u32x4* const*)dptrs, k, (unsigned*)out);
-  else hipLaunchKernelGGL(probe_multi<8>, dim3(tiles), dim3(256), 0, (hipStream_t)stream, (const u32x4* const*)dptrs, k, (unsigned*)out);
+  if (unroll == 16) hipLaunchKernelGGL((probe_multi<16, false>), dim3(tiles), dim3(256), 0, (hipStream_t)stream, (const u32x4* const*)dptrs, k, (unsigned*)out);
+  else if (unroll == -8) hipLaunchKernelGGL((probe_multi<8, true>), dim3(tiles), dim3(256), 0, (hipStream_t)stream, (const u32x4* const*)dptrs, k, (unsigned*)out);
+  else hipLaunchKernelGGL((probe_multi<8, false>), dim3(tiles), dim3(256), 0, (hipStream_t)stream, (const u32x4* const*)dptrs, k, (unsigned*)out);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

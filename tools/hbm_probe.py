@@ -39,6 +39,22 @@ for k in (8, 32, 128):
     for u in (8, 16):
         t = timeit(lambda: L.hbm_probe_multi(ptrs.data_ptr(), k, per, out.data_ptr(), u, s))
         res[f"multi_k{k}_u{u}_GBs"] = round(k * per / t / 1e9, 1)
+# the metric's shape: 128 streams x 500 MB in ONE 64 GB allocation, with and without a 16-B/lane output
+if os.environ.get("PROBE_BIG", "1") == "1":
+    del src
+    torch.cuda.empty_cache()
+    kb, pb = 128, 125_000_000 * 4
+    big = torch.empty(kb * pb // 4, dtype=torch.float32, device="cuda").normal_()
+    ptrs = torch.tensor([big.data_ptr() + i * pb for i in range(kb)], dtype=torch.int64, device="cuda")
+    outw = torch.empty(pb // 4, dtype=torch.float32, device="cuda")
+    for u, tag in ((8, "xor"), (-8, "wide_out")):
+        t = timeit(lambda: L.hbm_probe_multi(ptrs.data_ptr(), kb, pb, outw.data_ptr(), u, s), reps=5)
+        res[f"metric_shape_k128_500MB_{tag}_GBs"] = round(kb * pb / t / 1e9, 1)
+        if u < 0:
+            res[f"metric_shape_k128_500MB_{tag}_incl_write_GBs"] = round((kb + 1) * pb / t / 1e9, 1)
+    del big, outw
+    torch.cuda.empty_cache()
+    src = torch.empty(GB // 4, dtype=torch.float32, device="cuda").normal_()
 # 128 SEPARATE allocations (how bench.py lays out the clients)
 k, per = 128, (GB // 2 // 128) // 4096 * 4096
 sep = [torch.empty(per // 4, dtype=torch.float32, device="cuda").normal_() for _ in range(k)]
