@@ -692,18 +692,6 @@ int elems_per_vec(int dtype) {
     default: return 0;
   }
 }
-size_t in_bytes(int dtype) {
-  switch (dtype) {
-    case FA_DTYPE_F32: return 4;
-    case FA_DTYPE_BF16: case FA_DTYPE_F16: return 2;
-    default: return 8;
-  }
-}
-size_t out_bytes(int dtype, int mode) {
-  if (dtype == FA_DTYPE_I64) return mode == FA_MODE_SUM ? 8 : 4;
-  return in_bytes(dtype);
-}
-
 inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 }  // namespace
@@ -816,7 +804,6 @@ int fa_weighted_sum_multi(fa_ctx* ctx, int dtype, int mode, int32_t num_segments
   for (int i = 0; i < k; ++i) hc[i] = coef ? coef[i] : 0.0;
   int j = 0;
   int64_t t0 = 0;
-  const size_t ib = in_bytes(dtype), ob = out_bytes(dtype, mode);
   for (int s = 0; s < num_segments; ++s) {
     const int64_t n = seg_numel[s];
     if (n == 0) continue;
@@ -826,7 +813,6 @@ int fa_weighted_sum_multi(fa_ctx* ctx, int dtype, int mode, int32_t num_segments
       hp[(int64_t)j * k + i] = p;
       aligned = aligned && al16(p);
     }
-    (void)ib; (void)ob;
     hs[j] = Seg{n, t0, d_out[s], j * k, aligned ? 1 : 0};
     t0 += (n + tile_elems - 1) / tile_elems;
     ++j;
