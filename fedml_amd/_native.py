@@ -27,7 +27,7 @@ FA_OK, FA_ERR_INVALID, FA_ERR_DTYPE, FA_ERR_HIP, FA_ERR_NOMEM = 0, -1, -2, -3, -
 
 EXPORTED_SYMBOLS = (
     "fa_abi_version", "fa_ctx_create", "fa_ctx_destroy", "fa_weighted_sum",
-    "fa_weighted_sum_multi", "fa_weighted_sum_grouped", "fa_mix", "fa_ctx_set_variant", "fa_strerror", "fa_last_error",
+    "fa_weighted_sum_multi", "fa_weighted_sum_grouped", "fa_mix", "fa_ctx_set_variant", "fa_ctx_set_mix_band", "fa_strerror", "fa_last_error",
 )
 
 
@@ -54,6 +54,8 @@ def _declare(L):
     L.fa_ctx_destroy.argtypes = [_vp]
     L.fa_ctx_set_variant.restype = ctypes.c_int
     L.fa_ctx_set_variant.argtypes = [_vp, ctypes.c_int]
+    L.fa_ctx_set_mix_band.restype = ctypes.c_int
+    L.fa_ctx_set_mix_band.argtypes = [_vp, ctypes.c_int]
     L.fa_weighted_sum.restype = ctypes.c_int
     L.fa_weighted_sum.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int32,
                                   _P_vp, _P_d, ctypes.c_double, _vp, _vp]

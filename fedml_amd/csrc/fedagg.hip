@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <climits>
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
@@ -547,6 +548,103 @@ k_mix(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict__ co
 }
 
 // --------------------------------------------------------------------------------------------
+// Banded mixing (ring-like gossip): every entry of row r reads input (r + off + d) mod num_in with
+// d in {-1, 0, +1} (host-checked).  Rows are walked in order with a register sliding window over
+// the inputs, so each input tile is loaded ONCE per workgroup (k_mix re-reads neighbours through
+// L2/MALL: +8 % HBM traffic at 256 nodes).  Per group of RG rows the RG new window slots are loaded
+// together; each CSR entry picks its slot by a wave-uniform switch (scalar branches, no VALU select),
+// so the accumulation order is still the CSR order, bit for bit.
+template <int DT, int RG, bool POST>
+__global__ void __launch_bounds__(kBlock)
+k_mix_band(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict__ cols,
+           const double* __restrict__ vals, const void* const* __restrict__ in, int num_in, int off,
+           int64_t n) {
+  using T = Tr<DT, FA_MODE_MUL_W>;
+  constexpr int V = T::V;
+  constexpr int64_t TILE = (int64_t)kBlock * V;
+  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const float dz = 0.f;
+  auto wrap = [num_in](int c) { c %= num_in; return c < 0 ? c + num_in : c; };
+
+  if (base + TILE <= n) {
+    const int64_t e0 = base + (int64_t)threadIdx.x * V;
+    const int64_t boff = e0 * T::IN_BYTES;
+    u32x4 win[RG + 2];  // win[s] = input (r0 + off - 1 + s) mod num_in
+    win[0] = ld16<false>((const char*)in[wrap(off - 1)] + boff);
+    win[1] = ld16<false>((const char*)in[wrap(off)] + boff);
+    for (int r0 = 0; r0 < nrows; r0 += RG) {
+#pragma unroll
+      for (int g = 0; g < RG; ++g) win[2 + g] = ld16<false>((const char*)in[wrap(r0 + off + 1 + g)] + boff);
+#pragma unroll
+      for (int g = 0; g < RG; ++g) {
+        if (r0 + g < nrows) {  // wave-uniform
+          const MixRow row = rows[r0 + g];
+          float acc[V];
+#pragma unroll
+          for (int v = 0; v < V; ++v) acc[v] = -0.0f;
+          for (int j = row.begin; j < row.end; ++j) {
+            const int rel = wrap(cols[j] - (r0 + g + off) + 1);  // 0, 1 or 2 (host-checked)
+            const float c = (float)vals[j];
+            float x[V];
+            if (rel == 0) T::unpack(win[g], x);
+            else if (rel == 1) T::unpack(win[g + 1], x);
+            else T::unpack(win[g + 2], x);
+#pragma unroll
+            for (int v = 0; v < V; ++v)
+              acc[v] = accum<DT, FA_MODE_MUL_W>(acc[v], term<DT, FA_MODE_MUL_W>(x[v], c, dz));
+          }
+          T::stv((char*)row.out + e0 * T::OUT_BYTES, acc);
+          if constexpr (POST) {
+            const float sc = (float)row.scale;
+#pragma unroll
+            for (int v = 0; v < V; ++v) acc[v] = T::rnd(op_mul(acc[v], sc));
+            T::stv((char*)row.out2 + e0 * T::OUT_BYTES, acc);
+          }
+        }
+      }
+      win[0] = win[RG];
+      win[1] = win[RG + 1];
+    }
+  } else {
+    const int64_t end = min(base + TILE, n);
+    for (int r = 0; r < nrows; ++r) {
+      const MixRow row = rows[r];
+      for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
+        float acc = -0.0f;
+        for (int j = row.begin; j < row.end; ++j)
+          acc = accum<DT, FA_MODE_MUL_W>(
+              acc, term<DT, FA_MODE_MUL_W>(T::ld1(in[cols[j]], e), (float)vals[j], dz));
+        T::st1(row.out, e, acc);
+        if constexpr (POST) T::st1(row.out2, e, T::rnd(op_mul(acc, (float)row.scale)));
+      }
+    }
+  }
+}
+
+// The band offset `off` for which every entry of row r is input (r + off + {-1,0,1}) mod num_in,
+// or INT_MIN if the CSR is not banded that way.
+int band_offset(int32_t rows, const int32_t* row_ptr, const int32_t* cols, int32_t num_in) {
+  if (rows <= 0 || num_in < 3) return INT32_MIN;
+  auto md = [num_in](int x) { x %= num_in; return x < 0 ? x + num_in : x; };
+  int cand[3];
+  int nc = 0;
+  if (row_ptr[1] <= row_ptr[0]) return INT32_MIN;
+  const int c0 = cols[row_ptr[0]];
+  for (int d = -1; d <= 1; ++d) cand[nc++] = md(c0 - d);  // row 0: off in {c0+1, c0, c0-1}
+  for (int ci = 0; ci < nc; ++ci) {
+    const int off = cand[ci];
+    bool ok = true;
+    for (int r = 0; r < rows && ok; ++r)
+      for (int j = row_ptr[r]; j < row_ptr[r + 1] && ok; ++j) {
+        const int rel = md(cols[j] - (r + off) + 1);
+        ok = rel <= 2;
+      }
+    if (ok) return off;
+  }
+  return INT32_MIN;
+}
+
+// --------------------------------------------------------------------------------------------
 // Host side: error reporting, context, staging.
 thread_local char g_last_error[512] = "";
 
@@ -583,7 +681,8 @@ inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
 
 struct fa_ctx {
   int device = 0;
-  int variant = 0;  // kernel tuning variant (results identical for every variant)
+  int variant = 0;      // kernel tuning variant (results identical for every variant)
+  bool mix_band = true;  // banded (sliding-window) mixing kernel when the CSR allows it
   struct Slot {
     void* host = nullptr;
     void* dev = nullptr;
@@ -754,6 +853,13 @@ int fa_ctx_set_variant(fa_ctx* c, int variant) {
   if (!c || variant < 0 || variant >= kNumVariants)
     return fail(FA_ERR_INVALID, "fa_ctx_set_variant: variant must be in [0, %d)", kNumVariants);
   c->variant = variant;
+  return FA_OK;
+}
+
+// Tuning knob (not part of the arithmetic contract): 0 disables the banded mixing kernel.
+int fa_ctx_set_mix_band(fa_ctx* c, int enable) {
+  if (!c) return fail(FA_ERR_INVALID, "fa_ctx_set_mix_band: ctx is NULL");
+  c->mix_band = enable != 0;
   return FA_OK;
 }
 
@@ -977,6 +1083,22 @@ int fa_mix(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_p
   const int al = aligned ? 1 : 0;
   int maxdeg = 0;
   for (int r = 0; r < rows; ++r) maxdeg = std::max(maxdeg, row_ptr[r + 1] - row_ptr[r]);
+  const int band = (aligned && ctx->mix_band) ? band_offset(rows, row_ptr, cols, num_in) : INT32_MIN;
+  if (band != INT32_MIN) {
+#define FA_BAND(DT)                                                                                   \
+  if (post_scale)                                                                                     \
+    hipLaunchKernelGGL((k_mix_band<DT, 8, true>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, num_in, band, n); \
+  else                                                                                                \
+    hipLaunchKernelGGL((k_mix_band<DT, 8, false>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, num_in, band, n);
+    switch (dtype) {
+      case FA_DTYPE_F32: FA_BAND(FA_DTYPE_F32); break;
+      case FA_DTYPE_BF16: FA_BAND(FA_DTYPE_BF16); break;
+      case FA_DTYPE_F16: FA_BAND(FA_DTYPE_F16); break;
+    }
+#undef FA_BAND
+    FA_HIP(hipGetLastError());
+    return release(slot, st);
+  }
   // shape by row degree: ring-like (<= 3 entries), up to 4, or dense rows in passes of 8
 #define FA_MIX_SHAPE(DT, RG, MAXD)                                                                     \
   if (post_scale)                                                                                      \

@@ -83,9 +83,15 @@ class DistributedGossip:
             for i in idxs:
                 ops.append(dist.P2POp(dist.isend, local_models[self.mine.index(i)], r, self.group))
         reqs = dist.batch_isend_irecv(ops) if ops else []
-        inputs = list(local_models) + [halo[i] for i in self.halo_in]
-        index = {node: k for k, node in enumerate(self.mine)}
-        index.update({node: len(self.mine) + k for k, node in enumerate(self.halo_in)})
+        # inputs in ring order around this rank's block (left halo, own nodes, right halo): for a
+        # banded W the mixing rows then read inputs (row + const + {-1, 0, 1}) and take the
+        # sliding-window kernel
+        half = self.n // 2
+        nodes = sorted(list(self.mine) + list(self.halo_in), key=lambda v: (v - self.mine[0] + half) % self.n)
+        tensor_of = {node: local_models[k] for k, node in enumerate(self.mine)}
+        tensor_of.update(halo)
+        inputs = [tensor_of[v] for v in nodes]
+        index = {v: k for k, v in enumerate(nodes)}
         outs = [torch.empty_like(proto) for _ in self.mine]
         outs2 = [torch.empty_like(proto) for _ in self.mine] if post_scale is not None else None
 

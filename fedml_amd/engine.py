@@ -78,6 +78,9 @@ class AggEngine:
     def set_variant(self, variant: int):
         N.check(self._lib.fa_ctx_set_variant(self._ctx, int(variant)), "fa_ctx_set_variant")
 
+    def set_mix_band(self, enable: bool):
+        N.check(self._lib.fa_ctx_set_mix_band(self._ctx, int(bool(enable))), "fa_ctx_set_mix_band")
+
     def _stream(self, stream=None):
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         return N.ctypes.c_void_p(s.cuda_stream)

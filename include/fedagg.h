@@ -145,6 +145,9 @@ int fa_mix(fa_ctx *ctx, int dtype, int64_t n, int32_t rows, const int32_t *row_p
  * kernel's shape -- U clients per load group, S 16-byte vectors per lane, load cache policy,
  * double-buffered group prefetch.  0 = default; valid range [0, 9). */
 int fa_ctx_set_variant(fa_ctx *ctx, int variant);
+/* Performance tuning only: 0 disables the banded sliding-window mixing kernel (fa_mix then always
+ * uses the general CSR kernel); default 1. */
+int fa_ctx_set_mix_band(fa_ctx *ctx, int enable);
 
 /* Static name of a status code. */
 const char *fa_strerror(int code);

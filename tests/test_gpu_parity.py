@@ -230,3 +230,39 @@ def test_grouped_two_level_vs_oracle(eng, dtype, mode, gmode, P):
     got = eng.weighted_sum_grouped([x.cuda() for x in xs], mode, coef, div, gptr, gmode,
                                    gcoef if gmode != SUM else None, gdiv if gmode == MUL_N_DIV_N else None)
     assert bits_equal(got.cpu(), exp)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16], ids=str)
+@pytest.mark.parametrize("layout", ["ring", "halo"])
+def test_banded_mix_kernel_equals_general(dtype, layout):
+    """The sliding-window (banded) mixing kernel == the general CSR kernel == the oracle."""
+    from oracle import orc
+    from fedml_amd.engine import AggEngine
+    from fedml_amd.core.distributed.topology.topology_manager import SymmetricTopologyManager, gossip_rows
+    n = 37
+    m = SymmetricTopologyManager(n, 2)
+    m.generate_topology()
+    g = torch.Generator().manual_seed(11)
+    xs = [_rand((50_003,), dtype, g) for _ in range(n)]
+    rp, cs, vs = gossip_rows(m.topology)
+    if layout == "halo":  # rows 5..20 with inputs ordered [left halo, own, right halo] (distributed)
+        rows = list(range(5, 21))
+        rp, cs, vs = gossip_rows(m.topology, rows)
+        order = list(range(4, 22))
+        pos = {v: k for k, v in enumerate(order)}
+        cs = [pos[c] for c in cs]
+        xs = [xs[v] for v in order]
+    scale = [1.0 + 0.5 * i for i in range(len(rp) - 1)]
+    exp, exp2 = orc.mix(xs, rp, cs, vs, post_scale=scale)
+    outs = {}
+    for band in (True, False):
+        eng = AggEngine(0)
+        try:
+            eng.set_mix_band(band)
+            o, o2 = eng.mix([x.cuda() for x in xs], rp, cs, vs, post_scale=scale)
+            outs[band] = ([t.cpu() for t in o], [t.cpu() for t in o2])
+        finally:
+            eng.close()
+    for band in (True, False):
+        for a, b in zip(outs[band][0] + outs[band][1], exp + exp2):
+            assert bits_equal(a, b), band
