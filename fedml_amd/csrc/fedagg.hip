@@ -459,6 +459,80 @@ k_wsum_grouped(const Seg* __restrict__ segs, const double* __restrict__ coef,
 }
 
 // --------------------------------------------------------------------------------------------
+// FedOpt server step fused into the aggregation (simulation/mpi/fedopt/FedOptAggregator.py:
+// 104-131): per element the FedAvg average (ordered, in registers), the pseudo-gradient
+// g = param - avg, and torch.optim.SGD's update of the global parameter and its momentum buffer,
+// in place.  The reference runs FedAvg, a state_dict round trip and a CPU optimizer step; PyTorch's
+// CPU add(alpha) is a fused multiply-add, so every `x + a*y` here is one __fmaf_rn (pinned by the
+// g10 fixtures).  fp32 parameters; segments = parameter tensors (Seg.out = the parameter).
+enum { SGD_MOMENTUM = 1, SGD_NESTEROV = 2, SGD_WD = 4, SGD_FIRST = 8 };
+
+__device__ __forceinline__ float sgd_update(float p, float avg, float& buf, float neg_lr, float mom,
+                                            float damp1, float wd, int flags) {
+  float g = __fsub_rn(p, avg);
+  if (flags & SGD_WD) g = __fmaf_rn(p, wd, g);
+  if (flags & SGD_MOMENTUM) {
+    buf = (flags & SGD_FIRST) ? g : __fmaf_rn(g, damp1, __fmul_rn(buf, mom));
+    g = (flags & SGD_NESTEROV) ? __fmaf_rn(buf, mom, g) : buf;
+  }
+  return __fmaf_rn(g, neg_lr, p);
+}
+
+template <int U, bool NT>
+__global__ void __launch_bounds__(kBlock)
+k_fedavg_sgd(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
+             const void* const* __restrict__ ptrs, int k, void* const* __restrict__ bufs, float neg_lr,
+             float mom, float damp1, float wd, int flags) {
+  using B = WsumBody<FA_DTYPE_F32, FA_MODE_MUL_W, U, 1, NT>;
+  using T = typename B::T;
+  constexpr int V = T::V;
+  constexpr int64_t TILE = (int64_t)kBlock * V;
+  const int64_t tile = blockIdx.x;
+  const int s = nseg > 1 ? find_seg(segs, nseg, tile) : 0;
+  const Seg sg = segs[s];
+  float* param = (float*)sg.out;
+  float* mbuf = (float*)bufs[s];
+  const int64_t base = (tile - sg.tile_start) * TILE;
+  const void* const* in = ptrs + sg.ptr_base;
+  const float d = 0.f;
+
+  if (sg.aligned && base + TILE <= sg.numel) {
+    const int64_t e0 = base + (int64_t)threadIdx.x * V;
+    const int64_t boff = e0 * 4;
+    float acc[1][V];
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[0][v] = -0.0f;
+    for (int i0 = 0; i0 < k; i0 += U) {
+      u32x4 r[U][1];
+      B::load(r, in, i0, k, boff);
+      B::template consume<true>(acc, r, coef, i0, k, d);
+    }
+    u32x4 p4 = *(const u32x4*)(param + e0);
+    u32x4 b4 = {0, 0, 0, 0};
+    if ((flags & SGD_MOMENTUM) && !(flags & SGD_FIRST)) b4 = *(const u32x4*)(mbuf + e0);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      float b = __uint_as_float(b4[v]);
+      p4[v] = __float_as_uint(sgd_update(__uint_as_float(p4[v]), acc[0][v], b, neg_lr, mom, damp1, wd, flags));
+      b4[v] = __float_as_uint(b);
+    }
+    *(u32x4*)(param + e0) = p4;
+    if (flags & SGD_MOMENTUM) *(u32x4*)(mbuf + e0) = b4;
+  } else {
+    const int64_t end = min(base + TILE, sg.numel);
+    for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
+      float acc = -0.0f;
+      for (int i = 0; i < k; ++i)
+        acc = accum<FA_DTYPE_F32, FA_MODE_MUL_W>(
+            acc, term<FA_DTYPE_F32, FA_MODE_MUL_W>(T::ld1(in[i], e), T::coef(coef[i]), d));
+      float b = ((flags & SGD_MOMENTUM) && !(flags & SGD_FIRST)) ? mbuf[e] : 0.f;
+      param[e] = sgd_update(param[e], acc, b, neg_lr, mom, damp1, wd, flags);
+      if (flags & SGD_MOMENTUM) mbuf[e] = b;
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------------
 // Mixing / gossip kernel: one workgroup = one element tile, looping over every output row so that
 // an input shared by neighbouring rows is re-read from L2 / Infinity Cache, not HBM.  Rows go in
 // groups of RG: the loads of all RG rows (up to MAXD entries each, clamped like k_wsum) are issued
@@ -1020,6 +1094,76 @@ int fa_weighted_sum_grouped(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t
   }
 #undef FA_G_MODES
 #undef FA_G
+  FA_HIP(hipGetLastError());
+  return release(slot, st);
+}
+
+int fa_fedavg_sgd(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, int32_t k,
+                  const void* const* d_in, const double* coef, void* const* d_param, void* const* d_momentum,
+                  double lr, double momentum, double dampening, double weight_decay, int nesterov,
+                  int first_step, void* hip_stream) {
+  if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (k <= 0 || num_segments <= 0 || !seg_numel || !d_in || !coef || !d_param)
+    return fail(FA_ERR_INVALID, "fa_fedavg_sgd: invalid arguments");
+  if (momentum != 0.0 && !d_momentum) return fail(FA_ERR_INVALID, "fa_fedavg_sgd: momentum buffers are NULL");
+  if (nesterov && (momentum <= 0.0 || dampening != 0.0))
+    return fail(FA_ERR_INVALID, "fa_fedavg_sgd: nesterov needs momentum > 0 and dampening 0 (torch.optim.SGD)");
+  const int64_t tile_elems = (int64_t)kBlock * 4;
+  int nseg = 0;
+  int64_t tiles = 0;
+  for (int s = 0; s < num_segments; ++s) {
+    if (seg_numel[s] < 0) return fail(FA_ERR_INVALID, "segment %d has negative numel", s);
+    if (seg_numel[s] == 0) continue;
+    if (!d_param[s] || (momentum != 0.0 && !d_momentum[s])) return fail(FA_ERR_INVALID, "segment %d: NULL", s);
+    for (int i = 0; i < k; ++i)
+      if (!d_in[(int64_t)s * k + i]) return fail(FA_ERR_INVALID, "segment %d client %d: input NULL", s, i);
+    ++nseg;
+    tiles += (seg_numel[s] + tile_elems - 1) / tile_elems;
+  }
+  if (nseg == 0) return FA_OK;
+  if (tiles > 0x7FFFFFFFll) return fail(FA_ERR_INVALID, "too many tiles");
+  const size_t seg_bytes = align16(sizeof(Seg) * nseg);
+  const size_t coef_bytes = align16(sizeof(double) * k);
+  const size_t buf_bytes = align16(sizeof(void*) * nseg);
+  const size_t ptr_bytes = sizeof(void*) * (size_t)nseg * k;
+  const size_t bytes = seg_bytes + coef_bytes + buf_bytes + ptr_bytes;
+  DeviceGuard g(ctx->device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
+  hipStream_t st = (hipStream_t)hip_stream;
+  fa_ctx::Slot* slot = nullptr;
+  int rc = acquire_slot(ctx, bytes, &slot);
+  if (rc) return rc;
+  char* h = (char*)slot->host;
+  Seg* hs = (Seg*)h;
+  double* hc = (double*)(h + seg_bytes);
+  void** hb = (void**)(h + seg_bytes + coef_bytes);
+  const void** hp = (const void**)(h + seg_bytes + coef_bytes + buf_bytes);
+  for (int i = 0; i < k; ++i) hc[i] = coef[i];
+  int j = 0;
+  int64_t t0 = 0;
+  for (int s = 0; s < num_segments; ++s) {
+    const int64_t n = seg_numel[s];
+    if (n == 0) continue;
+    bool aligned = al16(d_param[s]) && (momentum == 0.0 || al16(d_momentum[s]));
+    for (int i = 0; i < k; ++i) {
+      const void* p = d_in[(int64_t)s * k + i];
+      hp[(int64_t)j * k + i] = p;
+      aligned = aligned && al16(p);
+    }
+    hs[j] = Seg{n, t0, d_param[s], j * k, aligned ? 1 : 0};
+    hb[j] = momentum != 0.0 ? d_momentum[s] : d_param[s];  // never dereferenced without momentum
+    t0 += (n + tile_elems - 1) / tile_elems;
+    ++j;
+  }
+  rc = stage(slot, bytes, st);
+  if (rc) return rc;
+  char* dv = (char*)slot->dev;
+  const int flags = (momentum != 0.0 ? SGD_MOMENTUM : 0) | (nesterov ? SGD_NESTEROV : 0) |
+                    (weight_decay != 0.0 ? SGD_WD : 0) | (first_step ? SGD_FIRST : 0);
+  hipLaunchKernelGGL((k_fedavg_sgd<8, true>), dim3((unsigned)tiles), dim3(kBlock), 0, st, (const Seg*)dv, nseg,
+                     (const double*)(dv + seg_bytes), (const void* const*)(dv + seg_bytes + coef_bytes + buf_bytes), k,
+                     (void* const*)(dv + seg_bytes + coef_bytes), (float)(-lr), (float)momentum,
+                     (float)(1.0 - dampening), (float)weight_decay, flags);
   FA_HIP(hipGetLastError());
   return release(slot, st);
 }

@@ -198,6 +198,46 @@ class AggEngine:
         N.check(rc, "fa_weighted_sum_grouped")
         return out
 
+    def fedavg_sgd(self, segments: Sequence[Sequence[torch.Tensor]], coef: Sequence[float],
+                   params: Sequence[torch.Tensor], momentum_bufs: Optional[Sequence[torch.Tensor]],
+                   lr: float, momentum: float = 0.0, dampening: float = 0.0, weight_decay: float = 0.0,
+                   nesterov: bool = False, first_step: bool = True, stream=None) -> None:
+        """FedAvg + torch.optim.SGD server step in one pass (fa_fedavg_sgd); params and momentum
+        buffers (fp32, contiguous, on this device) are updated in place."""
+        k = len(segments[0]) if segments else 0
+        if k == 0:
+            raise ValueError("fedavg_sgd: no client tensors")
+        if len(coef) != k or len(params) != len(segments):
+            raise ValueError("fedavg_sgd: one coefficient per client and one parameter per segment")
+        in_ptrs, numels = [], []
+        for s, (seg, p) in enumerate(zip(segments, params)):
+            if p.dtype != torch.float32:
+                raise TypeError(f"fedavg_sgd: parameter {s} is {p.dtype} (float32 only)")
+            _require_device(p, self.device, f"parameter {s}")
+            if len(seg) != k:
+                raise ValueError(f"segment {s}: {len(seg)} clients, expected {k}")
+            for i, t in enumerate(seg):
+                if t.dtype != torch.float32 or t.shape != p.shape:
+                    raise ValueError(f"segment {s} client {i}: must be float32 of shape {tuple(p.shape)}")
+                _require_device(t, self.device, f"segment {s} client {i}")
+                in_ptrs.append(t.data_ptr())
+            numels.append(p.numel())
+        if momentum != 0.0:
+            if momentum_bufs is None or len(momentum_bufs) != len(params):
+                raise ValueError("fedavg_sgd: momentum needs one buffer per parameter")
+            for b, p in zip(momentum_bufs, params):
+                if b.dtype != torch.float32 or b.shape != p.shape:
+                    raise ValueError("fedavg_sgd: momentum buffer dtype/shape mismatch")
+                _require_device(b, self.device, "momentum buffer")
+            mptr = N.ptr_array([b.data_ptr() for b in momentum_bufs])
+        else:
+            mptr = None
+        rc = self._lib.fa_fedavg_sgd(
+            self._ctx, len(params), N.i64_array(numels), k, N.ptr_array(in_ptrs), N.f64_array(coef),
+            N.ptr_array([p.data_ptr() for p in params]), mptr, float(lr), float(momentum), float(dampening),
+            float(weight_decay), int(bool(nesterov)), int(bool(first_step)), self._stream(stream))
+        N.check(rc, "fa_fedavg_sgd")
+
     def weighted_sum_table(self, dtype_code: int, mode: int, seg_numel: torch.Tensor, k: int,
                            in_ptrs: torch.Tensor, out_ptrs: torch.Tensor, coef: Optional[Sequence[float]] = None,
                            divisor: float = 1.0, stream=None) -> None:

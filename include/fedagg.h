@@ -130,6 +130,25 @@ int fa_weighted_sum_grouped(fa_ctx *ctx, int dtype, int mode, int64_t n, int32_t
                             void *hip_stream);
 
 /*
+ * FedOpt server step fused into the FedAvg pass (simulation/mpi/fedopt/FedOptAggregator.py:
+ * 104-131 with server_optimizer = "sgd"): for every parameter tensor s (fp32) and element e,
+ *   avg   = FedAvg of the clients (fa_weighted_sum MUL_W arithmetic, coef[i] = n_i / N)
+ *   g     = param - avg                          (the reference's pseudo-gradient)
+ *   g     = fma(param, weight_decay, g)          if weight_decay != 0
+ *   m     = g (first_step) | fma(g, 1 - dampening, op(m * momentum))     if momentum != 0
+ *   g     = nesterov ? fma(m, momentum, g) : m   if momentum != 0
+ *   param = fma(g, -lr, param)
+ * torch.optim.SGD semantics on CPU tensors (its add(alpha) is a fused multiply-add).  d_param[s]
+ * and d_momentum[s] are updated IN PLACE; d_momentum may be NULL when momentum == 0.  Layout of
+ * d_in as in fa_weighted_sum_multi.  Buffers that are not parameters (BatchNorm statistics) take
+ * the plain average: aggregate them with fa_weighted_sum(_multi).
+ */
+int fa_fedavg_sgd(fa_ctx *ctx, int32_t num_segments, const int64_t *seg_numel, int32_t k,
+                  const void *const *d_in, const double *coef, void *const *d_param,
+                  void *const *d_momentum, double lr, double momentum, double dampening,
+                  double weight_decay, int nesterov, int first_step, void *hip_stream);
+
+/*
  * Mixing / gossip: for every row r < rows, with CSR entries j in [row_ptr[r], row_ptr[r+1]):
  *   d_out[r][e] = ordered MUL_W reduction of d_in[cols[j]][e] * vals[j]   (entry order = CSR order)
  *   if post_scale: d_out2[r][e] = op(d_out[r][e] * post_scale[r])         (PushSum z = x / omega)

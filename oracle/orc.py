@@ -44,6 +44,10 @@ def lib():
                               ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_double),
                               ctypes.POINTER(ctypes.c_void_p)]
         L.orc_mix.restype = ctypes.c_int
+        L.orc_sgd_apply.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                    ctypes.c_int, ctypes.c_int]
+        L.orc_sgd_apply.restype = ctypes.c_int
         L.orc_f32_to_bf16.argtypes = [ctypes.c_float]
         L.orc_f32_to_bf16.restype = ctypes.c_uint16
         L.orc_f32_to_f16.argtypes = [ctypes.c_float]
@@ -90,3 +94,15 @@ def mix(xs, row_ptr, cols, vals, post_scale=None):
     if rc != 0:
         raise RuntimeError(f"orc_mix failed: {rc}")
     return outs, outs2
+
+
+def sgd_apply(avg, param, buf, lr, momentum=0.0, dampening=0.0, weight_decay=0.0, nesterov=False,
+              first_step=True):
+    """In-place FedOpt SGD step on fp32 CPU tensors (see orc_sgd_apply)."""
+    for t in (avg, param) + ((buf,) if buf is not None else ()):
+        assert t.dtype == torch.float32 and t.is_contiguous()
+    rc = lib().orc_sgd_apply(param.numel(), avg.data_ptr(), param.data_ptr(),
+                             buf.data_ptr() if buf is not None else None, float(lr), float(momentum),
+                             float(dampening), float(weight_decay), int(nesterov), int(first_step))
+    if rc != 0:
+        raise RuntimeError(f"orc_sgd_apply failed: {rc}")

@@ -539,6 +539,72 @@ def cases_topology_and_mixing(stm, tu):
                ref="sp/decentralized/client_pushsum.py:111-156"), {"W": W})
 
 
+def cases_fedopt():
+    """§8(f) next #2: FedOpt server step (simulation/mpi/fedopt/FedOptAggregator.py:48-131): FedAvg,
+    pseudo-gradient g = w_global - avg, torch optimizer step on the global parameters; buffers
+    take the average (cast into the buffer's dtype by load_state_dict).  Three rounds so the
+    momentum buffer's first and later updates are both recorded."""
+    for name, sub in [("fedml.simulation", "/simulation"), ("fedml.simulation.mpi", "/simulation/mpi"),
+                      ("fedml.simulation.mpi.fedopt", "/simulation/mpi/fedopt")]:
+        _stub_pkg(name, REF + sub)
+    optrepo = importlib.import_module("fedml.simulation.mpi.fedopt.optrepo")
+    g = {"OptRepo": optrepo.OptRepo}
+    rel = "simulation/mpi/fedopt/FedOptAggregator.py"
+    meth = {m: extract_method(rel, "FedOptAggregator", m, g) for m in
+            ("_instantiate_opt", "get_model_params", "get_global_model_params", "set_global_model_params",
+             "add_local_trained_result", "check_whether_all_receive", "aggregate", "set_model_global_grads")}
+
+    for opt_name, lr, mom in (("sgd", 0.7, 0.9), ("sgd", 1.0, 0.0)):
+        torch.manual_seed(5)
+        model = torch.nn.Sequential(torch.nn.Linear(33, 17), torch.nn.BatchNorm1d(17), torch.nn.Linear(17, 5))
+        with torch.no_grad():
+            model[1].running_mean.normal_()
+            model[1].running_var.uniform_(0.5, 2.0)
+        init = OrderedDict((k, v.clone()) for k, v in model.state_dict().items())
+
+        class Agg:  # the server_aggregator the FedOpt aggregator wraps (default_aggregator.py:17-23)
+            def __init__(self, m):
+                self.model = m
+
+            def get_model_params(self):
+                return self.model.state_dict()
+
+            def set_model_params(self, p):
+                self.model.load_state_dict(p)
+
+        W = 4
+        self_ = types.SimpleNamespace(aggregator=Agg(model), worker_num=W, model_dict={}, sample_num_dict={},
+                                      flag_client_model_uploaded_dict={i: False for i in range(W)},
+                                      args=Args(server_optimizer=opt_name, server_lr=lr, server_momentum=mom))
+        for m, f in meth.items():
+            setattr(self_, m, functools.partial(f, self_))
+        self_.opt = self_._instantiate_opt()
+        arrays, rounds = {}, []
+        for k, v in init.items():
+            arrays[f"init__{k}"] = tensor_to_np(v)
+        for r in range(3):
+            clients = gen_clients(800 + 10 * r + int(mom * 10), W,
+                                  [(k, tuple(v.shape), v.dtype) for k, v in init.items()])
+            n = gen_counts(800 + r, W)
+            for i in range(W):
+                self_.add_local_trained_result(i, dc(clients[i]), n[i])
+                for k in init:
+                    arrays[f"r{r}_x{i}__{k}"] = tensor_to_np(clients[i][k])
+            assert self_.check_whether_all_receive()
+            out = self_.aggregate()
+            for k, v in out.items():
+                arrays[f"r{r}_y__{k}"] = tensor_to_np(v)
+            rounds.append({"n": n})
+        meta = {"name": f"g10_fedopt_{opt_name}_lr{lr}_m{mom}", "kind": "fedopt", "server_optimizer": opt_name,
+                "server_lr": lr, "server_momentum": mom, "rounds": rounds, "keys": list(init.keys()),
+                "dtypes": [dtype_name(v) for v in init.values()],
+                "params": [k for k, _ in model.named_parameters()],
+                "ref": "simulation/mpi/fedopt/FedOptAggregator.py:48-131"}
+        path = os.path.join(HERE, meta["name"] + ".npz")
+        save_case(path, meta, arrays)
+        WRITTEN.append((meta["name"], os.path.getsize(path)))
+
+
 def layouts(ao):
     """Model layouts used by the configs: names/shapes/dtypes only (no weights)."""
     for name, sub in [("fedml.model", "/model"), ("fedml.model.cv", "/model/cv")]:
@@ -580,6 +646,7 @@ def main():
     cases_agg_operator(ao)
     cases_call_sites()
     cases_topology_and_mixing(stm, tu)
+    cases_fedopt()
     layouts(ao)
     total = sum(s for _, s in WRITTEN)
     for name, s in WRITTEN:

@@ -179,3 +179,41 @@ def check_case(engine, meta, arrays, what=""):
     assert len(got) == len(exp), (what, len(got), len(exp))
     for j, (g, e) in enumerate(zip(got, exp)):
         assert_dict_bits(g, e, f"{what}{meta['name']}[{j}]")
+
+
+def fedopt_replay(meta, arrays, weighted_sum, sgd_apply, to_dev=lambda t: t):
+    """Replay a FedOpt fixture: per round FedAvg (weighted_sum), then the SGD server step on the
+    parameters (sgd_apply, in place) and the averaged buffers cast into their dtype.  Returns the
+    list of per-round global state_dicts (CPU)."""
+    from golden_io import np_to_tensor
+    keys, dtypes, params = meta["keys"], meta["dtypes"], set(meta["params"])
+    state = OrderedDict((k, to_dev(np_to_tensor(arrays[f"init__{k}"], dt))) for k, dt in zip(keys, dtypes))
+    bufs = {}
+    outs = []
+    for r, rd in enumerate(meta["rounds"]):
+        n = rd["n"]
+        N = sum(n)
+        W = len(n)
+        new = OrderedDict()
+        for k, dt in zip(keys, dtypes):
+            xs = [to_dev(np_to_tensor(arrays[f"r{r}_x{i}__{k}"], dt)) for i in range(W)]
+            avg = weighted_sum([x.reshape(-1) for x in xs], MUL_W, [v / N for v in n]).reshape(xs[0].shape)
+            if k in params:
+                p = state[k].clone().contiguous()
+                first = k not in bufs
+                if meta["server_momentum"] != 0 and first:
+                    bufs[k] = torch.empty_like(p)
+                sgd_apply(avg.contiguous(), p, bufs.get(k) if meta["server_momentum"] != 0 else None,
+                          meta["server_lr"], meta["server_momentum"], 0.0, 0.0, False, first)
+                new[k] = p
+            else:
+                new[k] = avg.to(state[k].dtype)  # load_state_dict copy_: float -> int64 truncates
+        state = new
+        outs.append(OrderedDict((k, v.cpu()) for k, v in state.items()))
+    return outs
+
+
+def fedopt_expected(meta, arrays):
+    from golden_io import np_to_tensor
+    return [OrderedDict((k, np_to_tensor(arrays[f"r{r}_y__{k}"], dt)) for k, dt in zip(meta["keys"], meta["dtypes"]))
+            for r in range(len(meta["rounds"]))]

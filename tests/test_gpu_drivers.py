@@ -254,3 +254,38 @@ def test_arena_fused_fedavg_seq_golden():
     w = [n[i] / sum(n) for wk in sched for i in wk]
     got = arena.aggregate_grouped(sched, MUL_W, w, 1.0, SUM)
     assert_dict_bits(cpu(got), expected_dicts(meta, arr)[0], "fused fedavg_seq")
+
+
+@pytest.mark.parametrize("name", ["g10_fedopt_sgd_lr0.7_m0.9", "g10_fedopt_sgd_lr1.0_m0.0"])
+@pytest.mark.parametrize("where", ["cuda", "cpu"])
+def test_fedopt_fused_server_step_golden(name, where):
+    """FedOptAggregator (fused FedAvg + SGD step) == the reference's FedOptAggregator, 3 rounds."""
+    from golden_io import np_to_tensor
+    from refcases import fedopt_expected
+    from fedml_amd.simulation.mpi.fedopt_aggregator import FedOptAggregator
+    meta, arr = case(name)
+    model = torch.nn.Sequential(torch.nn.Linear(33, 17), torch.nn.BatchNorm1d(17), torch.nn.Linear(17, 5))
+    model.load_state_dict(OrderedDict((k, np_to_tensor(arr[f"init__{k}"], dt))
+                                      for k, dt in zip(meta["keys"], meta["dtypes"])))
+    model = model.to("cuda:0" if where == "cuda" else "cpu")
+
+    class Agg:
+        def __init__(self, m):
+            self.model = m
+
+        def get_model_params(self):
+            return self.model.state_dict()
+
+        def set_model_params(self, p):
+            self.model.load_state_dict(p)
+
+    args = types.SimpleNamespace(server_optimizer=meta["server_optimizer"], server_lr=meta["server_lr"],
+                                 server_momentum=meta["server_momentum"])
+    fo = FedOptAggregator(worker_num=4, server_aggregator=Agg(model), args=args)
+    for r, (rd, exp) in enumerate(zip(meta["rounds"], fedopt_expected(meta, arr))):
+        for i in range(4):
+            fo.add_local_trained_result(i, OrderedDict((k, np_to_tensor(arr[f"r{r}_x{i}__{k}"], dt))
+                                                       for k, dt in zip(meta["keys"], meta["dtypes"])), rd["n"][i])
+        assert fo.check_whether_all_receive()
+        got = fo.aggregate()
+        assert_dict_bits(cpu(got), exp, f"{name} round {r}")

@@ -266,3 +266,27 @@ def test_banded_mix_kernel_equals_general(dtype, layout):
     for band in (True, False):
         for a, b in zip(outs[band][0] + outs[band][1], exp + exp2):
             assert bits_equal(a, b), band
+
+
+@pytest.mark.parametrize("momentum,dampening,wd,nesterov", [(0.9, 0.0, 0.0, False), (0.0, 0.0, 0.0, False),
+                                                            (0.5, 0.1, 0.01, False), (0.9, 0.0, 0.001, True)])
+@pytest.mark.parametrize("P", [7, 4099, 262_147])
+def test_fedavg_sgd_fused_vs_oracle(eng, momentum, dampening, wd, nesterov, P):
+    """fa_fedavg_sgd == FedAvg then the oracle's torch.optim.SGD step, two consecutive steps."""
+    from oracle import orc
+    g = torch.Generator().manual_seed(P)
+    K = 9
+    xs = [torch.randn(P, generator=g) for _ in range(K)]
+    counts = [int(v) for v in torch.randint(50, 601, (K,), generator=g)]
+    w = [c / sum(counts) for c in counts]
+    p_ref = torch.randn(P, generator=g)
+    b_ref = torch.zeros(P)
+    p_gpu, b_gpu = p_ref.cuda(), torch.zeros(P, device="cuda")
+    for step in range(2):
+        avg = orc.weighted_sum(xs, MUL_W, w)
+        orc.sgd_apply(avg, p_ref, b_ref if momentum else None, 0.3, momentum, dampening, wd, nesterov, step == 0)
+        eng.fedavg_sgd([[x.cuda() for x in xs]], w, [p_gpu], [b_gpu] if momentum else None, 0.3, momentum,
+                       dampening, wd, nesterov, first_step=(step == 0))
+        assert bits_equal(p_gpu.cpu(), p_ref), step
+        if momentum:
+            assert bits_equal(b_gpu.cpu(), b_ref), step

@@ -32,8 +32,11 @@ class _Orc:
     mix = staticmethod(orc.mix)
 
 
-@pytest.mark.parametrize("path", [p for p in CASES if "topologies" not in p],
-                         ids=lambda p: os.path.basename(p)[:-4])
+GENERIC = [p for p in CASES if "topologies" not in p and "fedopt" not in p]
+FEDOPT = [p for p in CASES if "fedopt" in p]
+
+
+@pytest.mark.parametrize("path", GENERIC, ids=lambda p: os.path.basename(p)[:-4])
 def test_c_oracle_matches_golden(path):
     meta, arrays = load_case(path)
     check_case(_Orc, meta, arrays, "c-oracle:")
@@ -101,8 +104,7 @@ def _port_replay(meta, arrays):
     raise ValueError(kind)
 
 
-@pytest.mark.parametrize("path", [p for p in CASES if "topologies" not in p],
-                         ids=lambda p: os.path.basename(p)[:-4])
+@pytest.mark.parametrize("path", GENERIC, ids=lambda p: os.path.basename(p)[:-4])
 def test_torch_port_matches_golden(path):
     meta, arrays = load_case(path)
     got = _port_replay(meta, arrays)
@@ -158,3 +160,13 @@ def test_topologies_fixture_shapes():
         assert W.shape == (256, 256) and W.dtype == np.float32
         assert np.all(W.sum(1) > 0.99)
         assert W[0, 0] == np.float32(1 / 3) and W[0, 255] == np.float32(1 / 3)
+
+
+@pytest.mark.parametrize("path", FEDOPT, ids=lambda p: os.path.basename(p)[:-4])
+def test_c_oracle_fedopt_matches_golden(path):
+    """FedAvg + torch.optim.SGD server step (FedOptAggregator.py:104-131), three rounds."""
+    from refcases import fedopt_expected, fedopt_replay
+    meta, arrays = load_case(path)
+    got = fedopt_replay(meta, arrays, orc.weighted_sum, orc.sgd_apply)
+    for r, (g, e) in enumerate(zip(got, fedopt_expected(meta, arrays))):
+        assert_dict_bits(g, e, f"fedopt round {r}")
