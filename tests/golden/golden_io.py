@@ -45,7 +45,7 @@ def tensor_to_np(t: torch.Tensor) -> np.ndarray:
 def np_to_tensor(a: np.ndarray, dtype_name: str) -> torch.Tensor:
     if dtype_name == "bfloat16":
         return torch.from_numpy(a.view(np.int16).copy()).view(torch.bfloat16)
-    t = torch.from_numpy(np.ascontiguousarray(a).copy())
+    t = torch.from_numpy(np.array(a, copy=True, order="C"))  # keeps 0-d arrays 0-d (ascontiguousarray would not)
     assert t.dtype == _NAME_TO_TORCH[dtype_name], (t.dtype, dtype_name)
     return t
 
