@@ -14,7 +14,7 @@ from refcases import MUL_N_DIV_N, MUL_W, SUM, assert_dict_bits, bits_equal, chec
 
 pytestmark = pytest.mark.gpu
 
-CASES = [p for p in list_cases() if "topologies" not in p]
+CASES = [p for p in list_cases() if "topologies" not in p and "fedopt" not in p]
 
 
 @pytest.fixture(scope="module")
