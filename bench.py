@@ -45,7 +45,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", default="metric", choices=["metric", "resnet18", "vit_bf16", "hier", "gossip", "host"])
+    p.add_argument("--config", default="metric",
+                   choices=["metric", "resnet18", "vit_bf16", "hier", "gossip", "host", "secagg"])
     p.add_argument("--clients", type=int, default=None)
     p.add_argument("--params", type=int, default=None)
     p.add_argument("--variant", type=int, default=0, help="kernel variant (fa_ctx_set_variant)")
@@ -386,6 +387,76 @@ def wl_host(args, eng, rank, world, timer):
                 roofline_note="value includes pageable->pinned packing, H2D over PCIe and the D2H of the result")
 
 
+def wl_secagg(args, eng, rank, world, timer):
+    """§8(f) #4: the LightSecAgg server reconstruction (lsa_fedml_aggregator.py:101-175) for N = K
+    clients (U = N, T = N/2, the reference's setting) with ResNet-18-size models: LCC-decode the
+    aggregate mask from the clients' (U x d/(U-T)) encoded-mask buffer, then sum the K masked int64
+    models, cancel the mask, reduce mod p, dequantize and average -> float32.  The U x U Lagrange
+    coefficients (host, O(U^2) scalars, computed once per active set) are outside the step."""
+    if world > 1:
+        raise SystemExit("secagg config: single GPU (the driver's multi-GPU runs use the metric config)")
+    from fedml_amd.core.mpc.lightsecagg import MOD_END, gen_Lagrange_coeffs
+    K = args.clients or 128
+    P = args.params or RESNET18_P
+    p, q = 2 ** 15 - 19, 10
+    U, T = K, K // 2
+    m = -(-P // (U - T))
+    g = torch.Generator(device="cuda").manual_seed(11)
+    arena = torch.randint(0, p, (K, P), generator=g, dtype=torch.int64, device="cuda")
+    xs = [arena[i] for i in range(K)]
+    F = torch.randint(0, p, (U, m), generator=g, dtype=torch.int64, device="cuda")
+    coef = gen_Lagrange_coeffs(np.arange(U) + K + 1, np.arange(K) + 1, p).tolist()
+    state = {}
+
+    def step():
+        mask = eng.lcc_decode(coef, F, p, P)
+        with timer:
+            _, real = eng.finite_sum([xs], p, MOD_END, masks=[mask], finite=False, q_bits=q, scale=1 / K)
+        state["mask"], state["real"] = mask, real[0]
+
+    def parity():
+        if args.check_samples <= 0:
+            return None
+        from oracle import orc
+        gi = torch.Generator(device="cuda").manual_seed(99)
+        idx = torch.randint(0, P, (args.check_samples,), generator=gi, device="cuda")
+        _, exp = orc.finite_sum([x.index_select(0, idx).cpu() for x in xs], p, MOD_END,
+                                mask=state["mask"].index_select(0, idx).cpu(), q_bits=q, scale=1 / K)
+        ok = torch.equal(state["real"].index_select(0, idx).cpu().view(torch.int32), exp.view(torch.int32))
+        # the decoded mask: every column of a row block is independent -> check a sampled slice
+        cols = torch.arange(0, min(m, 4096), device="cuda")
+        dec = orc.lcc_decode(torch.tensor(coef, dtype=torch.int64)[: U - T], F[:, cols].cpu(), p, (U - T) * cols.numel())
+        got = state["mask"].reshape(-1)
+        rows_ok = all(torch.equal(got[j * m: j * m + cols.numel()].cpu(), dec[j * cols.numel():(j + 1) * cols.numel()])
+                      for j in range(U - T) if j * m + cols.numel() <= P)
+        return (f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on {args.check_samples} sampled elements; "
+                f"LCC mask {'bit-exact' if rows_ok else 'MISMATCH'} on {cols.numel()} columns x {U - T} rows")
+
+    def cpu(budget_s):
+        from oracle import secagg_port
+        Kc, Pc = K, 1_000_000
+        rng = np.random.RandomState(0)
+        models = [{"w": rng.randint(0, p, size=Pc).astype(np.int64)} for _ in range(Kc)]
+        mask = rng.randint(0, p, size=Pc).astype(np.int64)
+        best, runs, t_end = float("inf"), 0, time.perf_counter() + budget_s
+        while runs < 3 or (time.perf_counter() < t_end and runs < 30):
+            t0 = time.perf_counter()
+            secagg_port.lsa_reconstruct(models, mask, [Pc], p, q)
+            best = min(best, time.perf_counter() - t0)
+            runs += 1
+        return {"value": round((Kc * Pc * 8 + Pc * 8 + Pc * 4) / best / 1e9, 2), "unit": "GB/s", "cores": 1,
+                "kind": "port", "sample": f"K={Kc} x P={Pc} int64 masked models + mask, best of {runs} runs of "
+                                          "oracle/secagg_port.lsa_reconstruct (numpy restatement of "
+                                          "lsa_fedml_aggregator.py:140-166); mask decoding not included"}
+
+    recon = K * P * 8 + P * 8 + P * 4
+    return dict(name=f"lightsecagg_reconstruct_N{K}_P{P}_int64", dtype="int64", step=step, parity=parity,
+                data="synthetic masked finite models uniform in Z_p (p = 2^15-19, q = 10 bits), resident in HBM",
+                bytes_total=recon + U * m * 8 + P * 8, launch_bytes=recon, clients=K, params=P, cpu_K=K, cpu=cpu,
+                roofline_note="dominant kernel = fa_finite_sum (K masked models + mask in, fp32 out); value also "
+                              "counts the LCC mask decoding (U x m int64 in, P int64 out)")
+
+
 # ----------------------------------------------------------------------------- CPU baseline
 def cpu_baseline(K, budget_s):
     """The reference's CPU cost: oracle/torch_port.py (op-for-op restatement of agg_operator.py's
@@ -431,7 +502,7 @@ def main():
         eng.set_variant(args.variant)
     timer = Timed()
     wl = {"metric": wl_metric, "resnet18": wl_layout, "vit_bf16": wl_layout, "hier": wl_hier,
-          "gossip": wl_gossip, "host": wl_host}[args.config](args, eng, rank, world, timer)
+          "gossip": wl_gossip, "host": wl_host, "secagg": wl_secagg}[args.config](args, eng, rank, world, timer)
 
     for _ in range(args.warmup):
         wl["step"]()
@@ -458,7 +529,7 @@ def main():
     parity = wl["parity"]()
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl.get("cpu_K"):
-        cpu = cpu_baseline(wl["cpu_K"], args.cpu_seconds)
+        cpu = wl["cpu"](args.cpu_seconds) if wl.get("cpu") else cpu_baseline(wl["cpu_K"], args.cpu_seconds)
 
     if rank == 0:
         line = {
@@ -473,7 +544,8 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": wl["dtype"],
-            "data": "synthetic N(0,1) client updates (seeds 1000+i), n_i ~ U{50..600} (seed 7); resident in HBM",
+            "data": wl.get("data", "synthetic N(0,1) client updates (seeds 1000+i), n_i ~ U{50..600} (seed 7); "
+                                   "resident in HBM"),
             "config": {"workload": wl["name"], "clients": wl["clients"], "params_per_client": wl["params"],
                        "parallelism": f"client-groups x{world}" +
                                       (f", {args.collective} over RCCL in {args.chunks} chunks" if world > 1 else ""),

@@ -27,8 +27,13 @@ FA_OK, FA_ERR_INVALID, FA_ERR_DTYPE, FA_ERR_HIP, FA_ERR_NOMEM = 0, -1, -2, -3, -
 
 EXPORTED_SYMBOLS = (
     "fa_abi_version", "fa_ctx_create", "fa_ctx_destroy", "fa_weighted_sum",
-    "fa_weighted_sum_multi", "fa_weighted_sum_grouped", "fa_fedavg_sgd", "fa_mix", "fa_ctx_set_variant", "fa_ctx_set_mix_band", "fa_strerror", "fa_last_error",
+    "fa_weighted_sum_multi", "fa_weighted_sum_grouped", "fa_fedavg_sgd", "fa_mix", "fa_ctx_set_variant",
+    "fa_ctx_set_mix_band", "fa_strerror", "fa_last_error",
+    # include/fedagg_finite.h
+    "fa_finite_sum", "fa_finite_quantize", "fa_lcc_decode",
 )
+
+MOD_FIRST, MOD_EACH, MOD_END, REAL_F64 = 1, 2, 4, 8  # enum fa_finite_flags
 
 
 class FedAggNativeError(RuntimeError):
@@ -73,6 +78,15 @@ def _declare(L):
     L.fa_mix.restype = ctypes.c_int
     L.fa_mix.argtypes = [_vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int32, _P_i32, _P_i32, _P_d,
                          ctypes.c_int32, _P_vp, _P_vp, _P_d, _P_vp, _vp]
+    L.fa_finite_sum.restype = ctypes.c_int
+    L.fa_finite_sum.argtypes = [_vp, ctypes.c_int32, _P_i64, ctypes.c_int32, _P_vp, _P_vp, ctypes.c_int64,
+                                ctypes.c_int, _P_vp, ctypes.c_int32, ctypes.c_double, _P_vp, _vp]
+    L.fa_finite_quantize.restype = ctypes.c_int
+    L.fa_finite_quantize.argtypes = [_vp, ctypes.c_int, ctypes.c_int32, _P_i64, _P_vp, _P_vp, ctypes.c_int64,
+                                     ctypes.c_int32, _P_vp, _vp]
+    L.fa_lcc_decode.restype = ctypes.c_int
+    L.fa_lcc_decode.argtypes = [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, _P_i64, _vp, ctypes.c_int64,
+                                ctypes.c_int64, _vp, _vp]
     L.fa_strerror.restype = ctypes.c_char_p
     L.fa_strerror.argtypes = [ctypes.c_int]
     L.fa_last_error.restype = ctypes.c_char_p

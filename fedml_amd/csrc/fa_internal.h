@@ -1,0 +1,93 @@
+// fa_internal.h -- pieces shared by the translation units of libfedagg.so (not part of the ABI):
+// the context with its pinned/device staging slots, error reporting, the segment table.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "fedagg.h"
+
+namespace fa_detail {
+
+constexpr int kBlock = 256;
+constexpr int kSlots = 8;
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+// Device-resident descriptor of one state_dict tensor (staged per call from pinned host memory).
+struct Seg {
+  int64_t numel;
+  int64_t tile_start;  // first tile (workgroup) of this segment
+  void* out;
+  int32_t ptr_base;    // index of client 0's pointer for this segment in the pointer table
+  int32_t aligned;     // every input and the output are 16-byte aligned
+};
+static_assert(sizeof(Seg) == 32, "Seg layout");
+
+// Wave-uniform lookup of the segment that owns `tile` (segments sorted by tile_start).
+template <class S>
+__device__ __forceinline__ int find_seg(const S* __restrict__ segs, int nseg, int64_t tile) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (segs[mid].tile_start <= tile) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Record the calling thread's last error (fa_last_error) and return `code`.
+int fail(int code, const char* fmt, ...);
+const char* last_error();
+
+#define FA_HIP(call)                                                                     \
+  do {                                                                                   \
+    hipError_t e_ = (call);                                                              \
+    if (e_ != hipSuccess) return ::fa_detail::fail(FA_ERR_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = true;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) { prev = -1; }
+    if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+}  // namespace fa_detail
+
+struct fa_ctx {
+  int device = 0;
+  int variant = 0;       // kernel tuning variant (results identical for every variant)
+  bool mix_band = true;  // banded (sliding-window) mixing kernel when the CSR allows it
+  struct Slot {
+    void* host = nullptr;
+    void* dev = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev = nullptr;
+    bool pending = false;
+  } slots[fa_detail::kSlots];
+  int next = 0;
+};
+
+namespace fa_detail {
+
+// Take the next staging slot with >= bytes of room; waits only if that slot's previous call is
+// still in flight (kSlots calls ago).
+int acquire_slot(fa_ctx* ctx, size_t bytes, fa_ctx::Slot** out);
+// Copy the slot's first `bytes` host bytes to its device buffer (async on `st`).
+int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st);
+// Mark the slot busy until the work queued on `st` so far has finished.
+int release(fa_ctx::Slot* s, hipStream_t st);
+
+}  // namespace fa_detail

@@ -31,26 +31,15 @@
 #include <new>
 #include <type_traits>
 
-#include "fedagg.h"
+#include "fa_internal.h"
+
+using namespace fa_detail;
 
 namespace {
 
-constexpr int kBlock = 256;
-constexpr int kSlots = 8;
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 
 // --------------------------------------------------------------------------------------------
 // Device-resident descriptors (staged per call from pinned host memory).
-struct Seg {                // one state_dict tensor
-  int64_t numel;
-  int64_t tile_start;     // first tile (workgroup) of this segment
-  void* out;
-  int32_t ptr_base;       // index of client 0's pointer for this segment in the pointer table
-  int32_t aligned;        // every input and the output are 16-byte aligned
-};
-static_assert(sizeof(Seg) == 32, "Seg layout");
 
 struct MixRow {             // one output row of a mixing matrix
   int32_t begin, end;     // CSR entry range
@@ -269,15 +258,6 @@ __device__ __forceinline__ u32x4 ld16(const void* p) {
   else return *g;
 }
 
-// Wave-uniform lookup of the segment that owns `tile` (segments sorted by tile_start).
-__device__ __forceinline__ int find_seg(const Seg* __restrict__ segs, int nseg, int64_t tile) {
-  int lo = 0, hi = nseg - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (segs[mid].tile_start <= tile) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-}
 
 // --------------------------------------------------------------------------------------------
 // The ordered weighted-sum kernel.  One workgroup = one tile of kBlock*V*S elements of one segment:
@@ -718,91 +698,11 @@ int band_offset(int32_t rows, const int32_t* row_ptr, const int32_t* cols, int32
   return INT32_MIN;
 }
 
-// --------------------------------------------------------------------------------------------
-// Host side: error reporting, context, staging.
-thread_local char g_last_error[512] = "";
-
-int fail(int code, const char* fmt, ...) {
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
-  va_end(ap);
-  return code;
-}
-
-#define FA_HIP(call)                                                                     \
-  do {                                                                                   \
-    hipError_t e_ = (call);                                                              \
-    if (e_ != hipSuccess) return fail(FA_ERR_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
-  } while (0)
-
-struct DeviceGuard {
-  int prev = -1;
-  bool ok = true;
-  explicit DeviceGuard(int dev) {
-    if (hipGetDevice(&prev) != hipSuccess) { prev = -1; }
-    if (prev != dev) ok = hipSetDevice(dev) == hipSuccess;
-  }
-  ~DeviceGuard() {
-    int cur = -1;
-    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
-  }
-};
-
-inline size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
-
 }  // namespace
 
-struct fa_ctx {
-  int device = 0;
-  int variant = 0;      // kernel tuning variant (results identical for every variant)
-  bool mix_band = true;  // banded (sliding-window) mixing kernel when the CSR allows it
-  struct Slot {
-    void* host = nullptr;
-    void* dev = nullptr;
-    size_t cap = 0;
-    hipEvent_t ev = nullptr;
-    bool pending = false;
-  } slots[kSlots];
-  int next = 0;
-};
-
+// --------------------------------------------------------------------------------------------
+// Host side (error reporting and the staging slots live in fa_detail, see fa_internal.h).
 namespace {
-
-// Take the next staging slot with >= bytes of room; waits only if that slot's previous call is
-// still in flight (kSlots calls ago).
-int acquire_slot(fa_ctx* ctx, size_t bytes, fa_ctx::Slot** out) {
-  fa_ctx::Slot& s = ctx->slots[ctx->next];
-  ctx->next = (ctx->next + 1) % kSlots;
-  if (s.pending) {
-    FA_HIP(hipEventSynchronize(s.ev));
-    s.pending = false;
-  }
-  if (s.cap < bytes) {
-    size_t cap = std::max(bytes, std::max<size_t>(2 * s.cap, 16384));
-    if (s.host) FA_HIP(hipHostFree(s.host));
-    if (s.dev) FA_HIP(hipFree(s.dev));
-    s.host = s.dev = nullptr;
-    s.cap = 0;
-    if (hipHostMalloc(&s.host, cap, hipHostMallocDefault) != hipSuccess)
-      return fail(FA_ERR_NOMEM, "hipHostMalloc(%zu) failed", cap);
-    if (hipMalloc(&s.dev, cap) != hipSuccess) return fail(FA_ERR_NOMEM, "hipMalloc(%zu) failed", cap);
-    s.cap = cap;
-  }
-  *out = &s;
-  return FA_OK;
-}
-
-int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st) {
-  FA_HIP(hipMemcpyAsync(s->dev, s->host, bytes, hipMemcpyHostToDevice, st));
-  return FA_OK;
-}
-
-int release(fa_ctx::Slot* s, hipStream_t st) {
-  FA_HIP(hipEventRecord(s->ev, st));
-  s->pending = true;
-  return FA_OK;
-}
 
 // Kernel variants (performance only; every variant computes the identical result).
 struct Variant { int U, S; bool NT, PF; };
@@ -865,9 +765,62 @@ int elems_per_vec(int dtype) {
     default: return 0;
   }
 }
-inline bool al16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 }  // namespace
+
+
+// ============================================================================================
+// fa_detail: host helpers shared with the other translation units (fa_internal.h).
+namespace fa_detail {
+
+namespace {
+thread_local char g_last_error[512] = "";
+}
+
+int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_last_error, sizeof(g_last_error), fmt, ap);
+  va_end(ap);
+  return code;
+}
+
+const char* last_error() { return g_last_error; }
+
+int acquire_slot(fa_ctx* ctx, size_t bytes, fa_ctx::Slot** out) {
+  fa_ctx::Slot& s = ctx->slots[ctx->next];
+  ctx->next = (ctx->next + 1) % kSlots;
+  if (s.pending) {
+    FA_HIP(hipEventSynchronize(s.ev));
+    s.pending = false;
+  }
+  if (s.cap < bytes) {
+    size_t cap = std::max(bytes, std::max<size_t>(2 * s.cap, 16384));
+    if (s.host) FA_HIP(hipHostFree(s.host));
+    if (s.dev) FA_HIP(hipFree(s.dev));
+    s.host = s.dev = nullptr;
+    s.cap = 0;
+    if (hipHostMalloc(&s.host, cap, hipHostMallocDefault) != hipSuccess)
+      return fail(FA_ERR_NOMEM, "hipHostMalloc(%zu) failed", cap);
+    if (hipMalloc(&s.dev, cap) != hipSuccess) return fail(FA_ERR_NOMEM, "hipMalloc(%zu) failed", cap);
+    s.cap = cap;
+  }
+  *out = &s;
+  return FA_OK;
+}
+
+int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st) {
+  FA_HIP(hipMemcpyAsync(s->dev, s->host, bytes, hipMemcpyHostToDevice, st));
+  return FA_OK;
+}
+
+int release(fa_ctx::Slot* s, hipStream_t st) {
+  FA_HIP(hipEventRecord(s->ev, st));
+  s->pending = true;
+  return FA_OK;
+}
+
+}  // namespace fa_detail
 
 // ============================================================================================ ABI
 extern "C" {
@@ -885,7 +838,7 @@ const char* fa_strerror(int code) {
   }
 }
 
-const char* fa_last_error(void) { return g_last_error; }
+const char* fa_last_error(void) { return fa_detail::last_error(); }
 
 int fa_ctx_create(int hip_device, fa_ctx** out) {
   if (!out) return fail(FA_ERR_INVALID, "fa_ctx_create: out is NULL");

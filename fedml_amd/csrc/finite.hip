@@ -1,0 +1,505 @@
+// finite.hip -- MI355X (gfx950) kernels + C ABI of the finite-field secure-aggregation family
+// (include/fedagg_finite.h): the server's masked-model reconstruction in Z_p, the fixed-point
+// quantisation (my_q / model_masking) and the LCC mask decoding of LightSecAgg.
+//
+// Design:
+//  * Same shape as the weighted sum (fedagg.hip): HBM-bound, one lane = one 16-byte vector of
+//    int64 (2 elements) of one tile, the K clients walked in order with U clamped loads in flight,
+//    non-temporal loads/stores, one launch per state_dict via the segment table.
+//  * The reduction is int64 with the reference's exact numpy semantics: two's-complement wrap on
+//    +/-, floor remainder for np.mod.  A 64-bit `%` is a ~100-instruction software routine on the
+//    GPU, so mod is layered: in-range operands (the protocol's normal case, values in [0, p))
+//    take a compare-and-subtract; |a| < 2^53 takes a float64 reciprocal quotient with a +-1
+//    fix-up; only the rest (adversarial / wrapped inputs) pays for the division.  Every layer
+//    returns the identical floor remainder, so the layering is invisible in the results.
+//  * Dequantisation (my_q_inv) is float64 exactly as numpy evaluates it, then float32 as
+//    torch.Tensor(ndarray) converts it, then the float32 "* (1 / len(active))".
+//  * LCC decoding is a tiny-K (U x U coefficients) int64 matrix product over m columns: one lane
+//    per column keeps RB row accumulators, the column's k inputs stream through (L2-resident when
+//    re-read for the next row block); coefficients are wave-uniform scalar loads.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+
+#include "fa_internal.h"
+#include "fedagg_finite.h"
+
+using namespace fa_detail;
+
+namespace {
+
+constexpr int kV = 2;                       // int64 elements per 16-byte vector
+constexpr int64_t kTile = (int64_t)kBlock * kV;
+constexpr int kU = 8;                       // clients per load group
+
+struct FSeg {
+  int64_t numel;
+  int64_t tile_start;
+  int32_t ptr_base;
+  int32_t aligned;
+  const long long* mask;  // may be null
+  long long* out_fin;     // may be null
+  void* out_real;         // may be null; float32, or float64 with FA_FINITE_REAL_F64
+};
+static_assert(sizeof(FSeg) == 48, "FSeg layout");
+
+struct ModP {
+  long long p;
+  double inv_p;   // RN(1 / p)
+  bool small;     // p <= 2^62: in-range sums cannot wrap
+};
+
+typedef const __attribute__((address_space(1))) u32x4* gp_u32x4;
+typedef __attribute__((address_space(1))) u32x4* gpw_u32x4;
+
+__device__ __forceinline__ long long wadd(long long a, long long b) {
+  return (long long)((unsigned long long)a + (unsigned long long)b);
+}
+__device__ __forceinline__ long long wsub(long long a, long long b) {
+  return (long long)((unsigned long long)a - (unsigned long long)b);
+}
+
+// np.mod(a, p) for any int64 a, p > 0
+__device__ __forceinline__ long long mod_any(long long a, const ModP& m) {
+  if ((unsigned long long)a < (unsigned long long)m.p) return a;
+  if (a > -(1ll << 53) && a < (1ll << 53)) {
+    const double q = floor(__dmul_rn((double)a, m.inv_p));
+    long long r = a - (long long)q * m.p;
+    if (r < 0) r += m.p;
+    else if (r >= m.p) r -= m.p;
+    return r;
+  }
+  const long long r = a % m.p;
+  return r < 0 ? r + m.p : r;
+}
+// np.mod(a + b, p) with wrapping a + b
+__device__ __forceinline__ long long mod_add(long long a, long long b, const ModP& m) {
+  if (m.small && (unsigned long long)a < (unsigned long long)m.p && (unsigned long long)b < (unsigned long long)m.p) {
+    const long long s = a + b;
+    return s >= m.p ? s - m.p : s;
+  }
+  return mod_any(wadd(a, b), m);
+}
+// np.mod(a - b, p) with wrapping a - b
+__device__ __forceinline__ long long mod_sub(long long a, long long b, const ModP& m) {
+  if ((unsigned long long)a < (unsigned long long)m.p && (unsigned long long)b < (unsigned long long)m.p) {
+    const long long d = a - b;
+    return d < 0 ? d + m.p : d;
+  }
+  return mod_any(wsub(a, b), m);
+}
+
+struct Dequant {
+  double half;       // (p - 1) / 2
+  double pd;         // (double)p
+  double inv_pow2q;  // 2^-q (exact: x / 2^q == x * 2^-q, no subnormal results for |x| < 2^63)
+  float scale;
+};
+
+// my_q_inv in float64 (numpy's evaluation)
+__device__ __forceinline__ double dequant64(long long v, const Dequant& dq) {
+  const double vd = (double)v;
+  const double xq = __dsub_rn(vd, dq.half) > 0.0 ? __dsub_rn(vd, dq.pd) : vd;
+  return __dmul_rn(xq, dq.inv_pow2q);
+}
+// ... then torch.Tensor's float32 conversion and the float32 "* scale"
+__device__ __forceinline__ float dequant(long long v, const Dequant& dq) {
+  return __fmul_rn(__double2float_rn(dequant64(v, dq)), dq.scale);
+}
+
+__device__ __forceinline__ long long lo64(u32x4 r) { return __builtin_bit_cast(long long, u32x2{r[0], r[1]}); }
+__device__ __forceinline__ long long hi64(u32x4 r) { return __builtin_bit_cast(long long, u32x2{r[2], r[3]}); }
+__device__ __forceinline__ u32x4 pack64(long long a, long long b) {
+  const u32x2 x = __builtin_bit_cast(u32x2, a), y = __builtin_bit_cast(u32x2, b);
+  return u32x4{x[0], x[1], y[0], y[1]};
+}
+
+template <bool EACH>
+__device__ __forceinline__ long long step(long long acc, long long x, const ModP& m) {
+  if constexpr (EACH) return mod_add(acc, x, m);
+  else return wadd(acc, x);
+}
+
+template <bool EACH>
+__device__ __forceinline__ void finish(long long& acc, const FSeg& sg, int64_t e, int flags, const ModP& m) {
+  if (sg.mask) {
+    const long long mk = sg.mask[e];
+    acc = (flags & FA_FINITE_MOD_END) ? mod_sub(acc, mk, m) : wsub(acc, mk);
+  } else if (flags & FA_FINITE_MOD_END) {
+    acc = mod_any(acc, m);
+  }
+}
+
+// ---------------------------------------------------------------------------------- reconstruct
+template <bool EACH>
+__global__ void __launch_bounds__(kBlock)
+k_finite_sum(const FSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int flags,
+             ModP m, Dequant dq) {
+  const int64_t tile = blockIdx.x;
+  const FSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
+  const int64_t base = (tile - sg.tile_start) * kTile;
+  const void* const* in = ptrs + sg.ptr_base;
+  const bool first = flags & FA_FINITE_MOD_FIRST;
+
+  if (sg.aligned && base + kTile <= sg.numel) {
+    const int64_t e0 = base + (int64_t)threadIdx.x * kV;
+    const int64_t boff = e0 * 8;
+    long long a0 = 0, a1 = 0;
+    for (int i0 = 0; i0 < k; i0 += kU) {
+      u32x4 r[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int i = min(i0 + u, k - 1);  // clamped: every load unconditional
+        r[u] = __builtin_nontemporal_load((gp_u32x4)((const char*)in[i] + boff));
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int i = i0 + u;
+        if (i < k) {  // wave-uniform
+          const long long x0 = lo64(r[u]), x1 = hi64(r[u]);
+          if (i == 0) {
+            a0 = first ? mod_any(x0, m) : x0;
+            a1 = first ? mod_any(x1, m) : x1;
+          } else {
+            a0 = step<EACH>(a0, x0, m);
+            a1 = step<EACH>(a1, x1, m);
+          }
+        }
+      }
+    }
+    finish<EACH>(a0, sg, e0, flags, m);
+    finish<EACH>(a1, sg, e0 + 1, flags, m);
+    if (sg.out_fin) __builtin_nontemporal_store(pack64(a0, a1), (gpw_u32x4)(sg.out_fin + e0));
+    if (sg.out_real) {
+      if (flags & FA_FINITE_REAL_F64) {
+        const u32x4 w = pack64(__double_as_longlong(dequant64(a0, dq)), __double_as_longlong(dequant64(a1, dq)));
+        __builtin_nontemporal_store(w, (gpw_u32x4)((double*)sg.out_real + e0));
+      } else {
+        *(float2*)((float*)sg.out_real + e0) = make_float2(dequant(a0, dq), dequant(a1, dq));
+      }
+    }
+  } else {
+    const int64_t end = min(base + kTile, sg.numel);
+    for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
+      long long acc = ((const long long*)in[0])[e];
+      if (first) acc = mod_any(acc, m);
+      for (int i = 1; i < k; ++i) acc = step<EACH>(acc, ((const long long*)in[i])[e], m);
+      finish<EACH>(acc, sg, e, flags, m);
+      if (sg.out_fin) sg.out_fin[e] = acc;
+      if (sg.out_real) {
+        if (flags & FA_FINITE_REAL_F64) ((double*)sg.out_real)[e] = dequant64(acc, dq);
+        else ((float*)sg.out_real)[e] = dequant(acc, dq);
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------------- quantise
+struct QSeg {
+  int64_t numel;
+  int64_t tile_start;
+  const void* x;
+  const long long* mask;  // may be null
+  long long* out;
+  int64_t aligned;
+};
+static_assert(sizeof(QSeg) == 48, "QSeg layout");
+
+struct QParams {
+  float pow2q_f;   // 2^q
+  float pf;        // (float)p
+  double pow2q_d;
+  double pd;       // (double)p
+  int q;
+};
+
+__device__ __forceinline__ long long d2i64(double v) {
+  // numpy astype(int64) on x86: truncation; NaN / +-Inf / out of range -> INT64_MIN
+  if (!(v >= -9223372036854775808.0 && v < 9223372036854775808.0)) return LLONG_MIN;
+  return (long long)v;
+}
+
+template <int DT>
+__device__ __forceinline__ long long quant1(const void* x, int64_t e, const QParams& qp) {
+  if constexpr (DT == FA_DTYPE_F32) {
+    const float t = rintf(__fmul_rn(((const float*)x)[e], qp.pow2q_f));
+    const float o = t < 0.0f ? __fadd_rn(t, qp.pf) : t;  // t + p * is_negative (NaN stays NaN)
+    return d2i64((double)o);
+  } else if constexpr (DT == FA_DTYPE_F64) {
+    const double t = rint(__dmul_rn(((const double*)x)[e], qp.pow2q_d));
+    const double o = t < 0.0 ? __dadd_rn(t, qp.pd) : t;
+    return d2i64(o);
+  } else {
+    const long long t = (long long)((unsigned long long)((const long long*)x)[e] << qp.q);
+    const double td = (double)t;
+    return d2i64(t < 0 ? __dadd_rn(td, qp.pd) : td);
+  }
+}
+
+template <int DT> struct QElems { static constexpr int V = DT == FA_DTYPE_F32 ? 4 : 2; };
+
+template <int DT, bool MASK>
+__global__ void __launch_bounds__(kBlock)
+k_finite_quant(const QSeg* __restrict__ segs, int nseg, QParams qp, ModP m) {
+  constexpr int V = QElems<DT>::V;
+  constexpr int64_t TILE = (int64_t)kBlock * V;
+  const int64_t tile = blockIdx.x;
+  const QSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
+  const int64_t base = (tile - sg.tile_start) * TILE;
+  const int64_t end = min(base + TILE, sg.numel);
+  // element-wise; the per-element loads are coalesced across the wave (V elements per lane)
+  const int64_t e0 = base + (int64_t)threadIdx.x * V;
+  if (sg.aligned && base + TILE <= sg.numel) {
+    long long v[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) v[j] = quant1<DT>(sg.x, e0 + j, qp);
+    if constexpr (MASK) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) v[j] = mod_add(v[j], sg.mask[e0 + j], m);
+    }
+#pragma unroll
+    for (int j = 0; j < V; j += 2)
+      __builtin_nontemporal_store(pack64(v[j], v[j + 1]), (gpw_u32x4)(sg.out + e0 + j));
+  } else {
+    for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
+      long long v = quant1<DT>(sg.x, e, qp);
+      if constexpr (MASK) v = mod_add(v, sg.mask[e], m);
+      sg.out[e] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------- LCC decode
+constexpr int kRB = 8;  // output rows per register block
+
+__global__ void __launch_bounds__(kBlock)
+k_lcc_decode(const long long* __restrict__ coef, int rows_needed, int k, int64_t m_cols,
+             const long long* __restrict__ f, int64_t n_out, long long* __restrict__ out, ModP md) {
+  const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool live = c < m_cols;
+  const int64_t cc = live ? c : m_cols - 1;  // clamped column: loads stay in bounds
+  for (int j0 = 0; j0 < rows_needed; j0 += kRB) {
+    unsigned long long acc[kRB];
+#pragma unroll
+    for (int r = 0; r < kRB; ++r) acc[r] = 0;
+    int i = 0;
+    for (; i + 4 <= k; i += 4) {
+      unsigned long long fv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) fv[u] = (unsigned long long)f[(int64_t)(i + u) * m_cols + cc];
+#pragma unroll
+      for (int r = 0; r < kRB; ++r) {
+        const int j = min(j0 + r, rows_needed - 1);  // uniform clamp; extra rows are never stored
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[r] += (unsigned long long)coef[(int64_t)j * k + i + u] * fv[u];
+      }
+    }
+    for (; i < k; ++i) {
+      const unsigned long long fv = (unsigned long long)f[(int64_t)i * m_cols + cc];
+#pragma unroll
+      for (int r = 0; r < kRB; ++r) {
+        const int j = min(j0 + r, rows_needed - 1);
+        acc[r] += (unsigned long long)coef[(int64_t)j * k + i] * fv;
+      }
+    }
+    if (live) {
+#pragma unroll
+      for (int r = 0; r < kRB; ++r) {
+        const int64_t e = (int64_t)(j0 + r) * m_cols + c;
+        if (j0 + r < rows_needed && e < n_out) out[e] = mod_any((long long)acc[r], md);
+      }
+    }
+  }
+}
+
+ModP make_modp(int64_t p) {
+  ModP m;
+  m.p = p;
+  m.inv_p = 1.0 / (double)p;
+  m.small = p <= (1ll << 62);
+  return m;
+}
+
+}  // namespace
+
+// ============================================================================================ ABI
+extern "C" {
+
+int fa_finite_sum(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, int32_t k,
+                  const void* const* d_in, const void* const* d_mask, int64_t prime, int flags,
+                  void* const* d_out_finite, int32_t q_bits, double scale, void* const* d_out_real,
+                  void* hip_stream) {
+  if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (k <= 0 || num_segments <= 0 || !seg_numel || !d_in)
+    return fail(FA_ERR_INVALID, "fa_finite_sum: invalid arguments");
+  if (prime <= 0) return fail(FA_ERR_INVALID, "fa_finite_sum: prime must be > 0");
+  if (flags & ~(FA_FINITE_MOD_FIRST | FA_FINITE_MOD_EACH | FA_FINITE_MOD_END | FA_FINITE_REAL_F64))
+    return fail(FA_ERR_INVALID, "fa_finite_sum: unknown flags 0x%x", flags);
+  if (d_out_real && (q_bits < 0 || q_bits > 62)) return fail(FA_ERR_INVALID, "fa_finite_sum: q_bits must be in [0, 62]");
+  int nseg = 0;
+  int64_t tiles = 0;
+  for (int s = 0; s < num_segments; ++s) {
+    if (seg_numel[s] < 0) return fail(FA_ERR_INVALID, "segment %d has negative numel", s);
+    if (seg_numel[s] == 0) continue;
+    const bool fo = d_out_finite && d_out_finite[s], ro = d_out_real && d_out_real[s];
+    if (!fo && !ro) return fail(FA_ERR_INVALID, "segment %d: no output", s);
+    for (int i = 0; i < k; ++i)
+      if (!d_in[(int64_t)s * k + i]) return fail(FA_ERR_INVALID, "segment %d client %d: input NULL", s, i);
+    ++nseg;
+    tiles += (seg_numel[s] + kTile - 1) / kTile;
+  }
+  if (nseg == 0) return FA_OK;
+  if (tiles > 0x7FFFFFFFll) return fail(FA_ERR_INVALID, "too many tiles");
+  const size_t seg_bytes = align16(sizeof(FSeg) * nseg);
+  const size_t ptr_bytes = sizeof(void*) * (size_t)nseg * k;
+  const size_t bytes = seg_bytes + ptr_bytes;
+  DeviceGuard g(ctx->device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
+  hipStream_t st = (hipStream_t)hip_stream;
+  fa_ctx::Slot* slot = nullptr;
+  int rc = acquire_slot(ctx, bytes, &slot);
+  if (rc) return rc;
+  char* h = (char*)slot->host;
+  FSeg* hs = (FSeg*)h;
+  const void** hp = (const void**)(h + seg_bytes);
+  int j = 0;
+  int64_t t0 = 0;
+  for (int s = 0; s < num_segments; ++s) {
+    const int64_t n = seg_numel[s];
+    if (n == 0) continue;
+    FSeg sg;
+    sg.numel = n;
+    sg.tile_start = t0;
+    sg.ptr_base = j * k;
+    sg.mask = d_mask ? (const long long*)d_mask[s] : nullptr;
+    sg.out_fin = d_out_finite ? (long long*)d_out_finite[s] : nullptr;
+    sg.out_real = d_out_real ? d_out_real[s] : nullptr;
+    const uintptr_t ra = (flags & FA_FINITE_REAL_F64) ? 15u : 7u;
+    bool aligned = (!sg.out_fin || al16(sg.out_fin)) && (!sg.out_real || ((uintptr_t)sg.out_real & ra) == 0);
+    for (int i = 0; i < k; ++i) {
+      const void* p = d_in[(int64_t)s * k + i];
+      hp[(int64_t)j * k + i] = p;
+      aligned = aligned && al16(p);
+    }
+    sg.aligned = aligned ? 1 : 0;
+    hs[j] = sg;
+    t0 += (n + kTile - 1) / kTile;
+    ++j;
+  }
+  rc = stage(slot, bytes, st);
+  if (rc) return rc;
+  const char* dv = (const char*)slot->dev;
+  const ModP mp = make_modp(prime);
+  Dequant dq;
+  dq.half = (double)(prime - 1) / 2.0;
+  dq.pd = (double)prime;
+  dq.inv_pow2q = std::ldexp(1.0, -q_bits);
+  dq.scale = (float)scale;
+  const dim3 grid((unsigned)tiles), blk(kBlock);
+  if (flags & FA_FINITE_MOD_EACH)
+    hipLaunchKernelGGL((k_finite_sum<true>), grid, blk, 0, st, (const FSeg*)dv, nseg,
+                       (const void* const*)(dv + seg_bytes), k, flags, mp, dq);
+  else
+    hipLaunchKernelGGL((k_finite_sum<false>), grid, blk, 0, st, (const FSeg*)dv, nseg,
+                       (const void* const*)(dv + seg_bytes), k, flags, mp, dq);
+  FA_HIP(hipGetLastError());
+  return release(slot, st);
+}
+
+int fa_finite_quantize(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t* seg_numel,
+                       const void* const* d_x, const void* const* d_mask, int64_t prime, int32_t q_bits,
+                       void* const* d_out, void* hip_stream) {
+  if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (num_segments <= 0 || !seg_numel || !d_x || !d_out) return fail(FA_ERR_INVALID, "fa_finite_quantize: invalid arguments");
+  if (dtype != FA_DTYPE_F32 && dtype != FA_DTYPE_F64 && dtype != FA_DTYPE_I64)
+    return fail(FA_ERR_DTYPE, "fa_finite_quantize: dtype %d not supported (F32, F64, I64)", dtype);
+  if (prime <= 0) return fail(FA_ERR_INVALID, "fa_finite_quantize: prime must be > 0");
+  if (q_bits < 0 || q_bits > 62) return fail(FA_ERR_INVALID, "fa_finite_quantize: q_bits must be in [0, 62]");
+  const int V = dtype == FA_DTYPE_F32 ? 4 : 2;
+  const int64_t tile_elems = (int64_t)kBlock * V;
+  const bool mask = d_mask != nullptr;
+  int nseg = 0;
+  int64_t tiles = 0;
+  for (int s = 0; s < num_segments; ++s) {
+    if (seg_numel[s] < 0) return fail(FA_ERR_INVALID, "segment %d has negative numel", s);
+    if (seg_numel[s] == 0) continue;
+    if (!d_x[s] || !d_out[s] || (mask && !d_mask[s])) return fail(FA_ERR_INVALID, "segment %d: NULL pointer", s);
+    ++nseg;
+    tiles += (seg_numel[s] + tile_elems - 1) / tile_elems;
+  }
+  if (nseg == 0) return FA_OK;
+  if (tiles > 0x7FFFFFFFll) return fail(FA_ERR_INVALID, "too many tiles");
+  const size_t bytes = sizeof(QSeg) * nseg;
+  DeviceGuard g(ctx->device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
+  hipStream_t st = (hipStream_t)hip_stream;
+  fa_ctx::Slot* slot = nullptr;
+  int rc = acquire_slot(ctx, bytes, &slot);
+  if (rc) return rc;
+  QSeg* hs = (QSeg*)slot->host;
+  int j = 0;
+  int64_t t0 = 0;
+  for (int s = 0; s < num_segments; ++s) {
+    const int64_t n = seg_numel[s];
+    if (n == 0) continue;
+    const bool al = al16(d_x[s]) && al16(d_out[s]) && (!mask || al16(d_mask[s]));
+    hs[j] = QSeg{n, t0, d_x[s], mask ? (const long long*)d_mask[s] : nullptr, (long long*)d_out[s], al ? 1 : 0};
+    t0 += (n + tile_elems - 1) / tile_elems;
+    ++j;
+  }
+  rc = stage(slot, bytes, st);
+  if (rc) return rc;
+  QParams qp;
+  qp.pow2q_f = std::ldexp(1.0f, q_bits);
+  qp.pf = (float)prime;
+  qp.pow2q_d = std::ldexp(1.0, q_bits);
+  qp.pd = (double)prime;
+  qp.q = q_bits;
+  const ModP mp = make_modp(prime);
+  const QSeg* ds = (const QSeg*)slot->dev;
+  const dim3 grid((unsigned)tiles), blk(kBlock);
+#define FA_Q(DT)                                                                              \
+  if (mask) hipLaunchKernelGGL((k_finite_quant<DT, true>), grid, blk, 0, st, ds, nseg, qp, mp); \
+  else hipLaunchKernelGGL((k_finite_quant<DT, false>), grid, blk, 0, st, ds, nseg, qp, mp);
+  switch (dtype) {
+    case FA_DTYPE_F32: FA_Q(FA_DTYPE_F32); break;
+    case FA_DTYPE_F64: FA_Q(FA_DTYPE_F64); break;
+    default: FA_Q(FA_DTYPE_I64); break;
+  }
+#undef FA_Q
+  FA_HIP(hipGetLastError());
+  return release(slot, st);
+}
+
+int fa_lcc_decode(fa_ctx* ctx, int32_t rows, int32_t k, int64_t m, const int64_t* coef, const void* d_f,
+                  int64_t prime, int64_t n_out, void* d_out, void* hip_stream) {
+  if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (rows <= 0 || k <= 0 || m <= 0 || !coef || !d_f || !d_out)
+    return fail(FA_ERR_INVALID, "fa_lcc_decode: invalid arguments");
+  if (prime <= 0) return fail(FA_ERR_INVALID, "fa_lcc_decode: prime must be > 0");
+  if (n_out < 0 || n_out > (int64_t)rows * m) return fail(FA_ERR_INVALID, "fa_lcc_decode: n_out must be in [0, rows*m]");
+  if (n_out == 0) return FA_OK;
+  const int rows_needed = (int)((n_out + m - 1) / m);
+  const int64_t blocks = (m + kBlock - 1) / kBlock;
+  if (blocks > 0x7FFFFFFFll) return fail(FA_ERR_INVALID, "too many columns");
+  const size_t bytes = sizeof(int64_t) * (size_t)rows_needed * k;
+  DeviceGuard g(ctx->device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
+  hipStream_t st = (hipStream_t)hip_stream;
+  fa_ctx::Slot* slot = nullptr;
+  int rc = acquire_slot(ctx, bytes, &slot);
+  if (rc) return rc;
+  memcpy(slot->host, coef, bytes);
+  rc = stage(slot, bytes, st);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_lcc_decode, dim3((unsigned)blocks), dim3(kBlock), 0, st, (const long long*)slot->dev,
+                     rows_needed, k, m, (const long long*)d_f, n_out, (long long*)d_out, make_modp(prime));
+  FA_HIP(hipGetLastError());
+  return release(slot, st);
+}
+
+}  // extern "C"

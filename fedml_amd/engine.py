@@ -291,6 +291,95 @@ class AggEngine:
         N.check(rc, "fa_mix")
         return list(outs), (list(outs2) if outs2 is not None else None)
 
+    # ------------------------------------------------------------------ finite field (SecAgg)
+    def finite_sum(self, segments: Sequence[Sequence[torch.Tensor]], prime: int, flags: int,
+                   masks: Optional[Sequence[Optional[torch.Tensor]]] = None, finite: bool = True,
+                   q_bits: Optional[int] = None, scale: float = 1.0,
+                   stream=None) -> Tuple[Optional[List[torch.Tensor]], Optional[List[torch.Tensor]]]:
+        """Finite-field client sum (fa_finite_sum) over int64 segments[s][i]; returns
+        (finite int64 outputs or None, dequantized outputs or None): float32 (* scale), or my_q_inv's
+        float64 with the REAL_F64 flag."""
+        k = len(segments[0]) if segments else 0
+        if k == 0:
+            raise ValueError("finite_sum: no client tensors")
+        if not finite and q_bits is None:
+            raise ValueError("finite_sum: nothing to output")
+        in_ptrs, numels, mptrs, fin, real = [], [], [], [], []
+        for s, seg in enumerate(segments):
+            if len(seg) != k:
+                raise ValueError(f"segment {s}: {len(seg)} clients, expected {k}")
+            shape = seg[0].shape
+            for i, t in enumerate(seg):
+                if t.dtype != torch.int64:
+                    raise TypeError(f"finite_sum: segment {s} client {i} is {t.dtype} (int64 only)")
+                if t.shape != shape:
+                    raise RuntimeError(f"segment {s} client {i}: shape {tuple(t.shape)} != {tuple(shape)}")
+                _require_device(t, self.device, f"segment {s} client {i}")
+                in_ptrs.append(t.data_ptr())
+            m = masks[s] if masks is not None else None
+            if m is not None:
+                if m.dtype != torch.int64 or m.numel() != seg[0].numel():
+                    raise ValueError(f"finite_sum: mask {s} must be int64 with {seg[0].numel()} elements")
+                _require_device(m, self.device, f"mask {s}")
+            mptrs.append(m.data_ptr() if m is not None else None)
+            numels.append(seg[0].numel())
+            if finite:
+                fin.append(torch.empty(shape, dtype=torch.int64, device=self.device))
+            if q_bits is not None:
+                rdt = torch.float64 if flags & N.REAL_F64 else torch.float32
+                real.append(torch.empty(shape, dtype=rdt, device=self.device))
+        rc = self._lib.fa_finite_sum(
+            self._ctx, len(segments), N.i64_array(numels), k, N.ptr_array(in_ptrs),
+            N.ptr_array(mptrs) if masks is not None else None, int(prime), int(flags),
+            N.ptr_array([t.data_ptr() for t in fin]) if finite else None, int(q_bits or 0), float(scale),
+            N.ptr_array([t.data_ptr() for t in real]) if q_bits is not None else None, self._stream(stream))
+        N.check(rc, "fa_finite_sum")
+        return (fin if finite else None), (real if q_bits is not None else None)
+
+    def finite_quantize(self, xs: Sequence[torch.Tensor], prime: int, q_bits: int,
+                        masks: Optional[Sequence[torch.Tensor]] = None, stream=None) -> List[torch.Tensor]:
+        """my_q (+ model_masking with masks) of same-dtype device tensors (fa_finite_quantize)."""
+        if len(xs) == 0:
+            return []
+        dt = xs[0].dtype
+        if dt not in (torch.float32, torch.float64, torch.int64):
+            raise TypeError(f"finite_quantize: unsupported dtype {dt} (float32, float64, int64)")
+        outs = []
+        for s, t in enumerate(xs):
+            if t.dtype != dt:
+                raise TypeError(f"finite_quantize: tensor {s} is {t.dtype}, expected {dt}")
+            _require_device(t, self.device, f"tensor {s}")
+            outs.append(torch.empty(t.shape, dtype=torch.int64, device=self.device))
+            if masks is not None:
+                m = masks[s]
+                if m.dtype != torch.int64 or m.numel() != t.numel():
+                    raise ValueError(f"finite_quantize: mask {s} must be int64 with {t.numel()} elements")
+                _require_device(m, self.device, f"mask {s}")
+        rc = self._lib.fa_finite_quantize(
+            self._ctx, DTYPE_CODE[dt], len(xs), N.i64_array([t.numel() for t in xs]),
+            N.ptr_array([t.data_ptr() for t in xs]),
+            N.ptr_array([m.data_ptr() for m in masks]) if masks is not None else None, int(prime), int(q_bits),
+            N.ptr_array([o.data_ptr() for o in outs]), self._stream(stream))
+        N.check(rc, "fa_finite_quantize")
+        return outs
+
+    def lcc_decode(self, coef: Sequence[Sequence[int]], f: torch.Tensor, prime: int, n_out: int,
+                   stream=None) -> torch.Tensor:
+        """First n_out entries of np.mod(coef.dot(f), p) (int64 wrap), f an int64 (k x m) device tensor."""
+        if f.dtype != torch.int64 or f.dim() != 2:
+            raise ValueError("lcc_decode: f must be a 2-D int64 tensor")
+        _require_device(f, self.device, "lcc f")
+        rows = len(coef)
+        k, m = f.shape
+        flat = [int(v) for row in coef for v in row]
+        if rows == 0 or len(flat) != rows * k:
+            raise ValueError(f"lcc_decode: coef must be rows x {k}")
+        out = torch.empty(int(n_out), dtype=torch.int64, device=self.device)
+        rc = self._lib.fa_lcc_decode(self._ctx, rows, k, m, N.i64_array(flat), f.data_ptr(), int(prime), int(n_out),
+                                     out.data_ptr(), self._stream(stream))
+        N.check(rc, "fa_lcc_decode")
+        return out
+
 
 def get_engine(device: Optional[int] = None) -> AggEngine:
     return AggEngine.get(device)

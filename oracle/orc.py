@@ -48,6 +48,16 @@ def lib():
                                     ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                     ctypes.c_int, ctypes.c_int]
         L.orc_sgd_apply.restype = ctypes.c_int
+        L.orc_finite_sum.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p,
+                                     ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_double,
+                                     ctypes.c_void_p]
+        L.orc_finite_sum.restype = ctypes.c_int
+        L.orc_finite_quantize.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_int64, ctypes.c_int32, ctypes.c_void_p]
+        L.orc_finite_quantize.restype = ctypes.c_int
+        L.orc_lcc_decode.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
+        L.orc_lcc_decode.restype = ctypes.c_int
         L.orc_f32_to_bf16.argtypes = [ctypes.c_float]
         L.orc_f32_to_bf16.restype = ctypes.c_uint16
         L.orc_f32_to_f16.argtypes = [ctypes.c_float]
@@ -106,3 +116,47 @@ def sgd_apply(avg, param, buf, lr, momentum=0.0, dampening=0.0, weight_decay=0.0
                              float(dampening), float(weight_decay), int(nesterov), int(first_step))
     if rc != 0:
         raise RuntimeError(f"orc_sgd_apply failed: {rc}")
+
+
+MOD_FIRST, MOD_EACH, MOD_END, REAL_F64 = 1, 2, 4, 8
+
+
+def finite_sum(xs, p, flags, mask=None, q_bits=None, scale=1.0):
+    """Finite-field client sum (see orc_finite_sum).  Returns (finite int64, real or None); the real
+    output (float32 dequantized * fp32(scale), or float64 with REAL_F64) only when q_bits is given."""
+    xs = [x.contiguous() for x in xs]
+    assert all(x.dtype == torch.int64 and x.numel() == xs[0].numel() for x in xs)
+    n = xs[0].numel()
+    fin = torch.empty(n, dtype=torch.int64)
+    real = torch.empty(n, dtype=torch.float64 if flags & REAL_F64 else torch.float32) if q_bits is not None else None
+    m = mask.contiguous() if mask is not None else None
+    rc = lib().orc_finite_sum(n, len(xs), (ctypes.c_void_p * len(xs))(*[x.data_ptr() for x in xs]),
+                              m.data_ptr() if m is not None else None, int(p), int(flags), fin.data_ptr(),
+                              int(q_bits or 0), float(scale), real.data_ptr() if real is not None else None)
+    if rc != 0:
+        raise RuntimeError(f"orc_finite_sum failed: {rc}")
+    return fin, real
+
+
+def finite_quantize(x, p, q_bits, mask=None):
+    """my_q (+ model_masking when mask is given) of a float32 / float64 / int64 CPU tensor."""
+    x = x.contiguous()
+    out = torch.empty(x.numel(), dtype=torch.int64)
+    m = mask.contiguous() if mask is not None else None
+    rc = lib().orc_finite_quantize(_DT[x.dtype], x.numel(), x.data_ptr(), m.data_ptr() if m is not None else None,
+                                   int(p), int(q_bits), out.data_ptr())
+    if rc != 0:
+        raise RuntimeError(f"orc_finite_quantize failed: {rc}")
+    return out
+
+
+def lcc_decode(coef, f, p, n_out):
+    """np.mod(coef.dot(f), p).reshape(-1)[:n_out] with int64 wrap (coef rows x k, f k x m)."""
+    coef = coef.contiguous()
+    f = f.contiguous()
+    rows, k = coef.shape
+    out = torch.empty(n_out, dtype=torch.int64)
+    rc = lib().orc_lcc_decode(rows, k, f.shape[1], coef.data_ptr(), f.data_ptr(), int(p), int(n_out), out.data_ptr())
+    if rc != 0:
+        raise RuntimeError(f"orc_lcc_decode failed: {rc}")
+    return out

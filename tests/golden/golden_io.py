@@ -91,3 +91,13 @@ def list_cases():
     return sorted(
         os.path.join(GOLDEN_DIR, f) for f in os.listdir(GOLDEN_DIR) if f.endswith(".npz")
     )
+
+
+FINITE_PREFIXES = ("g11_", "g12_", "g13_", "g14_", "g15_")  # SecAgg / LightSecAgg families
+
+
+def aggregation_cases():
+    """Fixtures replayed by the generic aggregation replay (refcases.replay): everything except
+    the topology tables, FedOpt rounds and the finite-field families, which have their own."""
+    return [p for p in list_cases() if "topologies" not in p and "fedopt" not in p
+            and not os.path.basename(p).startswith(FINITE_PREFIXES)]

@@ -605,6 +605,191 @@ def cases_fedopt():
         WRITTEN.append((meta["name"], os.path.getsize(path)))
 
 
+def load_mpc():
+    for name, sub in [("fedml", ""), ("fedml.core", "/core"), ("fedml.core.mpc", "/core/mpc")]:
+        _stub_pkg(name, REF + sub)
+    return (importlib.import_module("fedml.core.mpc.lightsecagg"),
+            importlib.import_module("fedml.core.mpc.secagg"))
+
+
+def _np_dict_to_torch(d):
+    return OrderedDict((k, torch.from_numpy(np.array(v, dtype=np.int64, copy=True))) for k, v in d.items())
+
+
+def _adversarial_i64(rng, shape, p):
+    """int64 values in and far outside [0, p): negatives, multiples of p, near the int64 ends."""
+    n = int(np.prod(shape))
+    v = rng.randint(0, p, size=n).astype(np.int64)
+    sel = rng.randint(0, 6, size=n)
+    big = rng.randint(-2 ** 62, 2 ** 62, size=n, dtype=np.int64) * 2 + rng.randint(0, 2, size=n)
+    v = np.where(sel == 1, -v, v)
+    v = np.where(sel == 2, v + p * rng.randint(1, 9, size=n), v)
+    v = np.where(sel == 3, big, v)
+    v = np.where(sel == 4, np.int64(2 ** 63 - 1) - rng.randint(0, 3, size=n), v)
+    return v.reshape(shape)
+
+
+def _real_values(rng, shape, q):
+    """float64 values that stress my_q: ties at the 2^-q grid, both signs, large and tiny."""
+    n = int(np.prod(shape))
+    sel = rng.randint(0, 6, size=n)
+    v = rng.standard_normal(n)
+    v = np.where(sel == 1, (rng.randint(-2000, 2000, size=n) + 0.5) / 2.0 ** q, v)  # exact ties
+    v = np.where(sel == 2, rng.standard_normal(n) * 2.0 ** rng.randint(0, 40, size=n), v)  # large
+    v = np.where(sel == 3, rng.standard_normal(n) * 2.0 ** -rng.randint(q, q + 30, size=n), v)  # tiny
+    return v.reshape(shape)
+
+
+def cases_secagg():
+    """§8(f) next #4: finite-field secure aggregation (core/mpc/lightsecagg.py, core/mpc/secagg.py,
+    cross_silo/lightsecagg/lsa_fedml_aggregator.py:101-175, cross_silo/secagg/sa_fedml_aggregator.py:
+    138-184), generated by running the reference's functions on seeded inputs."""
+    import warnings
+    lsa, sa = load_mpc()
+    np.random.seed(1234)  # mask_encoding draws its noise from the global numpy RNG
+    rng = np.random.RandomState(77)
+    layout = [("fc.weight", (5, 7)), ("fc.bias", (5,)), ("bn.num_batches_tracked", ()), ("v", (13,))]
+
+    # S1: aggregate_models_in_finite (lightsecagg.py:134-145 == secagg.py:148-159)
+    for p, K in ((2 ** 15 - 19, 5), (2 ** 61 - 1, 4), (2 ** 15 - 19, 1)):
+        clients = [OrderedDict((k, _adversarial_i64(rng, s, p)) for k, s in layout) for _ in range(K)]
+        out = lsa.aggregate_models_in_finite(dc(clients), p)
+        assert out2_equal(out, sa.aggregate_models_in_finite(dc(clients), p))
+        write(f"g11_finite_sum_p{p}_K{K}", [_np_dict_to_torch(c) for c in clients], [_np_dict_to_torch(out)],
+              dict(kind="finite_sum", p=p, ref="core/mpc/lightsecagg.py:134-145"))
+
+    # S2: my_q / transform_tensor_to_finite (+ model_masking) on float32 / float64 / int64 tensors
+    for p, q in ((2 ** 15 - 19, 8), (2 ** 31 - 1, 16), (2 ** 61 - 1, 20)):
+        d = OrderedDict()
+        d["w32"] = torch.from_numpy(_real_values(rng, (67,), q).astype(np.float32))
+        sp = torch.tensor([0.0, -0.0, float("nan"), float("inf"), -float("inf"), 3e38, -3e38, 2.0 ** 62,
+                           -2.0 ** 63, 2.0 ** 63, 0.5 / 2 ** q, -0.5 / 2 ** q, 1.5 / 2 ** q, -2.5 / 2 ** q],
+                          dtype=torch.float32)
+        d["special32"] = sp
+        d["w64"] = torch.from_numpy(_real_values(rng, (3, 11), q))
+        d["special64"] = sp.double()
+        d["n64"] = torch.from_numpy(rng.randint(-10 ** 6, 10 ** 6, size=(9,)).astype(np.int64))
+        d["n64_big"] = torch.tensor([2 ** 62, -2 ** 62, 2 ** 63 - 1, -2 ** 63, 7, -7, 0], dtype=torch.int64)
+        d["scalar"] = torch.tensor(5, dtype=torch.int64)
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore")
+            fin = lsa.transform_tensor_to_finite(OrderedDict((k, v.clone()) for k, v in d.items()), p, q)
+            fin_copy = {k: np.array(v, copy=True) for k, v in fin.items()}
+            dims = [int(np.prod(v.shape)) for v in d.values()]
+            mask = rng.randint(p, size=(sum(dims), 1))
+            masked = lsa.model_masking(fin, dims, mask, p)
+        outs = [_np_dict_to_torch(fin_copy), _np_dict_to_torch(masked)]
+        meta, arrays = pack([d], outs, dict(kind="finite_quantize", p=p, q_bits=q,
+                                            ref="core/mpc/lightsecagg.py:83-95,150-154,187-192"))
+        arrays["mask"] = mask.astype(np.int64)
+        name = f"g12_my_q_p{p}_q{q}"
+        meta["name"] = name
+        save_case(os.path.join(HERE, name + ".npz"), meta, arrays)
+        WRITTEN.append((name, os.path.getsize(os.path.join(HERE, name + ".npz"))))
+
+    # S3: my_q_inv / transform_finite_to_tensor (lightsecagg.py:157-185), incl. 0-d -> shape [1]
+    for p, q in ((2 ** 15 - 19, 8), (2 ** 61 - 1, 20), (2 ** 15 - 18, 4)):
+        fin = OrderedDict((k, _adversarial_i64(rng, s, p)) for k, s in layout)
+        fin["in_range"] = rng.randint(0, p, size=(41,)).astype(np.int64)
+        fin["edge"] = np.array([0, 1, (p - 1) // 2, (p - 1) // 2 + 1, p // 2, p - 1, p, -1], dtype=np.int64)
+        src = _np_dict_to_torch(fin)
+        out = lsa.transform_finite_to_tensor(OrderedDict((k, np.array(v, copy=True)) for k, v in fin.items()), p, q)
+        write(f"g13_my_q_inv_p{p}_q{q}", [src], [OrderedDict((k, v.clone()) for k, v in out.items())],
+              dict(kind="finite_dequantize", p=p, q_bits=q, ref="core/mpc/lightsecagg.py:157-185"))
+
+    # S4: LightSecAgg end to end (client masking + encoded-mask exchange, server LCC decoding and
+    # reconstruction), lsa_fedml_aggregator.py:101-175
+    g = {"LCC_decoding_with_points": lsa.LCC_decoding_with_points,
+         "transform_finite_to_tensor": lsa.transform_finite_to_tensor}
+    rel = "cross_silo/lightsecagg/lsa_fedml_aggregator.py"
+    mrec = extract_method(rel, "LightSecAggAggregator", "aggregate_mask_reconstruction", g)
+    arec = extract_method(rel, "LightSecAggAggregator", "aggregate_model_reconstruction", g)
+    for N, p, q in ((5, 2 ** 15 - 19, 8), (8, 2 ** 31 - 1, 16), (3, 2 ** 15 - 19, 10)):
+        U, T = N, N // 2
+        model = [("fc.weight", (6, 11)), ("fc.bias", (6,)), ("bn.running_mean", (6,)),
+                 ("bn.num_batches_tracked", ()), ("head", (37,))]
+        weights = []
+        for i in range(N):
+            w = OrderedDict()
+            for k, s in model:
+                if k.endswith("num_batches_tracked"):
+                    w[k] = torch.tensor(3 + i, dtype=torch.int64)
+                else:
+                    w[k] = torch.from_numpy((rng.standard_normal(s) * 0.5).astype(np.float32))
+            weights.append(w)
+        dims = [int(np.prod(s)) for _, s in model]
+        total = sum(dims)
+        d = int(np.ceil(float(total) / (U - T))) * (U - T)
+        local_masks = [np.random.randint(p, size=(d, 1)) for _ in range(N)]
+        enc = [lsa.mask_encoding(d, N, U, T, p, local_masks[j]) for j in range(N)]
+        masked = []
+        for i in range(N):
+            fin = lsa.transform_tensor_to_finite(OrderedDict((k, v.clone()) for k, v in weights[i].items()), p, q)
+            masked.append(lsa.model_masking(fin, dims, local_masks[i], p))
+        active = list(range(N))
+        agg_enc = {i: lsa.compute_aggregate_encoded_mask({j: enc[j][i] for j in range(N)}, p, active)
+                   for i in range(N)}
+        self_ = types.SimpleNamespace(
+            total_dimension=total, client_num=N, targeted_number_active_clients=U, privacy_guarantee=T,
+            prime_number=p, precision_parameter=q, dimensions=dims,
+            aggregate_encoded_mask_dict={i: np.array(v) for i, v in agg_enc.items()},
+            model_dict={i: {k: np.array(v, copy=True) for k, v in masked[i].items()} for i in range(N)},
+            set_global_model_params=lambda params: None)
+        self_.aggregate_mask_reconstruction = functools.partial(mrec, self_)
+        inputs = [_np_dict_to_torch(m) for m in masked]
+        amask = self_.aggregate_mask_reconstruction(active)
+        out = arec(self_, active, active)
+        F = np.zeros((U, d // (U - T)), dtype=np.int64)
+        for i in active:
+            F[i, :] = agg_enc[i]
+        meta, arrays = pack(inputs, [OrderedDict((k, v.clone()) for k, v in out.items())],
+                            dict(kind="lsa_reconstruct", p=p, q_bits=q, N=N, U=U, T=T, dims=dims, d=d,
+                                 ref="cross_silo/lightsecagg/lsa_fedml_aggregator.py:101-175"))
+        arrays["F"] = F
+        arrays["aggregate_mask"] = np.asarray(amask, dtype=np.int64).reshape(-1)
+        name = f"g14_lsa_reconstruct_N{N}_p{p}"
+        meta["name"] = name
+        save_case(os.path.join(HERE, name + ".npz"), meta, arrays)
+        WRITTEN.append((name, os.path.getsize(os.path.join(HERE, name + ".npz"))))
+        # the true aggregate is recovered: sum of the local masks == the decoded mask (mod p)
+        ok = np.array_equal(np.mod(sum(m[:total, 0] for m in local_masks), p), arrays["aggregate_mask"][:total])
+        print(f"lsa N={N} p={p}: decoded mask == sum of local masks: {ok}")
+
+    # S5: SecAgg model reconstruction (sa_fedml_aggregator.py:138-184) with a given aggregate mask:
+    # flags all set (every client summed, mod after each add) and the real server flow, where
+    # check_whether_all_receive (:84-90) has already cleared every flag (only client 0's model is kept)
+    arec_sa = extract_method("cross_silo/secagg/sa_fedml_aggregator.py", "SecAggAggregator",
+                             "aggregate_model_reconstruction",
+                             {"transform_finite_to_tensor": sa.transform_finite_to_tensor})
+    for N, p, q, flags in ((4, 2 ** 15 - 19, 8, "all"), (4, 2 ** 15 - 19, 8, "none"),
+                           (5, 2 ** 61 - 1, 12, "some")):
+        model = [("w", (9, 4)), ("b", (9,)), ("nbt", ())]
+        dims = [int(np.prod(s)) for _, s in model]
+        total = sum(dims)
+        clients = [OrderedDict((k, _adversarial_i64(rng, s, p)) for k, s in model) for _ in range(N)]
+        amask = rng.randint(0, p, size=total).astype(np.int64)
+        fl = {i: {"all": True, "none": False, "some": i % 2 == 1}[flags] for i in range(N)}
+        self_ = types.SimpleNamespace(
+            prime_number=p, precision_parameter=q, dimensions=dims,
+            model_dict={i: {k: np.array(v, copy=True) for k, v in clients[i].items()} for i in range(N)},
+            flag_client_model_uploaded_dict=dict(fl),
+            aggregate_mask_reconstruction=lambda *a: amask)
+        active = list(range(N))
+        out = arec_sa(self_, active, active, None, None)
+        meta, arrays = pack([_np_dict_to_torch(c) for c in clients], [OrderedDict((k, v.clone()) for k, v in out.items())],
+                            dict(kind="sa_reconstruct", p=p, q_bits=q, flags=[fl[i] for i in range(N)], dims=dims,
+                                 ref="cross_silo/secagg/sa_fedml_aggregator.py:138-184"))
+        arrays["aggregate_mask"] = amask
+        name = f"g15_sa_reconstruct_{flags}_p{p}"
+        meta["name"] = name
+        save_case(os.path.join(HERE, name + ".npz"), meta, arrays)
+        WRITTEN.append((name, os.path.getsize(os.path.join(HERE, name + ".npz"))))
+
+
+def out2_equal(a, b):
+    return all(np.array_equal(np.asarray(a[k]), np.asarray(b[k])) for k in a)
+
+
 def layouts(ao):
     """Model layouts used by the configs: names/shapes/dtypes only (no weights)."""
     for name, sub in [("fedml.model", "/model"), ("fedml.model.cv", "/model/cv")]:
@@ -641,12 +826,19 @@ def layouts(ao):
 
 
 def main():
+    if len(sys.argv) > 1:  # regenerate only the named families, e.g. `make_golden.py secagg`
+        for part in sys.argv[1:]:
+            globals()["cases_" + part]()
+        for name, s in WRITTEN:
+            print(f"{name:45s} {s:9d} B")
+        return
     ao = load_agg_operator()
     stm, tu = load_topology()
     cases_agg_operator(ao)
     cases_call_sites()
     cases_topology_and_mixing(stm, tu)
     cases_fedopt()
+    cases_secagg()
     layouts(ao)
     total = sum(s for _, s in WRITTEN)
     for name, s in WRITTEN:

@@ -217,3 +217,19 @@ def fedopt_expected(meta, arrays):
     from golden_io import np_to_tensor
     return [OrderedDict((k, np_to_tensor(arrays[f"r{r}_y__{k}"], dt)) for k, dt in zip(meta["keys"], meta["dtypes"]))
             for r in range(len(meta["rounds"]))]
+
+
+# ----------------------------------------------------------------------------- finite field (SecAgg)
+MOD_FIRST, MOD_EACH, MOD_END, REAL_F64 = 1, 2, 4, 8
+
+
+def sa_order_and_flags(uploaded):
+    """SecAgg reconstruction (sa_fedml_aggregator.py:150-164): clients summed and the mod flags, given
+    the per-client upload flags of the first-round active clients [0..N)."""
+    order = [0] + [i for i in range(1, len(uploaded)) if uploaded[i]]
+    return order, MOD_EACH | MOD_END | (MOD_FIRST if uploaded[0] else 0)
+
+
+def finite_case_inputs(meta, arrays):
+    """(clients as int64/float CPU tensors per key) for a finite-field fixture."""
+    return client_dicts(meta, arrays)

@@ -1,0 +1,297 @@
+"""GPU parity of the finite-field (SecAgg / LightSecAgg) kernels: the reference's fixtures g11-g15
+bit-for-bit through the drop-in functions and aggregators, and the C oracle on larger seeded and
+adversarial inputs (wrap-around, out-of-range values, every flag combination, ragged / misaligned
+segments)."""
+from __future__ import annotations
+
+import os
+import types
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+import torch
+
+from golden_io import FINITE_PREFIXES, client_dicts, expected_dicts, list_cases, load_case
+from refcases import MOD_EACH, MOD_END, MOD_FIRST, REAL_F64, assert_dict_bits, bits_equal, sa_order_and_flags
+
+pytestmark = pytest.mark.gpu
+
+CASES = list_cases()
+FIN = {kind: [p for p in CASES if os.path.basename(p).startswith(kind)] for kind in FINITE_PREFIXES}
+ids = lambda p: os.path.basename(p)[:-4]  # noqa: E731
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from fedml_amd.engine import get_engine
+    return get_engine(0)
+
+
+def _np_dict(d):
+    return OrderedDict((k, v.numpy().copy() if v.dim() else v.numpy()[()]) for k, v in d.items())
+
+
+# ----------------------------------------------------------------------------- golden, drop-in API
+@pytest.mark.parametrize("path", FIN["g11_"], ids=ids)
+@pytest.mark.parametrize("where", ["numpy", "cuda"])
+def test_aggregate_models_in_finite_golden(path, where):
+    from fedml_amd.core.mpc.lightsecagg import aggregate_models_in_finite
+    meta, arrays = load_case(path)
+    cl = client_dicts(meta, arrays)
+    exp = expected_dicts(meta, arrays)[0]
+    ins = [_np_dict(c) for c in cl] if where == "numpy" else \
+        [OrderedDict((k, v.to(DEV)) for k, v in c.items()) for c in cl]
+    out = aggregate_models_in_finite(ins, meta["p"])
+    for k in meta["keys"]:
+        got = torch.as_tensor(np.asarray(out[k])) if where == "numpy" else out[k].cpu()
+        assert torch.equal(got.reshape(exp[k].shape), exp[k]), k
+
+
+@pytest.mark.parametrize("path", FIN["g12_"], ids=ids)
+@pytest.mark.parametrize("where", ["cpu", "cuda"])
+def test_transform_to_finite_and_masking_golden(path, where):
+    from fedml_amd.core.mpc.lightsecagg import model_masking, transform_tensor_to_finite
+    meta, arrays = load_case(path)
+    x = client_dicts(meta, arrays)[0]
+    q_out, masked = expected_dicts(meta, arrays)
+    src = OrderedDict((k, v.to(DEV) if where == "cuda" else v) for k, v in x.items())
+    fin = transform_tensor_to_finite(src, meta["p"], meta["q_bits"])
+    back = lambda v: v.cpu() if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))  # noqa: E731
+    for k in meta["keys"]:
+        assert torch.equal(back(fin[k]).reshape(q_out[k].shape), q_out[k]), k
+    dims = [int(np.prod(s)) for s in meta["shapes"]]
+    mask = torch.from_numpy(arrays["mask"])
+    mask = mask.to(DEV) if where == "cuda" else mask.numpy()
+    out = model_masking(fin, dims, mask, meta["p"])
+    for k in meta["keys"]:
+        assert torch.equal(back(out[k]).reshape(masked[k].shape), masked[k]), k
+
+
+@pytest.mark.parametrize("path", FIN["g12_"], ids=ids)
+def test_fused_quantize_mask_golden(eng, path):
+    """my_q + model_masking in one kernel pass == the reference's two passes."""
+    meta, arrays = load_case(path)
+    x = client_dicts(meta, arrays)[0]
+    masked = expected_dicts(meta, arrays)[1]
+    mask = torch.from_numpy(arrays["mask"].reshape(-1)).to(DEV)
+    pos = 0
+    for k in meta["keys"]:
+        n = x[k].numel()
+        t = x[k].reshape(-1).to(DEV)
+        got = eng.finite_quantize([t], meta["p"], meta["q_bits"], masks=[mask[pos:pos + n]])[0]
+        assert torch.equal(got.cpu().reshape(masked[k].shape), masked[k]), k
+        pos += n
+
+
+@pytest.mark.parametrize("path", FIN["g13_"], ids=ids)
+@pytest.mark.parametrize("where", ["numpy", "cuda"])
+def test_transform_to_tensor_golden(path, where):
+    from fedml_amd.core.mpc.lightsecagg import my_q_inv, transform_finite_to_tensor
+    from oracle import orc
+    meta, arrays = load_case(path)
+    x = client_dicts(meta, arrays)[0]
+    exp = expected_dicts(meta, arrays)[0]
+    src = _np_dict(x) if where == "numpy" else OrderedDict((k, v.to(DEV)) for k, v in x.items())
+    out = transform_finite_to_tensor(src, meta["p"], meta["q_bits"])
+    for k in meta["keys"]:
+        assert out[k].dtype == torch.float32 and tuple(out[k].shape) == tuple(exp[k].shape), k
+        assert bits_equal(out[k].cpu(), exp[k]), k
+        # my_q_inv itself: float64, as numpy evaluates it
+        r = my_q_inv(x[k].to(DEV) if where == "cuda" else x[k].numpy(), meta["q_bits"], meta["p"])
+        r = r.cpu() if isinstance(r, torch.Tensor) else torch.as_tensor(np.asarray(r))
+        _, ref = orc.finite_sum([x[k].reshape(-1)], meta["p"], REAL_F64, q_bits=meta["q_bits"])
+        assert r.dtype == torch.float64 and bits_equal(r.reshape(-1), ref), k
+
+
+class _Trainer:
+    def __init__(self, shapes):
+        self.params = OrderedDict((k, torch.zeros(s)) for k, s in shapes)
+        self.received = None
+
+    def get_model_params(self):
+        return self.params
+
+    def set_model_params(self, p):
+        self.received = p
+
+
+@pytest.mark.parametrize("path", FIN["g14_"], ids=ids)
+def test_lightsecagg_aggregator_golden(path):
+    from fedml_amd.cross_silo.lightsecagg import LightSecAggAggregator
+    meta, arrays = load_case(path)
+    cl = client_dicts(meta, arrays)
+    exp = expected_dicts(meta, arrays)[0]
+    N = meta["N"]
+    tr = _Trainer(list(zip(meta["keys"], meta["shapes"])))
+    args = types.SimpleNamespace(prime_number=meta["p"], precision_parameter=meta["q_bits"])
+    agg = LightSecAggAggregator(None, None, 0, {}, {}, {}, N, DEV, args, tr)
+    agg.get_global_model_params()
+    assert agg.dimensions == meta["dims"]
+    for i in range(N):
+        agg.add_local_trained_result(i, _np_dict(cl[i]), 10 + i)
+        agg.add_local_aggregate_encoded_mask(i, arrays["F"][i].tolist())
+    assert agg.check_whether_all_receive() and agg.check_whether_all_aggregate_encoded_mask_receive()
+    active = list(range(N))
+    mask = agg.aggregate_mask_reconstruction(active)
+    assert torch.equal(mask.reshape(-1).cpu(), torch.from_numpy(arrays["aggregate_mask"]))
+    out = agg.aggregate_model_reconstruction(active, active)
+    assert tr.received is out
+    assert_dict_bits(OrderedDict((k, v.cpu()) for k, v in out.items()), exp, "lsa")
+
+
+@pytest.mark.parametrize("path", FIN["g15_"], ids=ids)
+def test_secagg_aggregator_golden(path):
+    from fedml_amd.cross_silo.secagg import SecAggAggregator
+    meta, arrays = load_case(path)
+    cl = client_dicts(meta, arrays)
+    exp = expected_dicts(meta, arrays)[0]
+    N = meta["num_clients"]
+    tr = _Trainer(list(zip(meta["keys"], meta["shapes"])))
+    args = types.SimpleNamespace(prime_number=meta["p"], precision_parameter=meta["q_bits"], worker_num=N)
+
+    class WithMask(SecAggAggregator):
+        def aggregate_mask_reconstruction(self, active_clients, SS_rx, public_key_list):  # noqa: N803
+            return arrays["aggregate_mask"]
+
+    agg = WithMask(None, None, 0, {}, {}, {}, N, DEV, args, tr)
+    agg.get_global_model_params()
+    for i in range(N):
+        agg.add_local_trained_result(i, _np_dict(cl[i]), 1)
+    agg.flag_client_model_uploaded_dict = {i: bool(f) for i, f in enumerate(meta["flags"])}
+    out = agg.aggregate_model_reconstruction(list(range(N)), list(range(N)), None, None)
+    assert_dict_bits(OrderedDict((k, v.cpu()) for k, v in out.items()), exp, "secagg")
+    with pytest.raises(NotImplementedError):
+        SecAggAggregator(None, None, 0, {}, {}, {}, N, DEV, args, tr).aggregate_mask_reconstruction([], None, None)
+
+
+# ----------------------------------------------------------------------------- vs the C oracle
+def _adversarial(g, n, p):
+    v = torch.randint(0, p, (n,), generator=g, dtype=torch.int64)
+    sel = torch.randint(0, 8, (n,), generator=g)
+    big = torch.randint(-2 ** 62, 2 ** 62, (n,), generator=g, dtype=torch.int64) * 2
+    v = torch.where(sel == 1, -v, v)
+    v = torch.where(sel == 2, big, v)
+    v = torch.where(sel == 3, torch.full_like(v, 2 ** 63 - 1), v)
+    v = torch.where(sel == 4, torch.full_like(v, -2 ** 63), v)
+    v = torch.where(sel == 5, v + p, v)
+    return v
+
+
+@pytest.mark.parametrize("p", [2 ** 15 - 19, 2 ** 31 - 1, 2 ** 61 - 1, 2 ** 62 + 135, 2 ** 63 - 25, 7])
+@pytest.mark.parametrize("flags", [0, MOD_EACH, MOD_END, MOD_EACH | MOD_END, MOD_FIRST | MOD_EACH | MOD_END])
+@pytest.mark.parametrize("adversarial", [False, True])
+def test_finite_sum_vs_oracle(eng, p, flags, adversarial):
+    from oracle import orc
+    g = torch.Generator().manual_seed(p % 1000 + flags + 10 * adversarial)
+    k, n = 11, 70001  # 11 clients: the clamped last load group; ragged tail tile
+    if adversarial:
+        xs = [_adversarial(g, n, p) for _ in range(k)]
+        mask = _adversarial(g, n, p)
+    else:
+        xs = [torch.randint(0, p, (n,), generator=g, dtype=torch.int64) for _ in range(k)]
+        mask = torch.randint(0, p, (n,), generator=g, dtype=torch.int64)
+    q = 16
+    scale = 1 / k
+    ref_f, ref_r = orc.finite_sum(xs, p, flags, mask=mask, q_bits=q, scale=scale)
+    fin, real = eng.finite_sum([[x.to(DEV) for x in xs]], p, flags, masks=[mask.to(DEV)], q_bits=q, scale=scale)
+    assert torch.equal(fin[0].cpu(), ref_f)
+    assert bits_equal(real[0].cpu(), ref_r)
+    # no mask, float64 real output
+    ref_f, ref_r = orc.finite_sum(xs, p, flags | REAL_F64, q_bits=q)
+    fin, real = eng.finite_sum([[x.to(DEV) for x in xs]], p, flags | REAL_F64, q_bits=q)
+    assert torch.equal(fin[0].cpu(), ref_f)
+    assert bits_equal(real[0].cpu(), ref_r)
+
+
+def test_finite_sum_multi_segment_misaligned(eng):
+    """Many segments in one launch, some views 8-byte (not 16-byte) aligned -> scalar path."""
+    from oracle import orc
+    p = 2 ** 15 - 19
+    g = torch.Generator().manual_seed(5)
+    sizes = [1, 3, 512, 513, 4096, 1000, 0, 77]
+    k = 5
+    big = [torch.randint(0, p, (sum(sizes) + 16,), generator=g, dtype=torch.int64) for _ in range(k)]
+    masks_big = torch.randint(0, p, (sum(sizes) + 16,), generator=g, dtype=torch.int64)
+    segs, masks, pos = [], [], 1  # offset 1 element: misaligned
+    for s in sizes:
+        segs.append([b[pos:pos + s] for b in big])
+        masks.append(masks_big[pos:pos + s])
+        pos += s
+    fin, real = eng.finite_sum([[t.to(DEV) for t in seg] for seg in segs], p, MOD_END,
+                               masks=[m.to(DEV) for m in masks], q_bits=8, scale=0.2)
+    for seg, m, f, r in zip(segs, masks, fin, real):
+        rf, rr = orc.finite_sum(seg, p, MOD_END, mask=m, q_bits=8, scale=0.2) if seg[0].numel() else (
+            torch.empty(0, dtype=torch.int64), torch.empty(0))
+        assert torch.equal(f.cpu().reshape(-1), rf) and bits_equal(r.cpu().reshape(-1), rr)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.int64])
+@pytest.mark.parametrize("p,q", [(2 ** 15 - 19, 8), (2 ** 31 - 1, 16), (2 ** 61 - 1, 30), (2 ** 24 + 1, 0)])
+def test_finite_quantize_vs_oracle(eng, dtype, p, q):
+    from oracle import orc
+    g = torch.Generator().manual_seed(q + 3)
+    n = 50003
+    if dtype == torch.int64:
+        x = torch.randint(-2 ** 40, 2 ** 40, (n,), generator=g, dtype=torch.int64)
+        x[:4] = torch.tensor([2 ** 63 - 1, -2 ** 63, 0, -1])
+    else:
+        x = (torch.randn(n, generator=g, dtype=torch.float64) *
+             torch.exp2(torch.randint(-20, 40, (n,), generator=g).double())).to(dtype)
+        x[:8] = torch.tensor([float("nan"), float("inf"), -float("inf"), -0.0, 0.5 / 2 ** q, -1.5 / 2 ** q,
+                              2.0 ** 70, -2.0 ** 63 / 2 ** q], dtype=dtype)
+    mask = torch.randint(0, p, (n,), generator=g, dtype=torch.int64)
+    got = eng.finite_quantize([x.to(DEV)], p, q)[0].cpu()
+    assert torch.equal(got, orc.finite_quantize(x, p, q))
+    got = eng.finite_quantize([x.to(DEV)], p, q, masks=[mask.to(DEV)])[0].cpu()
+    assert torch.equal(got, orc.finite_quantize(x, p, q, mask=mask))
+
+
+@pytest.mark.parametrize("N,p", [(5, 2 ** 15 - 19), (16, 2 ** 15 - 19), (33, 2 ** 31 - 1), (8, 2 ** 61 - 1)])
+def test_lcc_decode_vs_oracle(eng, N, p):
+    from fedml_amd.core.mpc.lightsecagg import gen_Lagrange_coeffs
+    from oracle import orc
+    U, T = N, N // 2
+    m = 3001
+    g = torch.Generator().manual_seed(N)
+    F = torch.randint(0, p, (U, m), generator=g, dtype=torch.int64)
+    coef = gen_Lagrange_coeffs(np.arange(U) + N + 1, np.arange(N) + 1, p)
+    n_out = (U - T) * m - 5
+    got = eng.lcc_decode(coef.tolist(), F.to(DEV), p, n_out).cpu()
+    assert torch.equal(got, orc.lcc_decode(torch.from_numpy(coef), F, p, n_out))
+
+
+def test_lsa_round_trip_recovers_average(eng):
+    """Full protocol on device at a larger size: quantize + mask per client, sum, cancel the
+    decoded mask -> the average of the clients' fixed-point models (size-independent property)."""
+    from fedml_amd.core.mpc import lightsecagg as lsa
+    p, q, N = 2 ** 15 - 19, 6, 6
+    n = 300000
+    g = torch.Generator().manual_seed(9)
+    xs = [(torch.rand(n, generator=g) - 0.5).to(DEV) for _ in range(N)]
+    masks = [torch.randint(0, p, (n,), generator=g, dtype=torch.int64).to(DEV) for _ in range(N)]
+    masked = [eng.finite_quantize([x], p, q, masks=[m])[0] for x, m in zip(xs, masks)]
+    total_mask = eng.finite_sum([masks], p, MOD_EACH)[0][0]
+    _, real = eng.finite_sum([masked], p, MOD_END, masks=[total_mask], q_bits=q, scale=1 / N)
+    plain = eng.finite_sum([[eng.finite_quantize([x], p, q)[0] for x in xs]], p, MOD_EACH)[0][0]
+    expect = lsa.my_q_inv(plain, q, p).float() * np.float32(1 / N)
+    assert torch.equal(real[0], expect)
+    assert torch.allclose(real[0], torch.stack(xs).mean(0), atol=N * 2 ** -q)
+
+
+def test_finite_errors(eng):
+    from fedml_amd._native import FedAggNativeError
+    x = torch.zeros(10, dtype=torch.int64, device=DEV)
+    with pytest.raises(FedAggNativeError):
+        eng.finite_sum([[x]], 0, 0)  # prime must be > 0
+    with pytest.raises(FedAggNativeError):
+        eng.finite_sum([[x]], 7, 64)  # unknown flag
+    with pytest.raises(FedAggNativeError):
+        eng.finite_sum([[x]], 7, 0, finite=False, q_bits=63)
+    with pytest.raises(FedAggNativeError):
+        eng.finite_quantize([x], 7, -1)
+    with pytest.raises(TypeError):
+        eng.finite_quantize([x.half()], 7, 1)
+    with pytest.raises(FedAggNativeError):
+        eng.lcc_decode([[1, 2]], torch.zeros((2, 3), dtype=torch.int64, device=DEV), 7, 7)  # n_out > rows*m

@@ -9,12 +9,12 @@ import numpy as np
 import pytest
 import torch
 
-from golden_io import client_dicts, expected_dicts, list_cases, load_case
+from golden_io import aggregation_cases, client_dicts, expected_dicts, list_cases, load_case
 from refcases import MUL_N_DIV_N, MUL_W, SUM, assert_dict_bits, bits_equal, check_case
 
 pytestmark = pytest.mark.gpu
 
-CASES = [p for p in list_cases() if "topologies" not in p and "fedopt" not in p]
+CASES = aggregation_cases()
 
 
 @pytest.fixture(scope="module")

@@ -12,13 +12,15 @@ import torch
 from conftest import ROOT, gpu_available
 from fedml_amd import _native as N
 
-HDR = os.path.join(ROOT, "include", "fedagg.h")
+HDRS = [os.path.join(ROOT, "include", h) for h in ("fedagg.h", "fedagg_finite.h")]
 
 
 def declared_functions():
-    src = open(HDR).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(fa_[a-z_]+)\s*\(", src)))
+    fns = set()
+    for h in HDRS:
+        src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
+        fns |= set(re.findall(r"\b(fa_[a-z_]+)\s*\(", src))
+    return sorted(fns)
 
 
 def test_header_declares_expected_entry_points():
@@ -54,6 +56,12 @@ def test_invalid_arguments_return_codes_without_device():
     rc = L.fa_ctx_create(0, None)
     assert rc == N.FA_ERR_INVALID
     rc = L.fa_mix(None, N.F32, 10, 1, None, None, None, 1, None, None, None, None, None)
+    assert rc == N.FA_ERR_INVALID
+    rc = L.fa_finite_sum(None, 1, None, 1, None, None, 7, 0, None, 0, 1.0, None, None)
+    assert rc == N.FA_ERR_INVALID
+    rc = L.fa_finite_quantize(None, N.F32, 1, None, None, None, 7, 8, None, None)
+    assert rc == N.FA_ERR_INVALID
+    rc = L.fa_lcc_decode(None, 1, 1, 1, None, None, 7, 1, None, None)
     assert rc == N.FA_ERR_INVALID
 
 

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from golden_io import client_dicts, expected_dicts, list_cases, load_case
+from golden_io import aggregation_cases, client_dicts, expected_dicts, list_cases, load_case
 from refcases import assert_dict_bits, check_case, dsgd_csr
 
 from oracle import orc, torch_port
@@ -32,7 +32,7 @@ class _Orc:
     mix = staticmethod(orc.mix)
 
 
-GENERIC = [p for p in CASES if "topologies" not in p and "fedopt" not in p]
+GENERIC = aggregation_cases()
 FEDOPT = [p for p in CASES if "fedopt" in p]
 
 

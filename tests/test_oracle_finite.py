@@ -1,0 +1,143 @@
+"""Pin the finite-field oracle (oracle/finite_oracle.c) to the reference's SecAgg / LightSecAgg
+fixtures g11-g15 bit-for-bit (CPU only); also checks the product's host-side Lagrange
+coefficients (pure Python, no device) through the LCC decoding fixture."""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from golden_io import client_dicts, expected_dicts, list_cases, load_case
+from refcases import MOD_EACH, MOD_END, REAL_F64, assert_dict_bits, bits_equal, sa_order_and_flags
+
+from oracle import orc
+
+CASES = list_cases()
+FIN = {kind: [p for p in CASES if os.path.basename(p).startswith(kind)] for kind in
+       ("g11_", "g12_", "g13_", "g14_", "g15_")}
+ids = lambda p: os.path.basename(p)[:-4]  # noqa: E731
+
+
+def test_inventory():
+    for kind, paths in FIN.items():
+        assert len(paths) >= 3, kind
+
+
+@pytest.mark.parametrize("path", FIN["g11_"], ids=ids)
+def test_finite_sum_matches_golden(path):
+    meta, arrays = load_case(path)
+    cl = client_dicts(meta, arrays)
+    exp = expected_dicts(meta, arrays)[0]
+    for k in meta["keys"]:
+        fin, _ = orc.finite_sum([c[k].reshape(-1) for c in cl], meta["p"], MOD_EACH)
+        assert torch.equal(fin.reshape(exp[k].shape), exp[k]), k
+
+
+@pytest.mark.parametrize("path", FIN["g12_"], ids=ids)
+def test_quantize_and_masking_match_golden(path):
+    meta, arrays = load_case(path)
+    x = client_dicts(meta, arrays)[0]
+    q_out, masked = expected_dicts(meta, arrays)
+    mask = torch.from_numpy(arrays["mask"].reshape(-1))
+    pos = 0
+    for k in meta["keys"]:
+        n = x[k].numel()
+        got = orc.finite_quantize(x[k].reshape(-1), meta["p"], meta["q_bits"])
+        assert torch.equal(got.reshape(q_out[k].shape), q_out[k]), k
+        got_m = orc.finite_quantize(x[k].reshape(-1), meta["p"], meta["q_bits"], mask=mask[pos:pos + n])
+        assert torch.equal(got_m.reshape(masked[k].shape), masked[k]), k
+        pos += n
+
+
+@pytest.mark.parametrize("path", FIN["g13_"], ids=ids)
+def test_dequantize_matches_golden(path):
+    meta, arrays = load_case(path)
+    x = client_dicts(meta, arrays)[0]
+    exp = expected_dicts(meta, arrays)[0]
+    for k in meta["keys"]:
+        _, real = orc.finite_sum([x[k].reshape(-1)], meta["p"], 0, q_bits=meta["q_bits"], scale=1.0)
+        assert bits_equal(real, exp[k].reshape(-1)), k
+        # my_q_inv's float64, rounded to float32, is the same value
+        _, r64 = orc.finite_sum([x[k].reshape(-1)], meta["p"], REAL_F64, q_bits=meta["q_bits"])
+        assert r64.dtype == torch.float64 and bits_equal(r64.float(), exp[k].reshape(-1)), k
+
+
+def _lsa_mask(meta, arrays):
+    from fedml_amd.core.mpc.lightsecagg import gen_Lagrange_coeffs  # host-side product code (pure Python)
+    N, U = meta["N"], meta["U"]
+    alpha_s = np.arange(N) + 1
+    beta_s = np.arange(U) + (N + 1)
+    coef = torch.from_numpy(gen_Lagrange_coeffs(beta_s, alpha_s[list(range(N))], meta["p"]))
+    F = torch.from_numpy(arrays["F"])
+    return orc.lcc_decode(coef, F, meta["p"], meta["d"])
+
+
+@pytest.mark.parametrize("path", FIN["g14_"], ids=ids)
+def test_lsa_mask_decoding_matches_golden(path):
+    meta, arrays = load_case(path)
+    got = _lsa_mask(meta, arrays)
+    assert torch.equal(got, torch.from_numpy(arrays["aggregate_mask"]))
+
+
+@pytest.mark.parametrize("path", FIN["g14_"], ids=ids)
+def test_lsa_reconstruction_matches_golden(path):
+    meta, arrays = load_case(path)
+    cl = client_dicts(meta, arrays)
+    exp = expected_dicts(meta, arrays)[0]
+    mask = torch.from_numpy(arrays["aggregate_mask"])
+    pos = 0
+    for k, d in zip(meta["keys"], meta["dims"]):
+        _, real = orc.finite_sum([c[k].reshape(-1) for c in cl], meta["p"], MOD_END, mask=mask[pos:pos + d],
+                                 q_bits=meta["q_bits"], scale=1 / meta["N"])
+        assert bits_equal(real, exp[k].reshape(-1)), k
+        pos += d
+
+
+@pytest.mark.parametrize("path", FIN["g15_"], ids=ids)
+def test_sa_reconstruction_matches_golden(path):
+    meta, arrays = load_case(path)
+    cl = client_dicts(meta, arrays)
+    exp = expected_dicts(meta, arrays)[0]
+    order, flags = sa_order_and_flags(meta["flags"])
+    mask = torch.from_numpy(arrays["aggregate_mask"])
+    pos = 0
+    for k, d in zip(meta["keys"], meta["dims"]):
+        _, real = orc.finite_sum([cl[i][k].reshape(-1) for i in order], meta["p"], flags, mask=mask[pos:pos + d],
+                                 q_bits=meta["q_bits"], scale=1 / meta["num_clients"])
+        assert bits_equal(real, exp[k].reshape(-1)), k
+        pos += d
+
+
+def test_lagrange_coeffs_wrap_like_numpy():
+    """The host coefficients reproduce the reference's int64 overflow for a large prime: the
+    decoded mask of the p = 2^31-1 fixture is NOT the true mask sum, and still matches."""
+    path = [p for p in FIN["g14_"] if "2147483647" in p][0]
+    meta, arrays = load_case(path)
+    assert torch.equal(_lsa_mask(meta, arrays), torch.from_numpy(arrays["aggregate_mask"]))
+
+
+def test_flag_codes_match_public_header():
+    import re
+    from conftest import ROOT
+    from fedml_amd import _native as N
+    hdr = open(os.path.join(ROOT, "include", "fedagg_finite.h")).read()
+    want = {"FA_FINITE_MOD_FIRST": (orc.MOD_FIRST, N.MOD_FIRST), "FA_FINITE_MOD_EACH": (orc.MOD_EACH, N.MOD_EACH),
+            "FA_FINITE_MOD_END": (orc.MOD_END, N.MOD_END), "FA_FINITE_REAL_F64": (orc.REAL_F64, N.REAL_F64)}
+    for name, (a, b) in want.items():
+        m = re.search(rf"\b{name}\s*=\s*(\d+)", hdr)
+        assert m and int(m.group(1)) == a == b, name
+
+
+@pytest.mark.parametrize("path", FIN["g14_"], ids=ids)
+def test_numpy_port_matches_golden(path):
+    """oracle/secagg_port.py (bench.py's CPU baseline for the secagg config) reproduces g14."""
+    from oracle import secagg_port
+    meta, arrays = load_case(path)
+    cl = client_dicts(meta, arrays)
+    exp = expected_dicts(meta, arrays)[0]
+    models = [{k: v.numpy() for k, v in c.items()} for c in cl]
+    got = secagg_port.lsa_reconstruct(models, arrays["aggregate_mask"], meta["dims"], meta["p"], meta["q_bits"])
+    for k in meta["keys"]:
+        assert bits_equal(got[k].reshape(-1), exp[k].reshape(-1)), k
