@@ -76,6 +76,15 @@ __device__ __forceinline__ long long mod_any(long long a, const ModP& m) {
   const long long r = a % m.p;
   return r < 0 ? r + m.p : r;
 }
+
+// np.mod(a, p) for 0 <= a < 2^53 (no division routine)
+__device__ __forceinline__ long long mod_nonneg53(long long a, const ModP& m) {
+  const double q = floor(__dmul_rn((double)a, m.inv_p));
+  long long r = a - (long long)q * m.p;
+  if (r < 0) r += m.p;
+  else if (r >= m.p) r -= m.p;
+  return r;
+}
 // np.mod(a + b, p) with wrapping a + b
 __device__ __forceinline__ long long mod_add(long long a, long long b, const ModP& m) {
   if (m.small && (unsigned long long)a < (unsigned long long)m.p && (unsigned long long)b < (unsigned long long)m.p) {
@@ -124,10 +133,8 @@ __device__ __forceinline__ long long step(long long acc, long long x, const ModP
   else return wadd(acc, x);
 }
 
-template <bool EACH>
-__device__ __forceinline__ void finish(long long& acc, const FSeg& sg, int64_t e, int flags, const ModP& m) {
-  if (sg.mask) {
-    const long long mk = sg.mask[e];
+__device__ __forceinline__ void finish(long long& acc, bool has_mask, long long mk, int flags, const ModP& m) {
+  if (has_mask) {
     acc = (flags & FA_FINITE_MOD_END) ? mod_sub(acc, mk, m) : wsub(acc, mk);
   } else if (flags & FA_FINITE_MOD_END) {
     acc = mod_any(acc, m);
@@ -149,6 +156,8 @@ k_finite_sum(const FSeg* __restrict__ segs, int nseg, const void* const* __restr
     const int64_t e0 = base + (int64_t)threadIdx.x * kV;
     const int64_t boff = e0 * 8;
     long long a0 = 0, a1 = 0;
+    // the mask is needed only at the end: issue its load first, it lands while the clients stream
+    const u32x4 mk = sg.mask ? __builtin_nontemporal_load((gp_u32x4)(sg.mask + e0)) : u32x4{0, 0, 0, 0};
     for (int i0 = 0; i0 < k; i0 += kU) {
       u32x4 r[kU];
 #pragma unroll
@@ -171,8 +180,8 @@ k_finite_sum(const FSeg* __restrict__ segs, int nseg, const void* const* __restr
         }
       }
     }
-    finish<EACH>(a0, sg, e0, flags, m);
-    finish<EACH>(a1, sg, e0 + 1, flags, m);
+    finish(a0, sg.mask != nullptr, lo64(mk), flags, m);
+    finish(a1, sg.mask != nullptr, hi64(mk), flags, m);
     if (sg.out_fin) __builtin_nontemporal_store(pack64(a0, a1), (gpw_u32x4)(sg.out_fin + e0));
     if (sg.out_real) {
       if (flags & FA_FINITE_REAL_F64) {
@@ -188,7 +197,7 @@ k_finite_sum(const FSeg* __restrict__ segs, int nseg, const void* const* __restr
       long long acc = ((const long long*)in[0])[e];
       if (first) acc = mod_any(acc, m);
       for (int i = 1; i < k; ++i) acc = step<EACH>(acc, ((const long long*)in[i])[e], m);
-      finish<EACH>(acc, sg, e, flags, m);
+      finish(acc, sg.mask != nullptr, sg.mask ? sg.mask[e] : 0, flags, m);
       if (sg.out_fin) sg.out_fin[e] = acc;
       if (sg.out_real) {
         if (flags & FA_FINITE_REAL_F64) ((double*)sg.out_real)[e] = dequant64(acc, dq);
@@ -274,35 +283,22 @@ k_finite_quant(const QSeg* __restrict__ segs, int nseg, QParams qp, ModP m) {
 }
 
 // ---------------------------------------------------------------------------------- LCC decode
-constexpr int kRB = 8;  // output rows per register block
+// General path: exact int64 (wrapping) multiply-accumulate, RB output rows per register block.
+constexpr int kRB = 8;
 
-__global__ void __launch_bounds__(kBlock)
-k_lcc_decode(const long long* __restrict__ coef, int rows_needed, int k, int64_t m_cols,
-             const long long* __restrict__ f, int64_t n_out, long long* __restrict__ out, ModP md) {
-  const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-  const bool live = c < m_cols;
-  const int64_t cc = live ? c : m_cols - 1;  // clamped column: loads stay in bounds
-  for (int j0 = 0; j0 < rows_needed; j0 += kRB) {
+__device__ __forceinline__ void lcc_rows_i64(const long long* __restrict__ coef, int j0, int j1, int k, int64_t m_cols,
+                                             const long long* __restrict__ f, int64_t c, int64_t cc, bool live,
+                                             int64_t n_out, long long* __restrict__ out, const ModP& md) {
+  for (; j0 < j1; j0 += kRB) {
     unsigned long long acc[kRB];
 #pragma unroll
     for (int r = 0; r < kRB; ++r) acc[r] = 0;
-    int i = 0;
-    for (; i + 4 <= k; i += 4) {
-      unsigned long long fv[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) fv[u] = (unsigned long long)f[(int64_t)(i + u) * m_cols + cc];
-#pragma unroll
-      for (int r = 0; r < kRB; ++r) {
-        const int j = min(j0 + r, rows_needed - 1);  // uniform clamp; extra rows are never stored
-#pragma unroll
-        for (int u = 0; u < 4; ++u) acc[r] += (unsigned long long)coef[(int64_t)j * k + i + u] * fv[u];
-      }
-    }
-    for (; i < k; ++i) {
+#pragma unroll 4
+    for (int i = 0; i < k; ++i) {
       const unsigned long long fv = (unsigned long long)f[(int64_t)i * m_cols + cc];
 #pragma unroll
       for (int r = 0; r < kRB; ++r) {
-        const int j = min(j0 + r, rows_needed - 1);
+        const int j = min(j0 + r, j1 - 1);  // uniform clamp; extra rows are never stored
         acc[r] += (unsigned long long)coef[(int64_t)j * k + i] * fv;
       }
     }
@@ -310,7 +306,78 @@ k_lcc_decode(const long long* __restrict__ coef, int rows_needed, int k, int64_t
 #pragma unroll
       for (int r = 0; r < kRB; ++r) {
         const int64_t e = (int64_t)(j0 + r) * m_cols + c;
-        if (j0 + r < rows_needed && e < n_out) out[e] = mod_any((long long)acc[r], md);
+        if (j0 + r < j1 && e < n_out) out[e] = mod_any((long long)acc[r], md);
+      }
+    }
+  }
+}
+
+// redo: when non-null, only the blocks the float64 kernel flagged are (re)computed here.
+__global__ void __launch_bounds__(kBlock)
+k_lcc_decode(const long long* __restrict__ coef, int rows_needed, int k, int64_t m_cols,
+             const long long* __restrict__ f, int64_t n_out, long long* __restrict__ out, ModP md,
+             const int* __restrict__ redo) {
+  if (redo && !redo[blockIdx.x]) return;
+  const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool live = c < m_cols;
+  lcc_rows_i64(coef, 0, rows_needed, k, m_cols, f, c, live ? c : m_cols - 1, live, n_out, out, md);
+}
+
+// Fast path when every partial sum is an exactly representable double: coefficients in [0, p)
+// (checked on the host), (p-1)^2 * k < 2^53 (host) and every f in [0, p) (checked per lane while
+// streaming; a block that meets an out-of-range value flags itself in `redo`, and k_lcc_decode,
+// launched right after on the same stream, recomputes exactly those blocks on the int64 path).  Then
+// fma(c, f, acc) is exact integer arithmetic and float64 FMA -- full rate on CDNA4 -- replaces the
+// ~6-instruction int64 multiply.  Coefficients are transposed per pass ([pass][i][RB]) so the RB
+// wave-uniform values of one i are adjacent scalar loads.
+constexpr int kRBF = 32;
+
+__global__ void __launch_bounds__(kBlock)
+k_lcc_decode_f64(const double* __restrict__ coefT, int rows_needed, int k, int64_t m_cols,
+                 const long long* __restrict__ f, int64_t n_out, long long* __restrict__ out, ModP md,
+                 int* __restrict__ redo) {
+  const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+  const bool live = c < m_cols;
+  const int64_t cc = live ? c : m_cols - 1;  // clamped column: loads stay in bounds
+  const unsigned long long up = (unsigned long long)md.p;
+  for (int j0 = 0; j0 < rows_needed; j0 += kRBF) {
+    const double* __restrict__ cT = coefT + (int64_t)(j0 / kRBF) * k * kRBF;
+    double acc[kRBF];
+#pragma unroll
+    for (int r = 0; r < kRBF; ++r) acc[r] = 0.0;
+    bool ok = true;
+    // f loads run kPF rows ahead (register ring) so a wave keeps kPF loads in flight while its
+    // FMAs consume the current row; the empty asm keeps the compiler from hoisting the next
+    // rows' scalar coefficient loads (kRBF SGPR pairs each) above the current FMAs.
+    constexpr int kPF = 4;
+    unsigned long long ring[kPF];
+#pragma unroll
+    for (int u = 0; u < kPF; ++u) ring[u] = (unsigned long long)f[(int64_t)min(u, k - 1) * m_cols + cc];
+    for (int i0 = 0; i0 < k; i0 += kPF) {
+#pragma unroll
+      for (int u = 0; u < kPF; ++u) {
+        const int i = i0 + u;
+        const unsigned long long fv = ring[u];
+        ring[u] = (unsigned long long)f[(int64_t)min(i + kPF, k - 1) * m_cols + cc];
+        if (i < k) {  // wave-uniform
+          ok = ok && fv < up;
+          const double fd = (double)(unsigned)fv;
+#pragma unroll
+          for (int r = 0; r < kRBF; ++r) acc[r] = __fma_rn(cT[i * kRBF + r], fd, acc[r]);
+        }
+        asm volatile("" ::: "memory");
+      }
+    }
+    const int j1 = min(j0 + kRBF, rows_needed);
+    if (__ballot(!ok) != 0) {  // wave-uniform: hand the block to the int64 kernel
+      if (threadIdx.x % 64 == 0) redo[blockIdx.x] = 1;
+      return;
+    }
+    if (live) {
+#pragma unroll
+      for (int r = 0; r < kRBF; ++r) {
+        const int64_t e = (int64_t)(j0 + r) * m_cols + c;
+        if (j0 + r < j1 && e < n_out) out[e] = mod_nonneg53((long long)acc[r], md);
       }
     }
   }
@@ -385,7 +452,7 @@ int fa_finite_sum(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, i
       hp[(int64_t)j * k + i] = p;
       aligned = aligned && al16(p);
     }
-    sg.aligned = aligned ? 1 : 0;
+    sg.aligned = (aligned && (!sg.mask || al16(sg.mask))) ? 1 : 0;
     hs[j] = sg;
     t0 += (n + kTile - 1) / kTile;
     ++j;
@@ -486,18 +553,47 @@ int fa_lcc_decode(fa_ctx* ctx, int32_t rows, int32_t k, int64_t m, const int64_t
   const int rows_needed = (int)((n_out + m - 1) / m);
   const int64_t blocks = (m + kBlock - 1) / kBlock;
   if (blocks > 0x7FFFFFFFll) return fail(FA_ERR_INVALID, "too many columns");
-  const size_t bytes = sizeof(int64_t) * (size_t)rows_needed * k;
+  // float64 path precondition: coefficients in [0, p) and (p-1)^2 * k < 2^53
+  bool f64 = (unsigned __int128)(prime - 1) * (unsigned __int128)(prime - 1) * (unsigned __int128)k <
+             ((unsigned __int128)1 << 53);
+  for (int64_t t = 0; f64 && t < (int64_t)rows_needed * k; ++t) f64 = coef[t] >= 0 && coef[t] < prime;
+  const int passes = (rows_needed + kRBF - 1) / kRBF;
+  const size_t i64_bytes = align16(sizeof(int64_t) * (size_t)rows_needed * k);
+  const size_t f64_bytes = f64 ? align16(sizeof(double) * (size_t)passes * k * kRBF) : 0;
+  const size_t redo_bytes = f64 ? sizeof(int) * (size_t)blocks : 0;
+  const size_t bytes = i64_bytes + f64_bytes + redo_bytes;
   DeviceGuard g(ctx->device);
   if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
   hipStream_t st = (hipStream_t)hip_stream;
   fa_ctx::Slot* slot = nullptr;
   int rc = acquire_slot(ctx, bytes, &slot);
   if (rc) return rc;
-  memcpy(slot->host, coef, bytes);
+  char* h = (char*)slot->host;
+  memcpy(h, coef, sizeof(int64_t) * (size_t)rows_needed * k);
+  if (f64) {
+    double* cT = (double*)(h + i64_bytes);
+    for (int ps = 0; ps < passes; ++ps)
+      for (int i = 0; i < k; ++i)
+        for (int r = 0; r < kRBF; ++r) {
+          const int j = ps * kRBF + r;
+          cT[((int64_t)ps * k + i) * kRBF + r] = j < rows_needed ? (double)coef[(int64_t)j * k + i] : 0.0;
+        }
+  }
   rc = stage(slot, bytes, st);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_lcc_decode, dim3((unsigned)blocks), dim3(kBlock), 0, st, (const long long*)slot->dev,
-                     rows_needed, k, m, (const long long*)d_f, n_out, (long long*)d_out, make_modp(prime));
+  char* dv = (char*)slot->dev;
+  const ModP mp = make_modp(prime);
+  if (f64 && ctx->variant != 1) {  // variant 1 forces the int64 path (A/B and test hook)
+    int* redo = (int*)(dv + i64_bytes + f64_bytes);
+    FA_HIP(hipMemsetAsync(redo, 0, redo_bytes, st));
+    hipLaunchKernelGGL(k_lcc_decode_f64, dim3((unsigned)blocks), dim3(kBlock), 0, st, (const double*)(dv + i64_bytes),
+                       rows_needed, k, m, (const long long*)d_f, n_out, (long long*)d_out, mp, redo);
+    hipLaunchKernelGGL(k_lcc_decode, dim3((unsigned)blocks), dim3(kBlock), 0, st, (const long long*)dv,
+                       rows_needed, k, m, (const long long*)d_f, n_out, (long long*)d_out, mp, (const int*)redo);
+  } else {
+    hipLaunchKernelGGL(k_lcc_decode, dim3((unsigned)blocks), dim3(kBlock), 0, st, (const long long*)dv,
+                       rows_needed, k, m, (const long long*)d_f, n_out, (long long*)d_out, mp, (const int*)nullptr);
+  }
   FA_HIP(hipGetLastError());
   return release(slot, st);
 }

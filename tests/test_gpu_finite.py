@@ -295,3 +295,27 @@ def test_finite_errors(eng):
         eng.finite_quantize([x.half()], 7, 1)
     with pytest.raises(FedAggNativeError):
         eng.lcc_decode([[1, 2]], torch.zeros((2, 3), dtype=torch.int64, device=DEV), 7, 7)  # n_out > rows*m
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_lcc_decode_redo_and_int64_paths(eng, variant):
+    """Out-of-range encoded-mask values in a few blocks: the float64 kernel hands those blocks to
+    the int64 kernel (redo flags); variant 1 forces the int64 kernel everywhere."""
+    from fedml_amd.core.mpc.lightsecagg import gen_Lagrange_coeffs
+    from oracle import orc
+    N, p = 12, 2 ** 15 - 19
+    U, T = N, N // 2
+    m = 5000
+    g = torch.Generator().manual_seed(3)
+    F = torch.randint(0, p, (U, m), generator=g, dtype=torch.int64)
+    F[3, 1000] = -5
+    F[0, 4999] = p + 7
+    F[7, 300] = 2 ** 62 + 11
+    coef = gen_Lagrange_coeffs(np.arange(U) + N + 1, np.arange(N) + 1, p)
+    n_out = (U - T) * m
+    try:
+        eng.set_variant(variant)
+        got = eng.lcc_decode(coef.tolist(), F.to(DEV), p, n_out).cpu()
+    finally:
+        eng.set_variant(0)
+    assert torch.equal(got, orc.lcc_decode(torch.from_numpy(coef), F, p, n_out))
