@@ -402,8 +402,9 @@ def wl_secagg(args, eng, rank, world, timer):
     U, T = K, K // 2
     m = -(-P // (U - T))
     g = torch.Generator(device="cuda").manual_seed(11)
-    arena = torch.randint(0, p, (K, P), generator=g, dtype=torch.int64, device="cuda")
-    xs = [arena[i] for i in range(K)]
+    Ppad = -(-P // 64) * 64  # rows 512-byte aligned, as ClientArena lays them out (fedml_amd/arena.py)
+    arena = torch.randint(0, p, (K, Ppad), generator=g, dtype=torch.int64, device="cuda")
+    xs = [arena[i, :P] for i in range(K)]
     F = torch.randint(0, p, (U, m), generator=g, dtype=torch.int64, device="cuda")
     coef = gen_Lagrange_coeffs(np.arange(U) + K + 1, np.arange(K) + 1, p).tolist()
     state = {}

@@ -326,54 +326,56 @@ k_lcc_decode(const long long* __restrict__ coef, int rows_needed, int k, int64_t
 // Fast path when every partial sum is an exactly representable double: coefficients in [0, p)
 // (checked on the host), (p-1)^2 * k < 2^53 (host) and every f in [0, p) (checked per lane while
 // streaming; a block that meets an out-of-range value flags itself in `redo`, and k_lcc_decode,
-// launched right after on the same stream, recomputes exactly those blocks on the int64 path).  Then
-// fma(c, f, acc) is exact integer arithmetic and float64 FMA -- full rate on CDNA4 -- replaces the
-// ~6-instruction int64 multiply.  Coefficients are transposed per pass ([pass][i][RB]) so the RB
-// wave-uniform values of one i are adjacent scalar loads.
+// launched right after on the same stream, recomputes exactly those blocks on the int64 path).
+// Then fma(c, f, acc) is exact integer arithmetic and float64 FMA -- full rate on CDNA4 -- replaces
+// the ~6-instruction int64 multiply.  The coefficients of one pass (kRBF rows x up to kLdsI rows of
+// f, transposed: [i][r]) are staged once per block in LDS and read as wave-wide broadcasts; the f
+// loads run kPF rows ahead in a register ring.
 constexpr int kRBF = 32;
+constexpr int kLdsI = 128;  // f rows per LDS chunk: 128 x 32 doubles = 32 KiB
 
 __global__ void __launch_bounds__(kBlock)
 k_lcc_decode_f64(const double* __restrict__ coefT, int rows_needed, int k, int64_t m_cols,
                  const long long* __restrict__ f, int64_t n_out, long long* __restrict__ out, ModP md,
                  int* __restrict__ redo) {
+  __shared__ double cs[kLdsI * kRBF];
   const int64_t c = (int64_t)blockIdx.x * kBlock + threadIdx.x;
   const bool live = c < m_cols;
   const int64_t cc = live ? c : m_cols - 1;  // clamped column: loads stay in bounds
   const unsigned long long up = (unsigned long long)md.p;
+  constexpr int kPF = 4;
+  bool ok = true;
   for (int j0 = 0; j0 < rows_needed; j0 += kRBF) {
     const double* __restrict__ cT = coefT + (int64_t)(j0 / kRBF) * k * kRBF;
     double acc[kRBF];
 #pragma unroll
     for (int r = 0; r < kRBF; ++r) acc[r] = 0.0;
-    bool ok = true;
-    // f loads run kPF rows ahead (register ring) so a wave keeps kPF loads in flight while its
-    // FMAs consume the current row; the empty asm keeps the compiler from hoisting the next
-    // rows' scalar coefficient loads (kRBF SGPR pairs each) above the current FMAs.
-    constexpr int kPF = 4;
-    unsigned long long ring[kPF];
+    for (int ib = 0; ib < k; ib += kLdsI) {
+      const int ni = min(kLdsI, k - ib);
+      __syncthreads();  // previous chunk fully consumed
+      for (int t = threadIdx.x; t < ni * kRBF; t += kBlock) cs[t] = cT[(int64_t)ib * kRBF + t];
+      __syncthreads();
+      unsigned long long ring[kPF];
 #pragma unroll
-    for (int u = 0; u < kPF; ++u) ring[u] = (unsigned long long)f[(int64_t)min(u, k - 1) * m_cols + cc];
-    for (int i0 = 0; i0 < k; i0 += kPF) {
+      for (int u = 0; u < kPF; ++u) ring[u] = (unsigned long long)f[(int64_t)(ib + min(u, ni - 1)) * m_cols + cc];
+      for (int i0 = 0; i0 < ni; i0 += kPF) {
 #pragma unroll
-      for (int u = 0; u < kPF; ++u) {
-        const int i = i0 + u;
-        const unsigned long long fv = ring[u];
-        ring[u] = (unsigned long long)f[(int64_t)min(i + kPF, k - 1) * m_cols + cc];
-        if (i < k) {  // wave-uniform
-          ok = ok && fv < up;
-          const double fd = (double)(unsigned)fv;
+        for (int u = 0; u < kPF; ++u) {
+          const int i = i0 + u;
+          const unsigned long long fv = ring[u];
+          ring[u] = (unsigned long long)f[(int64_t)(ib + min(i + kPF, ni - 1)) * m_cols + cc];
+          if (i < ni) {  // wave-uniform
+            ok = ok && fv < up;
+            const double fd = (double)(unsigned)fv;
 #pragma unroll
-          for (int r = 0; r < kRBF; ++r) acc[r] = __fma_rn(cT[i * kRBF + r], fd, acc[r]);
+            for (int r = 0; r < kRBF; ++r) acc[r] = __fma_rn(cs[i * kRBF + r], fd, acc[r]);
+          }
         }
-        asm volatile("" ::: "memory");
       }
     }
     const int j1 = min(j0 + kRBF, rows_needed);
-    if (__ballot(!ok) != 0) {  // wave-uniform: hand the block to the int64 kernel
-      if (threadIdx.x % 64 == 0) redo[blockIdx.x] = 1;
-      return;
-    }
-    if (live) {
+    const bool wave_ok = __ballot(!ok) == 0;  // every lane votes (no short-circuit around the ballot)
+    if (live && wave_ok) {
 #pragma unroll
       for (int r = 0; r < kRBF; ++r) {
         const int64_t e = (int64_t)(j0 + r) * m_cols + c;
@@ -381,6 +383,9 @@ k_lcc_decode_f64(const double* __restrict__ coefT, int rows_needed, int k, int64
       }
     }
   }
+  // every wave stays to the end (the block shares LDS and barriers); a wave that saw an
+  // out-of-range f hands the block to the int64 kernel
+  if (__ballot(!ok) != 0 && threadIdx.x % 64 == 0) redo[blockIdx.x] = 1;
 }
 
 ModP make_modp(int64_t p) {
