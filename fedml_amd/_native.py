@@ -31,6 +31,8 @@ EXPORTED_SYMBOLS = (
     "fa_ctx_set_mix_band", "fa_strerror", "fa_last_error",
     # include/fedagg_finite.h
     "fa_finite_sum", "fa_finite_quantize", "fa_lcc_decode",
+    # include/fedagg_robust.h
+    "fa_coord_median", "fa_pairwise_sqdist", "fa_pairwise_sqdist_scratch_bytes",
 )
 
 MOD_FIRST, MOD_EACH, MOD_END, REAL_F64 = 1, 2, 4, 8  # enum fa_finite_flags
@@ -87,6 +89,12 @@ def _declare(L):
     L.fa_lcc_decode.restype = ctypes.c_int
     L.fa_lcc_decode.argtypes = [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, _P_i64, _vp, ctypes.c_int64,
                                 ctypes.c_int64, _vp, _vp]
+    L.fa_coord_median.restype = ctypes.c_int
+    L.fa_coord_median.argtypes = [_vp, ctypes.c_int, ctypes.c_int32, _P_i64, ctypes.c_int32, _P_vp, _P_vp, _vp]
+    L.fa_pairwise_sqdist.restype = ctypes.c_int
+    L.fa_pairwise_sqdist.argtypes = [_vp, ctypes.c_int32, _P_i64, ctypes.c_int32, _P_vp, _vp, _vp, ctypes.c_size_t, _vp]
+    L.fa_pairwise_sqdist_scratch_bytes.restype = ctypes.c_size_t
+    L.fa_pairwise_sqdist_scratch_bytes.argtypes = [ctypes.c_int32, _P_i64, ctypes.c_int32]
     L.fa_strerror.restype = ctypes.c_char_p
     L.fa_strerror.argtypes = [ctypes.c_int]
     L.fa_last_error.restype = ctypes.c_char_p

@@ -380,6 +380,68 @@ class AggEngine:
         N.check(rc, "fa_lcc_decode")
         return out
 
+    # ------------------------------------------------------------------ robust aggregation
+    def coord_median(self, segments: Sequence[Sequence[torch.Tensor]],
+                     outs: Optional[Sequence[torch.Tensor]] = None, stream=None) -> List[torch.Tensor]:
+        """Coordinate-wise median over clients (fa_coord_median): segments[s][i] = client i's
+        tensor of segment s (one dtype: float32, bfloat16, float16, float64); one launch."""
+        k = len(segments[0]) if segments else 0
+        if k == 0:
+            raise ValueError("coord_median: no client tensors")
+        dt = segments[0][0].dtype
+        if dt not in (torch.float32, torch.bfloat16, torch.float16, torch.float64):
+            raise TypeError(f"coord_median: unsupported dtype {dt}")
+        in_ptrs, numels, results = [], [], []
+        for s, seg in enumerate(segments):
+            if len(seg) != k:
+                raise ValueError(f"segment {s}: {len(seg)} clients, expected {k}")
+            for i, t in enumerate(seg):
+                if t.dtype != dt or t.shape != seg[0].shape:
+                    raise ValueError(f"segment {s} client {i}: dtype/shape mismatch")
+                _require_device(t, self.device, f"segment {s} client {i}")
+                in_ptrs.append(t.data_ptr())
+            if outs is not None:
+                o = outs[s]
+                if o.dtype != dt or o.numel() != seg[0].numel():
+                    raise ValueError(f"segment {s}: output must be {dt} with {seg[0].numel()} elements")
+                _require_device(o, self.device, f"segment {s} output")
+            else:
+                o = torch.empty(seg[0].shape, dtype=dt, device=self.device)
+            results.append(o)
+            numels.append(seg[0].numel())
+        rc = self._lib.fa_coord_median(self._ctx, DTYPE_CODE[dt], len(segments), N.i64_array(numels), k,
+                                       N.ptr_array(in_ptrs), N.ptr_array([o.data_ptr() for o in results]),
+                                       self._stream(stream))
+        N.check(rc, "fa_coord_median")
+        return results
+
+    def pairwise_sqdist(self, segments: Sequence[Sequence[torch.Tensor]], stream=None) -> torch.Tensor:
+        """K x K float64 matrix of squared Euclidean distances between the clients' float32 vectors
+        (segments[s][i] = client i's piece s), fa_pairwise_sqdist."""
+        k = len(segments[0]) if segments else 0
+        if k < 2:
+            raise ValueError("pairwise_sqdist: need at least two clients")
+        in_ptrs, numels = [], []
+        for s, seg in enumerate(segments):
+            if len(seg) != k:
+                raise ValueError(f"segment {s}: {len(seg)} clients, expected {k}")
+            for i, t in enumerate(seg):
+                if t.dtype != torch.float32 or t.numel() != seg[0].numel():
+                    raise ValueError(f"segment {s} client {i}: float32 of {seg[0].numel()} elements expected")
+                _require_device(t, self.device, f"segment {s} client {i}")
+                in_ptrs.append(t.data_ptr())
+            numels.append(seg[0].numel())
+        nl = N.i64_array(numels)
+        need = self._lib.fa_pairwise_sqdist_scratch_bytes(len(segments), nl, k)
+        scratch = getattr(self, "_pd_scratch", None)
+        if scratch is None or scratch.numel() < need:
+            scratch = self._pd_scratch = torch.empty(max(need, 1), dtype=torch.uint8, device=self.device)
+        d = torch.empty((k, k), dtype=torch.float64, device=self.device)
+        rc = self._lib.fa_pairwise_sqdist(self._ctx, len(segments), nl, k, N.ptr_array(in_ptrs), d.data_ptr(),
+                                          scratch.data_ptr(), scratch.numel(), self._stream(stream))
+        N.check(rc, "fa_pairwise_sqdist")
+        return d
+
 
 def get_engine(device: Optional[int] = None) -> AggEngine:
     return AggEngine.get(device)

@@ -1,0 +1,55 @@
+/*
+ * fedagg_robust.h -- C ABI of the robust-aggregation kernels (libfedagg.so), same context,
+ * memory, stream and error conventions as fedagg.h.  Entries and the reference code each replaces
+ * (paths relative to liuliuliu0605/FedML python/fedml/):
+ *
+ *   fa_coord_median     core/security/defense/coordinate_wise_median_defense.py:26-31
+ *                       torch.median(torch.cat(client vectors, -1), dim=-1).values
+ *   fa_pairwise_sqdist  core/security/defense/krum_defense.py:52-66 (_compute_krum_score's
+ *                       compute_euclidean_distance(v_i, v_j) ** 2 for every pair)
+ *
+ * Contract (bit-exact; pinned by tests/golden/g16_*): for every element e, out[e] is the input
+ * element (bit pattern) that ATen's median selects: the first NaN in client order if any client
+ * holds a NaN there; otherwise the element of rank (k-1)/2 when the k values are ordered by
+ * (value, client index), -0.0 == +0.0.  dtype: F32, BF16, F16, F64.
+ *
+ * fa_pairwise_sqdist is floating-point work whose summation order differs from the reference's
+ * float32 `norm()` (itself order-dependent): D[i][j] = sum_e (x_i[e] - x_j[e])^2 with float32
+ * differences, float32 sums over <= 64 coordinates, float64 above; relative error <= 1e-6 vs the
+ * exact sum (tests/test_gpu_robust.py).  The Krum selection built on it is checked bit-for-bit
+ * against the reference (tests/golden/g18_*).
+ */
+#ifndef FEDAGG_ROBUST_H
+#define FEDAGG_ROBUST_H
+
+#include <stddef.h>
+
+#include "fedagg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/*
+ * A whole (vectorized) state_dict in one launch: d_in[s * k + i] = client i's tensor of segment s
+ * (seg_numel[s] elements of `dtype`), d_out[s] the median tensor of segment s.
+ */
+int fa_coord_median(fa_ctx *ctx, int dtype, int32_t num_segments, const int64_t *seg_numel, int32_t k,
+                    const void *const *d_in, void *const *d_out, void *hip_stream);
+
+/*
+ * Pairwise squared Euclidean distances of k float32 client vectors (2 <= k <= 128), each given
+ * as num_segments pieces (d_in[s * k + i], seg_numel[s] elements): d_dist = k x k float64 device
+ * matrix (symmetric, zero diagonal).  d_scratch: device buffer of at least
+ * fa_pairwise_sqdist_scratch_bytes(...) bytes (per-block partial sums; caller-owned, reusable).
+ */
+int fa_pairwise_sqdist(fa_ctx *ctx, int32_t num_segments, const int64_t *seg_numel, int32_t k,
+                       const void *const *d_in, void *d_dist, void *d_scratch, size_t scratch_bytes,
+                       void *hip_stream);
+size_t fa_pairwise_sqdist_scratch_bytes(int32_t num_segments, const int64_t *seg_numel, int32_t k);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FEDAGG_ROBUST_H */

@@ -160,3 +160,35 @@ def lcc_decode(coef, f, p, n_out):
     if rc != 0:
         raise RuntimeError(f"orc_lcc_decode failed: {rc}")
     return out
+
+
+def coord_median(xs):
+    """torch.median over the client axis (see orc_coord_median) of same-shape CPU tensors."""
+    xs = [x.contiguous() for x in xs]
+    L = lib()
+    if not hasattr(L, "_median_declared"):
+        L.orc_coord_median.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_int32,
+                                       ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]
+        L.orc_coord_median.restype = ctypes.c_int
+        L.orc_pairwise_sqdist.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p),
+                                          ctypes.c_void_p]
+        L.orc_pairwise_sqdist.restype = ctypes.c_int
+        L._median_declared = True
+    out = torch.empty_like(xs[0])
+    rc = L.orc_coord_median(_DT[xs[0].dtype], xs[0].numel(), len(xs),
+                            (ctypes.c_void_p * len(xs))(*[x.data_ptr() for x in xs]), out.data_ptr())
+    if rc != 0:
+        raise RuntimeError(f"orc_coord_median failed: {rc}")
+    return out
+
+
+def pairwise_sqdist(xs):
+    """K x K float64 matrix of exact squared Euclidean distances of float32 CPU vectors."""
+    coord_median([torch.zeros(1)])  # declares the robust entry points
+    xs = [x.contiguous().reshape(-1) for x in xs]
+    k = len(xs)
+    d = torch.empty((k, k), dtype=torch.float64)
+    rc = lib().orc_pairwise_sqdist(xs[0].numel(), k, (ctypes.c_void_p * k)(*[x.data_ptr() for x in xs]), d.data_ptr())
+    if rc != 0:
+        raise RuntimeError(f"orc_pairwise_sqdist failed: {rc}")
+    return d

@@ -1,0 +1,82 @@
+/*
+ * robust_oracle.c -- CPU restatement of the reference's robust aggregation arithmetic.
+ *
+ * TEST INFRASTRUCTURE ONLY (same rules as fedagg_oracle.c).
+ *
+ * Parity: pinned by the g16 / g18 fixtures (tests/golden/make_golden.py, cases_robust), which ran
+ * the reference's defenses.  Restated (paths relative to python/fedml/):
+ *   orc_coord_median   core/security/defense/coordinate_wise_median_defense.py:26-31:
+ *                      torch.median(stack of the K client vectors, dim=-1).values, i.e. ATen's
+ *                      median_with_indices_impl: if the K values hold a NaN, the FIRST NaN (in
+ *                      client order); otherwise the element of rank (K-1)/2 when the values are
+ *                      ordered by (value, client index) -- -0.0 and +0.0 compare equal, so the
+ *                      client index decides which zero is returned.
+ *   orc_pairwise_sqdist  core/security/defense/krum_defense.py:52-66 (compute_euclidean_distance
+ *                      = (v_i - v_j).norm(), squared): the exact float64 sum of squared float32
+ *                      differences -- the value the reference's float32 norm approximates; the
+ *                      GPU kernel is checked against it with a stated tolerance (krum_defense's
+ *                      own float32 norm is order-dependent), and the Krum SELECTION bit-for-bit
+ *                      against the fixtures.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+enum { ORC_F32 = 0, ORC_BF16 = 1, ORC_F16 = 2, ORC_F64 = 3 };
+
+float orc_bf16_to_f32(uint16_t h);
+float orc_f16_to_f32(uint16_t h);
+
+static double ld(int dt, const void *p, int64_t e) {
+    switch (dt) {
+        case ORC_F32: return ((const float *)p)[e];
+        case ORC_BF16: return orc_bf16_to_f32(((const uint16_t *)p)[e]);
+        case ORC_F16: return orc_f16_to_f32(((const uint16_t *)p)[e]);
+        default: return ((const double *)p)[e];
+    }
+}
+
+static void cp(int dt, void *dst, int64_t e, const void *src) {
+    const size_t s = dt == ORC_F32 ? 4 : dt == ORC_F64 ? 8 : 2;
+    memcpy((char *)dst + e * s, (const char *)src + e * s, s);
+}
+
+int orc_coord_median(int dtype, int64_t n, int32_t k, const void *const *in, void *out) {
+    if (k <= 0 || k > 4096 || n < 0) return -1;
+    if (dtype != ORC_F32 && dtype != ORC_BF16 && dtype != ORC_F16 && dtype != ORC_F64) return -2;
+    int32_t idx[4096];
+    double val[4096];
+    const int32_t r = (k - 1) / 2;
+    for (int64_t e = 0; e < n; ++e) {
+        int32_t nan_at = -1;
+        for (int32_t i = 0; i < k; ++i) {
+            val[i] = ld(dtype, in[i], e);
+            if (isnan(val[i]) && nan_at < 0) nan_at = i;
+        }
+        if (nan_at >= 0) { cp(dtype, out, e, in[nan_at]); continue; }
+        /* insertion sort of client indices by (value, index): stable on the index */
+        for (int32_t i = 0; i < k; ++i) {
+            int32_t j = i;
+            while (j > 0 && val[idx[j - 1]] > val[i]) { idx[j] = idx[j - 1]; --j; }
+            idx[j] = i;
+        }
+        cp(dtype, out, e, in[idx[r]]);
+    }
+    return 0;
+}
+
+/* d[i*k + j] = sum_e (x_i[e] - x_j[e])^2 in float64 (float32 inputs), every ordered pair */
+int orc_pairwise_sqdist(int64_t n, int32_t k, const float *const *x, double *d) {
+    if (k <= 0 || n < 0) return -1;
+    for (int32_t i = 0; i < k; ++i)
+        for (int32_t j = 0; j < k; ++j) {
+            double s = 0.0;
+            if (i != j)
+                for (int64_t e = 0; e < n; ++e) {
+                    const double t = (double)x[i][e] - (double)x[j][e];
+                    s += t * t;
+                }
+            d[(int64_t)i * k + j] = s;
+        }
+    return 0;
+}

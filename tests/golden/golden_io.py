@@ -94,10 +94,11 @@ def list_cases():
 
 
 FINITE_PREFIXES = ("g11_", "g12_", "g13_", "g14_", "g15_")  # SecAgg / LightSecAgg families
+ROBUST_PREFIXES = ("g16_", "g17_", "g18_")  # coordinate-wise median, trimmed mean, Krum
 
 
 def aggregation_cases():
     """Fixtures replayed by the generic aggregation replay (refcases.replay): everything except
-    the topology tables, FedOpt rounds and the finite-field families, which have their own."""
+    the topology tables, FedOpt rounds, the finite-field and robust families, which have their own."""
     return [p for p in list_cases() if "topologies" not in p and "fedopt" not in p
-            and not os.path.basename(p).startswith(FINITE_PREFIXES)]
+            and not os.path.basename(p).startswith(FINITE_PREFIXES + ROBUST_PREFIXES)]

@@ -786,6 +786,127 @@ def cases_secagg():
         WRITTEN.append((name, os.path.getsize(os.path.join(HERE, name + ".npz"))))
 
 
+def load_defenses():
+    for name, sub in [("fedml", ""), ("fedml.core", "/core"), ("fedml.core.security", "/core/security"),
+                      ("fedml.core.security.common", "/core/security/common"),
+                      ("fedml.core.security.defense", "/core/security/defense")]:
+        _stub_pkg(name, REF + sub)
+    med = importlib.import_module("fedml.core.security.defense.coordinate_wise_median_defense")
+    tm = importlib.import_module("fedml.core.security.defense.coordinate_wise_trimmed_mean_defense")
+    kr = importlib.import_module("fedml.core.security.defense.krum_defense")
+    return med.CoordinateWiseMedianDefense, tm.CoordinateWiseTrimmedMeanDefense, kr.KrumDefense
+
+
+def _robust_clients(seed, K, layout, special=True, levels=None):
+    g = torch.Generator().manual_seed(seed)
+    clients = []
+    for i in range(K):
+        d = OrderedDict()
+        for key, shape, dt in layout:
+            if dt in (torch.int64,):
+                d[key] = torch.randint(0, 9, shape, generator=g, dtype=dt)
+                continue
+            v = torch.randn(shape, generator=g, dtype=torch.float64)
+            if levels:  # few distinct values -> many ties
+                v = torch.round(v * levels) / levels
+            if special:
+                u = torch.rand(shape, generator=g)
+                v = torch.where(u < 0.03, torch.zeros_like(v), v)
+                v = torch.where((u >= 0.03) & (u < 0.06), -torch.zeros_like(v), v)
+                v = torch.where((u >= 0.06) & (u < 0.07), torch.full_like(v, float("inf")), v)
+                v = torch.where((u >= 0.07) & (u < 0.08), torch.full_like(v, -float("inf")), v)
+                v = torch.where((u >= 0.08) & (u < 0.085), torch.full_like(v, float("nan")), v)
+            d[key] = v.to(dt)
+        clients.append(d)
+    return clients
+
+
+def cases_robust():
+    """§8(f) next #3: robust aggregation (core/security/defense/coordinate_wise_median_defense.py,
+    coordinate_wise_trimmed_mean_defense.py + common/utils.py:213-232, krum_defense.py)."""
+    Median, Trimmed, Krum = load_defenses()
+    flat = [("fc.weight", (10, 50), torch.float32), ("fc.bias", (10,), torch.float32)]
+    bn = [("conv.weight", (4, 3, 3, 3), torch.float32), ("bn.weight", (4,), torch.float32),
+          ("bn.bias", (4,), torch.float32), ("bn.running_mean", (4,), torch.float32),
+          ("bn.running_var", (4,), torch.float32), ("bn.num_batches_tracked", (), torch.int64),
+          ("fc.weight", (3, 4), torch.float32), ("fc.bias", (3,), torch.float32)]
+    # R1: coordinate-wise median (torch.median over the client axis = lower median, NaN first)
+    seed = 900
+    for K in (1, 2, 3, 4, 5, 8, 13, 32, 64, 100):
+        for levels in (None, 4):
+            seed += 1
+            clients = _robust_clients(seed, K, flat, levels=levels)
+            n = gen_counts(seed, K)
+            out = Median(Args()).defend_on_aggregation(list(zip(n, dc(clients))))
+            write(f"g16_median_f32_K{K}" + ("_ties" if levels else ""), clients, [out],
+                  dict(kind="median", n=n, ref="core/security/defense/coordinate_wise_median_defense.py:18-44"))
+    for dt, tag, K in ((torch.bfloat16, "bf16", 7), (torch.float16, "f16", 6), (torch.float64, "f64", 9)):
+        lay = [(k, s, dt) for k, s, _ in flat]
+        clients = _robust_clients(950 + K, K, lay, levels=8)
+        n = gen_counts(950 + K, K)
+        out = Median(Args()).defend_on_aggregation(list(zip(n, dc(clients))))
+        write(f"g16_median_{tag}_K{K}", clients, [out], dict(kind="median", n=n,
+              ref="core/security/defense/coordinate_wise_median_defense.py:18-44"))
+    # a non-BN int64 key: torch.cat promotes to float32, the key comes back float32
+    lay = flat + [("step", (3,), torch.int64)]
+    clients = _robust_clients(960, 5, lay)
+    n = gen_counts(960, 5)
+    out = Median(Args()).defend_on_aggregation(list(zip(n, dc(clients))))
+    write("g16_median_mixed_int_K5", clients, [out], dict(kind="median", n=n,
+          ref="core/security/defense/coordinate_wise_median_defense.py:18-44"))
+    # BatchNorm statistics: vectorize_weight skips them but the write-back walk does not -> error
+    clients = _robust_clients(961, 5, bn, special=False)
+    n = gen_counts(961, 5)
+    try:
+        Median(Args()).defend_on_aggregation(list(zip(n, dc(clients))))
+        err = None
+    except Exception as e:  # noqa: BLE001
+        err = [type(e).__name__, str(e)]
+    assert err is not None
+    write("g16_median_bn_error_K5", clients, [clients[0]], dict(kind="median", n=n, error=err,
+          ref="core/security/defense/coordinate_wise_median_defense.py:35-43"))
+
+    # R2: "trimmed mean": sorts clients by sample count (compute_a_score) and drops beta*K per end
+    for K, beta, counts in ((10, 0.1, None), (10, 0.25, None), (7, 0.49, None), (6, 0.0, None),
+                            (9, 0.2, [5, 3, 5, 1, 3, 5, 2, 2, 9])):
+        n = counts or gen_counts(970 + K, K)
+        clients = _robust_clients(970 + K, K, flat, special=False)
+        raw = list(zip(n, clients))
+        sel = Trimmed(Args(beta=beta)).defend_before_aggregation(raw)
+        idx = [next(i for i, (_, c) in enumerate(raw) if c is sc) for _, sc in sel]
+        write(f"g17_trimmed_K{K}_b{beta}", clients, [clients[0]],
+              dict(kind="trimmed", n=n, beta=beta, selected=idx,
+                   ref="core/security/defense/coordinate_wise_trimmed_mean_defense.py:20-28, common/utils.py:213-232"))
+
+    # R3: Krum / multi-Krum selection and scores
+    for K, f, m, lay in ((10, 2, 1, flat), (16, 3, 4, flat), (12, 2, 3, bn), (8, 1, 1, flat)):
+        clients = _robust_clients(980 + K, K, lay, special=False)
+        g = torch.Generator().manual_seed(K)
+        for b in range(f):  # byzantine clients: scaled noise
+            for k2, v in clients[b * 3 % K].items():
+                if v.is_floating_point():
+                    clients[b * 3 % K][k2] = v + 5.0 * torch.randn(v.shape, generator=g).to(v.dtype)
+        n = gen_counts(980 + K, K)
+        raw = list(zip(n, clients))
+        d = Krum(Args(byzantine_client_num=f, krum_param_m=m))
+        sel = d.defend_before_aggregation(raw)
+        idx = [next(i for i, (_, c) in enumerate(raw) if c is sc) for _, sc in sel]
+        import fedml.core.security.common.utils as su
+        scores = d._compute_krum_score([su.vectorize_weight(c) for c in clients])
+        write(f"g18_krum_K{K}_f{f}_m{m}", clients, [clients[0]],
+              dict(kind="krum", n=n, byzantine_client_num=f, krum_param_m=m, selected=idx, scores=scores,
+                   ref="core/security/defense/krum_defense.py:27-66"))
+    try:
+        Krum(Args(byzantine_client_num=4, krum_param_m=1)).defend_before_aggregation(
+            list(zip([1] * 9, _robust_clients(1, 9, flat, special=False))))
+        err = None
+    except ValueError as e:
+        err = ["ValueError", str(e)]
+    assert err is not None
+    with open(os.path.join(HERE, "g18_krum_errors.json"), "w") as fh:
+        json.dump({"K9_f4_m1": err}, fh)
+
+
 def out2_equal(a, b):
     return all(np.array_equal(np.asarray(a[k]), np.asarray(b[k])) for k in a)
 

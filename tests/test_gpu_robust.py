@@ -1,0 +1,141 @@
+"""GPU parity of the robust-aggregation kernels: coordinate-wise median bit-for-bit against the
+reference fixtures (g16) and the C oracle (every K bucket, NaN / +-0 / ties, all dtypes,
+multi-segment), Krum's pairwise distances against the exact float64 oracle (rtol 1e-6) and the
+Krum / multi-Krum selection against the reference (g18)."""
+from __future__ import annotations
+
+import os
+import types
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+import torch
+
+from golden_io import ROBUST_PREFIXES, client_dicts, expected_dicts, list_cases, load_case
+from refcases import assert_dict_bits, bits_equal
+
+pytestmark = pytest.mark.gpu
+
+CASES = list_cases()
+ROB = {kind: [p for p in CASES if os.path.basename(p).startswith(kind)] for kind in ROBUST_PREFIXES}
+ids = lambda p: os.path.basename(p)[:-4]  # noqa: E731
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from fedml_amd.engine import get_engine
+    return get_engine(0)
+
+
+@pytest.mark.parametrize("path", ROB["g16_"], ids=ids)
+@pytest.mark.parametrize("where", ["cpu", "cuda"])
+def test_median_defense_golden(path, where):
+    from fedml_amd.core.security.defense.coordinate_wise_median_defense import CoordinateWiseMedianDefense
+    meta, arrays = load_case(path)
+    cl = client_dicts(meta, arrays)
+    if where == "cuda":
+        cl = [OrderedDict((k, v.to(DEV)) for k, v in c.items()) for c in cl]
+    raw = list(zip(meta["n"], cl))
+    d = CoordinateWiseMedianDefense(types.SimpleNamespace())
+    if meta.get("error"):
+        with pytest.raises(RuntimeError) as ei:
+            d.defend_on_aggregation(raw)
+        assert str(ei.value) == meta["error"][1]
+        return
+    out = d.defend_on_aggregation(raw)
+    assert out is cl[0]  # client 0's dict, modified in place (reference :36-44)
+    assert_dict_bits(OrderedDict((k, v.cpu()) for k, v in out.items()), expected_dicts(meta, arrays)[0], meta["name"])
+
+
+def _column_data(g, k, n, dtype, zeros=0.05):
+    xs = []
+    for i in range(k):
+        v = torch.randn(n, generator=g, dtype=torch.float64)
+        u = torch.rand(n, generator=g)
+        v = torch.where(u < zeros, torch.zeros_like(v), v)
+        v = torch.where((u >= zeros) & (u < 2 * zeros), -torch.zeros_like(v), v)
+        v = torch.where((u >= 0.5) & (u < 0.52), torch.round(v * 2) / 2, v)  # ties
+        v = torch.where((u >= 0.9) & (u < 0.901), torch.full_like(v, float("nan")), v)
+        v = torch.where((u >= 0.95) & (u < 0.96), torch.full_like(v, float("inf")) * torch.sign(v - 0.1), v)
+        xs.append(v.to(dtype))
+    return xs
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 5, 7, 8, 9, 16, 17, 31, 32, 33, 63, 64, 65, 100, 127, 128, 129, 150])
+def test_median_vs_oracle_f32(eng, k):
+    from oracle import orc
+    g = torch.Generator().manual_seed(k)
+    n = 3000 if k > 128 else 20001
+    xs = _column_data(g, k, n, torch.float32)
+    got = eng.coord_median([[x.to(DEV) for x in xs]])[0].cpu()
+    assert bits_equal(got, orc.coord_median(xs))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16, torch.float64])
+@pytest.mark.parametrize("k", [3, 6, 32, 40, 96])
+def test_median_vs_oracle_dtypes(eng, dtype, k):
+    from oracle import orc
+    g = torch.Generator().manual_seed(100 + k)
+    xs = _column_data(g, k, 5003, dtype, zeros=0.2)
+    got = eng.coord_median([[x.to(DEV) for x in xs]])[0].cpu()
+    assert bits_equal(got, orc.coord_median(xs))
+
+
+def test_median_all_zero_columns(eng):
+    """Columns of only +-0 in every sign pattern: ATen returns the zero of rank (K-1)/2 by index."""
+    from oracle import orc
+    k = 5
+    pats = torch.arange(2 ** k)
+    xs = [torch.where((pats >> i) & 1 == 1, -torch.zeros(2 ** k), torch.zeros(2 ** k)) for i in range(k)]
+    got = eng.coord_median([[x.to(DEV) for x in xs]])[0].cpu()
+    assert bits_equal(got, orc.coord_median(xs))
+    assert torch.equal(got.view(torch.int32), orc.coord_median(xs).view(torch.int32))
+
+
+def test_median_multi_segment(eng):
+    from oracle import orc
+    g = torch.Generator().manual_seed(7)
+    k, sizes = 24, [1, 255, 256, 257, 1000, 0, 13]
+    cols = [_column_data(g, k, s, torch.float32) for s in sizes]
+    outs = eng.coord_median([[x.to(DEV) for x in c] for c in cols])
+    for c, o in zip(cols, outs):
+        assert bits_equal(o.cpu(), orc.coord_median(c) if c[0].numel() else torch.empty(0))
+
+
+@pytest.mark.parametrize("k", [2, 3, 5, 16, 31, 64, 97, 128])
+def test_pairwise_sqdist_vs_oracle(eng, k):
+    from oracle import orc
+    g = torch.Generator().manual_seed(k)
+    sizes = [70001, 5, 64, 1000]
+    xs = [[torch.randn(s, generator=g) * (1 + (i % 3)) for s in sizes] for i in range(k)]
+    D = eng.pairwise_sqdist([[xs[i][s].to(DEV) for i in range(k)] for s in range(len(sizes))]).cpu()
+    ref = orc.pairwise_sqdist([torch.cat(x) for x in xs])
+    assert torch.equal(D, D.T) and torch.all(D.diag() == 0)
+    np.testing.assert_allclose(D.numpy(), ref.numpy(), rtol=1e-6)
+
+
+@pytest.mark.parametrize("path", ROB["g18_"], ids=ids)
+@pytest.mark.parametrize("where", ["cpu", "cuda"])
+def test_krum_defense_golden(path, where):
+    from fedml_amd.core.security.defense.krum_defense import KrumDefense
+    meta, arrays = load_case(path)
+    cl = client_dicts(meta, arrays)
+    if where == "cuda":
+        cl = [OrderedDict((k, v.to(DEV)) for k, v in c.items()) for c in cl]
+    raw = list(zip(meta["n"], cl))
+    d = KrumDefense(types.SimpleNamespace(byzantine_client_num=meta["byzantine_client_num"],
+                                          krum_param_m=meta["krum_param_m"]))
+    sel = d.defend_before_aggregation(raw)
+    assert [next(i for i, (_, c) in enumerate(raw) if c is sc) for _, sc in sel] == meta["selected"]
+    np.testing.assert_allclose(d._compute_krum_score(cl), meta["scores"], rtol=1e-5)
+
+
+def test_robust_errors(eng):
+    from fedml_amd._native import FedAggNativeError
+    x = torch.zeros(10, device=DEV)
+    with pytest.raises(FedAggNativeError):
+        eng.pairwise_sqdist([[x] * 129])
+    with pytest.raises(TypeError):
+        eng.coord_median([[x.long()]])

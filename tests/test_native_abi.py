@@ -12,7 +12,7 @@ import torch
 from conftest import ROOT, gpu_available
 from fedml_amd import _native as N
 
-HDRS = [os.path.join(ROOT, "include", h) for h in ("fedagg.h", "fedagg_finite.h")]
+HDRS = [os.path.join(ROOT, "include", h) for h in ("fedagg.h", "fedagg_finite.h", "fedagg_robust.h")]
 
 
 def declared_functions():
