@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="metric",
-                   choices=["metric", "resnet18", "vit_bf16", "hier", "gossip", "host", "secagg"])
+                   choices=["metric", "resnet18", "vit_bf16", "hier", "gossip", "host", "secagg", "median", "krum"])
     p.add_argument("--clients", type=int, default=None)
     p.add_argument("--params", type=int, default=None)
     p.add_argument("--variant", type=int, default=0, help="kernel variant (fa_ctx_set_variant)")
@@ -458,6 +458,108 @@ def wl_secagg(args, eng, rank, world, timer):
                               "counts the LCC mask decoding (U x m int64 in, P int64 out)")
 
 
+def _robust_inputs(K, P):
+    Ppad = -(-P // 64) * 64  # ClientArena row alignment
+    g = torch.Generator(device="cuda").manual_seed(21)
+    arena = torch.randn((K, Ppad), generator=g, device="cuda")
+    return [arena[i, :P] for i in range(K)]
+
+
+def _robust_cpu(fn, K, Pc, budget_s, what):
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
+    torch.set_num_threads(threads)
+    g = torch.Generator().manual_seed(0)
+    xs = [torch.randn(Pc, generator=g) for _ in range(K)]
+    best, runs, t_end = float("inf"), 0, time.perf_counter() + budget_s
+    while runs < 2 or (time.perf_counter() < t_end and runs < 20):
+        t0 = time.perf_counter()
+        fn(xs)
+        best = min(best, time.perf_counter() - t0)
+        runs += 1
+    return best, runs, torch.get_num_threads(), f"K={K} x P={Pc} fp32 host-resident, best of {runs} runs of {what}"
+
+
+def wl_median(args, eng, rank, world, timer):
+    """§8(f) #3: coordinate-wise median (coordinate_wise_median_defense.py:18-44) of K client
+    weight vectors of ResNet-18 size: one fa_coord_median launch (a selection per coordinate)."""
+    if world > 1:
+        raise SystemExit("median config: single GPU")
+    K = args.clients or 32
+    P = args.params or RESNET18_P
+    xs = _robust_inputs(K, P)
+    out = torch.empty(P, device="cuda")
+
+    def step():
+        with timer:
+            eng.coord_median([xs], outs=[out])
+
+    def parity():
+        if args.check_samples <= 0:
+            return None
+        from oracle import orc
+        gi = torch.Generator(device="cuda").manual_seed(99)
+        idx = torch.randint(0, P, (args.check_samples,), generator=gi, device="cuda")
+        exp = orc.coord_median([x.index_select(0, idx).cpu() for x in xs])
+        ok = torch.equal(out.index_select(0, idx).cpu().view(torch.int32), exp.view(torch.int32))
+        return f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on {args.check_samples} sampled coordinates"
+
+    def cpu(budget_s):
+        from oracle import robust_port
+        Pc = 1_000_000
+        best, runs, th, sample = _robust_cpu(robust_port.median_port, K, Pc, budget_s,
+                                             "oracle/robust_port.median_port (cat + torch.median, "
+                                             "coordinate_wise_median_defense.py:26-31)")
+        return {"value": round((K * Pc * 4 + Pc * 4) / best / 1e9, 2), "unit": "GB/s", "cores": th, "kind": "port",
+                "sample": sample}
+
+    return dict(name=f"coord_median_K{K}_P{P}_fp32", dtype="fp32", step=step, parity=parity,
+                bytes_total=K * P * 4 + P * 4, launch_bytes=K * P * 4 + P * 4, clients=K, params=P, cpu_K=K, cpu=cpu,
+                data="synthetic N(0,1) client weight vectors, resident in HBM (rows 256-byte aligned)")
+
+
+def wl_krum(args, eng, rank, world, timer):
+    """§8(f) #3: Krum's pairwise squared distances (krum_defense.py:52-66) of K client weight
+    vectors of ResNet-18 size: one fa_pairwise_sqdist pass (each client read once)."""
+    if world > 1:
+        raise SystemExit("krum config: single GPU")
+    K = args.clients or 32
+    P = args.params or RESNET18_P
+    xs = _robust_inputs(K, P)
+    state = {}
+
+    def step():
+        with timer:
+            state["D"] = eng.pairwise_sqdist([xs])
+
+    def parity():
+        if args.check_samples <= 0:
+            return None
+        from oracle import orc
+        sl = slice(0, min(P, 1 << 20))
+        # distances restricted to a prefix of the coordinates, on device, vs the exact oracle
+        D = eng.pairwise_sqdist([[x[sl] for x in xs]]).cpu()
+        ref = orc.pairwise_sqdist([x[sl].cpu() for x in xs])
+        err = float(((D - ref).abs() / ref.clamp_min(1e-300)).max())
+        return f"max relative error {err:.2e} vs exact float64 oracle on the first {sl.stop} coordinates (tolerance 1e-6)"
+
+    def cpu(budget_s):
+        from oracle import robust_port
+        Pc = 1_000_000
+        Kc = min(K, 16)
+        best, runs, th, sample = _robust_cpu(robust_port.krum_distances_port, Kc, Pc, budget_s,
+                                             "oracle/robust_port.krum_distances_port (one (v_i - v_j).norm() per "
+                                             "ordered pair, krum_defense.py:52-66)")
+        return {"value": round(Kc * Pc * 4 / best / 1e9, 3), "unit": "GB/s", "cores": th, "kind": "port",
+                "sample": sample}
+
+    pairs = K * (K - 1) // 2
+    return dict(name=f"krum_pairdist_K{K}_P{P}_fp32", dtype="fp32", step=step, parity=parity,
+                bytes_total=K * P * 4, launch_bytes=K * P * 4, clients=K, params=P, cpu_K=K, cpu=cpu,
+                data="synthetic N(0,1) client weight vectors, resident in HBM (rows 256-byte aligned)",
+                roofline_note=f"VALU work {pairs} pairs x 3 flop per coordinate = {3 * pairs * P / 1e9:.1f} GFLOP/step; "
+                              "achieved here is the HBM rate (each client read once)")
+
+
 # ----------------------------------------------------------------------------- CPU baseline
 def cpu_baseline(K, budget_s):
     """The reference's CPU cost: oracle/torch_port.py (op-for-op restatement of agg_operator.py's
@@ -503,7 +605,8 @@ def main():
         eng.set_variant(args.variant)
     timer = Timed()
     wl = {"metric": wl_metric, "resnet18": wl_layout, "vit_bf16": wl_layout, "hier": wl_hier,
-          "gossip": wl_gossip, "host": wl_host, "secagg": wl_secagg}[args.config](args, eng, rank, world, timer)
+          "gossip": wl_gossip, "host": wl_host, "secagg": wl_secagg, "median": wl_median,
+          "krum": wl_krum}[args.config](args, eng, rank, world, timer)
 
     for _ in range(args.warmup):
         wl["step"]()

@@ -7,10 +7,10 @@
 // values into registers as order-preserving uint32 keys (floats mapped so that unsigned order ==
 // numeric order, -0.0 folded onto +0.0), sorts them with a bitonic network padded to P2 = next
 // power of two with max-key sentinels (P2 (P2 log2 P2 ...)/4 compare-exchanges, each a v_min_u32 +
-// v_max_u32 on compile-time register indices), and takes key[(K-1)/2] (uniform index -> indexed
-// VGPR move).  ATen's exact rules are kept: a NaN anywhere in the column returns the FIRST NaN;
-// among equal values the client index decides, which only matters for +-0 -- when the selected
-// key is zero, a short in-order rescan of the column finds which zero ATen returns.
+// v_max_u32 on compile-time register indices), and takes key[(K-1)/2] (uniform index -> one select
+// chain).  ATen's exact rules are kept: a NaN anywhere in the column returns the FIRST NaN; among
+// equal values the client index decides, which only matters for +-0 -- both cases (a NaN seen, or
+// a zero selected) take a short in-order rescan of the column.
 // Compute per coordinate ~P2 log2^2 P2 ops vs K*s bytes of HBM: memory-bound to K ~ 64, roughly
 // balanced at K = 128.  Larger K: a rank-counting kernel (O(K^2) per coordinate, L2-resident).
 #include <hip/hip_runtime.h>
@@ -27,7 +27,6 @@ using namespace fa_detail;
 
 namespace {
 
-constexpr unsigned kZeroKey = 0x80000000u;
 constexpr int kMaxP2 = 64;  // largest column one lane sorts (a 128-key network takes the compiler minutes)
 
 template <int DT> struct MedT;
@@ -60,12 +59,13 @@ template <> struct MedT<FA_DTYPE_F16> {
   }
 };
 
-// order-preserving key of a non-NaN float; -0.0 and +0.0 share the key of +0.0
+// order-preserving key of a float (unsigned order == numeric order for non-NaN values; -0.0 sorts
+// just below +0.0, which the zero rescan below accounts for)
 __device__ __forceinline__ unsigned fkey(float x) {
-  unsigned u = __float_as_uint(x);
-  if (x == 0.0f) u = 0u;
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  const unsigned u = __float_as_uint(x);
+  return u ^ ((unsigned)((int)u >> 31) | 0x80000000u);
 }
+constexpr unsigned kPosZeroKey = 0x80000000u, kNegZeroKey = 0x7FFFFFFFu;
 __device__ __forceinline__ float fkey_inv(unsigned k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
 }
@@ -98,10 +98,19 @@ __device__ __forceinline__ void bitonic_sort(unsigned (&key)[P2]) {
   }
 }
 
-// ATen's choice among zeros: the selected rank r falls in the block of (equal) zeros, which ATen
+// Rare cases, resolved by an in-order rescan of the column: a NaN anywhere -> ATen returns the
+// FIRST NaN; a zero selected -> the selected rank r falls in the block of (equal) zeros, which ATen
 // orders by client index -> the (r - #negatives)-th zero in client order.
 template <int DT>
-__device__ __noinline__ void store_zero(const void* const* in, int k, int64_t e, int r, int negc, void* out) {
+__device__ __forceinline__ void store_rare(const void* const* in, int k, int64_t e, int r, bool nan, void* out) {
+  if (nan) {
+    for (int i = 0; i < k; ++i) {
+      const float x = MedT<DT>::load(in[i], e);
+      if (x != x) { MedT<DT>::store_bits(out, e, in[i]); return; }
+    }
+  }
+  int negc = 0;
+  for (int i = 0; i < k; ++i) negc += MedT<DT>::load(in[i], e) < 0.0f;
   int seen = 0;
   for (int i = 0; i < k; ++i) {
     const float x = MedT<DT>::load(in[i], e);
@@ -122,15 +131,12 @@ k_median(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict_
   const int64_t ec = live ? e : sg.numel - 1;
   const void* const* in = ptrs + sg.ptr_base;
   unsigned key[P2];
-  int nan_at = -1, negc = 0;
+  bool nan = false;
 #pragma unroll
   for (int i = 0; i < P2; ++i) {
     const float x = MedT<DT>::load(in[min(i, k - 1)], ec);  // clamped: every load unconditional
-    const bool real = i < k;                                 // P2 - k < P2 / 2 sentinels
-    const bool isn = x != x;
-    nan_at = (real && isn && nan_at < 0) ? i : nan_at;
-    negc += real && x < 0.0f;
-    key[i] = (real && !isn) ? fkey(x) : 0xFFFFFFFFu;
+    nan = nan || (i < k && x != x);                          // P2 - k < P2 / 2 sentinels
+    key[i] = i < k ? fkey(x) : 0xFFFFFFFFu;
   }
   bitonic_sort<P2>(key);
   const int r = (k - 1) >> 1;
@@ -138,8 +144,7 @@ k_median(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict_
 #pragma unroll
   for (int i = 1; i < P2; ++i) kr = (i == r) ? key[i] : kr;  // uniform r: folds to one select chain
   if (!live) return;
-  if (nan_at >= 0) MedT<DT>::store_bits(sg.out, e, in[nan_at]);
-  else if (kr == kZeroKey) store_zero<DT>(in, k, e, r, negc, sg.out);
+  if (nan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, nan, sg.out);
   else MedT<DT>::store(sg.out, e, fkey_inv(kr));
 }
 
@@ -160,17 +165,13 @@ k_median2(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict
   const int64_t ec = live ? e : sg.numel - 1;
   const void* const* in = ptrs + sg.ptr_base;
   unsigned key[H];
-  int nan_at = -1, negc = 0;
+  bool nan = false;
 #pragma unroll
   for (int i = 0; i < H; ++i) {
     const int c = half * H + i;
-    const int cc = min(c, k - 1);  // clamped: the load is unconditional
-    const float x = MedT<DT>::load(in[cc], ec);
-    const bool real = c < k;
-    const bool isn = x != x;
-    nan_at = (real && isn && nan_at < 0) ? c : nan_at;
-    negc += real && x < 0.0f;
-    key[i] = (real && !isn) ? fkey(x) : 0xFFFFFFFFu;
+    const float x = MedT<DT>::load(in[min(c, k - 1)], ec);  // clamped: the load is unconditional
+    nan = nan || (c < k && x != x);
+    key[i] = c < k ? fkey(x) : 0xFFFFFFFFu;
   }
   bitonic_sort<H>(key);
   // cross-lane step of the 128-key bitonic merge (partner = lane ^ 1)
@@ -193,17 +194,14 @@ k_median2(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict
       }
     }
   }
-  const int other_nan = __shfl_xor(nan_at, 1);
-  const int other_neg = __shfl_xor(negc, 1);
+  const int partner_nan = __shfl_xor((int)nan, 1);  // every lane shuffles (no short-circuit)
+  nan = nan || partner_nan != 0;
   if (half != 0 || !live) return;
-  const int first_nan = nan_at >= 0 ? nan_at : other_nan;
-  negc += other_neg;
   const int r = (k - 1) >> 1;
   unsigned kr = key[0];
 #pragma unroll
   for (int i = 1; i < H; ++i) kr = (i == r) ? key[i] : kr;
-  if (first_nan >= 0) MedT<DT>::store_bits(sg.out, e, in[first_nan]);
-  else if (kr == kZeroKey) store_zero<DT>(in, k, e, r, negc, sg.out);
+  if (nan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, nan, sg.out);
   else MedT<DT>::store(sg.out, e, fkey_inv(kr));
 }
 
