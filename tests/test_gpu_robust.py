@@ -139,3 +139,48 @@ def test_robust_errors(eng):
         eng.pairwise_sqdist([[x] * 129])
     with pytest.raises(TypeError):
         eng.coord_median([[x.long()]])
+
+
+def _reset_defender():
+    from fedml_amd.core.security.fedml_defender import FedMLDefender
+    FedMLDefender.get_instance().init(types.SimpleNamespace())
+
+
+@pytest.mark.parametrize("path", [p for p in ROB["g16_"] if "error" not in p and "mixed" not in p][:6],
+                         ids=ids)
+def test_wise_median_through_server_aggregator(path):
+    """ServerAggregator.aggregate with defense_type=wise_median == the reference's defended aggregate."""
+    from fedml_amd.ml.aggregator.default_aggregator import DefaultServerAggregator
+    meta, arrays = load_case(path)
+    cl = client_dicts(meta, arrays)
+    try:
+        agg = DefaultServerAggregator(torch.nn.Linear(50, 10), types.SimpleNamespace(
+            enable_defense=True, defense_type="wise_median", federated_optimizer="FedAvg"))
+        out = agg.aggregate(list(zip(meta["n"], cl)))
+    finally:
+        _reset_defender()
+    assert_dict_bits(OrderedDict((k, v.cpu()) for k, v in out.items()), expected_dicts(meta, arrays)[0], meta["name"])
+
+
+@pytest.mark.parametrize("path", ROB["g18_"], ids=ids)
+def test_krum_through_server_aggregator(path):
+    """on_before_aggregation (krum / multikrum) keeps the reference's clients; aggregate then
+    averages them on the engine exactly as FedMLAggOperator.agg would."""
+    from fedml_amd.ml.aggregator.agg_operator import FedMLAggOperator
+    from fedml_amd.ml.aggregator.default_aggregator import DefaultServerAggregator
+    meta, arrays = load_case(path)
+    cl = client_dicts(meta, arrays)
+    raw = list(zip(meta["n"], cl))
+    dt = "multikrum" if meta["krum_param_m"] > 1 else "krum"
+    args = types.SimpleNamespace(enable_defense=True, defense_type=dt, federated_optimizer="FedAvg",
+                                 byzantine_client_num=meta["byzantine_client_num"], krum_param_m=meta["krum_param_m"])
+    try:
+        agg = DefaultServerAggregator(torch.nn.Linear(50, 10), args)
+        kept, _ = agg.on_before_aggregation(raw)
+        out = agg.aggregate(kept)
+    finally:
+        _reset_defender()
+    assert [next(i for i, (_, c) in enumerate(raw) if c is sc) for _, sc in kept] == meta["selected"]
+    ref = FedMLAggOperator.agg(types.SimpleNamespace(federated_optimizer="FedAvg"), kept)
+    assert_dict_bits(OrderedDict((k, v.cpu()) for k, v in out.items()),
+                     OrderedDict((k, v.cpu()) for k, v in ref.items()), "krum+fedavg")
