@@ -46,7 +46,8 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="metric",
-                   choices=["metric", "resnet18", "vit_bf16", "hier", "gossip", "host", "secagg", "median", "krum"])
+                   choices=["metric", "fragmented", "resnet18", "vit_bf16", "hier", "gossip", "host", "secagg", "median",
+                            "krum"])
     p.add_argument("--clients", type=int, default=None)
     p.add_argument("--params", type=int, default=None)
     p.add_argument("--variant", type=int, default=0, help="kernel variant (fa_ctx_set_variant)")
@@ -264,6 +265,64 @@ def wl_layout(args, eng, rank, world, timer):
     tag = ("resnet18gn" if resnet else "vitb16_bf16") + ("" if args.layout == "arena" else "_tensors")
     return dict(name=f"fedavg_{tag}_K{K}_P{P}", dtype="fp32" if resnet else "bf16", step=step, parity=parity,
                 bytes_total=K * in_b + out_b, launch_bytes=None, clients=K, params=P, cpu_K=None)
+
+
+def fragmented_layout(P, n_tensors=200):
+    """The metric's P split ViT-style (SURVEY.md §8(d) "fragmented" variant): a repeating pattern of
+    transformer-block tensor shapes, ~n_tensors tensors summing to exactly P fp32 elements."""
+    D, M = 768, 3072
+    block = [[D], [D], [3 * D, D], [3 * D], [D, D], [D], [D], [D], [M, D], [M], [D, M], [D]]
+    per = sum(int(np.prod(s)) for s in block)
+    reps = max(1, P // per)
+    shapes = [s for _ in range(reps) for s in block]
+    # scale the large matrices so that the whole layout holds exactly P elements
+    total = sum(int(np.prod(s)) for s in shapes)
+    while len(shapes) > n_tensors or total > P:
+        total -= int(np.prod(shapes.pop()))
+    rest = P - total
+    while rest > 0:
+        take = min(rest, D * M)
+        shapes.append([take])
+        rest -= take
+    return [(f"t{i}", s, "float32") for i, s in enumerate(shapes)]
+
+
+def wl_fragmented(args, eng, rank, world, timer):
+    """The metric shape (K=128 x P=125 M fp32) with every client update split ViT-style into ~200
+    separately allocated tensors, aggregated through the state_dict API (fedml_amd/ml/aggregator/
+    state_dict_agg.aggregate: host pointer tables via fedml_amd._host, one launch per dtype group)."""
+    if world > 1:
+        raise SystemExit("fragmented config: single GPU")
+    from fedml_amd.ml.aggregator.state_dict_agg import MUL_W, aggregate
+    K = args.clients or 128
+    P = args.params or 125_000_000
+    layout = fragmented_layout(P)
+    counts = client_counts(K)
+    N = sum(counts)
+    w = [c / N for c in counts]
+    dicts = make_layout_clients(range(K), layout)
+    res = {}
+
+    def step():
+        with timer:
+            res["out"] = aggregate(dicts, MUL_W, w)
+
+    def parity():
+        if args.check_samples <= 0:
+            return None
+        from oracle import orc
+        bad = 0
+        for name, shape, _ in layout[:: max(1, len(layout) // 16)]:
+            n = int(np.prod(shape))
+            idx = torch.arange(0, n, max(1, n // 256), device="cuda")
+            exp = orc.weighted_sum([d[name].reshape(-1).index_select(0, idx).cpu() for d in dicts], MUL_W, w)
+            got = res["out"][name].reshape(-1).index_select(0, idx).cpu()
+            bad += int((got.view(torch.int32) != exp.view(torch.int32)).sum())
+        return f"{'bit-exact' if bad == 0 else f'{bad} MISMATCHES'} vs oracle on a strided sample of 16 keys"
+
+    return dict(name=f"fedavg_fragmented{len(layout)}_K{K}_P{P}_fp32", dtype="fp32", step=step, parity=parity,
+                bytes_total=K * P * 4 + P * 4, launch_bytes=None, clients=K, params=P, cpu_K=None,
+                roofline_note="kernel time = the whole aggregate() call (host pointer tables + launch + kernel)")
 
 
 def wl_hier(args, eng, rank, world, timer):
@@ -582,8 +641,29 @@ def cpu_baseline(K, budget_s):
         runs += 1
     gbs = (K * P * 4 + P * 4) / best / 1e9
     return {"value": round(gbs, 2), "unit": "GB/s", "cores": torch.get_num_threads(), "kind": "port",
+            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
             "sample": f"K={K} x P={P} fp32 host-resident, best of {runs} runs of oracle/torch_port.agg('FedAvg') "
                       f"(op-for-op restatement of agg_operator.py:35-44)"}
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def measured_ceiling():
+    """Best read-stream rate measured on an MI355X box by tools/hbm_probe.py (profiles/)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "r01_hbm_probe.json")) as f:
+            return json.load(f).get("read_best_GBs")
+    except (OSError, ValueError):
+        return None
 
 
 def pmc_traffic(workload):
@@ -604,7 +684,7 @@ def main():
     if args.variant:
         eng.set_variant(args.variant)
     timer = Timed()
-    wl = {"metric": wl_metric, "resnet18": wl_layout, "vit_bf16": wl_layout, "hier": wl_hier,
+    wl = {"metric": wl_metric, "fragmented": wl_fragmented, "resnet18": wl_layout, "vit_bf16": wl_layout, "hier": wl_hier,
           "gossip": wl_gossip, "host": wl_host, "secagg": wl_secagg, "median": wl_median,
           "krum": wl_krum}[args.config](args, eng, rank, world, timer)
 
@@ -634,6 +714,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl.get("cpu_K"):
         cpu = wl["cpu"](args.cpu_seconds) if wl.get("cpu") else cpu_baseline(wl["cpu_K"], args.cpu_seconds)
+        cpu.setdefault("cpu_model", cpu_model())
+        cpu.setdefault("os_cpu_count", os.cpu_count())
 
     if rank == 0:
         line = {
@@ -659,6 +741,7 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                          "traffic": pmc_traffic(wl["name"]),
                          "kernel_avg_ms": round(kernel_ms, 4) if kernel_ms else None,
+                         "measured_read_ceiling": measured_ceiling(),
                          "algorithmic_bytes_per_launch": int(launch_bytes) if launch_bytes else None},
             "cpu_baseline": cpu,
             "parity": parity,

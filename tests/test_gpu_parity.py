@@ -290,3 +290,22 @@ def test_fedavg_sgd_fused_vs_oracle(eng, momentum, dampening, wd, nesterov, P):
         assert bits_equal(p_gpu.cpu(), p_ref), step
         if momentum:
             assert bits_equal(b_gpu.cpu(), b_ref), step
+
+
+def test_more_than_2g_elements(eng):
+    """Maximum-size edge: P > 2^31 elements per client (64-bit element indexing in every tile and
+    the scalar tail); checked on samples at the start, across the 2^31 boundary and at the end."""
+    from oracle import orc
+    P = 2 ** 31 + 1029  # ragged tail tile too
+    g = torch.Generator(device="cuda").manual_seed(5)
+    xs = [torch.randn(P, generator=g, device="cuda") for _ in range(2)]
+    w = [0.3, 0.7]
+    out = eng.weighted_sum(xs, MUL_W, w)
+    # contiguous slices (plain copies): torch's index_select/gather kernels fault on tensors of
+    # more than 2^31 elements on this ROCm build (diagnosed with tools/diag_large.py)
+    spans = [(0, 4096), (2 ** 31 - 4096, 2 ** 31 + 4096), (P - 4096, P)]
+    pick = lambda t: torch.cat([t[a:b].cpu() for a, b in spans])  # noqa: E731
+    exp = orc.weighted_sum([pick(x) for x in xs], MUL_W, w)
+    assert bits_equal(pick(out), exp)
+    del xs, out
+    torch.cuda.empty_cache()
