@@ -57,8 +57,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     p.add_argument("--check-samples", type=int, default=65536)
     p.add_argument("--pinned", action="store_true", help="host config: client updates already in pinned memory")
-    p.add_argument("--layout", default="arena", choices=["arena", "tensors"],
-                   help="arena: client updates in one ClientArena allocation (fedml_amd/arena.py); "
+    p.add_argument("--layout", default="tiled", choices=["arena", "tiled", "tensors"],
+                   help="arena: client updates as rows of one ClientArena allocation (fedml_amd/arena.py); "
+                        "tiled: tile-interleaved ClientArena (4-KiB tiles of all clients contiguous); "
                         "tensors: one allocation per client tensor")
     return p.parse_args()
 
@@ -120,6 +121,24 @@ def make_arena_rows(idx, P, dtype=torch.float32):
     return rows
 
 
+def make_tiled_arena(idx, P, dtype=torch.float32):
+    """Client updates in a TILE-INTERLEAVED ClientArena (same values as make_flat_clients)."""
+    from fedml_amd.arena import ArenaLayout, ClientArena
+    arena = ClientArena(ArenaLayout([("w", (P,), dtype)]), capacity=len(idx), zero=False, tiled=True)
+    for j, i in enumerate(idx):
+        g = torch.Generator(device="cuda").manual_seed(1000 + i)
+        arena.write(j, {"w": torch.randn(P, generator=g, device="cuda", dtype=torch.float32).to(dtype)})
+    torch.cuda.synchronize()
+    arena._scratch.clear()
+    return arena
+
+
+def tiled_gather(buf, row, idx):
+    """Logical elements ``idx`` of client row ``row`` of a tiled arena group [tiles, capacity, E]."""
+    _, cap, E = buf.shape
+    return buf.view(-1).index_select(0, (idx // E) * (cap * E) + row * E + idx % E)
+
+
 def load_layout(name):
     with open(os.path.join(ROOT, "tests", "golden", "layouts.json")) as f:
         return json.load(f)[name]
@@ -179,7 +198,13 @@ def wl_metric(args, eng, rank, world, timer):
     N = sum(counts)
     mine = split(K, rank, world)
     w = [counts[i] / N for i in mine]
-    xs = make_arena_rows(mine, P) if args.layout == "arena" else make_flat_clients(mine, P)
+    tiled = args.layout == "tiled"
+    if tiled:
+        arena = make_tiled_arena(mine, P)
+        buf, rows = arena.bufs[torch.float32], list(range(len(mine)))
+        xs = None
+    else:
+        xs = make_arena_rows(mine, P) if args.layout == "arena" else make_flat_clients(mine, P)
     out = torch.empty(P, device="cuda")
     if world > 1:
         from fedml_amd.distributed.group_reduce import GroupReducer
@@ -187,15 +212,26 @@ def wl_metric(args, eng, rank, world, timer):
         def timed_sum(xs_, mode, coef, div, o):
             with timer:
                 return eng.weighted_sum(xs_, mode, coef, div, out=o)
+
+        class TimedEngine:  # the tiled local step, HIP-event timed like timed_sum
+            def weighted_sum_tiled(self, *a, **kw):
+                with timer:
+                    return eng.weighted_sum_tiled(*a, **kw)
         red = GroupReducer(collective=args.collective, chunks=args.chunks, local_sum=timed_sum)
 
         def step():
-            red.fedavg(xs, w, out=out)
+            if tiled:
+                red.fedavg_tiled(TimedEngine(), buf, rows, w, P, out=out)
+            else:
+                red.fedavg(xs, w, out=out)
         launches = args.chunks
     else:
         def step():
             with timer:
-                eng.weighted_sum(xs, MUL_W, w, out=out)
+                if tiled:
+                    eng.weighted_sum_tiled(buf, rows, MUL_W, w, n=P, out=out)
+                else:
+                    eng.weighted_sum(xs, MUL_W, w, out=out)
         launches = 1
 
     def parity():
@@ -204,11 +240,16 @@ def wl_metric(args, eng, rank, world, timer):
         from oracle import orc
         gi = torch.Generator(device="cuda").manual_seed(99)
         idx = torch.randint(0, P, (args.check_samples,), generator=gi, device="cuda")
-        exp = orc.weighted_sum([x.index_select(0, idx).cpu() for x in xs], MUL_W, w)
+        if tiled:
+            sampled = [tiled_gather(buf, r, idx).cpu() for r in rows]
+        else:
+            sampled = [x.index_select(0, idx).cpu() for x in xs]
+        exp = orc.weighted_sum(sampled, MUL_W, w)
         ok = torch.equal(out.index_select(0, idx).cpu().view(torch.int32), exp.view(torch.int32))
         return f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on {args.check_samples} sampled elements"
 
-    return dict(name=f"fedavg_flat_K{K}_P{P}_fp32" + ("" if args.layout == "arena" else "_tensors"),
+    suffix = {"arena": "", "tiled": "_tiled", "tensors": "_tensors"}[args.layout]
+    return dict(name=f"fedavg_flat_K{K}_P{P}_fp32" + suffix,
                 dtype="fp32", step=step, parity=parity,
                 bytes_total=K * P * 4 + P * 4, launch_bytes=(len(mine) * P * 4 + P * 4) / launches,
                 clients=K, params=P, cpu_K=K)
@@ -226,13 +267,14 @@ def wl_layout(args, eng, rank, world, timer):
     w = [counts[i] / N for i in mine]
     dicts = make_layout_clients(mine, layout)
     arena = None
-    if args.layout == "arena":
+    if args.layout in ("arena", "tiled"):
         from fedml_amd.arena import ArenaLayout, ClientArena
         arena = ClientArena(ArenaLayout([(n, tuple(s), getattr(torch, dt)) for n, s, dt in layout]),
-                            capacity=len(mine))
+                            capacity=len(mine), tiled=args.layout == "tiled")
         for j, d in enumerate(dicts):
             arena.write(j, d)
-        dicts = [arena.slot(j) for j in range(len(mine))]
+        if not arena.tiled:
+            dicts = [arena.slot(j) for j in range(len(mine))]
         torch.cuda.synchronize()
     P = sum(int(np.prod(s)) for _, s, _ in layout)
     size = {"int64": 8, "bfloat16": 2, "float32": 4}
@@ -262,7 +304,7 @@ def wl_layout(args, eng, rank, world, timer):
             bad += int((got.view(ib) != exp.view(ib)).sum())
         return f"{'bit-exact' if bad == 0 else f'{bad} MISMATCHES'} vs oracle on a strided sample of every key"
 
-    tag = ("resnet18gn" if resnet else "vitb16_bf16") + ("" if args.layout == "arena" else "_tensors")
+    tag = ("resnet18gn" if resnet else "vitb16_bf16") + {"arena": "", "tiled": "_tiled", "tensors": "_tensors"}[args.layout]
     return dict(name=f"fedavg_{tag}_K{K}_P{P}", dtype="fp32" if resnet else "bf16", step=step, parity=parity,
                 bytes_total=K * in_b + out_b, launch_bytes=None, clients=K, params=P, cpu_K=None)
 
@@ -337,7 +379,12 @@ def wl_hier(args, eng, rank, world, timer):
     N = sum(counts)
     my_groups = split(G, rank, world)
     clients = [i for g in my_groups for i in range(g * M, (g + 1) * M)]
-    xs = (make_arena_rows if args.layout == "arena" else make_flat_clients)(clients, P)
+    tiled = args.layout == "tiled" and world == 1  # multi-rank hierarchical: flat rows (GroupReducer slices)
+    if tiled:
+        arena = make_tiled_arena(clients, P)
+        buf, rows, xs = arena.bufs[torch.float32], list(range(len(clients))), None
+    else:
+        xs = (make_arena_rows if args.layout in ("arena", "tiled") else make_flat_clients)(clients, P)
     gcounts = [counts[g * M:(g + 1) * M] for g in my_groups]
     gn = [sum(c) for c in gcounts]
     w = [c / gn[j] for j, cs in enumerate(gcounts) for c in cs]
@@ -357,7 +404,12 @@ def wl_hier(args, eng, rank, world, timer):
         launches = args.chunks
     else:
         def step():
-            timed_grouped(xs, MUL_W, w, 1.0, gptr, MUL_N_DIV_N, gn, [float(N)] * len(gn), out)
+            if tiled:
+                with timer:
+                    eng.weighted_sum_grouped_tiled(buf, rows, MUL_W, w, 1.0, gptr, MUL_N_DIV_N, gn,
+                                                   [float(N)] * len(gn), n=P, out=out)
+            else:
+                timed_grouped(xs, MUL_W, w, 1.0, gptr, MUL_N_DIV_N, gn, [float(N)] * len(gn), out)
         launches = 1
 
     def parity():
@@ -366,7 +418,8 @@ def wl_hier(args, eng, rank, world, timer):
         from oracle import orc
         gi = torch.Generator(device="cuda").manual_seed(98)
         idx = torch.randint(0, P, (min(args.check_samples, 8192),), generator=gi, device="cuda")
-        sample = [x.index_select(0, idx).cpu() for x in xs]
+        sample = ([tiled_gather(buf, r, idx).cpu() for r in rows] if tiled else
+                  [x.index_select(0, idx).cpu() for x in xs])
         terms = []
         for j in range(len(my_groups)):
             Gj = orc.weighted_sum(sample[gptr[j]:gptr[j + 1]], 0, w[gptr[j]:gptr[j + 1]])
@@ -375,7 +428,7 @@ def wl_hier(args, eng, rank, world, timer):
         ok = torch.equal(out.index_select(0, idx).cpu().view(torch.int32), exp.view(torch.int32))
         return f"{'bit-exact' if ok else 'MISMATCH'} vs oracle (group FedAvg -> cloud term -> ordered sum) on {idx.numel()} sampled elements"
 
-    return dict(name=f"hier_fedavg_G{G}x{M}_P{P}_fp32", dtype="fp32", step=step, parity=parity,
+    return dict(name=f"hier_fedavg_G{G}x{M}_P{P}_fp32" + ("_tiled" if tiled else ""), dtype="fp32", step=step, parity=parity,
                 bytes_total=G * M * P * 4 + P * 4, launch_bytes=(len(clients) * P * 4 + P * 4) / launches,
                 clients=G * M, params=P, cpu_K=None)
 
@@ -395,13 +448,13 @@ def wl_gossip(args, eng, rank, world, timer):
             with timer:
                 return eng.mix(xs_, rp, cs, vs, ps, outs, outs2)
         dg = DistributedGossip(W, local_mix=timed_mix)
-        xs = (make_arena_rows if args.layout == "arena" else make_flat_clients)(dg.mine, P)
+        xs = (make_arena_rows if args.layout in ("arena", "tiled") else make_flat_clients)(dg.mine, P)
 
         def step():
             dg.step(xs)
         rows = len(dg.mine)
     else:
-        xs = (make_arena_rows if args.layout == "arena" else make_flat_clients)(range(n), P)
+        xs = (make_arena_rows if args.layout in ("arena", "tiled") else make_flat_clients)(range(n), P)
         rp, cs, vs = gossip_rows(W)
         outs = [torch.empty(P, device="cuda") for _ in range(n)]
 

@@ -18,7 +18,8 @@ import torch  # noqa: F401  (load torch's HIP runtime before libfedagg.so)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfedagg.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
+TILE_BYTES = 4096  # FA_TILE_BYTES
 
 F32, BF16, F16, F64, I64 = 0, 1, 2, 3, 4
 MUL_W, MUL_N_DIV_N, SUM = 0, 1, 2
@@ -27,7 +28,8 @@ FA_OK, FA_ERR_INVALID, FA_ERR_DTYPE, FA_ERR_HIP, FA_ERR_NOMEM = 0, -1, -2, -3, -
 
 EXPORTED_SYMBOLS = (
     "fa_abi_version", "fa_ctx_create", "fa_ctx_destroy", "fa_weighted_sum",
-    "fa_weighted_sum_multi", "fa_weighted_sum_grouped", "fa_fedavg_sgd", "fa_mix", "fa_ctx_set_variant",
+    "fa_weighted_sum_multi", "fa_weighted_sum_tiled", "fa_weighted_sum_grouped", "fa_weighted_sum_grouped_tiled",
+    "fa_fedavg_sgd", "fa_mix", "fa_ctx_set_variant",
     "fa_ctx_set_mix_band", "fa_strerror", "fa_last_error",
     # include/fedagg_finite.h
     "fa_finite_sum", "fa_finite_quantize", "fa_lcc_decode",
@@ -69,6 +71,13 @@ def _declare(L):
     L.fa_weighted_sum_multi.restype = ctypes.c_int
     L.fa_weighted_sum_multi.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int32, _P_i64,
                                         ctypes.c_int32, _P_vp, _P_d, ctypes.c_double, _P_vp, _vp]
+    L.fa_weighted_sum_tiled.restype = ctypes.c_int
+    L.fa_weighted_sum_tiled.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int32, _P_vp,
+                                        ctypes.c_int64, _P_d, ctypes.c_double, _vp, _vp]
+    L.fa_weighted_sum_grouped_tiled.restype = ctypes.c_int
+    L.fa_weighted_sum_grouped_tiled.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int32,
+                                                _P_vp, ctypes.c_int64, _P_d, ctypes.c_double, ctypes.c_int32,
+                                                _P_i32, ctypes.c_int, _P_d, _P_d, _vp, _vp]
     L.fa_weighted_sum_grouped.restype = ctypes.c_int
     L.fa_weighted_sum_grouped.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int32,
                                           _P_vp, _P_d, ctypes.c_double, ctypes.c_int32, _P_i32, ctypes.c_int,

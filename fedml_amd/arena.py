@@ -13,6 +13,16 @@ each key padded to a 64-element (256-byte for fp32) boundary so every key and ev
 dtype group over K row pointers (fa_weighted_sum with n = P_group), and the result lives in an
 output arena with the same offsets, exposed as per-key views in the model's key order.
 
+Tiled layout (``tiled=True``): each dtype group is stored tile-interleaved, ``[tiles, capacity, E]``
+with E elements = 4 KiB (``FA_TILE_BYTES``): tile t of client r sits at (t * capacity + r) * 4 KiB.
+A workgroup of the aggregation kernel reads tile t of all K clients -- with the client-major
+layout those are K 4-KiB pieces 500 MB apart (at the metric size), tiled they are ONE contiguous
+K * 4 KiB run.  Measured on MI355X at the metric size (tools/layout_probe.py): the bare read
+pattern streams at 6.54-6.76 TB/s tiled vs 6.12-6.28 TB/s client-major.  The logical per-group
+offsets are unchanged (same ArenaLayout), only the physical placement differs, so client rows are
+not addressable as tensor views: ingest goes through ``write`` (one strided device copy per
+dtype group) and ``read`` gathers a client back.
+
 Ingest: ``write(i, state_dict)`` copies a client's tensors into row i (device -> device, or host
 -> device).  Host updates (what the reference's transports deliver, e.g. mpi_receive_thread.py:25)
 go through a pinned staging ring: the client's tensors are packed into pinned memory, one async
@@ -66,16 +76,31 @@ class ArenaLayout:
         return out
 
 
+TILE_BYTES = 4096  # FA_TILE_BYTES (include/fedagg.h)
+
+
+def tile_elems(dt: torch.dtype) -> int:
+    return TILE_BYTES // torch.empty((), dtype=dt).element_size()
+
+
 class ClientArena:
     def __init__(self, layout: ArenaLayout, capacity: int, device=None, engine: Optional[AggEngine] = None,
-                 zero: bool = True):
+                 zero: bool = True, tiled: bool = False):
         self.layout = layout
         self.capacity = int(capacity)
+        self.tiled = bool(tiled)
         self.engine = engine or get_engine(None if device is None else torch.device(device).index)
         self.device = self.engine.device
         alloc = torch.zeros if zero else torch.empty  # zeroed padding keeps padded outputs finite
-        self.bufs: Dict[torch.dtype, torch.Tensor] = {
-            dt: alloc((self.capacity, n), dtype=dt, device=self.device) for dt, n in layout.group_numel.items()}
+        if self.tiled:
+            self.bufs: Dict[torch.dtype, torch.Tensor] = {
+                dt: alloc((-(-n // tile_elems(dt)), self.capacity, tile_elems(dt)), dtype=dt, device=self.device)
+                for dt, n in layout.group_numel.items()}
+        else:
+            self.bufs = {dt: alloc((self.capacity, n), dtype=dt, device=self.device)
+                         for dt, n in layout.group_numel.items()}
+        self._scratch: Dict[torch.dtype, torch.Tensor] = {}
+        self._stage_dev: Dict[torch.dtype, torch.Tensor] = {}  # copy-stream row staging (tiled host ingest)
         self._copy_stream = None
         self._staging: List[Tuple[Dict[torch.dtype, torch.Tensor], Optional[torch.cuda.Event]]] = []
         self._next_stage = 0
@@ -87,10 +112,38 @@ class ClientArena:
 
     def slot(self, i: int) -> "OrderedDict[str, torch.Tensor]":
         """Client i's tensors (views into the arena), in the model's key order."""
+        if self.tiled:
+            raise TypeError("a tiled arena's rows are not tensor views: use write(i, sd) / read(i)")
         return self.layout.views(self.bufs, i)
 
     def rows(self, dt: torch.dtype, clients: Sequence[int]) -> List[torch.Tensor]:
+        if self.tiled:
+            raise TypeError("a tiled arena's rows are not tensor views: use write(i, sd) / read(i)")
         return [self.bufs[dt][i] for i in clients]
+
+    def tile_view(self, dt: torch.dtype, i: int) -> torch.Tensor:
+        """Tiled arena: client i's dtype group as a strided [tiles, E] view (row-major flat order)."""
+        if not self.tiled:
+            raise TypeError("tile_view: not a tiled arena")
+        return self.bufs[dt][:, i, :]
+
+    def _row_scratch(self, dt: torch.dtype) -> torch.Tensor:
+        """A contiguous logical row of group dt, padded to whole tiles (tiled ingest/read)."""
+        t = self._scratch.get(dt)
+        if t is None:
+            nt, _, E = self.bufs[dt].shape
+            t = self._scratch[dt] = torch.zeros(nt * E, dtype=dt, device=self.device)
+        return t
+
+    def read(self, i: int) -> "OrderedDict[str, torch.Tensor]":
+        """Client i's tensors as new device tensors (a copy; works for both layouts)."""
+        if not 0 <= i < self.capacity:
+            raise IndexError(f"arena row {i} out of range [0, {self.capacity})")
+        self._wait_ingest()
+        if not self.tiled:
+            return OrderedDict((k, v.clone()) for k, v in self.slot(i).items())
+        rows = {dt: self.tile_view(dt, i).reshape(-1) for dt in self.bufs}  # reshape of a strided view copies
+        return OrderedDict((k, v.clone()) for k, v in self.layout.views(rows, None).items())
 
     # ------------------------------------------------------------------ ingest
     def write(self, i: int, state_dict) -> None:
@@ -98,14 +151,21 @@ class ClientArena:
         tensors: packed into pinned staging and sent with one H2D per dtype group)."""
         if not 0 <= i < self.capacity:
             raise IndexError(f"arena row {i} out of range [0, {self.capacity})")
-        slot = self.slot(i)
-        for k, v in slot.items():
+        for k in self.layout.keys:
+            dt, _, shape, _ = self.layout.where[k]
             t = state_dict[k]  # KeyError on a missing key, like the reference's per-key access
-            if t.dtype != v.dtype or tuple(t.shape) != tuple(v.shape):
-                raise TypeError(f"arena: key {k!r} is {t.dtype}{tuple(t.shape)}, layout says {v.dtype}{tuple(v.shape)}")
+            if t.dtype != dt or tuple(t.shape) != shape:
+                raise TypeError(f"arena: key {k!r} is {t.dtype}{tuple(t.shape)}, layout says {dt}{shape}")
         first = state_dict[self.layout.keys[0]]
         if first.is_cuda:
-            for k, v in slot.items():
+            if self.tiled:  # pack the logical row, then one strided tile scatter per dtype group
+                rows = {dt: self._row_scratch(dt) for dt in self.bufs}
+                for k, v in self.layout.views(rows, None).items():
+                    v.copy_(state_dict[k])
+                for dt, r in rows.items():
+                    self.tile_view(dt, i).copy_(r.view(self.bufs[dt].shape[0], -1))
+                return
+            for k, v in self.slot(i).items():
                 v.copy_(state_dict[k])
             return
         self._write_host(i, state_dict)
@@ -124,7 +184,7 @@ class ClientArena:
     def _write_host(self, i: int, state_dict) -> None:
         if self._copy_stream is None:
             self._copy_stream = torch.cuda.Stream(self.device)
-        if all(state_dict[k].is_pinned() for k in self.layout.keys):
+        if not self.tiled and all(state_dict[k].is_pinned() for k in self.layout.keys):
             # already page-locked (e.g. a transport that receives into pinned buffers): DMA directly
             slot = self.slot(i)
             with torch.cuda.stream(self._copy_stream):
@@ -140,7 +200,15 @@ class ClientArena:
             v.copy_(state_dict[k])
         with torch.cuda.stream(self._copy_stream):
             for dt, buf in pinned.items():
-                self.bufs[dt][i].copy_(buf, non_blocking=True)
+                if self.tiled:  # H2D of the logical row, then the strided tile scatter, same stream
+                    nt, _, E = self.bufs[dt].shape
+                    r = self._stage_dev.get(dt)
+                    if r is None:
+                        r = self._stage_dev[dt] = torch.zeros(nt * E, dtype=dt, device=self.device)
+                    r[:buf.numel()].copy_(buf, non_blocking=True)
+                    self.tile_view(dt, i).copy_(r.view(nt, E))
+                else:
+                    self.bufs[dt][i].copy_(buf, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self._copy_stream)
         self._staging[idx] = (pinned, ev)
@@ -165,9 +233,12 @@ class ClientArena:
         self._wait_ingest()
         outs: Dict[torch.dtype, torch.Tensor] = {}
         for dt, buf in self.bufs.items():
-            odt = out_dtype(dt, mode)
             o = out[dt] if out is not None else None
-            outs[dt] = self.engine.weighted_sum_rows(buf, clients, mode, coef, divisor, out=o)
+            if self.tiled:
+                outs[dt] = self.engine.weighted_sum_tiled(buf, clients, mode, coef, divisor,
+                                                          n=self.layout.group_numel[dt], out=o)
+            else:
+                outs[dt] = self.engine.weighted_sum_rows(buf, clients, mode, coef, divisor, out=o)
         res = OrderedDict()
         for k in self.layout.keys:
             dt, off, shape, n = self.layout.where[k]
@@ -186,8 +257,13 @@ class ClientArena:
             gptr.append(gptr[-1] + len(g))
         outs: Dict[torch.dtype, torch.Tensor] = {}
         for dt, buf in self.bufs.items():
-            outs[dt] = self.engine.weighted_sum_grouped([buf[i] for i in order], mode, coef, divisor, gptr,
-                                                        group_mode, group_coef, group_divisor)
+            if self.tiled:
+                outs[dt] = self.engine.weighted_sum_grouped_tiled(buf, order, mode, coef, divisor, gptr, group_mode,
+                                                                  group_coef, group_divisor,
+                                                                  n=self.layout.group_numel[dt])
+            else:
+                outs[dt] = self.engine.weighted_sum_grouped([buf[i] for i in order], mode, coef, divisor, gptr,
+                                                            group_mode, group_coef, group_divisor)
         res = OrderedDict()
         for k in self.layout.keys:
             dt, off, shape, n = self.layout.where[k]

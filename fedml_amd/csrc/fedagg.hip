@@ -272,15 +272,22 @@ struct WsumBody {
   static constexpr int V = T::V;
   static constexpr int64_t SLOT_BYTES = (int64_t)kBlock * V * T::IN_BYTES;
 
+  // sst: bytes between the input slots of one lane (SLOT_BYTES for flat inputs; the arena's tile
+  // stride for tile-interleaved inputs, fa_weighted_sum_tiled)
   __device__ static void load(u32x4 (&r)[U][S], const void* const* __restrict__ in, int i0, int k,
-                              int64_t boff) {
+                              int64_t boff, int64_t sst = SLOT_BYTES) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int i = min(i0 + u, k - 1);  // clamped: every load unconditional
       const char* p = (const char*)in[i] + boff;
 #pragma unroll
-      for (int s = 0; s < S; ++s) r[u][s] = ld16<NT>(p + s * SLOT_BYTES);
+      for (int s = 0; s < S; ++s) r[u][s] = ld16<NT>(p + s * sst);
     }
+  }
+  // element index of flat element e in an input whose 4-KiB slots are `sst` bytes apart
+  __device__ static int64_t phys(int64_t e, int64_t sst) {
+    constexpr int64_t TV = (int64_t)kBlock * V;
+    return (e / TV) * (sst / T::IN_BYTES) + e % TV;
   }
   template <bool GUARD>
   __device__ static void consume(A (&acc)[S][V], const u32x4 (&r)[U][S], const double* __restrict__ coef,
@@ -304,7 +311,7 @@ struct WsumBody {
 template <int DT, int MODE, int U, int S, bool NT, bool PF>
 __global__ void __launch_bounds__(kBlock)
 k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
-       const void* const* __restrict__ ptrs, int k, double divisor) {
+       const void* const* __restrict__ ptrs, int k, double divisor, int64_t sstr) {
   using B = WsumBody<DT, MODE, U, S, NT>;
   using T = typename B::T;
   using A = typename B::A;
@@ -313,13 +320,15 @@ k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
 
   const int64_t tile = blockIdx.x;
   const Seg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
-  const int64_t base = (tile - sg.tile_start) * TILE;
+  const int64_t tl = tile - sg.tile_start;
+  const int64_t base = tl * TILE;
   const void* const* in = ptrs + sg.ptr_base;
   const typename T::D d = T::div(divisor);
+  const int64_t sst = sstr ? sstr : B::SLOT_BYTES;  // flat: slot s of tile tl is tile tl*S+s
 
   if (sg.aligned && base + TILE <= sg.numel) {
     const int64_t e0 = base + (int64_t)threadIdx.x * V;
-    const int64_t boff = e0 * T::IN_BYTES;
+    const int64_t boff = tl * S * sst + (int64_t)threadIdx.x * V * T::IN_BYTES;
     A acc[S][V];
 #pragma unroll
     for (int s = 0; s < S; ++s)
@@ -327,17 +336,17 @@ k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
       for (int v = 0; v < V; ++v) acc[s][v] = T::zero();
     if constexpr (PF) {
       u32x4 ra[U][S], rb[U][S];
-      B::load(ra, in, 0, k, boff);
+      B::load(ra, in, 0, k, boff, sst);
       int i0 = 0;
       // two groups per trip so the ping-pong buffers keep fixed registers
       for (; i0 + 2 * U < k; i0 += 2 * U) {
-        B::load(rb, in, i0 + U, k, boff);
+        B::load(rb, in, i0 + U, k, boff, sst);
         B::template consume<false>(acc, ra, coef, i0, k, d);
-        B::load(ra, in, i0 + 2 * U, k, boff);
+        B::load(ra, in, i0 + 2 * U, k, boff, sst);
         B::template consume<false>(acc, rb, coef, i0 + U, k, d);
       }
       if (i0 + U < k) {
-        B::load(rb, in, i0 + U, k, boff);
+        B::load(rb, in, i0 + U, k, boff, sst);
         B::template consume<false>(acc, ra, coef, i0, k, d);
         B::template consume<true>(acc, rb, coef, i0 + U, k, d);
       } else {
@@ -346,7 +355,7 @@ k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
     } else {
       for (int i0 = 0; i0 < k; i0 += U) {
         u32x4 r[U][S];
-        B::load(r, in, i0, k, boff);
+        B::load(r, in, i0, k, boff, sst);
         B::template consume<true>(acc, r, coef, i0, k, d);
       }
     }
@@ -357,8 +366,9 @@ k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
     const int64_t end = min(base + TILE, sg.numel);
     for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
       A acc = T::zero();
+      const int64_t pe = B::phys(e, sst);
       for (int i = 0; i < k; ++i)
-        acc = accum<DT, MODE>(acc, term<DT, MODE>(T::ld1(in[i], e), T::coef(coef[i]), d));
+        acc = accum<DT, MODE>(acc, term<DT, MODE>(T::ld1(in[i], pe), T::coef(coef[i]), d));
       T::st1(sg.out, e, acc);
     }
   }
@@ -384,7 +394,7 @@ template <int DT, int MODE, int U, bool NT>
 __global__ void __launch_bounds__(kBlock)
 k_wsum_grouped(const Seg* __restrict__ segs, const double* __restrict__ coef,
                const void* const* __restrict__ ptrs, double divisor,
-               const GroupDesc* __restrict__ groups, int ngroups, int gmode) {
+               const GroupDesc* __restrict__ groups, int ngroups, int gmode, int64_t sstr) {
   using B = WsumBody<DT, MODE, U, 1, NT>;
   using T = typename B::T;
   using A = typename B::A;
@@ -395,6 +405,7 @@ k_wsum_grouped(const Seg* __restrict__ segs, const double* __restrict__ coef,
   const int64_t base = tile * TILE;
   const void* const* in = ptrs;
   const typename T::D d = T::div(divisor);
+  const int64_t sst = sstr ? sstr : B::SLOT_BYTES;
 
   auto epilogue = [&](A g, const GroupDesc& gd) -> A {
     if (gmode == FA_MODE_MUL_W) return T::rnd(op_mul(g, (A)gd.mul));
@@ -404,7 +415,7 @@ k_wsum_grouped(const Seg* __restrict__ segs, const double* __restrict__ coef,
 
   if (sg.aligned && base + TILE <= sg.numel) {
     const int64_t e0 = base + (int64_t)threadIdx.x * V;
-    const int64_t boff = e0 * T::IN_BYTES;
+    const int64_t boff = tile * sst + (int64_t)threadIdx.x * V * T::IN_BYTES;
     A out[V];
 #pragma unroll
     for (int v = 0; v < V; ++v) out[v] = T::zero();
@@ -415,7 +426,7 @@ k_wsum_grouped(const Seg* __restrict__ segs, const double* __restrict__ coef,
       for (int v = 0; v < V; ++v) acc[0][v] = T::zero();
       for (int i0 = gd.begin; i0 < gd.end; i0 += U) {
         u32x4 r[U][1];
-        B::load(r, in, i0, gd.end, boff);
+        B::load(r, in, i0, gd.end, boff, sst);
         B::template consume<true>(acc, r, coef, i0, gd.end, d);
       }
 #pragma unroll
@@ -426,11 +437,12 @@ k_wsum_grouped(const Seg* __restrict__ segs, const double* __restrict__ coef,
     const int64_t end = min(base + TILE, sg.numel);
     for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
       A out = T::zero();
+      const int64_t pe = B::phys(e, sst);
       for (int g = 0; g < ngroups; ++g) {
         const GroupDesc gd = groups[g];
         A acc = T::zero();
         for (int i = gd.begin; i < gd.end; ++i)
-          acc = accum<DT, MODE>(acc, term<DT, MODE>(T::ld1(in[i], e), T::coef(coef[i]), d));
+          acc = accum<DT, MODE>(acc, term<DT, MODE>(T::ld1(in[i], pe), T::coef(coef[i]), d));
         out = accum<DT, MODE>(out, epilogue(acc, gd));
       }
       T::st1(sg.out, e, out);
@@ -721,16 +733,16 @@ constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 template <int DT, int MODE, int U, int S, bool NT, bool PF>
 void launch_wsum(int64_t tiles, hipStream_t st, const Seg* segs, int nseg, const double* coef,
-                 const void* const* ptrs, int k, double divisor) {
+                 const void* const* ptrs, int k, double divisor, int64_t sstr) {
   hipLaunchKernelGGL((k_wsum<DT, MODE, U, S, NT, PF>), dim3((unsigned)tiles), dim3(kBlock), 0, st, segs,
-                     nseg, coef, ptrs, k, divisor);
+                     nseg, coef, ptrs, k, divisor, sstr);
 }
 
 template <int DT, int MODE>
 void dispatch_variant(int variant, int64_t tiles, hipStream_t st, const Seg* segs, int nseg,
-                      const double* coef, const void* const* ptrs, int k, double divisor) {
+                      const double* coef, const void* const* ptrs, int k, double divisor, int64_t sstr) {
 #define FA_V(ID, U, S, NT, PF) \
-  case ID: launch_wsum<DT, MODE, U, S, NT, PF>(tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
+  case ID: launch_wsum<DT, MODE, U, S, NT, PF>(tiles, st, segs, nseg, coef, ptrs, k, divisor, sstr); break;
   switch (variant) {
     FA_V(1, 4, 1, true, false)
     FA_V(2, 16, 1, true, false)
@@ -740,18 +752,18 @@ void dispatch_variant(int variant, int64_t tiles, hipStream_t st, const Seg* seg
     FA_V(6, 4, 4, true, false)
     FA_V(7, 8, 1, true, true)
     FA_V(8, 4, 2, true, true)
-    default: launch_wsum<DT, MODE, 8, 1, true, false>(tiles, st, segs, nseg, coef, ptrs, k, divisor);
+    default: launch_wsum<DT, MODE, 8, 1, true, false>(tiles, st, segs, nseg, coef, ptrs, k, divisor, sstr);
   }
 #undef FA_V
 }
 
 template <int DT>
 int dispatch_mode(int mode, int variant, int64_t tiles, hipStream_t st, const Seg* segs, int nseg,
-                  const double* coef, const void* const* ptrs, int k, double divisor) {
+                  const double* coef, const void* const* ptrs, int k, double divisor, int64_t sstr) {
   switch (mode) {
-    case FA_MODE_MUL_W: dispatch_variant<DT, FA_MODE_MUL_W>(variant, tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
-    case FA_MODE_MUL_N_DIV_N: dispatch_variant<DT, FA_MODE_MUL_N_DIV_N>(variant, tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
-    case FA_MODE_SUM: dispatch_variant<DT, FA_MODE_SUM>(variant, tiles, st, segs, nseg, coef, ptrs, k, divisor); break;
+    case FA_MODE_MUL_W: dispatch_variant<DT, FA_MODE_MUL_W>(variant, tiles, st, segs, nseg, coef, ptrs, k, divisor, sstr); break;
+    case FA_MODE_MUL_N_DIV_N: dispatch_variant<DT, FA_MODE_MUL_N_DIV_N>(variant, tiles, st, segs, nseg, coef, ptrs, k, divisor, sstr); break;
+    case FA_MODE_SUM: dispatch_variant<DT, FA_MODE_SUM>(variant, tiles, st, segs, nseg, coef, ptrs, k, divisor, sstr); break;
     default: return fail(FA_ERR_DTYPE, "unknown mode %d", mode);
   }
   return FA_OK;
@@ -890,9 +902,12 @@ int fa_ctx_set_mix_band(fa_ctx* c, int enable) {
   return FA_OK;
 }
 
-int fa_weighted_sum_multi(fa_ctx* ctx, int dtype, int mode, int32_t num_segments,
-                          const int64_t* seg_numel, int32_t k, const void* const* d_in,
-                          const double* coef, double divisor, void* const* d_out, void* hip_stream) {
+namespace {
+// fa_weighted_sum_multi / fa_weighted_sum_tiled.  sstr = 0: flat inputs; otherwise (one segment)
+// tile-interleaved inputs whose FA_TILE_BYTES slots are sstr bytes apart.
+int wsum_impl(fa_ctx* ctx, int dtype, int mode, int32_t num_segments, const int64_t* seg_numel, int32_t k,
+              const void* const* d_in, const double* coef, double divisor, void* const* d_out,
+              void* hip_stream, int64_t sstr) {
   if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
   if (k <= 0) return fail(FA_ERR_INVALID, "k must be > 0 (got %d)", k);
   if (num_segments <= 0 || !seg_numel || !d_in || !d_out)
@@ -946,6 +961,7 @@ int fa_weighted_sum_multi(fa_ctx* ctx, int dtype, int mode, int32_t num_segments
       hp[(int64_t)j * k + i] = p;
       aligned = aligned && al16(p);
     }
+    if (sstr && !aligned) return fail(FA_ERR_INVALID, "tiled inputs and the output must be 16-byte aligned");
     hs[j] = Seg{n, t0, d_out[s], j * k, aligned ? 1 : 0};
     t0 += (n + tile_elems - 1) / tile_elems;
     ++j;
@@ -958,28 +974,47 @@ int fa_weighted_sum_multi(fa_ctx* ctx, int dtype, int mode, int32_t num_segments
   const void* const* dp = (const void* const*)(d + seg_bytes + coef_bytes);
 
   switch (dtype) {
-    case FA_DTYPE_F32: rc = dispatch_mode<FA_DTYPE_F32>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor); break;
-    case FA_DTYPE_BF16: rc = dispatch_mode<FA_DTYPE_BF16>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor); break;
-    case FA_DTYPE_F16: rc = dispatch_mode<FA_DTYPE_F16>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor); break;
-    case FA_DTYPE_F64: rc = dispatch_mode<FA_DTYPE_F64>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor); break;
-    case FA_DTYPE_I64: rc = dispatch_mode<FA_DTYPE_I64>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor); break;
+    case FA_DTYPE_F32: rc = dispatch_mode<FA_DTYPE_F32>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor, sstr); break;
+    case FA_DTYPE_BF16: rc = dispatch_mode<FA_DTYPE_BF16>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor, sstr); break;
+    case FA_DTYPE_F16: rc = dispatch_mode<FA_DTYPE_F16>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor, sstr); break;
+    case FA_DTYPE_F64: rc = dispatch_mode<FA_DTYPE_F64>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor, sstr); break;
+    case FA_DTYPE_I64: rc = dispatch_mode<FA_DTYPE_I64>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor, sstr); break;
   }
   if (rc) return rc;
   FA_HIP(hipGetLastError());
   return release(slot, st);
+}
+}  // namespace
+
+int fa_weighted_sum_multi(fa_ctx* ctx, int dtype, int mode, int32_t num_segments,
+                          const int64_t* seg_numel, int32_t k, const void* const* d_in,
+                          const double* coef, double divisor, void* const* d_out, void* hip_stream) {
+  return wsum_impl(ctx, dtype, mode, num_segments, seg_numel, k, d_in, coef, divisor, d_out, hip_stream, 0);
 }
 
 int fa_weighted_sum(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t k, const void* const* d_in,
                     const double* coef, double divisor, void* d_out, void* hip_stream) {
   if (n < 0) return fail(FA_ERR_INVALID, "n must be >= 0");
   void* outs[1] = {d_out};
-  return fa_weighted_sum_multi(ctx, dtype, mode, 1, &n, k, d_in, coef, divisor, outs, hip_stream);
+  return wsum_impl(ctx, dtype, mode, 1, &n, k, d_in, coef, divisor, outs, hip_stream, 0);
 }
 
-int fa_weighted_sum_grouped(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t k, const void* const* d_in,
-                            const double* coef, double divisor, int32_t num_groups, const int32_t* group_ptr,
-                            int group_mode, const double* group_coef, const double* group_divisor,
-                            void* d_out, void* hip_stream) {
+int fa_weighted_sum_tiled(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t k, const void* const* d_in,
+                          int64_t tile_stride, const double* coef, double divisor, void* d_out,
+                          void* hip_stream) {
+  if (n < 0) return fail(FA_ERR_INVALID, "n must be >= 0");
+  if (tile_stride <= 0 || tile_stride % FA_TILE_BYTES)
+    return fail(FA_ERR_INVALID, "tile_stride must be a positive multiple of %d (got %lld)", FA_TILE_BYTES,
+                (long long)tile_stride);
+  void* outs[1] = {d_out};
+  return wsum_impl(ctx, dtype, mode, 1, &n, k, d_in, coef, divisor, outs, hip_stream, tile_stride);
+}
+
+namespace {
+int grouped_impl(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t k, const void* const* d_in,
+                 const double* coef, double divisor, int32_t num_groups, const int32_t* group_ptr,
+                 int group_mode, const double* group_coef, const double* group_divisor,
+                 void* d_out, void* hip_stream, int64_t sstr) {
   if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
   if (k <= 0 || n < 0 || !d_in || !d_out || num_groups <= 0 || !group_ptr)
     return fail(FA_ERR_INVALID, "fa_weighted_sum_grouped: invalid arguments");
@@ -1000,6 +1035,7 @@ int fa_weighted_sum_grouped(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t
     aligned = aligned && al16(d_in[i]);
   }
   if (n == 0) return FA_OK;
+  if (sstr && !aligned) return fail(FA_ERR_INVALID, "tiled inputs and the output must be 16-byte aligned");
   const int64_t tile_elems = (int64_t)kBlock * elems_per_vec(dtype);
   const int64_t tiles = (n + tile_elems - 1) / tile_elems;
   if (tiles > 0x7FFFFFFFll) return fail(FA_ERR_INVALID, "too many tiles");
@@ -1032,7 +1068,7 @@ int fa_weighted_sum_grouped(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t
   const void* const* dp = (const void* const*)(dv + seg_bytes + coef_bytes + grp_bytes);
   const dim3 grid((unsigned)tiles), blk(kBlock);
 #define FA_G(DT, MODE) \
-  hipLaunchKernelGGL((k_wsum_grouped<DT, MODE, 8, true>), grid, blk, 0, st, ds, dc, dp, divisor, dg, num_groups, group_mode)
+  hipLaunchKernelGGL((k_wsum_grouped<DT, MODE, 8, true>), grid, blk, 0, st, ds, dc, dp, divisor, dg, num_groups, group_mode, sstr)
 #define FA_G_MODES(DT)                                   \
   switch (mode) {                                        \
     case FA_MODE_MUL_W: FA_G(DT, FA_MODE_MUL_W); break;  \
@@ -1049,6 +1085,26 @@ int fa_weighted_sum_grouped(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t
 #undef FA_G
   FA_HIP(hipGetLastError());
   return release(slot, st);
+}
+}  // namespace
+
+int fa_weighted_sum_grouped(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t k, const void* const* d_in,
+                            const double* coef, double divisor, int32_t num_groups, const int32_t* group_ptr,
+                            int group_mode, const double* group_coef, const double* group_divisor,
+                            void* d_out, void* hip_stream) {
+  return grouped_impl(ctx, dtype, mode, n, k, d_in, coef, divisor, num_groups, group_ptr, group_mode, group_coef,
+                      group_divisor, d_out, hip_stream, 0);
+}
+
+int fa_weighted_sum_grouped_tiled(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t k, const void* const* d_in,
+                                  int64_t tile_stride, const double* coef, double divisor, int32_t num_groups,
+                                  const int32_t* group_ptr, int group_mode, const double* group_coef,
+                                  const double* group_divisor, void* d_out, void* hip_stream) {
+  if (tile_stride <= 0 || tile_stride % FA_TILE_BYTES)
+    return fail(FA_ERR_INVALID, "tile_stride must be a positive multiple of %d (got %lld)", FA_TILE_BYTES,
+                (long long)tile_stride);
+  return grouped_impl(ctx, dtype, mode, n, k, d_in, coef, divisor, num_groups, group_ptr, group_mode, group_coef,
+                      group_divisor, d_out, hip_stream, tile_stride);
 }
 
 int fa_fedavg_sgd(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, int32_t k,

@@ -48,9 +48,11 @@ def _engine_local_grouped(xs, mode, coef, divisor, gptr, gmode, gcoef, gdiv, out
                                                              gdiv, out=out)
 
 
-def chunk_bounds(n: int, chunks: int) -> List[tuple]:
-    chunks = max(1, min(chunks, n)) if n > 0 else 1
-    return [(n * c // chunks, n * (c + 1) // chunks) for c in range(chunks)]
+def chunk_bounds(n: int, chunks: int, align: int = 1) -> List[tuple]:
+    """``chunks`` consecutive ranges covering [0, n); inner bounds are multiples of ``align``."""
+    units = -(-n // align)
+    chunks = max(1, min(chunks, units)) if units > 0 else 1
+    return [(min(n, units * c // chunks * align), min(n, units * (c + 1) // chunks * align)) for c in range(chunks)]
 
 
 class GroupReducer:
@@ -119,6 +121,20 @@ class GroupReducer:
                 self.local_sum(terms, SUM, None, 1.0, part)
         return self._run(flat, local, out, mode=MUL_W)
 
+    def fedavg_tiled(self, engine, buf: torch.Tensor, rows: Sequence[int], weights: Sequence[float], n: int,
+                     out: Optional[torch.Tensor] = None):
+        """``fedavg`` over rows of a tile-interleaved ClientArena group ``buf`` ([tiles, capacity, E],
+        fedml_amd/arena.py): chunks are whole tiles, each chunk one fa_weighted_sum_tiled launch."""
+        E = buf.shape[2]
+        w = list(weights)
+        rows = list(rows)
+
+        def local(part, a, b):
+            if a % E:
+                raise ValueError("fedavg_tiled: chunk does not start on a tile boundary")
+            engine.weighted_sum_tiled(buf, rows, MUL_W, w, n=b - a, t0=a // E, out=part)
+        return self._run_n(n, buf.dtype, buf.device, local, out, MUL_W, align=E)
+
     def sum(self, xs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None):
         """Plain global sum (FedAvg_seq / FedDyn branches)."""
         flat = [x.reshape(-1) for x in xs]
@@ -127,21 +143,21 @@ class GroupReducer:
 
     # -------------------------------------------------------------- implementation
     def _run(self, flat, local, out, mode):
-        n = flat[0].numel()
-        dev = flat[0].device
+        return self._run_n(flat[0].numel(), flat[0].dtype, flat[0].device, local, out, mode)
+
+    def _run_n(self, n, dtype, dev, local, out, mode, align: int = 1):
         if out is None:
-            out = torch.empty(n, dtype=torch.float32 if flat[0].dtype == torch.int64 and mode != SUM
-                              else flat[0].dtype, device=dev)
+            out = torch.empty(n, dtype=torch.float32 if dtype == torch.int64 and mode != SUM else dtype, device=dev)
         works = []
         gathered = []
         if self.collective == "reduce_scatter":
-            if n % self.world:
-                raise ValueError("reduce_scatter needs P divisible by the world size")
+            if n % self.world or (n // self.world) % align:
+                raise ValueError("reduce_scatter needs P divisible by the world size (and shards of whole tiles)")
             S = n // self.world
             shard = torch.empty(S, dtype=out.dtype, device=dev)
             # chunk-major staging: chunk [a, b) of every rank's shard is laid out contiguously
             # (rank-major inside the chunk), which is what reduce_scatter_tensor consumes
-            for a, b in chunk_bounds(S, self.chunks):
+            for a, b in chunk_bounds(S, self.chunks, align):
                 L = b - a
                 base = self.world * a
                 for r in range(self.world):
@@ -156,7 +172,7 @@ class GroupReducer:
             for w in works:
                 w.wait()
             return shard
-        for a, b in chunk_bounds(n, self.chunks):
+        for a, b in chunk_bounds(n, self.chunks, align):
             part = out[a:b]
             local(part, a, b)
             if self.world == 1:

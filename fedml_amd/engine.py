@@ -168,6 +168,73 @@ class AggEngine:
         N.check(rc, "fa_weighted_sum")
         return out
 
+    def _tiled_args(self, buf: torch.Tensor, rows: Sequence[int], t0: int, n: Optional[int], what: str):
+        """Pointer table of a tile-interleaved arena group ``buf`` = [tiles, capacity, E] (E elements =
+        N.TILE_BYTES): rows ``rows`` starting at tile ``t0``, ``n`` logical elements."""
+        if buf.dim() != 3 or not buf.is_contiguous() or buf.shape[2] * buf.element_size() != N.TILE_BYTES:
+            raise ValueError(f"{what}: buf must be a contiguous [tiles, capacity, {N.TILE_BYTES}-byte tile] tensor")
+        _require_device(buf, self.device, "arena")
+        if buf.dtype not in DTYPE_CODE:
+            raise TypeError(f"{what}: unsupported dtype {buf.dtype}")
+        ntile, cap, E = buf.shape
+        if len(rows) == 0:
+            raise ValueError(f"{what}: no rows")
+        if min(rows) < 0 or max(rows) >= cap:
+            raise IndexError(f"{what}: row out of range")
+        if not 0 <= t0 <= ntile:
+            raise IndexError(f"{what}: first tile {t0} out of range")
+        avail = (ntile - t0) * E
+        n = avail if n is None else int(n)
+        if not 0 <= n <= avail:
+            raise ValueError(f"{what}: {n} elements from tile {t0} exceed the arena ({avail})")
+        stride = cap * N.TILE_BYTES
+        base = buf.data_ptr() + t0 * stride
+        return n, N.ptr_array([base + r * N.TILE_BYTES for r in rows]), stride
+
+    def weighted_sum_tiled(self, buf: torch.Tensor, rows: Sequence[int], mode: int,
+                           coef: Optional[Sequence[float]] = None, divisor: float = 1.0, n: Optional[int] = None,
+                           t0: int = 0, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """Ordered reduction over rows of a TILE-INTERLEAVED arena group (fa_weighted_sum_tiled):
+        ``buf[t, r, :]`` is tile t of client row r, so one workgroup's K tiles are one contiguous run.
+        Reduces ``n`` elements (default: all) starting at tile ``t0``; the output is flat."""
+        n, ptrs, stride = self._tiled_args(buf, rows, t0, n, "weighted_sum_tiled")
+        k = len(rows)
+        if mode != SUM and (coef is None or len(coef) != k):
+            raise ValueError("weighted_sum_tiled: need one coefficient per row")
+        odt = out_dtype(buf.dtype, mode)
+        if out is None:
+            out = torch.empty(n, dtype=odt, device=self.device)
+        elif out.dtype != odt or out.numel() != n:
+            raise ValueError(f"weighted_sum_tiled: output must be {odt} with {n} elements")
+        _require_device(out, self.device, "output")
+        rc = self._lib.fa_weighted_sum_tiled(
+            self._ctx, DTYPE_CODE[buf.dtype], int(mode), n, k, ptrs, stride,
+            N.f64_array(coef) if coef is not None else None, float(divisor), out.data_ptr(), self._stream(stream))
+        N.check(rc, "fa_weighted_sum_tiled")
+        return out
+
+    def weighted_sum_grouped_tiled(self, buf: torch.Tensor, rows: Sequence[int], mode: int,
+                                   coef: Optional[Sequence[float]], divisor: float, group_ptr: Sequence[int],
+                                   group_mode: int, group_coef: Optional[Sequence[float]] = None,
+                                   group_divisor: Optional[Sequence[float]] = None, n: Optional[int] = None,
+                                   t0: int = 0, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """fa_weighted_sum_grouped over rows of a tile-interleaved arena group (see weighted_sum_tiled)."""
+        if buf.dtype not in (torch.float32, torch.bfloat16, torch.float16, torch.float64):
+            raise TypeError(f"weighted_sum_grouped_tiled: unsupported dtype {buf.dtype}")
+        n, ptrs, stride = self._tiled_args(buf, rows, t0, n, "weighted_sum_grouped_tiled")
+        if out is None:
+            out = torch.empty(n, dtype=buf.dtype, device=self.device)
+        elif out.dtype != buf.dtype or out.numel() != n:
+            raise ValueError(f"weighted_sum_grouped_tiled: output must be {buf.dtype} with {n} elements")
+        _require_device(out, self.device, "output")
+        rc = self._lib.fa_weighted_sum_grouped_tiled(
+            self._ctx, DTYPE_CODE[buf.dtype], int(mode), n, len(rows), ptrs, stride,
+            N.f64_array(coef) if coef is not None else None, float(divisor), len(group_ptr) - 1,
+            N.i32_array(group_ptr), int(group_mode), N.f64_array(group_coef) if group_coef is not None else None,
+            N.f64_array(group_divisor) if group_divisor is not None else None, out.data_ptr(), self._stream(stream))
+        N.check(rc, "fa_weighted_sum_grouped_tiled")
+        return out
+
     def weighted_sum_grouped(self, xs: Sequence[torch.Tensor], mode: int, coef: Optional[Sequence[float]],
                              divisor: float, group_ptr: Sequence[int], group_mode: int,
                              group_coef: Optional[Sequence[float]] = None,

@@ -77,7 +77,7 @@ enum fa_status {
     FA_ERR_NOMEM = -4     /* staging allocation failed                     */
 };
 
-#define FA_ABI_VERSION 1
+#define FA_ABI_VERSION 2
 
 /* ABI version of the loaded library (== FA_ABI_VERSION of the header it was built with). */
 int fa_abi_version(void);
@@ -112,6 +112,21 @@ int fa_weighted_sum_multi(fa_ctx *ctx, int dtype, int mode, int32_t num_segments
                            void *hip_stream);
 
 /*
+ * Tile-interleaved inputs (the ClientArena "tiled" layout, fedml_amd/arena.py): each input is a
+ * sequence of FA_TILE_BYTES slots placed `tile_stride` bytes apart, i.e. element e of client i is at
+ *   d_in[i] + (e / E) * tile_stride + (e % E) * sizeof(dtype),   E = FA_TILE_BYTES / sizeof(dtype).
+ * An arena of `capacity` clients stores tile t of client r at base + (t * capacity + r) * FA_TILE_BYTES,
+ * so d_in[i] = base + r_i * FA_TILE_BYTES and tile_stride = capacity * FA_TILE_BYTES: the K slots one
+ * workgroup reads are one contiguous run.  tile_stride == FA_TILE_BYTES is a flat input.  Inputs and
+ * d_out 16-byte aligned; d_out is flat.  Same arithmetic per element as fa_weighted_sum.
+ * Replaces the same loop (agg_operator.py:37-44); the layout is this engine's, not the reference's.
+ */
+#define FA_TILE_BYTES 4096
+int fa_weighted_sum_tiled(fa_ctx *ctx, int dtype, int mode, int64_t n, int32_t k,
+                          const void *const *d_in, int64_t tile_stride, const double *coef,
+                          double divisor, void *d_out, void *hip_stream);
+
+/*
  * Two-level (grouped) reduction in one pass, one flat vector per client:
  *   clients [group_ptr[g], group_ptr[g+1]) form group g (group_ptr[0] = 0, group_ptr[G] = k,
  *   groups non-empty); G_g = the ordered `mode` reduction of the group's clients (coef[i],
@@ -128,6 +143,12 @@ int fa_weighted_sum_grouped(fa_ctx *ctx, int dtype, int mode, int64_t n, int32_t
                             int32_t num_groups, const int32_t *group_ptr, int group_mode,
                             const double *group_coef, const double *group_divisor, void *d_out,
                             void *hip_stream);
+/* fa_weighted_sum_grouped over tile-interleaved inputs (addressing as fa_weighted_sum_tiled). */
+int fa_weighted_sum_grouped_tiled(fa_ctx *ctx, int dtype, int mode, int64_t n, int32_t k,
+                                  const void *const *d_in, int64_t tile_stride, const double *coef,
+                                  double divisor, int32_t num_groups, const int32_t *group_ptr,
+                                  int group_mode, const double *group_coef,
+                                  const double *group_divisor, void *d_out, void *hip_stream);
 
 /*
  * FedOpt server step fused into the FedAvg pass (simulation/mpi/fedopt/FedOptAggregator.py:

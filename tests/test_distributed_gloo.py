@@ -160,3 +160,71 @@ def _case_gossip(rank, world):
 
 def test_gossip_gloo_world2():
     _spawn(_case_gossip)
+
+
+def test_chunk_bounds_alignment():
+    from fedml_amd.distributed.group_reduce import chunk_bounds
+    for n, c, a in [(10, 3, 1), (10_000, 3, 1024), (5, 8, 1024), (1024 * 8, 8, 1024), (1024 * 8 + 1, 16, 1024)]:
+        b = chunk_bounds(n, c, a)
+        assert b[0][0] == 0 and b[-1][1] == n
+        assert all(x[1] == y[0] for x, y in zip(b, b[1:]))
+        assert all(lo % a == 0 for lo, _ in b)
+        assert len(b) <= c
+    assert chunk_bounds(10, 3) == [(0, 3), (3, 6), (6, 10)]
+
+
+class _OracleTiledEngine:
+    """Stands in for AggEngine.weighted_sum_tiled on CPU: gathers the logical elements of a
+    [tiles, capacity, E] buffer and reduces them with the oracle."""
+
+    def weighted_sum_tiled(self, buf, rows, mode, coef=None, divisor=1.0, n=None, t0=0, out=None):
+        _, cap, E = buf.shape
+        assert t0 >= 0 and n is not None
+        xs = [buf[t0:, r, :].reshape(-1)[:n] for r in rows]
+        return _oracle_sum(xs, mode, coef, divisor, out)
+
+
+def _tiled_buf(xs, E=1024):
+    n = xs[0].numel()
+    nt = -(-n // E)
+    buf = torch.zeros(nt, len(xs), E)
+    for j, x in enumerate(xs):
+        f = torch.zeros(nt * E)
+        f[:n] = x
+        buf[:, j, :] = f.view(nt, E)
+    return buf
+
+
+def _case_group_reduce_tiled(rank, world):
+    from oracle import orc
+    from fedml_amd.distributed.group_reduce import GroupReducer
+    K, P = 6, 1024 * 13 + 77
+    xs, counts = _clients(K, P, seed=11)
+    N = sum(counts)
+    per = K // world
+    mine = list(range(rank * per, (rank + 1) * per))
+    parts = [orc.weighted_sum([xs[i] for i in range(r * per, (r + 1) * per)], 0,
+                              [counts[i] / N for i in range(r * per, (r + 1) * per)]) for r in range(world)]
+    exp = orc.weighted_sum(parts, 2)
+    buf = _tiled_buf([xs[i] for i in mine])
+    for coll in ("reduce", "all_reduce", "ordered"):
+        for chunks in (1, 3, 8):
+            red = GroupReducer(collective=coll, chunks=chunks, local_sum=_oracle_sum)
+            got = red.fedavg_tiled(_OracleTiledEngine(), buf, list(range(per)), [counts[i] / N for i in mine], P)
+            if rank == 0 or coll == "all_reduce":
+                assert _bits(got, exp), (coll, chunks)
+    # reduce_scatter: shards of whole tiles
+    P2 = 1024 * 8
+    xs2 = [x[:P2].contiguous() for x in xs]
+    exp2 = orc.weighted_sum([orc.weighted_sum([xs2[i] for i in range(r * per, (r + 1) * per)], 0,
+                                              [counts[i] / N for i in range(r * per, (r + 1) * per)])
+                             for r in range(world)], 2)
+    red = GroupReducer(collective="reduce_scatter", chunks=3, local_sum=_oracle_sum)
+    shard = red.fedavg_tiled(_OracleTiledEngine(), _tiled_buf([xs2[i] for i in mine]), list(range(per)),
+                             [counts[i] / N for i in mine], P2)
+    S = P2 // world
+    assert _bits(shard, exp2[rank * S:(rank + 1) * S])
+
+
+def test_group_reduce_tiled_gloo_world2():
+    _spawn(_case_group_reduce_tiled)

@@ -1,0 +1,46 @@
+// layout_probe.hip -- tool only: is the client-major arena ([K][P], 128 streams) or a tile-interleaved
+// arena ([P/T][K][T], each workgroup's reads one contiguous K*T run) closer to the read ceiling?
+// Same 16-B non-temporal loads, U = 8 in flight, one 16-B store per lane, no arithmetic.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) u32x4* gp;
+typedef __attribute__((address_space(1))) u32x4* gpw;
+
+// rows: client i at base + i*row16 (16-B units); workgroup b = 4-KiB column tile b
+__global__ void __launch_bounds__(256) lp_rows(const u32x4* __restrict__ base, int64_t row16, int k, u32x4* out) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  u32x4 acc = {0, 0, 0, 0};
+  for (int i0 = 0; i0 < k; i0 += 8) {
+    u32x4 r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) r[u] = __builtin_nontemporal_load((gp)(base + (int64_t)min(i0 + u, k - 1) * row16 + e));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc ^= r[u];
+  }
+  __builtin_nontemporal_store(acc, (gpw)(out + e));
+}
+
+// tiled: tile t holds T16 16-B units of each client, client-major inside the tile
+// (tile t, client i) at base + (t*k + i)*T16; workgroup b covers 256 units of one tile.
+__global__ void __launch_bounds__(256) lp_tiled(const u32x4* __restrict__ base, int64_t T16, int k, u32x4* out) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;   // output unit
+  const int64_t t = e / T16, o = e - t * T16;
+  const u32x4* tb = base + t * k * T16 + o;
+  u32x4 acc = {0, 0, 0, 0};
+  for (int i0 = 0; i0 < k; i0 += 8) {
+    u32x4 r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) r[u] = __builtin_nontemporal_load((gp)(tb + (int64_t)min(i0 + u, k - 1) * T16));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc ^= r[u];
+  }
+  __builtin_nontemporal_store(acc, (gpw)(out + e));
+}
+
+extern "C" int lp_run(int mode, const void* base, int64_t p16, int k, int64_t t16, void* out, void* stream) {
+  const int64_t blocks = p16 / 256;
+  if (mode == 0) hipLaunchKernelGGL(lp_rows, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const u32x4*)base, p16, k, (u32x4*)out);
+  else hipLaunchKernelGGL(lp_tiled, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const u32x4*)base, t16, k, (u32x4*)out);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
