@@ -52,6 +52,9 @@ def parse():
     p.add_argument("--params", type=int, default=None)
     p.add_argument("--variant", type=int, default=0, help="kernel variant (fa_ctx_set_variant)")
     p.add_argument("--chunks", type=int, default=8, help="pipeline chunks of the cross-GPU reduce")
+    p.add_argument("--cu-mask", type=int, default=192,
+                   help="N > 1: run the local partials on a stream restricted to this many CUs (0 = off), "
+                        "leaving the rest to RCCL's kernels (fa_stream_create_cu_masked)")
     p.add_argument("--collective", default="reduce", choices=["reduce", "reduce_scatter", "all_reduce", "ordered"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
@@ -217,7 +220,8 @@ def wl_metric(args, eng, rank, world, timer):
             def weighted_sum_tiled(self, *a, **kw):
                 with timer:
                     return eng.weighted_sum_tiled(*a, **kw)
-        red = GroupReducer(collective=args.collective, chunks=args.chunks, local_sum=timed_sum)
+        red = GroupReducer(collective=args.collective, chunks=args.chunks, local_sum=timed_sum,
+                           stream=eng.cu_masked_stream(args.cu_mask) if args.cu_mask else None)
 
         def step():
             if tiled:
@@ -397,7 +401,8 @@ def wl_hier(args, eng, rank, world, timer):
 
     if world > 1:
         from fedml_amd.distributed.group_reduce import GroupReducer
-        red = GroupReducer(collective=args.collective, chunks=args.chunks, local_grouped=timed_grouped)
+        red = GroupReducer(collective=args.collective, chunks=args.chunks, local_grouped=timed_grouped,
+                           stream=eng.cu_masked_stream(args.cu_mask) if args.cu_mask else None)
 
         def step():
             red.hierarchical_groups(xs, gcounts, N, out=out)
@@ -787,7 +792,9 @@ def main():
                                    "resident in HBM"),
             "config": {"workload": wl["name"], "clients": wl["clients"], "params_per_client": wl["params"],
                        "parallelism": f"client-groups x{world}" +
-                                      (f", {args.collective} over RCCL in {args.chunks} chunks" if world > 1 else ""),
+                                      (f", {args.collective} over RCCL in {args.chunks} chunks"
+                                       + (f", local partials on {args.cu_mask} CUs" if args.cu_mask else "")
+                                       if world > 1 else ""),
                        "kernel_variant": args.variant, "layout": args.layout},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s",

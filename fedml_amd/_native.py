@@ -30,7 +30,7 @@ EXPORTED_SYMBOLS = (
     "fa_abi_version", "fa_ctx_create", "fa_ctx_destroy", "fa_weighted_sum",
     "fa_weighted_sum_multi", "fa_weighted_sum_tiled", "fa_weighted_sum_grouped", "fa_weighted_sum_grouped_tiled",
     "fa_fedavg_sgd", "fa_mix", "fa_ctx_set_variant",
-    "fa_ctx_set_mix_band", "fa_strerror", "fa_last_error",
+    "fa_ctx_set_mix_band", "fa_stream_create_cu_masked", "fa_stream_destroy", "fa_strerror", "fa_last_error",
     # include/fedagg_finite.h
     "fa_finite_sum", "fa_finite_quantize", "fa_lcc_decode",
     # include/fedagg_robust.h
@@ -65,6 +65,10 @@ def _declare(L):
     L.fa_ctx_set_variant.argtypes = [_vp, ctypes.c_int]
     L.fa_ctx_set_mix_band.restype = ctypes.c_int
     L.fa_ctx_set_mix_band.argtypes = [_vp, ctypes.c_int]
+    L.fa_stream_create_cu_masked.restype = ctypes.c_int
+    L.fa_stream_create_cu_masked.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+    L.fa_stream_destroy.restype = ctypes.c_int
+    L.fa_stream_destroy.argtypes = [_vp]
     L.fa_weighted_sum.restype = ctypes.c_int
     L.fa_weighted_sum.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int32,
                                   _P_vp, _P_d, ctypes.c_double, _vp, _vp]

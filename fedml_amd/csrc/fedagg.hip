@@ -902,6 +902,37 @@ int fa_ctx_set_mix_band(fa_ctx* c, int enable) {
   return FA_OK;
 }
 
+// A stream whose kernels run on `cu_count` of the device's CUs, spread evenly over the CU mask (so
+// every XCD keeps a share).  The aggregation stream needs about half the CUs for the full HBM rate
+// (tools/cumask_probe.py: 128-224 of 256 CUs stream 6.64-6.67 TB/s); on multi-GPU rounds the rest
+// stay free for RCCL's kernels, so the collective of chunk c runs beside the partial of chunk c+1.
+int fa_stream_create_cu_masked(int hip_device, int cu_count, void** out_stream) {
+  if (!out_stream) return fail(FA_ERR_INVALID, "fa_stream_create_cu_masked: out_stream is NULL");
+  *out_stream = nullptr;
+  DeviceGuard g(hip_device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", hip_device);
+  hipDeviceProp_t prop;
+  FA_HIP(hipGetDeviceProperties(&prop, hip_device));
+  const int total = prop.multiProcessorCount;
+  if (cu_count <= 0 || cu_count > total)
+    return fail(FA_ERR_INVALID, "cu_count must be in [1, %d] (got %d)", total, cu_count);
+  const int words = (total + 31) / 32;
+  uint32_t mask[64] = {0};
+  if (words > 64) return fail(FA_ERR_INVALID, "device has too many CUs (%d)", total);
+  for (int i = 0; i < total; ++i)
+    if ((int64_t)i * cu_count / total != (int64_t)(i + 1) * cu_count / total) mask[i / 32] |= 1u << (i % 32);
+  hipStream_t s = nullptr;
+  FA_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask));
+  *out_stream = (void*)s;
+  return FA_OK;
+}
+
+int fa_stream_destroy(void* stream) {
+  if (!stream) return FA_OK;
+  FA_HIP(hipStreamDestroy((hipStream_t)stream));
+  return FA_OK;
+}
+
 namespace {
 // fa_weighted_sum_multi / fa_weighted_sum_tiled.  sstr = 0: flat inputs; otherwise (one segment)
 // tile-interleaved inputs whose FA_TILE_BYTES slots are sstr bytes apart.

@@ -59,7 +59,8 @@ class GroupReducer:
     """Group -> global reduction of flat parameter vectors over a process group."""
 
     def __init__(self, group=None, collective: str = "reduce", dst: int = 0, chunks: int = 8,
-                 local_sum: Optional[LocalSum] = None, local_grouped: Optional[Callable] = None):
+                 local_sum: Optional[LocalSum] = None, local_grouped: Optional[Callable] = None,
+                 stream: Optional[torch.cuda.Stream] = None):
         if collective not in ("reduce", "all_reduce", "reduce_scatter", "ordered"):
             raise ValueError(f"unknown collective {collective!r}")
         self.group = group
@@ -73,6 +74,9 @@ class GroupReducer:
             _engine_local_grouped if local_sum is None else None)
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        # optional stream for the local partials and the collectives' dependencies, e.g. a CU-masked
+        # stream (AggEngine.cu_masked_stream) that leaves CUs free for RCCL's kernels
+        self.stream = stream
 
     # -------------------------------------------------------------- public entry points
     def fedavg(self, xs: Sequence[torch.Tensor], weights: Sequence[float], out: Optional[torch.Tensor] = None):
@@ -148,6 +152,19 @@ class GroupReducer:
     def _run_n(self, n, dtype, dev, local, out, mode, align: int = 1):
         if out is None:
             out = torch.empty(n, dtype=torch.float32 if dtype == torch.int64 and mode != SUM else dtype, device=dev)
+        if self.stream is None:
+            return self._run_body(n, dev, local, out, align)
+        caller = torch.cuda.current_stream(dev)
+        self.stream.wait_stream(caller)      # inputs / out were produced on the caller's stream
+        out.record_stream(self.stream)
+        with torch.cuda.stream(self.stream):
+            res = self._run_body(n, dev, local, out, align)
+        caller.wait_stream(self.stream)      # the result is consumed on the caller's stream
+        if res is not out:
+            res.record_stream(caller)        # allocated on self.stream, used on the caller's
+        return res
+
+    def _run_body(self, n, dev, local, out, align):
         works = []
         gathered = []
         if self.collective == "reduce_scatter":

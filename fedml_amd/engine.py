@@ -65,6 +65,9 @@ class AggEngine:
             return eng
 
     def close(self):
+        for h in getattr(self, "_owned_streams", []):
+            self._lib.fa_stream_destroy(N.ctypes.c_void_p(h))
+        self._owned_streams = []
         if getattr(self, "_ctx", None) is not None and self._ctx.value:
             self._lib.fa_ctx_destroy(self._ctx)
             self._ctx = N.ctypes.c_void_p()
@@ -80,6 +83,15 @@ class AggEngine:
 
     def set_mix_band(self, enable: bool):
         N.check(self._lib.fa_ctx_set_mix_band(self._ctx, int(bool(enable))), "fa_ctx_set_mix_band")
+
+    def cu_masked_stream(self, cu_count: int) -> torch.cuda.ExternalStream:
+        """A torch stream whose kernels run on ``cu_count`` CUs of this device
+        (fa_stream_create_cu_masked); kept alive for the engine's lifetime."""
+        h = N.ctypes.c_void_p()
+        N.check(self._lib.fa_stream_create_cu_masked(self.device_index, int(cu_count), N.ctypes.byref(h)),
+                "fa_stream_create_cu_masked")
+        self._owned_streams = getattr(self, "_owned_streams", []) + [h.value]
+        return torch.cuda.ExternalStream(h.value, device=self.device)
 
     def _stream(self, stream=None):
         s = stream if stream is not None else torch.cuda.current_stream(self.device)

@@ -189,6 +189,15 @@ int fa_ctx_set_variant(fa_ctx *ctx, int variant);
  * uses the general CSR kernel); default 1. */
 int fa_ctx_set_mix_band(fa_ctx *ctx, int enable);
 
+/*
+ * A HIP stream restricted to `cu_count` of the device's CUs (spread evenly over the CU mask).
+ * Launch the aggregation on it during multi-GPU rounds: the HBM stream saturates with about half
+ * of the CUs, and the others stay free for the RCCL collective running beside it.  Destroy with
+ * fa_stream_destroy.  Not part of the arithmetic contract.
+ */
+int fa_stream_create_cu_masked(int hip_device, int cu_count, void **out_stream);
+int fa_stream_destroy(void *stream);
+
 /* Static name of a status code. */
 const char *fa_strerror(int code);
 /* Detail of the calling thread's last error ("" if none). */

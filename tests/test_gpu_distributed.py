@@ -62,3 +62,42 @@ def test_distributed_gossip_engine(pg):
     exp, _ = orc.mix(xs, *gossip_rows(m.topology))
     for a, b in zip(outs, exp):
         assert _bits(a, b)
+
+
+@pytest.mark.parametrize("collective", ["reduce", "all_reduce", "ordered", "reduce_scatter"])
+def test_group_reducer_tiled_on_cu_masked_stream(pg, collective):
+    """The bench's N > 1 local step: tiled arena partials on a CU-masked stream, collectives
+    ordered behind them, result handed back to the caller's stream."""
+    from oracle import orc
+    from fedml_amd.arena import ArenaLayout, ClientArena
+    from fedml_amd.distributed.group_reduce import GroupReducer
+    from fedml_amd.engine import get_engine
+    eng = get_engine(0)
+    g = torch.Generator().manual_seed(7)
+    K, P = 5, 1024 * 40
+    xs = [torch.randn(P, generator=g) for _ in range(K)]
+    counts = [int(v) for v in torch.randint(50, 601, (K,), generator=g)]
+    w = [c / sum(counts) for c in counts]
+    arena = ClientArena(ArenaLayout([("w", (P,), torch.float32)]), K, device="cuda:0", tiled=True)
+    for i, x in enumerate(xs):
+        arena.write(i, {"w": x.cuda()})
+    red = GroupReducer(collective=collective, chunks=3, stream=eng.cu_masked_stream(128))
+    got = red.fedavg_tiled(eng, arena.bufs[torch.float32], list(range(K)), w, P)
+    got = got.clone()  # consumed on the caller's stream
+    torch.cuda.synchronize()
+    assert _bits(got, orc.weighted_sum(xs, 0, w))
+
+
+def test_cu_masked_stream_engine(pg):
+    from oracle import orc
+    from fedml_amd.engine import get_engine
+    eng = get_engine(0)
+    s = eng.cu_masked_stream(64)
+    g = torch.Generator().manual_seed(3)
+    xs = [torch.randn(300_001, generator=g) for _ in range(6)]
+    ys = [x.cuda() for x in xs]
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        out = eng.weighted_sum(ys, 2)
+    s.synchronize()
+    assert _bits(out, orc.weighted_sum(xs, 2))

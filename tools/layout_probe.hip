@@ -44,3 +44,22 @@ extern "C" int lp_run(int mode, const void* base, int64_t p16, int k, int64_t t1
   else hipLaunchKernelGGL(lp_tiled, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const u32x4*)base, t16, k, (u32x4*)out);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+// CU-masked stream (hipExtStreamCreateWithCUMask): how many CUs does the tiled stream need for full
+// HBM rate?  (Leaving CUs free for RCCL's kernels on multi-GPU runs.)
+extern "C" int lp_masked_stream(int ncu_enabled, void** out_stream) {
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, 0) != hipSuccess) return -1;
+  const int total = prop.multiProcessorCount;
+  uint32_t mask[16] = {0};
+  int words = (total + 31) / 32;
+  // spread the disabled CUs evenly over the index space (XCDs/SEs interleave in the mask)
+  for (int i = 0; i < total; ++i) {
+    const bool on = (int64_t)i * ncu_enabled / total != (int64_t)(i + 1) * ncu_enabled / total;
+    if (on) mask[i / 32] |= 1u << (i % 32);
+  }
+  hipStream_t s;
+  if (hipExtStreamCreateWithCUMask(&s, words, mask) != hipSuccess) return -2;
+  *out_stream = (void*)s;
+  return total;
+}
