@@ -3,16 +3,15 @@
 // squared distances.
 //
 // Coordinate-wise median (k_median): torch.median over the client axis is a SELECTION, so the
-// result is one of the inputs, bit for bit.  One lane owns one coordinate: it streams the K client
-// values into registers as order-preserving uint32 keys (floats mapped so that unsigned order ==
-// numeric order, -0.0 folded onto +0.0), sorts them with a bitonic network padded to P2 = next
-// power of two with max-key sentinels (P2 (P2 log2 P2 ...)/4 compare-exchanges, each a v_min_u32 +
-// v_max_u32 on compile-time register indices), and takes key[(K-1)/2] (uniform index -> one select
-// chain).  ATen's exact rules are kept: a NaN anywhere in the column returns the FIRST NaN; among
-// equal values the client index decides, which only matters for +-0 -- both cases (a NaN seen, or
-// a zero selected) take a short in-order rescan of the column.
-// Compute per coordinate ~P2 log2^2 P2 ops vs K*s bytes of HBM: memory-bound to K ~ 64, roughly
-// balanced at K = 128.  Larger K: a rank-counting kernel (O(K^2) per coordinate, L2-resident).
+// result is one of the inputs, bit for bit.  One lane owns one coordinate: it loads the K client
+// values (all loads in flight at once), maps them to order-preserving uint32 keys (unsigned order
+// == numeric order, -0.0 just below +0.0), pads to P2 = next power of two with low/high sentinels
+// that put the lower median at rank P2/2 - 1, and selects that rank with a pruned odd-even merge
+// network (median_nets.h: 283 min/max for P2 = 32, 2,299 for P2 = 128, vs 480 / 3,584 for a full
+// bitonic sort).  ATen's exact rules are kept: a NaN anywhere in the column returns the FIRST NaN;
+// among equal values the client index decides, which only matters for +-0 -- both cases (a NaN
+// seen, or a zero selected) take a short in-order rescan of the column.
+// K <= 128 runs the network; larger K and float64 a rank-counting kernel (O(K^2) per coordinate).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -22,23 +21,32 @@
 
 #include "fa_internal.h"
 #include "fedagg_robust.h"
+#include "median_nets.h"
 
 using namespace fa_detail;
 
 namespace {
 
-constexpr int kMaxP2 = 64;  // largest column one lane sorts (a 128-key network takes the compiler minutes)
+constexpr int kMaxP2 = 128;  // largest column one lane selects from (median_nets.h)
+
+// Raw element loads in the global address space (global_load_*: vmcnt only).  Generic (flat)
+// loads also count in lgkmcnt, so every s_waitcnt for the next scalar pointer load drained them and
+// the per-client loads of a column ran one HBM round trip at a time.
+template <typename T>
+__device__ __forceinline__ T gld(const void* p, int64_t e) {
+  return ((const __attribute__((address_space(1))) T*)p)[e];
+}
 
 template <int DT> struct MedT;
 template <> struct MedT<FA_DTYPE_F32> {
   using S = unsigned;
-  __device__ static float load(const void* p, int64_t e) { return ((const float*)p)[e]; }
+  __device__ static float load(const void* p, int64_t e) { return gld<float>(p, e); }
   __device__ static void store(void* p, int64_t e, float v) { ((float*)p)[e] = v; }
   __device__ static void store_bits(void* p, int64_t e, const void* src) { ((unsigned*)p)[e] = ((const unsigned*)src)[e]; }
 };
 template <> struct MedT<FA_DTYPE_BF16> {
   __device__ static float load(const void* p, int64_t e) {
-    return __uint_as_float((unsigned)((const unsigned short*)p)[e] << 16);
+    return __uint_as_float((unsigned)gld<unsigned short>(p, e) << 16);
   }
   __device__ static void store(void* p, int64_t e, float v) {
     ((unsigned short*)p)[e] = (unsigned short)(__float_as_uint(v) >> 16);  // exact: v came from bf16
@@ -49,7 +57,7 @@ template <> struct MedT<FA_DTYPE_BF16> {
 };
 template <> struct MedT<FA_DTYPE_F16> {
   __device__ static float load(const void* p, int64_t e) {
-    return (float)__builtin_bit_cast(_Float16, ((const unsigned short*)p)[e]);
+    return (float)__builtin_bit_cast(_Float16, gld<unsigned short>(p, e));
   }
   __device__ static void store(void* p, int64_t e, float v) {
     ((unsigned short*)p)[e] = __builtin_bit_cast(unsigned short, (_Float16)v);  // exact: v came from f16
@@ -79,25 +87,6 @@ struct MSeg {
 };
 static_assert(sizeof(MSeg) == 32, "MSeg layout");
 
-template <int P2>
-__device__ __forceinline__ void bitonic_sort(unsigned (&key)[P2]) {
-#pragma unroll
-  for (int size = 2; size <= P2; size <<= 1) {
-#pragma unroll
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
-#pragma unroll
-      for (int i = 0; i < P2; ++i) {
-        const int j = i ^ stride;
-        if (j > i) {
-          const unsigned lo = min(key[i], key[j]), hi = max(key[i], key[j]);
-          if ((i & size) == 0) { key[i] = lo; key[j] = hi; }
-          else { key[i] = hi; key[j] = lo; }
-        }
-      }
-    }
-  }
-}
-
 // Rare cases, resolved by an in-order rescan of the column: a NaN anywhere -> ATen returns the
 // FIRST NaN; a zero selected -> the selected rank r falls in the block of (equal) zeros, which ATen
 // orders by client index -> the (r - #negatives)-th zero in client order.
@@ -121,6 +110,11 @@ __device__ __forceinline__ void store_rare(const void* const* in, int k, int64_t
   }
 }
 
+// One lane per coordinate.  Loads: the column's K client pointers first (scalar loads), then all
+// P2 element loads (clamped, unconditional) before any is consumed.  Keys: the K real keys, then
+// L = P2/2 - 1 - (K-1)/2 low sentinels (0, below every non-NaN key) and high sentinels
+// (0xFFFFFFFF) for the rest, so the lower median of the reals is rank P2/2 - 1 of all P2 keys --
+// which the pruned network select_mid<P2> (median_nets.h) computes.
 template <int DT, int P2>
 __global__ void __launch_bounds__(kBlock)
 k_median(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k) {
@@ -130,77 +124,23 @@ k_median(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict_
   const bool live = e < sg.numel;
   const int64_t ec = live ? e : sg.numel - 1;
   const void* const* in = ptrs + sg.ptr_base;
+  const void* p[P2];
+#pragma unroll
+  for (int i = 0; i < P2; ++i) p[i] = in[min(i, k - 1)];
+  float x[P2];
+#pragma unroll
+  for (int i = 0; i < P2; ++i) x[i] = MedT<DT>::load(p[i], ec);  // clamped: every load unconditional
+  const int lo_end = k + P2 / 2 - 1 - ((k - 1) >> 1);              // sentinels [k, lo_end) are low
   unsigned key[P2];
   bool nan = false;
 #pragma unroll
   for (int i = 0; i < P2; ++i) {
-    const float x = MedT<DT>::load(in[min(i, k - 1)], ec);  // clamped: every load unconditional
-    nan = nan || (i < k && x != x);                          // P2 - k < P2 / 2 sentinels
-    key[i] = i < k ? fkey(x) : 0xFFFFFFFFu;
+    nan = nan || (i < k && x[i] != x[i]);
+    key[i] = i < k ? fkey(x[i]) : (i < lo_end ? 0u : 0xFFFFFFFFu);
   }
-  bitonic_sort<P2>(key);
-  const int r = (k - 1) >> 1;
-  unsigned kr = key[0];
-#pragma unroll
-  for (int i = 1; i < P2; ++i) kr = (i == r) ? key[i] : kr;  // uniform r: folds to one select chain
+  const unsigned kr = select_mid<P2>(key);
   if (!live) return;
-  if (nan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, nan, sg.out);
-  else MedT<DT>::store(sg.out, e, fkey_inv(kr));
-}
-
-// 64 < K <= 128: two lanes per coordinate, each sorting the keys of 64 clients (lane 2p: clients
-// 0..63, lane 2p+1: clients 64..127, max-key sentinels past K).  One cross-lane bitonic step
-// (lane 2p keeps min(A[i], B[63-i]), a bitonic sequence holding the 64 smallest keys) and a 64-key
-// bitonic merge leave the 64 smallest keys sorted in lane 2p -- and rank (K-1)/2 <= 63 is among
-// them.  Segment tiles are kBlock/2 coordinates (MSeg.tile_start counts those tiles).
-template <int DT>
-__global__ void __launch_bounds__(kBlock)
-k_median2(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k) {
-  constexpr int H = kMaxP2;
-  const int64_t tile = blockIdx.x;
-  const MSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
-  const int half = threadIdx.x & 1;
-  const int64_t e = (tile - sg.tile_start) * (kBlock / 2) + (threadIdx.x >> 1);
-  const bool live = e < sg.numel;
-  const int64_t ec = live ? e : sg.numel - 1;
-  const void* const* in = ptrs + sg.ptr_base;
-  unsigned key[H];
-  bool nan = false;
-#pragma unroll
-  for (int i = 0; i < H; ++i) {
-    const int c = half * H + i;
-    const float x = MedT<DT>::load(in[min(c, k - 1)], ec);  // clamped: the load is unconditional
-    nan = nan || (c < k && x != x);
-    key[i] = c < k ? fkey(x) : 0xFFFFFFFFu;
-  }
-  bitonic_sort<H>(key);
-  // cross-lane step of the 128-key bitonic merge (partner = lane ^ 1)
-#pragma unroll
-  for (int i = 0; i < H / 2; ++i) {  // pairs (i, H-1-i): both partner values read before either is written
-    const unsigned o_hi = __shfl_xor(key[H - 1 - i], 1), o_lo = __shfl_xor(key[i], 1);
-    key[i] = half == 0 ? min(key[i], o_hi) : max(key[i], o_hi);
-    key[H - 1 - i] = half == 0 ? min(key[H - 1 - i], o_lo) : max(key[H - 1 - i], o_lo);
-  }
-  // bitonic merge of the (bitonic) lower half into ascending order
-#pragma unroll
-  for (int stride = H >> 1; stride > 0; stride >>= 1) {
-#pragma unroll
-    for (int i = 0; i < H; ++i) {
-      const int j = i ^ stride;
-      if (j > i) {
-        const unsigned lo = min(key[i], key[j]), hi = max(key[i], key[j]);
-        key[i] = lo;
-        key[j] = hi;
-      }
-    }
-  }
-  const int partner_nan = __shfl_xor((int)nan, 1);  // every lane shuffles (no short-circuit)
-  nan = nan || partner_nan != 0;
-  if (half != 0 || !live) return;
   const int r = (k - 1) >> 1;
-  unsigned kr = key[0];
-#pragma unroll
-  for (int i = 1; i < H; ++i) kr = (i == r) ? key[i] : kr;
   if (nan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, nan, sg.out);
   else MedT<DT>::store(sg.out, e, fkey_inv(kr));
 }
@@ -210,7 +150,7 @@ template <typename T> __device__ __forceinline__ T ldv(const void* p, int64_t e)
 
 template <int DT>
 __device__ __forceinline__ double load_d(const void* p, int64_t e) {
-  if constexpr (DT == FA_DTYPE_F64) return ((const double*)p)[e];
+  if constexpr (DT == FA_DTYPE_F64) return gld<double>(p, e);
   else return (double)MedT<DT>::load(p, e);
 }
 template <int DT>
@@ -244,7 +184,7 @@ k_median_rank(const MSeg* __restrict__ segs, int nseg, const void* const* __rest
 }
 
 template <int DT>
-void launch_median(int k, dim3 grid, dim3 grid2, hipStream_t st, const MSeg* ds, int nseg, const void* const* dp) {
+void launch_median(int k, dim3 grid, hipStream_t st, const MSeg* ds, int nseg, const void* const* dp) {
   if constexpr (DT == FA_DTYPE_F64) {
     hipLaunchKernelGGL((k_median_rank<DT>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);
   } else {
@@ -253,10 +193,7 @@ void launch_median(int k, dim3 grid, dim3 grid2, hipStream_t st, const MSeg* ds,
     if (k <= 16) { hipLaunchKernelGGL((k_median<DT, 16>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); return; }
     if (k <= 32) { hipLaunchKernelGGL((k_median<DT, 32>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); return; }
     if (k <= 64) { hipLaunchKernelGGL((k_median<DT, 64>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); return; }
-    if (k <= 2 * kMaxP2) {  // two lanes per coordinate: half the grid's coordinates per block
-      hipLaunchKernelGGL((k_median2<DT>), grid2, dim3(kBlock), 0, st, ds, nseg, dp, k);
-      return;
-    }
+    if (k <= kMaxP2) { hipLaunchKernelGGL((k_median<DT, 128>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); return; }
     hipLaunchKernelGGL((k_median_rank<DT>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);
   }
 }
@@ -273,9 +210,7 @@ int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t*
     return fail(FA_ERR_INVALID, "fa_coord_median: invalid arguments");
   if (dtype != FA_DTYPE_F32 && dtype != FA_DTYPE_BF16 && dtype != FA_DTYPE_F16 && dtype != FA_DTYPE_F64)
     return fail(FA_ERR_DTYPE, "fa_coord_median: dtype %d not supported (F32, BF16, F16, F64)", dtype);
-  // coordinates per tile: kBlock, or kBlock/2 when two lanes share a coordinate (64 < k <= 128)
-  const bool two_lane = dtype != FA_DTYPE_F64 && k > kMaxP2 && k <= 2 * kMaxP2;
-  const int64_t tile_elems = two_lane ? kBlock / 2 : kBlock;
+  const int64_t tile_elems = kBlock;  // coordinates per tile (one lane each)
   int nseg = 0;
   int64_t tiles = 0;
   for (int s = 0; s < num_segments; ++s) {
@@ -317,10 +252,10 @@ int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t*
   const void* const* dp = (const void* const*)(dv + seg_bytes);
   const dim3 grid((unsigned)tiles);
   switch (dtype) {
-    case FA_DTYPE_F32: launch_median<FA_DTYPE_F32>(k, grid, grid, st, ds, nseg, dp); break;
-    case FA_DTYPE_BF16: launch_median<FA_DTYPE_BF16>(k, grid, grid, st, ds, nseg, dp); break;
-    case FA_DTYPE_F16: launch_median<FA_DTYPE_F16>(k, grid, grid, st, ds, nseg, dp); break;
-    default: launch_median<FA_DTYPE_F64>(k, grid, grid, st, ds, nseg, dp); break;
+    case FA_DTYPE_F32: launch_median<FA_DTYPE_F32>(k, grid, st, ds, nseg, dp); break;
+    case FA_DTYPE_BF16: launch_median<FA_DTYPE_BF16>(k, grid, st, ds, nseg, dp); break;
+    case FA_DTYPE_F16: launch_median<FA_DTYPE_F16>(k, grid, st, ds, nseg, dp); break;
+    default: launch_median<FA_DTYPE_F64>(k, grid, st, ds, nseg, dp); break;
   }
   FA_HIP(hipGetLastError());
   return release(slot, st);
@@ -396,7 +331,7 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
       const int64_t ge = ev ? e0 + e : sg.numel - 1;
 #pragma unroll 8
       for (int c = t / kPE; c < kp; c += kBlock / kPE) {
-        const float v = ((const float*)in[min(c, k - 1)])[ge];
+        const float v = gld<float>(in[min(c, k - 1)], ge);
         lds[e * stride + c] = (ev && c < k) ? v : 0.0f;
       }
     }
