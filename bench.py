@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="metric",
-                   choices=["metric", "fragmented", "resnet18", "vit_bf16", "hier", "gossip", "host", "secagg", "median",
+                   choices=["metric", "fragmented", "resnet18", "vit_bf16", "hier", "gossip", "host", "secagg", "fedopt", "median",
                             "krum"])
     p.add_argument("--clients", type=int, default=None)
     p.add_argument("--params", type=int, default=None)
@@ -504,6 +504,88 @@ def wl_host(args, eng, rank, world, timer):
                 roofline_note="value includes pageable->pinned packing, H2D over PCIe and the D2H of the result")
 
 
+def wl_fedopt(args, eng, rank, world, timer):
+    """FedOpt server round (simulation/mpi/fedopt/FedOptAggregator.py:81-131, server_optimizer sgd,
+    momentum 0.9): FedAvg of K client updates + pseudo-gradient g = p - avg + torch.optim.SGD step of
+    the global model and its momentum buffer, fused in one pass (fa_fedavg_sgd).  Flat fp32 model,
+    client-major arena rows.  Bytes per step: K*P*4 read + param r/w + momentum r/w = (K + 4)*P*4."""
+    if world > 1:
+        raise SystemExit("--config fedopt is a single-GPU configuration")
+    K = args.clients or 128
+    P = args.params or 125_000_000
+    lr, mom = 1.0, 0.9
+    counts = client_counts(K)
+    w = [c / sum(counts) for c in counts]
+    tiled = args.layout == "tiled"
+    if tiled:
+        arena = make_tiled_arena(range(K), P)
+        buf, rows, xs = arena.bufs[torch.float32], list(range(K)), None
+    else:
+        xs = make_arena_rows(range(K), P)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    param = torch.randn(P, generator=g, device="cuda")
+    mbuf = torch.zeros(P, device="cuda")
+    state = {"first": True}
+
+    def run(p_, b_, first, n=None):
+        if tiled:
+            eng.fedavg_sgd_tiled(buf if n is None else buf[:n // buf.shape[2]], rows, w, p_, b_, lr, mom,
+                                 first_step=first)
+        else:
+            eng.fedavg_sgd([xs if n is None else [x[:n] for x in xs]], w, [p_], [b_], lr, mom, first_step=first)
+
+    def step():
+        with timer:
+            run(param, mbuf, state["first"])
+        state["first"] = False
+
+    def parity():
+        if args.check_samples <= 0:
+            return None
+        from oracle import orc
+        n = min(P, 1 << 20) // 1024 * 1024  # a fresh server state over the first n coordinates, two rounds
+        p_dev = torch.randn(n, generator=torch.Generator(device="cuda").manual_seed(6), device="cuda")
+        b_dev = torch.zeros(n, device="cuda")
+        p_cpu, b_cpu = p_dev.cpu(), b_dev.cpu()
+        idx = torch.arange(n, device="cuda")
+        cols = [tiled_gather(buf, r, idx).cpu() for r in rows] if tiled else [x[:n].cpu() for x in xs]
+        avg = orc.weighted_sum(cols, 0, w)
+        for first in (True, False):
+            run(p_dev, b_dev, first, n)
+            orc.sgd_apply(avg, p_cpu, b_cpu, lr, mom, first_step=first)
+        torch.cuda.synchronize()
+        ok = torch.equal(p_dev.cpu().view(torch.int32), p_cpu.view(torch.int32)) and \
+            torch.equal(b_dev.cpu().view(torch.int32), b_cpu.view(torch.int32))
+        return f"{'bit-exact' if ok else 'MISMATCH'} vs oracle (FedAvg + SGD momentum, 2 rounds) on {n} coordinates"
+
+    def cpu(budget_s):
+        import oracle.torch_port as tp
+        Kc, Pc = K, 2_000_000
+        gc = torch.Generator().manual_seed(0)
+        cl = [(counts[i], {"w": torch.randn(Pc, generator=gc)}) for i in range(Kc)]
+        model = torch.nn.Linear(1, 1, bias=False)
+        model.weight = torch.nn.Parameter(torch.randn(Pc, generator=gc))
+        opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=mom)
+        torch.set_num_threads(min(16, os.cpu_count() or 1))
+        best, runs, t_end = float("inf"), 0, time.perf_counter() + budget_s
+        while runs < 3 or (time.perf_counter() < t_end and runs < 50):
+            lst = [(n_, {"w": d["w"].clone()}) for n_, d in cl]  # agg() rebinds client 0's dict
+            t0 = time.perf_counter()
+            avg = tp.agg("FedAvg", lst)["w"]
+            opt.zero_grad()
+            model.weight.grad = model.weight.data - avg       # set_model_global_grads (:118-131)
+            opt.step()
+            best = min(best, time.perf_counter() - t0)
+            runs += 1
+        gbs = (Kc + 4) * Pc * 4 / best / 1e9
+        return {"value": round(gbs, 2), "unit": "GB/s", "cores": torch.get_num_threads(), "kind": "port",
+                "sample": f"K={Kc} x P={Pc} fp32 host-resident, best of {runs}: oracle/torch_port.agg('FedAvg') "
+                          f"+ pseudo-gradient + torch.optim.SGD(momentum={mom}) step"}
+
+    return dict(name=f"fedopt_sgd_K{K}_P{P}_fp32" + ("_tiled" if tiled else ""), dtype="fp32", step=step, parity=parity, cpu=cpu,
+                bytes_total=(K + 4) * P * 4, launch_bytes=(K + 4) * P * 4, clients=K, params=P, cpu_K=K)
+
+
 def wl_secagg(args, eng, rank, world, timer):
     """§8(f) #4: the LightSecAgg server reconstruction (lsa_fedml_aggregator.py:101-175) for N = K
     clients (U = N, T = N/2, the reference's setting) with ResNet-18-size models: LCC-decode the
@@ -743,7 +825,7 @@ def main():
         eng.set_variant(args.variant)
     timer = Timed()
     wl = {"metric": wl_metric, "fragmented": wl_fragmented, "resnet18": wl_layout, "vit_bf16": wl_layout, "hier": wl_hier,
-          "gossip": wl_gossip, "host": wl_host, "secagg": wl_secagg, "median": wl_median,
+          "gossip": wl_gossip, "host": wl_host, "secagg": wl_secagg, "fedopt": wl_fedopt, "median": wl_median,
           "krum": wl_krum}[args.config](args, eng, rank, world, timer)
 
     for _ in range(args.warmup):

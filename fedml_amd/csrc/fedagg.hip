@@ -474,7 +474,7 @@ template <int U, bool NT>
 __global__ void __launch_bounds__(kBlock)
 k_fedavg_sgd(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
              const void* const* __restrict__ ptrs, int k, void* const* __restrict__ bufs, float neg_lr,
-             float mom, float damp1, float wd, int flags) {
+             float mom, float damp1, float wd, int flags, int64_t sstr) {
   using B = WsumBody<FA_DTYPE_F32, FA_MODE_MUL_W, U, 1, NT>;
   using T = typename B::T;
   constexpr int V = T::V;
@@ -484,40 +484,45 @@ k_fedavg_sgd(const Seg* __restrict__ segs, int nseg, const double* __restrict__ 
   const Seg sg = segs[s];
   float* param = (float*)sg.out;
   float* mbuf = (float*)bufs[s];
-  const int64_t base = (tile - sg.tile_start) * TILE;
+  const int64_t tl = tile - sg.tile_start;
+  const int64_t base = tl * TILE;
   const void* const* in = ptrs + sg.ptr_base;
   const float d = 0.f;
+  const int64_t sst = sstr ? sstr : B::SLOT_BYTES;
+  const bool read_buf = (flags & SGD_MOMENTUM) && !(flags & SGD_FIRST);
 
   if (sg.aligned && base + TILE <= sg.numel) {
     const int64_t e0 = base + (int64_t)threadIdx.x * V;
-    const int64_t boff = e0 * 4;
+    const int64_t boff = tl * sst + (int64_t)threadIdx.x * V * 4;
+    // the parameter and momentum loads are issued first: their latency hides under the client stream
+    u32x4 p4 = ld16<true>(param + e0);
+    u32x4 b4 = {0, 0, 0, 0};
+    if (read_buf) b4 = ld16<true>(mbuf + e0);
     float acc[1][V];
 #pragma unroll
     for (int v = 0; v < V; ++v) acc[0][v] = -0.0f;
     for (int i0 = 0; i0 < k; i0 += U) {
       u32x4 r[U][1];
-      B::load(r, in, i0, k, boff);
+      B::load(r, in, i0, k, boff, sst);
       B::template consume<true>(acc, r, coef, i0, k, d);
     }
-    u32x4 p4 = *(const u32x4*)(param + e0);
-    u32x4 b4 = {0, 0, 0, 0};
-    if ((flags & SGD_MOMENTUM) && !(flags & SGD_FIRST)) b4 = *(const u32x4*)(mbuf + e0);
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       float b = __uint_as_float(b4[v]);
       p4[v] = __float_as_uint(sgd_update(__uint_as_float(p4[v]), acc[0][v], b, neg_lr, mom, damp1, wd, flags));
       b4[v] = __float_as_uint(b);
     }
-    *(u32x4*)(param + e0) = p4;
-    if (flags & SGD_MOMENTUM) *(u32x4*)(mbuf + e0) = b4;
+    __builtin_nontemporal_store(p4, (__attribute__((address_space(1))) u32x4*)(param + e0));
+    if (flags & SGD_MOMENTUM) __builtin_nontemporal_store(b4, (__attribute__((address_space(1))) u32x4*)(mbuf + e0));
   } else {
     const int64_t end = min(base + TILE, sg.numel);
     for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
+      const int64_t pe = B::phys(e, sst);
       float acc = -0.0f;
       for (int i = 0; i < k; ++i)
         acc = accum<FA_DTYPE_F32, FA_MODE_MUL_W>(
-            acc, term<FA_DTYPE_F32, FA_MODE_MUL_W>(T::ld1(in[i], e), T::coef(coef[i]), d));
-      float b = ((flags & SGD_MOMENTUM) && !(flags & SGD_FIRST)) ? mbuf[e] : 0.f;
+            acc, term<FA_DTYPE_F32, FA_MODE_MUL_W>(T::ld1(in[i], pe), T::coef(coef[i]), d));
+      float b = read_buf ? mbuf[e] : 0.f;
       param[e] = sgd_update(param[e], acc, b, neg_lr, mom, damp1, wd, flags);
       if (flags & SGD_MOMENTUM) mbuf[e] = b;
     }
@@ -1138,10 +1143,11 @@ int fa_weighted_sum_grouped_tiled(fa_ctx* ctx, int dtype, int mode, int64_t n, i
                       group_divisor, d_out, hip_stream, tile_stride);
 }
 
-int fa_fedavg_sgd(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, int32_t k,
-                  const void* const* d_in, const double* coef, void* const* d_param, void* const* d_momentum,
-                  double lr, double momentum, double dampening, double weight_decay, int nesterov,
-                  int first_step, void* hip_stream) {
+namespace {
+int fedavg_sgd_impl(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, int32_t k,
+                    const void* const* d_in, const double* coef, void* const* d_param, void* const* d_momentum,
+                    double lr, double momentum, double dampening, double weight_decay, int nesterov,
+                    int first_step, void* hip_stream, int64_t sstr) {
   if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
   if (k <= 0 || num_segments <= 0 || !seg_numel || !d_in || !coef || !d_param)
     return fail(FA_ERR_INVALID, "fa_fedavg_sgd: invalid arguments");
@@ -1190,6 +1196,7 @@ int fa_fedavg_sgd(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, i
       hp[(int64_t)j * k + i] = p;
       aligned = aligned && al16(p);
     }
+    if (sstr && !aligned) return fail(FA_ERR_INVALID, "tiled inputs, parameter and momentum must be 16-byte aligned");
     hs[j] = Seg{n, t0, d_param[s], j * k, aligned ? 1 : 0};
     hb[j] = momentum != 0.0 ? d_momentum[s] : d_param[s];  // never dereferenced without momentum
     t0 += (n + tile_elems - 1) / tile_elems;
@@ -1203,9 +1210,31 @@ int fa_fedavg_sgd(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, i
   hipLaunchKernelGGL((k_fedavg_sgd<8, true>), dim3((unsigned)tiles), dim3(kBlock), 0, st, (const Seg*)dv, nseg,
                      (const double*)(dv + seg_bytes), (const void* const*)(dv + seg_bytes + coef_bytes + buf_bytes), k,
                      (void* const*)(dv + seg_bytes + coef_bytes), (float)(-lr), (float)momentum,
-                     (float)(1.0 - dampening), (float)weight_decay, flags);
+                     (float)(1.0 - dampening), (float)weight_decay, flags, sstr);
   FA_HIP(hipGetLastError());
   return release(slot, st);
+}
+}  // namespace
+
+int fa_fedavg_sgd(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, int32_t k,
+                  const void* const* d_in, const double* coef, void* const* d_param, void* const* d_momentum,
+                  double lr, double momentum, double dampening, double weight_decay, int nesterov,
+                  int first_step, void* hip_stream) {
+  return fedavg_sgd_impl(ctx, num_segments, seg_numel, k, d_in, coef, d_param, d_momentum, lr, momentum,
+                         dampening, weight_decay, nesterov, first_step, hip_stream, 0);
+}
+
+int fa_fedavg_sgd_tiled(fa_ctx* ctx, int64_t n, int32_t k, const void* const* d_in, int64_t tile_stride,
+                        const double* coef, void* d_param, void* d_momentum, double lr, double momentum,
+                        double dampening, double weight_decay, int nesterov, int first_step, void* hip_stream) {
+  if (n < 0) return fail(FA_ERR_INVALID, "n must be >= 0");
+  if (tile_stride <= 0 || tile_stride % FA_TILE_BYTES)
+    return fail(FA_ERR_INVALID, "tile_stride must be a positive multiple of %d (got %lld)", FA_TILE_BYTES,
+                (long long)tile_stride);
+  void* params[1] = {d_param};
+  void* moms[1] = {d_momentum};
+  return fedavg_sgd_impl(ctx, 1, &n, k, d_in, coef, params, d_momentum ? moms : nullptr, lr, momentum, dampening,
+                         weight_decay, nesterov, first_step, hip_stream, tile_stride);
 }
 
 int fa_mix(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_ptr,

@@ -317,6 +317,28 @@ class AggEngine:
             float(weight_decay), int(bool(nesterov)), int(bool(first_step)), self._stream(stream))
         N.check(rc, "fa_fedavg_sgd")
 
+    def fedavg_sgd_tiled(self, buf: torch.Tensor, rows: Sequence[int], coef: Sequence[float], param: torch.Tensor,
+                         momentum_buf: Optional[torch.Tensor], lr: float, momentum: float = 0.0,
+                         dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,
+                         first_step: bool = True, stream=None) -> None:
+        """fedavg_sgd of ONE flat fp32 parameter over rows of a tile-interleaved arena group
+        (fa_fedavg_sgd_tiled); ``param`` / ``momentum_buf`` updated in place."""
+        if buf.dtype != torch.float32 or param.dtype != torch.float32:
+            raise TypeError("fedavg_sgd_tiled: float32 only")
+        n, ptrs, stride = self._tiled_args(buf, rows, 0, param.numel(), "fedavg_sgd_tiled")
+        if len(coef) != len(rows):
+            raise ValueError("fedavg_sgd_tiled: one coefficient per row")
+        _require_device(param, self.device, "parameter")
+        if momentum != 0.0:
+            if momentum_buf is None or momentum_buf.dtype != torch.float32 or momentum_buf.numel() != n:
+                raise ValueError("fedavg_sgd_tiled: momentum needs a float32 buffer like the parameter")
+            _require_device(momentum_buf, self.device, "momentum buffer")
+        rc = self._lib.fa_fedavg_sgd_tiled(
+            self._ctx, n, len(rows), ptrs, stride, N.f64_array(coef), param.data_ptr(),
+            momentum_buf.data_ptr() if momentum != 0.0 else None, float(lr), float(momentum), float(dampening),
+            float(weight_decay), int(bool(nesterov)), int(bool(first_step)), self._stream(stream))
+        N.check(rc, "fa_fedavg_sgd_tiled")
+
     def weighted_sum_table(self, dtype_code: int, mode: int, seg_numel: torch.Tensor, k: int,
                            in_ptrs: torch.Tensor, out_ptrs: torch.Tensor, coef: Optional[Sequence[float]] = None,
                            divisor: float = 1.0, stream=None) -> None:

@@ -168,6 +168,12 @@ int fa_fedavg_sgd(fa_ctx *ctx, int32_t num_segments, const int64_t *seg_numel, i
                   const void *const *d_in, const double *coef, void *const *d_param,
                   void *const *d_momentum, double lr, double momentum, double dampening,
                   double weight_decay, int nesterov, int first_step, void *hip_stream);
+/* fa_fedavg_sgd for ONE flat parameter over tile-interleaved inputs (addressing as
+ * fa_weighted_sum_tiled); d_param / d_momentum are flat, 16-byte aligned. */
+int fa_fedavg_sgd_tiled(fa_ctx *ctx, int64_t n, int32_t k, const void *const *d_in,
+                        int64_t tile_stride, const double *coef, void *d_param, void *d_momentum,
+                        double lr, double momentum, double dampening, double weight_decay,
+                        int nesterov, int first_step, void *hip_stream);
 
 /*
  * Mixing / gossip: for every row r < rows, with CSR entries j in [row_ptr[r], row_ptr[r+1]):

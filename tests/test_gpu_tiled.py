@@ -226,3 +226,24 @@ def test_tiled_arena_hierarchical(eng):
         b = tiled.hierarchical([[0, 1], [2, 3, 4], [5, 6]], counts, formula)
         for k in a:
             assert bits_equal(a[k].cpu(), b[k].cpu()), (formula, k)
+
+
+@pytest.mark.parametrize("momentum,nesterov,wd", [(0.0, False, 0.0), (0.9, False, 0.0), (0.9, True, 1e-4)])
+def test_fedavg_sgd_tiled_matches_flat(eng, momentum, nesterov, wd):
+    K, n = 9, 1024 * 21 + 13
+    xs = _inputs(torch.float32, K, n, 17)
+    w = [(i + 1) / 45 for i in range(K)]
+    g = torch.Generator().manual_seed(2)
+    p0 = torch.randn(n, generator=g)
+    pa, pb = p0.cuda(), p0.cuda()
+    ba, bb = torch.zeros(n, device="cuda:0"), torch.zeros(n, device="cuda:0")
+    buf = tiled_buf(xs, capacity=K + 2, rows=[K + 1 - j for j in range(K)])
+    rows = [K + 1 - j for j in range(K)]
+    for first in (True, False, False):
+        eng.fedavg_sgd([[x.cuda() for x in xs]], w, [pa], [ba] if momentum else None, 0.5, momentum,
+                       weight_decay=wd, nesterov=nesterov, first_step=first)
+        eng.fedavg_sgd_tiled(buf, rows, w, pb, bb if momentum else None, 0.5, momentum, weight_decay=wd,
+                             nesterov=nesterov, first_step=first)
+    assert bits_equal(pa.cpu(), pb.cpu())
+    if momentum:
+        assert bits_equal(ba.cpu(), bb.cpu())
