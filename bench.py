@@ -601,9 +601,16 @@ def wl_secagg(args, eng, rank, world, timer):
     U, T = K, K // 2
     m = -(-P // (U - T))
     g = torch.Generator(device="cuda").manual_seed(11)
-    Ppad = -(-P // 64) * 64  # rows 512-byte aligned, as ClientArena lays them out (fedml_amd/arena.py)
-    arena = torch.randint(0, p, (K, Ppad), generator=g, dtype=torch.int64, device="cuda")
-    xs = [arena[i, :P] for i in range(K)]
+    tiled = args.layout == "tiled"
+    if tiled:  # tile-interleaved arena [tiles, K, 512] (fedml_amd/arena.py, fa_finite_sum_tiled)
+        nt = -(-P // 512)
+        tbuf = torch.randint(0, p, (nt, K, 512), generator=g, dtype=torch.int64, device="cuda")
+        rows = list(range(K))
+        xs = None
+    else:
+        Ppad = -(-P // 64) * 64  # rows 512-byte aligned, as ClientArena lays them out (fedml_amd/arena.py)
+        arena = torch.randint(0, p, (K, Ppad), generator=g, dtype=torch.int64, device="cuda")
+        xs = [arena[i, :P] for i in range(K)]
     F = torch.randint(0, p, (U, m), generator=g, dtype=torch.int64, device="cuda")
     coef = gen_Lagrange_coeffs(np.arange(U) + K + 1, np.arange(K) + 1, p).tolist()
     state = {}
@@ -611,8 +618,13 @@ def wl_secagg(args, eng, rank, world, timer):
     def step():
         mask = eng.lcc_decode(coef, F, p, P)
         with timer:
-            _, real = eng.finite_sum([xs], p, MOD_END, masks=[mask], finite=False, q_bits=q, scale=1 / K)
-        state["mask"], state["real"] = mask, real[0]
+            if tiled:
+                _, real = eng.finite_sum_tiled(tbuf, rows, p, MOD_END, mask=mask, finite=False, q_bits=q,
+                                               scale=1 / K, n=P)
+            else:
+                _, real = eng.finite_sum([xs], p, MOD_END, masks=[mask], finite=False, q_bits=q, scale=1 / K)
+                real = real[0]
+        state["mask"], state["real"] = mask, real
 
     def parity():
         if args.check_samples <= 0:
@@ -620,7 +632,9 @@ def wl_secagg(args, eng, rank, world, timer):
         from oracle import orc
         gi = torch.Generator(device="cuda").manual_seed(99)
         idx = torch.randint(0, P, (args.check_samples,), generator=gi, device="cuda")
-        _, exp = orc.finite_sum([x.index_select(0, idx).cpu() for x in xs], p, MOD_END,
+        cols_in = ([tiled_gather(tbuf, r, idx).cpu() for r in rows] if tiled else
+                   [x.index_select(0, idx).cpu() for x in xs])
+        _, exp = orc.finite_sum(cols_in, p, MOD_END,
                                 mask=state["mask"].index_select(0, idx).cpu(), q_bits=q, scale=1 / K)
         ok = torch.equal(state["real"].index_select(0, idx).cpu().view(torch.int32), exp.view(torch.int32))
         # the decoded mask: every column of a row block is independent -> check a sampled slice
@@ -650,7 +664,7 @@ def wl_secagg(args, eng, rank, world, timer):
                                           "lsa_fedml_aggregator.py:140-166); mask decoding not included"}
 
     recon = K * P * 8 + P * 8 + P * 4
-    return dict(name=f"lightsecagg_reconstruct_N{K}_P{P}_int64", dtype="int64", step=step, parity=parity,
+    return dict(name=f"lightsecagg_reconstruct_N{K}_P{P}_int64" + ("_tiled" if tiled else ""), dtype="int64", step=step, parity=parity,
                 data="synthetic masked finite models uniform in Z_p (p = 2^15-19, q = 10 bits), resident in HBM",
                 bytes_total=recon + U * m * 8 + P * 8, launch_bytes=recon, clients=K, params=P, cpu_K=K, cpu=cpu,
                 roofline_note="dominant kernel = fa_finite_sum (K masked models + mask in, fp32 out); value also "

@@ -32,7 +32,7 @@ EXPORTED_SYMBOLS = (
     "fa_fedavg_sgd", "fa_fedavg_sgd_tiled", "fa_mix", "fa_ctx_set_variant",
     "fa_ctx_set_mix_band", "fa_stream_create_cu_masked", "fa_stream_destroy", "fa_strerror", "fa_last_error",
     # include/fedagg_finite.h
-    "fa_finite_sum", "fa_finite_quantize", "fa_lcc_decode",
+    "fa_finite_sum", "fa_finite_sum_tiled", "fa_finite_quantize", "fa_lcc_decode",
     # include/fedagg_robust.h
     "fa_coord_median", "fa_pairwise_sqdist", "fa_pairwise_sqdist_scratch_bytes",
 )
@@ -100,6 +100,9 @@ def _declare(L):
     L.fa_finite_sum.restype = ctypes.c_int
     L.fa_finite_sum.argtypes = [_vp, ctypes.c_int32, _P_i64, ctypes.c_int32, _P_vp, _P_vp, ctypes.c_int64,
                                 ctypes.c_int, _P_vp, ctypes.c_int32, ctypes.c_double, _P_vp, _vp]
+    L.fa_finite_sum_tiled.restype = ctypes.c_int
+    L.fa_finite_sum_tiled.argtypes = [_vp, ctypes.c_int64, ctypes.c_int32, _P_vp, ctypes.c_int64, _vp, ctypes.c_int64,
+                                      ctypes.c_int, _vp, ctypes.c_int32, ctypes.c_double, _vp, _vp]
     L.fa_finite_quantize.restype = ctypes.c_int
     L.fa_finite_quantize.argtypes = [_vp, ctypes.c_int, ctypes.c_int32, _P_i64, _P_vp, _P_vp, ctypes.c_int64,
                                      ctypes.c_int32, _P_vp, _vp]

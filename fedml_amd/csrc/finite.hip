@@ -145,16 +145,19 @@ __device__ __forceinline__ void finish(long long& acc, bool has_mask, long long 
 template <bool EACH>
 __global__ void __launch_bounds__(kBlock)
 k_finite_sum(const FSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int flags,
-             ModP m, Dequant dq) {
+             ModP m, Dequant dq, int64_t sstr) {
   const int64_t tile = blockIdx.x;
   const FSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
-  const int64_t base = (tile - sg.tile_start) * kTile;
+  const int64_t tl = tile - sg.tile_start;
+  const int64_t base = tl * kTile;
+  // input tile stride: kTile * 8 bytes (flat) or the arena's tile stride (tile-interleaved inputs)
+  const int64_t sst = sstr ? sstr : kTile * 8;
   const void* const* in = ptrs + sg.ptr_base;
   const bool first = flags & FA_FINITE_MOD_FIRST;
 
   if (sg.aligned && base + kTile <= sg.numel) {
     const int64_t e0 = base + (int64_t)threadIdx.x * kV;
-    const int64_t boff = e0 * 8;
+    const int64_t boff = tl * sst + (int64_t)threadIdx.x * kV * 8;
     long long a0 = 0, a1 = 0;
     // the mask is needed only at the end: issue its load first, it lands while the clients stream
     const u32x4 mk = sg.mask ? __builtin_nontemporal_load((gp_u32x4)(sg.mask + e0)) : u32x4{0, 0, 0, 0};
@@ -194,9 +197,10 @@ k_finite_sum(const FSeg* __restrict__ segs, int nseg, const void* const* __restr
   } else {
     const int64_t end = min(base + kTile, sg.numel);
     for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
-      long long acc = ((const long long*)in[0])[e];
+      const int64_t pe = (e / kTile) * (sst / 8) + e % kTile;
+      long long acc = ((const long long*)in[0])[pe];
       if (first) acc = mod_any(acc, m);
-      for (int i = 1; i < k; ++i) acc = step<EACH>(acc, ((const long long*)in[i])[e], m);
+      for (int i = 1; i < k; ++i) acc = step<EACH>(acc, ((const long long*)in[i])[pe], m);
       finish(acc, sg.mask != nullptr, sg.mask ? sg.mask[e] : 0, flags, m);
       if (sg.out_fin) sg.out_fin[e] = acc;
       if (sg.out_real) {
@@ -401,10 +405,11 @@ ModP make_modp(int64_t p) {
 // ============================================================================================ ABI
 extern "C" {
 
-int fa_finite_sum(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, int32_t k,
-                  const void* const* d_in, const void* const* d_mask, int64_t prime, int flags,
-                  void* const* d_out_finite, int32_t q_bits, double scale, void* const* d_out_real,
-                  void* hip_stream) {
+namespace {
+int finite_sum_impl(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, int32_t k,
+                    const void* const* d_in, const void* const* d_mask, int64_t prime, int flags,
+                    void* const* d_out_finite, int32_t q_bits, double scale, void* const* d_out_real,
+                    void* hip_stream, int64_t sstr) {
   if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
   if (k <= 0 || num_segments <= 0 || !seg_numel || !d_in)
     return fail(FA_ERR_INVALID, "fa_finite_sum: invalid arguments");
@@ -458,6 +463,7 @@ int fa_finite_sum(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, i
       aligned = aligned && al16(p);
     }
     sg.aligned = (aligned && (!sg.mask || al16(sg.mask))) ? 1 : 0;
+    if (sstr && !sg.aligned) return fail(FA_ERR_INVALID, "tiled inputs, mask and outputs must be aligned");
     hs[j] = sg;
     t0 += (n + kTile - 1) / kTile;
     ++j;
@@ -474,12 +480,36 @@ int fa_finite_sum(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, i
   const dim3 grid((unsigned)tiles), blk(kBlock);
   if (flags & FA_FINITE_MOD_EACH)
     hipLaunchKernelGGL((k_finite_sum<true>), grid, blk, 0, st, (const FSeg*)dv, nseg,
-                       (const void* const*)(dv + seg_bytes), k, flags, mp, dq);
+                       (const void* const*)(dv + seg_bytes), k, flags, mp, dq, sstr);
   else
     hipLaunchKernelGGL((k_finite_sum<false>), grid, blk, 0, st, (const FSeg*)dv, nseg,
-                       (const void* const*)(dv + seg_bytes), k, flags, mp, dq);
+                       (const void* const*)(dv + seg_bytes), k, flags, mp, dq, sstr);
   FA_HIP(hipGetLastError());
   return release(slot, st);
+}
+}  // namespace
+
+int fa_finite_sum(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, int32_t k,
+                  const void* const* d_in, const void* const* d_mask, int64_t prime, int flags,
+                  void* const* d_out_finite, int32_t q_bits, double scale, void* const* d_out_real,
+                  void* hip_stream) {
+  return finite_sum_impl(ctx, num_segments, seg_numel, k, d_in, d_mask, prime, flags, d_out_finite, q_bits, scale,
+                         d_out_real, hip_stream, 0);
+}
+
+int fa_finite_sum_tiled(fa_ctx* ctx, int64_t n, int32_t k, const void* const* d_in, int64_t tile_stride,
+                        const void* d_mask, int64_t prime, int flags, void* d_out_finite, int32_t q_bits,
+                        double scale, void* d_out_real, void* hip_stream) {
+  if (n < 0) return fail(FA_ERR_INVALID, "n must be >= 0");
+  if (tile_stride <= 0 || tile_stride % FA_TILE_BYTES)
+    return fail(FA_ERR_INVALID, "tile_stride must be a positive multiple of %d (got %lld)", FA_TILE_BYTES,
+                (long long)tile_stride);
+  const void* masks[1] = {d_mask};
+  void* fin[1] = {d_out_finite};
+  void* real[1] = {d_out_real};
+  return finite_sum_impl(ctx, 1, &n, k, d_in, d_mask ? masks : nullptr, prime, flags,
+                         d_out_finite ? fin : nullptr, q_bits, scale, d_out_real ? real : nullptr, hip_stream,
+                         tile_stride);
 }
 
 int fa_finite_quantize(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t* seg_numel,

@@ -437,6 +437,31 @@ class AggEngine:
         N.check(rc, "fa_finite_sum")
         return (fin if finite else None), (real if q_bits is not None else None)
 
+    def finite_sum_tiled(self, buf: torch.Tensor, rows: Sequence[int], prime: int, flags: int,
+                         mask: Optional[torch.Tensor] = None, finite: bool = True, q_bits: Optional[int] = None,
+                         scale: float = 1.0, n: Optional[int] = None, stream=None):
+        """finite_sum over rows of a tile-interleaved int64 arena group (fa_finite_sum_tiled);
+        returns (finite int64 output or None, dequantized output or None), flat."""
+        if buf.dtype != torch.int64:
+            raise TypeError("finite_sum_tiled: int64 arena only")
+        if not finite and q_bits is None:
+            raise ValueError("finite_sum_tiled: nothing to output")
+        n, ptrs, stride = self._tiled_args(buf, rows, 0, n, "finite_sum_tiled")
+        if mask is not None:
+            if mask.dtype != torch.int64 or mask.numel() != n:
+                raise ValueError(f"finite_sum_tiled: mask must be int64 with {n} elements")
+            _require_device(mask, self.device, "mask")
+        fin = torch.empty(n, dtype=torch.int64, device=self.device) if finite else None
+        real = None
+        if q_bits is not None:
+            real = torch.empty(n, dtype=torch.float64 if flags & N.REAL_F64 else torch.float32, device=self.device)
+        rc = self._lib.fa_finite_sum_tiled(
+            self._ctx, n, len(rows), ptrs, stride, mask.data_ptr() if mask is not None else None, int(prime),
+            int(flags), fin.data_ptr() if fin is not None else None, int(q_bits or 0), float(scale),
+            real.data_ptr() if real is not None else None, self._stream(stream))
+        N.check(rc, "fa_finite_sum_tiled")
+        return fin, real
+
     def finite_quantize(self, xs: Sequence[torch.Tensor], prime: int, q_bits: int,
                         masks: Optional[Sequence[torch.Tensor]] = None, stream=None) -> List[torch.Tensor]:
         """my_q (+ model_masking with masks) of same-dtype device tensors (fa_finite_quantize)."""

@@ -65,6 +65,14 @@ int fa_finite_sum(fa_ctx *ctx, int32_t num_segments, const int64_t *seg_numel, i
                   void *const *d_out_finite, int32_t q_bits, double scale, void *const *d_out_real,
                   void *hip_stream);
 
+/* fa_finite_sum for ONE flat segment over tile-interleaved client inputs (addressing as
+ * fa_weighted_sum_tiled, include/fedagg.h: element e of client i at d_in[i] + (e / 512) *
+ * tile_stride + (e % 512) * 8); mask and outputs flat.  All 16-byte aligned. */
+int fa_finite_sum_tiled(fa_ctx *ctx, int64_t n, int32_t k, const void *const *d_in,
+                        int64_t tile_stride, const void *d_mask, int64_t prime, int flags,
+                        void *d_out_finite, int32_t q_bits, double scale, void *d_out_real,
+                        void *hip_stream);
+
 /*
  * my_q of every element of segment s (dtype FA_DTYPE_F32, FA_DTYPE_F64 or FA_DTYPE_I64), written
  * as int64 to d_out[s]; with d_mask && d_mask[s], model_masking's out = mod(out + mask_s[e]).

@@ -319,3 +319,30 @@ def test_lcc_decode_redo_and_int64_paths(eng, variant):
     finally:
         eng.set_variant(0)
     assert torch.equal(got, orc.lcc_decode(torch.from_numpy(coef), F, p, n_out))
+
+
+@pytest.mark.parametrize("flags", [4, 1 | 2 | 4, 2])
+@pytest.mark.parametrize("real", [None, "f32", "f64"])
+def test_finite_sum_tiled_matches_flat(flags, real):
+    """fa_finite_sum_tiled == fa_finite_sum on the same clients (tile-interleaved arena input)."""
+    from fedml_amd.engine import get_engine
+    eng = get_engine(0)
+    K, n, p, q = 7, 512 * 9 + 100, 2 ** 31 - 1, 12
+    g = torch.Generator().manual_seed(flags)
+    xs = [torch.randint(-2 ** 40, 2 ** 40, (n,), generator=g, dtype=torch.int64) for _ in range(K)]
+    mask = torch.randint(0, p, (n,), generator=g, dtype=torch.int64).cuda()
+    nt = -(-n // 512)
+    buf = torch.zeros(nt, K + 1, 512, dtype=torch.int64)
+    rows = [K - j for j in range(K)]
+    for j, x in enumerate(xs):
+        f = torch.zeros(nt * 512, dtype=torch.int64)
+        f[:n] = x
+        buf[:, rows[j], :] = f.view(nt, 512)
+    buf = buf.cuda()
+    fl = flags | (8 if real == "f64" else 0)
+    qb = q if real else None
+    fin_a, real_a = eng.finite_sum([[x.cuda() for x in xs]], p, fl, masks=[mask], q_bits=qb, scale=0.25)
+    fin_b, real_b = eng.finite_sum_tiled(buf, rows, p, fl, mask=mask, q_bits=qb, scale=0.25, n=n)
+    assert torch.equal(fin_a[0].cpu(), fin_b.cpu())
+    if real:
+        assert torch.equal(real_a[0].cpu().view(torch.int8), real_b.cpu().view(torch.int8))
