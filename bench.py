@@ -60,11 +60,15 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     p.add_argument("--check-samples", type=int, default=65536)
     p.add_argument("--pinned", action="store_true", help="host config: client updates already in pinned memory")
-    p.add_argument("--layout", default="tiled", choices=["arena", "tiled", "tensors"],
+    p.add_argument("--layout", default=None, choices=["arena", "tiled", "tensors"],
                    help="arena: client updates as rows of one ClientArena allocation (fedml_amd/arena.py); "
                         "tiled: tile-interleaved ClientArena (4-KiB tiles of all clients contiguous); "
-                        "tensors: one allocation per client tensor")
-    return p.parse_args()
+                        "tensors: one allocation per client tensor.  Default: tiled, except gossip (arena: its "
+                        "row-sequential sliding window measured 5.12 ms client-major vs 5.52 ms tiled)")
+    a = p.parse_args()
+    if a.layout is None:
+        a.layout = "arena" if a.config == "gossip" else "tiled"
+    return a
 
 
 # ----------------------------------------------------------------------------- distributed setup
@@ -459,16 +463,47 @@ def wl_gossip(args, eng, rank, world, timer):
             dg.step(xs)
         rows = len(dg.mine)
     else:
-        xs = (make_arena_rows if args.layout in ("arena", "tiled") else make_flat_clients)(range(n), P)
         rp, cs, vs = gossip_rows(W)
-        outs = [torch.empty(P, device="cuda") for _ in range(n)]
+        tiled = args.layout == "tiled"
+        if tiled:  # both the models and the mixed models in tile-interleaved arenas (fa_mix_tiled)
+            arena = make_tiled_arena(range(n), P)
+            buf, nodes = arena.bufs[torch.float32], list(range(n))
+            obuf = torch.empty_like(buf)
 
-        def step():
-            with timer:
-                eng.mix(xs, rp, cs, vs, outs=outs)
+            def step():
+                with timer:
+                    eng.mix_tiled(buf, nodes, rp, cs, vs, obuf, nodes, n=P)
+        else:
+            xs = (make_arena_rows if args.layout == "arena" else make_flat_clients)(range(n), P)
+            outs = [torch.empty(P, device="cuda") for _ in range(n)]
+
+            def step():
+                with timer:
+                    eng.mix(xs, rp, cs, vs, outs=outs)
         rows = n
+
+        def parity():
+            if args.check_samples <= 0:
+                return None
+            from oracle import orc
+            gi = torch.Generator(device="cuda").manual_seed(97)
+            idx = torch.randint(0, P, (min(args.check_samples, 16384),), generator=gi, device="cuda")
+            if tiled:
+                sin = [tiled_gather(buf, r, idx).cpu() for r in nodes]
+                sout = [tiled_gather(obuf, r, idx).cpu() for r in nodes]
+            else:
+                sin = [x.index_select(0, idx).cpu() for x in xs]
+                sout = [o.index_select(0, idx).cpu() for o in outs]
+            exp, _ = orc.mix(sin, rp, cs, vs)
+            bad = sum(int((a.view(torch.int32) != b.view(torch.int32)).sum()) for a, b in zip(sout, exp))
+            return f"{'bit-exact' if bad == 0 else f'{bad} MISMATCHES'} vs oracle (DSGD rows) on {idx.numel()} sampled elements x {n} nodes"
     # survey §8(d): B = sum_i (deg_i + 1) * P * s + n * P * s  (ring: 4 n P s); compulsory = 2 n P s
-    return dict(name=f"gossip_ring_n{n}_P{P}_fp32", dtype="fp32", step=step, parity=lambda: None,
+    if world > 1:
+        def parity():
+            return None
+        tiled = False
+    return dict(name=f"gossip_ring_n{n}_P{P}_fp32" + ("_tiled" if tiled else ""), dtype="fp32", step=step,
+                parity=parity,
                 bytes_total=4 * n * P * 4, launch_bytes=2 * rows * P * 4, clients=n, params=P, cpu_K=None,
                 roofline_note="achieved uses compulsory bytes 2*rows*P*4 (each model read once, written once)")
 

@@ -539,16 +539,19 @@ k_fedavg_sgd(const Seg* __restrict__ segs, int nseg, const double* __restrict__ 
 template <int DT, int RG, int MAXD, bool POST>
 __global__ void __launch_bounds__(kBlock)
 k_mix(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict__ cols,
-      const double* __restrict__ vals, const void* const* __restrict__ in, int64_t n, int aligned) {
+      const double* __restrict__ vals, const void* const* __restrict__ in, int64_t n, int aligned,
+      int64_t isst, int64_t osst) {
   using T = Tr<DT, FA_MODE_MUL_W>;
   constexpr int V = T::V;
   constexpr int64_t TILE = (int64_t)kBlock * V;
   const int64_t base = (int64_t)blockIdx.x * TILE;
   const float dz = 0.f;
+  // 4-KiB slot strides of the inputs / outputs: TILE * bytes (flat) or an arena's tile stride
+  const int64_t ist = isst ? isst : TILE * T::IN_BYTES, ost = osst ? osst : TILE * T::OUT_BYTES;
 
   if (aligned && base + TILE <= n) {
-    const int64_t e0 = base + (int64_t)threadIdx.x * V;
-    const int64_t boff = e0 * T::IN_BYTES;
+    const int64_t boff = (int64_t)blockIdx.x * ist + (int64_t)threadIdx.x * V * T::IN_BYTES;
+    const int64_t ooff = (int64_t)blockIdx.x * ost + (int64_t)threadIdx.x * V * T::OUT_BYTES;
     for (int r0 = 0; r0 < nrows; r0 += RG) {
       int beg[RG], end[RG];
       int maxd = 0;
@@ -591,13 +594,13 @@ k_mix(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict__ co
       for (int g = 0; g < RG; ++g) {
         if (r0 + g < nrows) {
           const MixRow& row = rows[r0 + g];
-          T::stv((char*)row.out + e0 * T::OUT_BYTES, acc[g]);
+          T::stv((char*)row.out + ooff, acc[g]);
           if constexpr (POST) {
             const float s = (float)row.scale;
             float z[V];
 #pragma unroll
             for (int v = 0; v < V; ++v) z[v] = T::rnd(op_mul(acc[g][v], s));
-            T::stv((char*)row.out2 + e0 * T::OUT_BYTES, z);
+            T::stv((char*)row.out2 + ooff, z);
           }
         }
       }
@@ -607,12 +610,14 @@ k_mix(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict__ co
     for (int r = 0; r < nrows; ++r) {
       const MixRow row = rows[r];
       for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
+        const int64_t pi = (e / TILE) * (ist / T::IN_BYTES) + e % TILE;
+        const int64_t po = (e / TILE) * (ost / T::OUT_BYTES) + e % TILE;
         float acc = -0.0f;
         for (int j = row.begin; j < row.end; ++j)
           acc = accum<DT, FA_MODE_MUL_W>(
-              acc, term<DT, FA_MODE_MUL_W>(T::ld1(in[cols[j]], e), (float)vals[j], dz));
-        T::st1(row.out, e, acc);
-        if constexpr (POST) T::st1(row.out2, e, T::rnd(op_mul(acc, (float)row.scale)));
+              acc, term<DT, FA_MODE_MUL_W>(T::ld1(in[cols[j]], pi), (float)vals[j], dz));
+        T::st1(row.out, po, acc);
+        if constexpr (POST) T::st1(row.out2, po, T::rnd(op_mul(acc, (float)row.scale)));
       }
     }
   }
@@ -629,17 +634,18 @@ template <int DT, int RG, bool POST>
 __global__ void __launch_bounds__(kBlock)
 k_mix_band(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict__ cols,
            const double* __restrict__ vals, const void* const* __restrict__ in, int num_in, int off,
-           int64_t n) {
+           int64_t n, int64_t isst, int64_t osst) {
   using T = Tr<DT, FA_MODE_MUL_W>;
   constexpr int V = T::V;
   constexpr int64_t TILE = (int64_t)kBlock * V;
   const int64_t base = (int64_t)blockIdx.x * TILE;
   const float dz = 0.f;
+  const int64_t ist = isst ? isst : TILE * T::IN_BYTES, ost = osst ? osst : TILE * T::OUT_BYTES;
   auto wrap = [num_in](int c) { c %= num_in; return c < 0 ? c + num_in : c; };
 
   if (base + TILE <= n) {
-    const int64_t e0 = base + (int64_t)threadIdx.x * V;
-    const int64_t boff = e0 * T::IN_BYTES;
+    const int64_t boff = (int64_t)blockIdx.x * ist + (int64_t)threadIdx.x * V * T::IN_BYTES;
+    const int64_t ooff = (int64_t)blockIdx.x * ost + (int64_t)threadIdx.x * V * T::OUT_BYTES;
     u32x4 win[RG + 2];  // win[s] = input (r0 + off - 1 + s) mod num_in
     win[0] = ld16<false>((const char*)in[wrap(off - 1)] + boff);
     win[1] = ld16<false>((const char*)in[wrap(off)] + boff);
@@ -664,12 +670,12 @@ k_mix_band(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict
             for (int v = 0; v < V; ++v)
               acc[v] = accum<DT, FA_MODE_MUL_W>(acc[v], term<DT, FA_MODE_MUL_W>(x[v], c, dz));
           }
-          T::stv((char*)row.out + e0 * T::OUT_BYTES, acc);
+          T::stv((char*)row.out + ooff, acc);
           if constexpr (POST) {
             const float sc = (float)row.scale;
 #pragma unroll
             for (int v = 0; v < V; ++v) acc[v] = T::rnd(op_mul(acc[v], sc));
-            T::stv((char*)row.out2 + e0 * T::OUT_BYTES, acc);
+            T::stv((char*)row.out2 + ooff, acc);
           }
         }
       }
@@ -681,12 +687,14 @@ k_mix_band(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict
     for (int r = 0; r < nrows; ++r) {
       const MixRow row = rows[r];
       for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
+        const int64_t pi = (e / TILE) * (ist / T::IN_BYTES) + e % TILE;
+        const int64_t po = (e / TILE) * (ost / T::OUT_BYTES) + e % TILE;
         float acc = -0.0f;
         for (int j = row.begin; j < row.end; ++j)
           acc = accum<DT, FA_MODE_MUL_W>(
-              acc, term<DT, FA_MODE_MUL_W>(T::ld1(in[cols[j]], e), (float)vals[j], dz));
-        T::st1(row.out, e, acc);
-        if constexpr (POST) T::st1(row.out2, e, T::rnd(op_mul(acc, (float)row.scale)));
+              acc, term<DT, FA_MODE_MUL_W>(T::ld1(in[cols[j]], pi), (float)vals[j], dz));
+        T::st1(row.out, po, acc);
+        if constexpr (POST) T::st1(row.out2, po, T::rnd(op_mul(acc, (float)row.scale)));
       }
     }
   }
@@ -1237,9 +1245,11 @@ int fa_fedavg_sgd_tiled(fa_ctx* ctx, int64_t n, int32_t k, const void* const* d_
                          weight_decay, nesterov, first_step, hip_stream, tile_stride);
 }
 
-int fa_mix(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_ptr,
-           const int32_t* cols, const double* vals, int32_t num_in, const void* const* d_in,
-           void* const* d_out, const double* post_scale, void* const* d_out2, void* hip_stream) {
+namespace {
+int mix_impl(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_ptr,
+             const int32_t* cols, const double* vals, int32_t num_in, const void* const* d_in,
+             void* const* d_out, const double* post_scale, void* const* d_out2, void* hip_stream,
+             int64_t isst, int64_t osst) {
   if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
   if (rows <= 0 || n < 0 || !row_ptr || !cols || !vals || !d_in || !d_out || num_in <= 0)
     return fail(FA_ERR_INVALID, "fa_mix: invalid arguments");
@@ -1261,6 +1271,7 @@ int fa_mix(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_p
     aligned = aligned && al16(d_in[i]);
   }
   if (n == 0) return FA_OK;
+  if ((isst || osst) && !aligned) return fail(FA_ERR_INVALID, "fa_mix_tiled: inputs and outputs must be 16-byte aligned");
   const int V = elems_per_vec(dtype);
   const int64_t tiles = (n + (int64_t)kBlock * V - 1) / ((int64_t)kBlock * V);
   if (tiles > 0x7FFFFFFFll) return fail(FA_ERR_INVALID, "too many tiles");
@@ -1300,9 +1311,11 @@ int fa_mix(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_p
   if (band != INT32_MIN) {
 #define FA_BAND(DT)                                                                                   \
   if (post_scale)                                                                                     \
-    hipLaunchKernelGGL((k_mix_band<DT, 8, true>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, num_in, band, n); \
+    hipLaunchKernelGGL((k_mix_band<DT, 8, true>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, num_in, band, n, \
+                       isst, osst);                                                                   \
   else                                                                                                \
-    hipLaunchKernelGGL((k_mix_band<DT, 8, false>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, num_in, band, n);
+    hipLaunchKernelGGL((k_mix_band<DT, 8, false>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, num_in, band, n, \
+                       isst, osst);
     switch (dtype) {
       case FA_DTYPE_F32: FA_BAND(FA_DTYPE_F32); break;
       case FA_DTYPE_BF16: FA_BAND(FA_DTYPE_BF16); break;
@@ -1315,9 +1328,9 @@ int fa_mix(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_p
   // shape by row degree: ring-like (<= 3 entries), up to 4, or dense rows in passes of 8
 #define FA_MIX_SHAPE(DT, RG, MAXD)                                                                     \
   if (post_scale)                                                                                      \
-    hipLaunchKernelGGL((k_mix<DT, RG, MAXD, true>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, n, al); \
+    hipLaunchKernelGGL((k_mix<DT, RG, MAXD, true>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, n, al, isst, osst); \
   else                                                                                                 \
-    hipLaunchKernelGGL((k_mix<DT, RG, MAXD, false>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, n, al);
+    hipLaunchKernelGGL((k_mix<DT, RG, MAXD, false>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, n, al, isst, osst);
 #define FA_MIX_LAUNCH(DT)                        \
   if (maxdeg <= 3) { FA_MIX_SHAPE(DT, 4, 3) }    \
   else if (maxdeg <= 4) { FA_MIX_SHAPE(DT, 4, 4) } \
@@ -1331,6 +1344,24 @@ int fa_mix(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_p
 #undef FA_MIX_SHAPE
   FA_HIP(hipGetLastError());
   return release(slot, st);
+}
+}  // namespace
+
+int fa_mix(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_ptr,
+           const int32_t* cols, const double* vals, int32_t num_in, const void* const* d_in,
+           void* const* d_out, const double* post_scale, void* const* d_out2, void* hip_stream) {
+  return mix_impl(ctx, dtype, n, rows, row_ptr, cols, vals, num_in, d_in, d_out, post_scale, d_out2, hip_stream, 0, 0);
+}
+
+int fa_mix_tiled(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_ptr,
+                 const int32_t* cols, const double* vals, int32_t num_in, const void* const* d_in,
+                 int64_t in_tile_stride, void* const* d_out, int64_t out_tile_stride, const double* post_scale,
+                 void* const* d_out2, void* hip_stream) {
+  if (in_tile_stride <= 0 || in_tile_stride % FA_TILE_BYTES || out_tile_stride <= 0 ||
+      out_tile_stride % FA_TILE_BYTES)
+    return fail(FA_ERR_INVALID, "fa_mix_tiled: tile strides must be positive multiples of %d", FA_TILE_BYTES);
+  return mix_impl(ctx, dtype, n, rows, row_ptr, cols, vals, num_in, d_in, d_out, post_scale, d_out2, hip_stream,
+                  in_tile_stride, out_tile_stride);
 }
 
 }  // extern "C"

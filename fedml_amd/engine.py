@@ -392,6 +392,36 @@ class AggEngine:
         N.check(rc, "fa_mix")
         return list(outs), (list(outs2) if outs2 is not None else None)
 
+    def mix_tiled(self, buf_in: torch.Tensor, in_rows: Sequence[int], row_ptr: Sequence[int], cols: Sequence[int],
+                  vals: Sequence[float], buf_out: torch.Tensor, out_rows: Sequence[int],
+                  post_scale: Optional[Sequence[float]] = None, buf_out2: Optional[torch.Tensor] = None,
+                  n: Optional[int] = None, stream=None) -> None:
+        """fa_mix between tile-interleaved arena groups: input j = row in_rows[j] of ``buf_in``
+        ([tiles, cap, E]); output row r -> row out_rows[r] of ``buf_out`` (and ``buf_out2`` with
+        post_scale).  ``n`` logical elements (default: all)."""
+        n, iptr, istride = self._tiled_args(buf_in, in_rows, 0, n, "mix_tiled")
+        rows = len(row_ptr) - 1
+        if len(out_rows) != rows:
+            raise ValueError("mix_tiled: one output row per CSR row")
+        for b in [buf_out] + ([buf_out2] if buf_out2 is not None else []):
+            if b.dtype != buf_in.dtype or b.shape[0] != buf_in.shape[0] or b.shape[2] != buf_in.shape[2]:
+                raise ValueError("mix_tiled: output arena must match the input arena's dtype and tiles")
+            if b.data_ptr() == buf_in.data_ptr():
+                raise ValueError("mix_tiled: outputs must not alias inputs")
+        _, optr, ostride = self._tiled_args(buf_out, out_rows, 0, n, "mix_tiled output")
+        optr2 = None
+        if post_scale is not None:
+            if buf_out2 is None:
+                raise ValueError("mix_tiled: post_scale needs buf_out2")
+            _, optr2, ostride2 = self._tiled_args(buf_out2, out_rows, 0, n, "mix_tiled output2")
+            if ostride2 != ostride:
+                raise ValueError("mix_tiled: buf_out2 must have buf_out's capacity")
+        rc = self._lib.fa_mix_tiled(
+            self._ctx, DTYPE_CODE.get(buf_in.dtype, -1), n, rows, N.i32_array(row_ptr), N.i32_array(cols),
+            N.f64_array(vals), len(in_rows), iptr, istride, optr, ostride,
+            N.f64_array(post_scale) if post_scale is not None else None, optr2, self._stream(stream))
+        N.check(rc, "fa_mix_tiled")
+
     # ------------------------------------------------------------------ finite field (SecAgg)
     def finite_sum(self, segments: Sequence[Sequence[torch.Tensor]], prime: int, flags: int,
                    masks: Optional[Sequence[Optional[torch.Tensor]]] = None, finite: bool = True,

@@ -187,6 +187,15 @@ int fa_mix(fa_ctx *ctx, int dtype, int64_t n, int32_t rows, const int32_t *row_p
            const int32_t *cols, const double *vals, int32_t num_in, const void *const *d_in,
            void *const *d_out, const double *post_scale, void *const *d_out2, void *hip_stream);
 
+/* fa_mix over tile-interleaved inputs and outputs (addressing as fa_weighted_sum_tiled): input i's
+ * FA_TILE_BYTES slots are in_tile_stride bytes apart, every output row's (and d_out2's)
+ * out_tile_stride bytes apart -- a gossip round between two tiled ClientArenas.  Same arithmetic
+ * per element as fa_mix; inputs and outputs 16-byte aligned. */
+int fa_mix_tiled(fa_ctx *ctx, int dtype, int64_t n, int32_t rows, const int32_t *row_ptr,
+                 const int32_t *cols, const double *vals, int32_t num_in, const void *const *d_in,
+                 int64_t in_tile_stride, void *const *d_out, int64_t out_tile_stride,
+                 const double *post_scale, void *const *d_out2, void *hip_stream);
+
 /* Performance tuning only (results are identical for every variant): selects the weighted-sum
  * kernel's shape -- U clients per load group, S 16-byte vectors per lane, load cache policy,
  * double-buffered group prefetch.  0 = default; valid range [0, 9). */

@@ -247,3 +247,34 @@ def test_fedavg_sgd_tiled_matches_flat(eng, momentum, nesterov, wd):
     assert bits_equal(pa.cpu(), pb.cpu())
     if momentum:
         assert bits_equal(ba.cpu(), bb.cpu())
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16], ids=str)
+@pytest.mark.parametrize("topo", ["ring", "dense", "pushsum"])
+def test_mix_tiled_matches_flat(eng, dt, topo):
+    from fedml_amd.core.distributed.topology.topology_manager import SymmetricTopologyManager, gossip_rows
+    n, P = 10, 1024 * 7 + 300
+    if topo == "dense":
+        import numpy as np
+        W = np.full((n, n), 1.0 / n, dtype=np.float32)
+        rp, cs, vs = gossip_rows(W)
+    else:
+        m = SymmetricTopologyManager(n, 2)
+        m.generate_topology()
+        rp, cs, vs = gossip_rows(m.topology)
+    post = [1.0 / (i + 1.5) for i in range(n)] if topo == "pushsum" else None
+    xs = _inputs(dt, n, P, 31)
+    fo, fo2 = eng.mix([x.cuda() for x in xs], rp, cs, vs, post)
+    cap = n + 3
+    in_rows = [(3 * j + 1) % cap for j in range(n)]
+    out_rows = [(5 * r + 2) % cap for r in range(n)]
+    buf = tiled_buf(xs, capacity=cap, rows=in_rows)
+    obuf = torch.zeros_like(buf)
+    obuf2 = torch.zeros_like(buf) if post else None
+    eng.mix_tiled(buf, in_rows, rp, cs, vs, obuf, out_rows, post, obuf2, n=P)
+    E = buf.shape[2]
+    for r in range(n):
+        got = obuf[:, out_rows[r], :].reshape(-1)[:P].cpu()
+        assert bits_equal(got, fo[r].cpu()), r
+        if post:
+            assert bits_equal(obuf2[:, out_rows[r], :].reshape(-1)[:P].cpu(), fo2[r].cpu()), r
