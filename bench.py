@@ -86,6 +86,16 @@ def init_dist(args):
     return rank, world, local
 
 
+def masked_stream(eng, args):
+    """N > 1: the local partials' CU-masked stream (None = torch's current stream)."""
+    if not args.cu_mask:
+        return None
+    total = torch.cuda.get_device_properties(eng.device).multi_processor_count
+    if args.cu_mask >= total:
+        return None
+    return eng.cu_masked_stream(args.cu_mask)
+
+
 def barrier(world):
     if world > 1:
         import torch.distributed as dist
@@ -225,7 +235,7 @@ def wl_metric(args, eng, rank, world, timer):
                 with timer:
                     return eng.weighted_sum_tiled(*a, **kw)
         red = GroupReducer(collective=args.collective, chunks=args.chunks, local_sum=timed_sum,
-                           stream=eng.cu_masked_stream(args.cu_mask) if args.cu_mask else None)
+                           stream=masked_stream(eng, args))
 
         def step():
             if tiled:
@@ -406,7 +416,7 @@ def wl_hier(args, eng, rank, world, timer):
     if world > 1:
         from fedml_amd.distributed.group_reduce import GroupReducer
         red = GroupReducer(collective=args.collective, chunks=args.chunks, local_grouped=timed_grouped,
-                           stream=eng.cu_masked_stream(args.cu_mask) if args.cu_mask else None)
+                           stream=masked_stream(eng, args))
 
         def step():
             red.hierarchical_groups(xs, gcounts, N, out=out)
