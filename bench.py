@@ -25,6 +25,7 @@ from __future__ import annotations
 
 import argparse
 import json
+from collections import OrderedDict
 import os
 import sys
 import time
@@ -46,7 +47,8 @@ def parse():
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="metric",
-                   choices=["metric", "fragmented", "resnet18", "vit_bf16", "hier", "gossip", "host", "secagg", "fedopt", "median",
+                   choices=["metric", "fragmented", "resnet18", "vit_bf16", "hier", "gossip", "host", "secagg", "fedopt",
+                            "dropin_cpu", "median",
                             "krum"])
     p.add_argument("--clients", type=int, default=None)
     p.add_argument("--params", type=int, default=None)
@@ -325,6 +327,68 @@ def wl_layout(args, eng, rank, world, timer):
     tag = ("resnet18gn" if resnet else "vitb16_bf16") + {"arena": "", "tiled": "_tiled", "tensors": "_tensors"}[args.layout]
     return dict(name=f"fedavg_{tag}_K{K}_P{P}", dtype="fp32" if resnet else "bf16", step=step, parity=parity,
                 bytes_total=K * in_b + out_b, launch_bytes=None, clients=K, params=P, cpu_K=None)
+
+
+def wl_dropin_cpu(args, eng, rank, world, timer):
+    """The drop-in boundary as the reference's callers use it: FedMLAggOperator.agg(args,
+    [(n_i, state_dict_i)]) on CPU state_dicts (as unpickled from MPI / socket receive buffers),
+    ResNet-18-GN layout, K = 32; result returned as CPU tensors.  Step = pack to pinned + H2D +
+    aggregation + D2H (fedml_amd/ml/aggregator/state_dict_agg.py:_aggregate_host).  CPU baseline: the
+    reference's op sequence (oracle/torch_port.agg) on the same CPU dicts, 16 threads."""
+    if world > 1:
+        raise SystemExit("--config dropin_cpu is a single-GPU configuration")
+    from fedml_amd.ml.aggregator.agg_operator import FedMLAggOperator
+    layout = load_layout("resnet18_gn")
+    K = args.clients or 32
+    counts = client_counts(K)
+    dicts = []
+    g = torch.Generator().manual_seed(1)
+    for i in range(K):
+        d = OrderedDict()
+        for name, shape, dt in layout:
+            dt = getattr(torch, dt)
+            d[name] = (torch.randint(0, 100, tuple(shape), generator=g, dtype=dt) if dt == torch.int64
+                       else torch.randn(tuple(shape), generator=g).to(dt))
+        dicts.append(d)
+
+    class A:
+        federated_optimizer = "FedAvg"
+    res = {}
+
+    def step():
+        with timer:
+            res["out"] = FedMLAggOperator.agg(A(), list(zip(counts, dicts)))
+
+    P = sum(int(np.prod(s)) for _, s, _ in layout)
+    size = {"int64": 8, "bfloat16": 2, "float32": 4}
+    in_b = sum(int(np.prod(s)) * size[dt] for _, s, dt in layout)
+    out_b = sum(int(np.prod(s)) * 4 for _, s, dt in layout)
+
+    def parity():
+        import oracle.torch_port as tp
+        exp = tp.agg("FedAvg", [(n, OrderedDict((k, v.clone()) for k, v in d.items())) for n, d in zip(counts, dicts)])
+        bad = sum(int((res["out"][k].view(-1).view(torch.int32) != exp[k].view(-1).view(torch.int32)).sum())
+                  for k in exp)
+        return f"{'bit-exact' if bad == 0 else f'{bad} MISMATCHES'} vs the reference op sequence on every element"
+
+    def cpu(budget_s):
+        import oracle.torch_port as tp
+        torch.set_num_threads(min(16, os.cpu_count() or 1))
+        best, runs, t_end = float("inf"), 0, time.perf_counter() + budget_s
+        while runs < 3 or (time.perf_counter() < t_end and runs < 30):
+            lst = [(n, OrderedDict((k, v.clone()) for k, v in d.items())) for n, d in zip(counts, dicts)]
+            t0 = time.perf_counter()
+            tp.agg("FedAvg", lst)
+            best = min(best, time.perf_counter() - t0)
+            runs += 1
+        return {"value": round((K * in_b + out_b) / best / 1e9, 2), "unit": "GB/s", "cores": torch.get_num_threads(),
+                "kind": "port", "sample": f"the same K={K} ResNet-18-GN CPU state_dicts, best of {runs} runs of "
+                                          "oracle/torch_port.agg('FedAvg') (agg_operator.py:35-44)"}
+
+    return dict(name=f"dropin_agg_cpu_resnet18gn_K{K}_P{P}", dtype="fp32", step=step, parity=parity, cpu=cpu,
+                bytes_total=K * in_b + out_b, launch_bytes=None, clients=K, params=P, cpu_K=K,
+                data="synthetic CPU state_dicts (ResNet-18-GN layout), host-resident: the step includes H2D and D2H",
+                roofline_note="kernel time = the whole agg() call incl. PCIe transfers (host-resident inputs)")
 
 
 def fragmented_layout(P, n_tensors=200):
@@ -884,7 +948,7 @@ def main():
         eng.set_variant(args.variant)
     timer = Timed()
     wl = {"metric": wl_metric, "fragmented": wl_fragmented, "resnet18": wl_layout, "vit_bf16": wl_layout, "hier": wl_hier,
-          "gossip": wl_gossip, "host": wl_host, "secagg": wl_secagg, "fedopt": wl_fedopt, "median": wl_median,
+          "gossip": wl_gossip, "host": wl_host, "secagg": wl_secagg, "fedopt": wl_fedopt, "dropin_cpu": wl_dropin_cpu, "median": wl_median,
           "krum": wl_krum}[args.config](args, eng, rank, world, timer)
 
     for _ in range(args.warmup):

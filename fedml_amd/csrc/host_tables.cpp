@@ -7,7 +7,10 @@
 // DATA: all arithmetic stays in the HIP kernels behind the C ABI (include/fedagg.h).
 #include <torch/extension.h>
 
+#include <algorithm>
+#include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace py = pybind11;
@@ -149,7 +152,47 @@ py::tuple alloc_outputs(py::list shapes, py::list dtypes, const std::string& dev
   return py::make_tuple(arena, views, ptrs);
 }
 
+// pack_range(src, dst_off, nbytes, lo, hi, dst, nthreads): host-ingest packing.  Job j copies
+// nbytes[j] bytes from address src[j] to byte dst_off[j] of a virtual [K, row] staging matrix;
+// this call materialises the bytes [lo, hi) of that matrix at address `dst` (dst_off sorted,
+// ranges disjoint; bytes no job covers are left untouched).  The copy runs on `nthreads` threads
+// with the GIL released: unpickled client tensors sit in pageable memory, and one thread's memcpy
+// into pinned staging (~10 GB/s) would otherwise be slower than the PCIe link it feeds.
+void pack_range(torch::Tensor src, torch::Tensor dst_off, torch::Tensor nbytes, int64_t lo, int64_t hi,
+                int64_t dst, int64_t nthreads) {
+  TORCH_CHECK(src.dtype() == torch::kInt64 && dst_off.dtype() == torch::kInt64 && nbytes.dtype() == torch::kInt64,
+              "pack_range: int64 job tables");
+  TORCH_CHECK(src.is_contiguous() && dst_off.is_contiguous() && nbytes.is_contiguous(), "pack_range: contiguous");
+  const int64_t J = src.numel();
+  TORCH_CHECK(dst_off.numel() == J && nbytes.numel() == J, "pack_range: table sizes differ");
+  const int64_t* S = src.data_ptr<int64_t>();
+  const int64_t* D = dst_off.data_ptr<int64_t>();
+  const int64_t* B = nbytes.data_ptr<int64_t>();
+  char* out = reinterpret_cast<char*>(dst);
+  if (hi <= lo || J == 0) return;
+  auto work = [&](int64_t a, int64_t b) {  // bytes [a, b) of the matrix
+    int64_t j = std::upper_bound(D, D + J, a) - D - 1;  // last job starting at or before a
+    if (j < 0) j = 0;
+    for (; j < J && D[j] < b; ++j) {
+      const int64_t s0 = std::max(a, D[j]), s1 = std::min(b, D[j] + B[j]);
+      if (s1 > s0) std::memcpy(out + (s0 - lo), reinterpret_cast<const char*>(S[j]) + (s0 - D[j]), (size_t)(s1 - s0));
+    }
+  };
+  const int64_t total = hi - lo;
+  const int64_t nt = std::max<int64_t>(1, std::min<int64_t>(nthreads, total / (1 << 20) + 1));
+  py::gil_scoped_release nogil;
+  if (nt == 1) { work(lo, hi); return; }
+  std::vector<std::thread> th;
+  th.reserve(nt);
+  for (int64_t t = 0; t < nt; ++t) {
+    const int64_t a = lo + total * t / nt, b = lo + total * (t + 1) / nt;
+    th.emplace_back(work, a, b);
+  }
+  for (auto& x : th) x.join();
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("pack_range", &pack_range, "multi-threaded packing of host tensors into a pinned staging range");
   m.doc() = "host-side table builder of the fedml_amd aggregation engine (no tensor data access)";
   m.def("gather", &gather, "validate K client dicts x T keys, return the device pointer table");
   m.def("alloc_outputs", &alloc_outputs, "carve T aligned outputs out of one device allocation");

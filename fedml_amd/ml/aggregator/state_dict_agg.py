@@ -11,10 +11,15 @@ agg_operator.py:37-44 -- with the dtype semantics of the PyTorch ops it issues:
 
 Device placement: tensors already on a HIP device are aggregated in place on that device; CPU
 tensors (what the reference's transports deliver) are staged to the engine's device, aggregated
-there, and the result is returned on the CPU, matching the reference's output placement.
+there, and the result is returned on the CPU, matching the reference's output placement.  The CPU
+path (`_aggregate_host`) packs every client's tensors of one dtype into a client-major staging
+matrix with a multi-threaded C++ copy (`_host.pack_range`, GIL released) through a ring of pinned
+slots, each slot's H2D overlapping the packing of the next, then aggregates the device matrix in
+one launch per dtype and returns the result through one pinned D2H per dtype.
 """
 from __future__ import annotations
 
+import os
 from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence
 
@@ -55,8 +60,11 @@ def aggregate(dicts: Sequence[Dict[str, torch.Tensor]], mode: int, coef: Optiona
         ptrs, numel, codes, shapes, dev = _host.gather(list(dicts), keys)
     except ValueError:  # mixed devices / non-contiguous: the staging path below normalises them
         ptrs = None
-    if ptrs is not None and dev.startswith("cuda") and int(codes.min()) >= 0:
-        return _aggregate_device(keys, ptrs, numel, codes, shapes, dev, len(dicts), mode, coef, divisor, engine)
+    if ptrs is not None and int(codes.min()) >= 0:
+        if dev.startswith("cuda"):
+            return _aggregate_device(keys, ptrs, numel, codes, shapes, dev, len(dicts), mode, coef, divisor, engine)
+        if dev == "cpu" and os.environ.get("FEDML_AMD_HOST_PATH", "packed") == "packed":
+            return _aggregate_host(keys, ptrs, numel, codes, shapes, len(dicts), mode, coef, divisor, engine)
     return _aggregate_staged(dicts, keys, mode, coef, divisor, engine)
 
 
@@ -79,6 +87,96 @@ def _aggregate_device(keys, ptrs, numel, codes, shapes, dev, k, mode, coef, divi
                                    table.index_select(0, sel).reshape(-1).contiguous(),
                                    optrs.index_select(0, sel).contiguous(), coef, divisor)
     return OrderedDict(zip(keys, views))
+
+
+_ELEM = {0: 4, 1: 2, 2: 2, 3: 8, 4: 8}  # bytes per element of each dtype code
+_SLOT_BYTES = 64 << 20                  # pinned staging slot (two of them, ping-pong)
+
+
+class _HostStaging:
+    """Pinned slots + a device matrix per dtype group, reused across rounds of the same shape."""
+
+    def __init__(self, eng: AggEngine):
+        self.eng = eng
+        self.stream = torch.cuda.Stream(eng.device)
+        self.slots = [torch.empty(_SLOT_BYTES, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        self.events: List[Optional[torch.cuda.Event]] = [None, None]
+        self.dev: Dict[tuple, torch.Tensor] = {}
+        self.next = 0
+
+    def matrix(self, key: tuple, nbytes: int) -> torch.Tensor:
+        t = self.dev.get(key)
+        if t is None or t.numel() < nbytes:
+            t = self.dev[key] = torch.zeros(nbytes, dtype=torch.uint8, device=self.eng.device)
+        return t
+
+
+_STAGING: Dict[int, _HostStaging] = {}
+
+
+def _pack_threads() -> int:
+    env = os.environ.get("FEDML_AMD_PACK_THREADS")
+    return int(env) if env else max(1, min(16, os.cpu_count() or 1))
+
+
+def _aggregate_host(keys, ptrs, numel, codes, shapes, k, mode, coef, divisor, engine):
+    """CPU state_dicts: pack -> pinned -> H2D (overlapped) -> one launch per dtype -> D2H."""
+    eng = engine or get_engine(None)
+    st = _STAGING.get(eng.device_index)
+    if st is None:
+        st = _STAGING[eng.device_index] = _HostStaging(eng)
+    code_list = codes.tolist()
+    numel_list = numel.tolist()
+    groups: Dict[int, List[int]] = {}
+    for t, c in enumerate(code_list):
+        groups.setdefault(c, []).append(t)
+    table = ptrs.view(len(keys), k)
+    nthreads = _pack_threads()
+    cur = torch.cuda.current_stream(eng.device)
+    st.stream.wait_stream(cur)  # the device matrices may still be read by the previous round's launch
+    results: Dict[int, tuple] = {}
+    for c, idx in groups.items():
+        es = _ELEM[c]
+        offs, row = [], 0
+        for t in idx:
+            offs.append(row)
+            row += -(-max(numel_list[t], 1) * es // 256) * 256  # 256-byte aligned keys
+        total = row * k
+        mat = st.matrix((c,), total)
+        # job table, sorted by destination: client-major, keys in order inside a row
+        src = table.index_select(0, torch.tensor(idx, dtype=torch.int64)).t().contiguous().view(-1)
+        dst = (torch.arange(k, dtype=torch.int64).view(k, 1) * row + torch.tensor(offs, dtype=torch.int64)).view(-1)
+        nb = (torch.tensor([numel_list[t] for t in idx], dtype=torch.int64) * es).repeat(k)
+        for lo in range(0, total, _SLOT_BYTES):
+            hi = min(total, lo + _SLOT_BYTES)
+            j = st.next % 2
+            st.next += 1
+            if st.events[j] is not None:
+                st.events[j].synchronize()  # the H2D that last read this slot is done
+            _host.pack_range(src, dst, nb, lo, hi, st.slots[j].data_ptr(), nthreads)
+            with torch.cuda.stream(st.stream):
+                mat[lo:hi].copy_(st.slots[j][:hi - lo], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(st.stream)
+            st.events[j] = ev
+        results[c] = (idx, offs, row, mat)
+    cur.wait_stream(st.stream)
+    out = OrderedDict()
+    views: Dict[int, torch.Tensor] = {}
+    for c, (idx, offs, row, mat) in results.items():
+        dt = _CODE_DTYPE[c]
+        buf = mat[:row * k].view(dt).view(k, row // _ELEM[c])
+        o = eng.weighted_sum_rows(buf, list(range(k)), mode, coef, divisor)
+        host = torch.empty(o.numel(), dtype=o.dtype, pin_memory=True)
+        host.copy_(o, non_blocking=True)
+        views[c] = host
+    cur.synchronize()  # the reference returns materialised CPU tensors
+    for c, (idx, offs, row, mat) in results.items():
+        host = views[c]
+        for t, off in zip(idx, offs):
+            e0 = off // _ELEM[c]
+            out[keys[t]] = host[e0:e0 + numel_list[t]].view(shapes[t])
+    return OrderedDict((kk, out[kk]) for kk in keys)
 
 
 def _aggregate_staged(dicts, keys, mode, coef, divisor, engine):
