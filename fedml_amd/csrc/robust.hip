@@ -266,17 +266,39 @@ int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t*
 // ============================================================================================
 // Krum's pairwise squared distances (krum_defense.py:52-66): D[i][j] = sum_e (x_i[e] - x_j[e])^2
 // over the clients' weight vectors, float32 inputs, every pair (i < j) in ONE pass over the data.
-// A workgroup stages a chunk of kPE coordinates of all K clients in LDS (transposed [e][client],
+// A workgroup stages a chunk of coordinates of all K clients in LDS (transposed [e][client],
 // so 4 clients of one coordinate are one 16-byte LDS read), and each thread owns up to TPT 4x4
 // client-pair tiles (upper triangle) -- 16 differences per 2 LDS reads -- over a slice of the
-// chunk's coordinates.  Sums: float32 within a chunk slice (<= kPE terms), float64 across chunks.
+// chunk's coordinates (pair_split).  Sums: float32 within a chunk slice (<= kPE terms), float64
+// across chunks.
 // Per-block float64 partials of the upper triangle go to a scratch buffer and a second kernel
 // adds them in block order (deterministic).  VALU-bound for large K (K^2/2 pair updates per
 // coordinate against 4K bytes).
 namespace {
 
-constexpr int kPE = 64;       // coordinates per LDS chunk
+constexpr int kPE = 64;       // nominal coordinates per LDS chunk (see pair_split)
 constexpr int kMaxPairK = 128;
+
+// Work split of k_pairdist: ntiles 4x4 pair tiles; with ntiles <= kBlock every thread owns one
+// tile and one of `esplit` coordinate slices (esplit = kBlock / ntiles, so e.g. K = 32 keeps 252 of
+// 256 threads busy, not 144 as with a power-of-two split), `pe` = esplit * ceil(kPE / esplit)
+// coordinates per chunk; otherwise TPT tiles per thread over kPE coordinates.
+struct PairSplit { int kp, nb, ntiles, tpt, esplit, pe, nblocks; };
+PairSplit pair_split(int k) {
+  PairSplit q;
+  q.kp = (k + 3) & ~3;
+  q.nb = q.kp / 4;
+  q.ntiles = q.nb * (q.nb + 1) / 2;
+  q.tpt = (q.ntiles + kBlock - 1) / kBlock;
+  q.esplit = q.tpt == 1 ? std::min(kPE, kBlock / q.ntiles) : 1;
+  // coordinates per slice: as many as a <= 32 KiB chunk holds, 8..kPE (measured sweep, K = 8 / 32:
+  // 0.29 / 0.92 ms; larger chunks cost resident workgroups, smaller ones more barriers and float64
+  // conversions per coordinate)
+  const int per = std::max(8, std::min(kPE, (32 << 10) / (q.esplit * (q.kp + 4) * 4)));
+  q.nblocks = 1024;  // workgroups (each writes all pair partials once)
+  q.pe = q.esplit * per;
+  return q;
+}
 
 struct PSeg {
   int64_t numel;
@@ -290,8 +312,8 @@ static_assert(sizeof(PSeg) == 32, "PSeg layout");
 template <int TPT>
 __global__ void __launch_bounds__(kBlock)
 k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int kp,
-           int64_t nchunks, int ntiles, int esplit, double* __restrict__ partial) {
-  extern __shared__ float lds[];              // [kPE][kp + 4]
+           int64_t nchunks, int ntiles, int esplit, int pe, double* __restrict__ partial) {
+  extern __shared__ float lds[];              // [pe][kp + 4]
   const int stride = kp + 4;
   const int nb = kp / 4;
   const int t = threadIdx.x;
@@ -316,23 +338,35 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
   for (int q = 0; q < TPT; ++q)
 #pragma unroll
     for (int u = 0; u < 16; ++u) accd[q][u] = 0.0;
-  const int per = kPE / esplit;  // coordinates of a chunk per slice
+  const int per = pe / esplit;  // coordinates of a chunk per slice
+  const int se0 = t % pe, sc0 = t / pe, sde = kBlock % pe, sdc = kBlock / pe;  // staging walk
   for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
     const PSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, ch) : 0];
-    const int64_t e0 = (ch - sg.tile_start) * kPE;
+    const int64_t e0 = (ch - sg.tile_start) * pe;
     const void* const* in = ptrs + sg.ptr_base;
     __syncthreads();  // the previous chunk is consumed
     // stage: client c, coordinate e -> lds[e * stride + c]; clients >= k and coordinates past the
-    // segment end are zero (they add 0 to every sum).  Loads are unconditional (clamped) so the
-    // unrolled loop keeps 8 in flight per lane.
+    // segment end are zero (they add 0 to every sum).
     {
-      const int e = t & (kPE - 1);
-      const bool ev = e0 + e < sg.numel;
-      const int64_t ge = ev ? e0 + e : sg.numel - 1;
-#pragma unroll 8
-      for (int c = t / kPE; c < kp; c += kBlock / kPE) {
-        const float v = gld<float>(in[min(c, k - 1)], ge);
-        lds[e * stride + c] = (ev && c < k) ? v : 0.0f;
+      // element idx = c * pe + e, idx = t, t + kBlock, ...: (e, c) advanced by carry, no division
+      int e = se0, c = sc0;
+      while (c < kp) {
+        int eu[8], cu[8];
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          eu[u] = e;
+          cu[u] = c;
+          e += sde;
+          c += sdc;
+          if (e >= pe) { e -= pe; ++c; }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)  // 8 clamped, unconditional loads in flight per lane
+          v[u] = gld<float>(in[min(cu[u], k - 1)], min(e0 + eu[u], sg.numel - 1));
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (cu[u] < kp) lds[eu[u] * stride + cu[u]] = (e0 + eu[u] < sg.numel && cu[u] < k) ? v[u] : 0.0f;
       }
     }
     __syncthreads();
@@ -400,17 +434,29 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
 
 __global__ void __launch_bounds__(kBlock)
 k_pairdist_reduce(const double* __restrict__ partial, int nblocks, int k, double* __restrict__ d) {
+  // kRP pairs per workgroup, kBlock / kRP lanes per pair: lane l sums blocks l, l + L, ... (each
+  // load row = kRP consecutive pairs), then the L lane sums are added in lane order -- a fixed
+  // order, so the result is deterministic.  (A single thread per pair made this a serial chain of
+  // nblocks loads: ~0.5 ms of latency at 1,024 blocks.)
+  constexpr int kRP = 8, L = kBlock / kRP;
+  __shared__ double red[L][kRP + 1];
   const int64_t npairs = (int64_t)k * (k - 1) / 2;
-  for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < npairs; p += (int64_t)gridDim.x * kBlock) {
-    double s = 0.0;
-    for (int b = 0; b < nblocks; ++b) s += partial[(int64_t)b * npairs + p];
-    // p -> (i, j)
-    int i = 0;
+  const int pl = threadIdx.x % kRP, lane = threadIdx.x / kRP;
+  const int64_t p = (int64_t)blockIdx.x * kRP + pl;
+  double s = 0.0;
+  if (p < npairs)
+    for (int b = lane; b < nblocks; b += L) s += partial[(int64_t)b * npairs + p];
+  red[lane][pl] = s;
+  __syncthreads();
+  if (lane == 0 && p < npairs) {
+    double t = 0.0;
+    for (int l = 0; l < L; ++l) t += red[l][pl];
+    int i = 0;  // p -> (i, j)
     int64_t rem = p;
     while (rem >= k - 1 - i) { rem -= k - 1 - i; ++i; }
     const int j = i + 1 + (int)rem;
-    d[(int64_t)i * k + j] = s;
-    d[(int64_t)j * k + i] = s;
+    d[(int64_t)i * k + j] = t;
+    d[(int64_t)j * k + i] = t;
   }
   if (blockIdx.x == 0)
     for (int i = threadIdx.x; i < k; i += kBlock) d[(int64_t)i * k + i] = 0.0;
@@ -426,17 +472,8 @@ int fa_pairwise_sqdist(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_num
   if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
   if (k < 2 || k > kMaxPairK || num_segments <= 0 || !seg_numel || !d_in || !d_dist)
     return fail(FA_ERR_INVALID, "fa_pairwise_sqdist: invalid arguments (2 <= k <= %d)", kMaxPairK);
-  const int kp = (k + 3) & ~3;
-  const int nb = kp / 4;
-  const int ntiles = nb * (nb + 1) / 2;
-  int tpt = (ntiles + kBlock - 1) / kBlock;
-  int esplit = 1;
-  if (tpt == 1) {
-    esplit = kBlock / ntiles;
-    int p2 = 1;
-    while (p2 * 2 <= esplit && p2 * 2 <= kPE) p2 *= 2;
-    esplit = p2;
-  }
+  const PairSplit q = pair_split(k);
+  const int kp = q.kp, ntiles = q.ntiles, tpt = q.tpt, esplit = q.esplit, pe = q.pe;
   if (tpt > 3) return fail(FA_ERR_INVALID, "fa_pairwise_sqdist: k too large");
   int nseg = 0;
   int64_t nchunks = 0;
@@ -446,10 +483,10 @@ int fa_pairwise_sqdist(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_num
     for (int i = 0; i < k; ++i)
       if (!d_in[(int64_t)s * k + i]) return fail(FA_ERR_INVALID, "segment %d client %d: input NULL", s, i);
     ++nseg;
-    nchunks += (seg_numel[s] + kPE - 1) / kPE;
+    nchunks += (seg_numel[s] + pe - 1) / pe;
   }
   const int64_t npairs = (int64_t)k * (k - 1) / 2;
-  const int nblocks = (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, 1024));
+  const int nblocks = (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, q.nblocks));
   if (scratch_bytes < sizeof(double) * (size_t)npairs * nblocks || !d_scratch)
     return fail(FA_ERR_INVALID, "fa_pairwise_sqdist: scratch must hold %zu bytes",
                 sizeof(double) * (size_t)npairs * nblocks);
@@ -475,23 +512,23 @@ int fa_pairwise_sqdist(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_num
     if (n == 0) continue;
     for (int i = 0; i < k; ++i) hp[(int64_t)j * k + i] = d_in[(int64_t)s * k + i];
     hs[j] = PSeg{n, c0, j * k, 0, 0};
-    c0 += (n + kPE - 1) / kPE;
+    c0 += (n + pe - 1) / pe;
     ++j;
   }
   rc = stage(slot, seg_bytes + ptr_bytes, st);
   if (rc) return rc;
   const char* dv = (const char*)slot->dev;
-  size_t lds = sizeof(float) * (size_t)kPE * (kp + 4);
+  size_t lds = sizeof(float) * (size_t)pe * (kp + 4);
   lds = std::max(lds, sizeof(double) * 16 * (size_t)ntiles);
   const dim3 grid((unsigned)nblocks), blk(kBlock);
 #define FA_PD(T)                                                                                     \
   hipLaunchKernelGGL((k_pairdist<T>), grid, blk, lds, st, (const PSeg*)dv, nseg,                       \
-                     (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit, (double*)d_scratch)
+                     (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit, pe, (double*)d_scratch)
   if (tpt == 1) FA_PD(1);
   else if (tpt == 2) FA_PD(2);
   else FA_PD(3);
 #undef FA_PD
-  hipLaunchKernelGGL(k_pairdist_reduce, dim3((unsigned)std::min<int64_t>((npairs + kBlock - 1) / kBlock, 64)), blk, 0,
+  hipLaunchKernelGGL(k_pairdist_reduce, dim3((unsigned)((npairs + 7) / 8)), blk, 0,
                      st, (const double*)d_scratch, nblocks, k, (double*)d_dist);
   FA_HIP(hipGetLastError());
   return release(slot, st);
@@ -499,10 +536,11 @@ int fa_pairwise_sqdist(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_num
 
 size_t fa_pairwise_sqdist_scratch_bytes(int32_t num_segments, const int64_t* seg_numel, int32_t k) {
   if (k < 2 || num_segments <= 0 || !seg_numel) return 0;
+  const PairSplit q = pair_split(k);
   int64_t nchunks = 0;
   for (int s = 0; s < num_segments; ++s)
-    if (seg_numel[s] > 0) nchunks += (seg_numel[s] + kPE - 1) / kPE;
-  const int64_t nblocks = std::max<int64_t>(1, std::min<int64_t>(nchunks, 1024));
+    if (seg_numel[s] > 0) nchunks += (seg_numel[s] + q.pe - 1) / q.pe;
+  const int64_t nblocks = std::max<int64_t>(1, std::min<int64_t>(nchunks, q.nblocks));
   return sizeof(double) * (size_t)((int64_t)k * (k - 1) / 2) * (size_t)nblocks;
 }
 
