@@ -38,9 +38,27 @@ __global__ void __launch_bounds__(256) lp_tiled(const u32x4* __restrict__ base, 
   __builtin_nontemporal_store(acc, (gpw)(out + e));
 }
 
+// tiled, XCD-aware: workgroup b runs on XCD b % 8; give each XCD a contiguous eighth of the tiles
+__global__ void __launch_bounds__(256) lp_tiled_xcd(const u32x4* __restrict__ base, int k, u32x4* out) {
+  const int64_t nb = gridDim.x, q = nb / 8, b = blockIdx.x;
+  const int64_t tile = b < 8 * q ? (b % 8) * q + b / 8 : b;
+  const int64_t e = tile * 256 + threadIdx.x;
+  const u32x4* tb = base + tile * k * 256 + threadIdx.x;
+  u32x4 acc = {0, 0, 0, 0};
+  for (int i0 = 0; i0 < k; i0 += 8) {
+    u32x4 r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) r[u] = __builtin_nontemporal_load((gp)(tb + (int64_t)min(i0 + u, k - 1) * 256));
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc ^= r[u];
+  }
+  __builtin_nontemporal_store(acc, (gpw)(out + e));
+}
+
 extern "C" int lp_run(int mode, const void* base, int64_t p16, int k, int64_t t16, void* out, void* stream) {
   const int64_t blocks = p16 / 256;
   if (mode == 0) hipLaunchKernelGGL(lp_rows, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const u32x4*)base, p16, k, (u32x4*)out);
+  else if (mode == 2) hipLaunchKernelGGL(lp_tiled_xcd, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const u32x4*)base, k, (u32x4*)out);
   else hipLaunchKernelGGL(lp_tiled, dim3(blocks), dim3(256), 0, (hipStream_t)stream, (const u32x4*)base, t16, k, (u32x4*)out);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

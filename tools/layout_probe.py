@@ -13,8 +13,8 @@ res = {}
 for rep in range(3):
     big = torch.empty(K * P, dtype=torch.float32, device="cuda").normal_()
     out = torch.empty(p16 * 4, dtype=torch.float32, device="cuda")
-    for name, mode, t16 in [("rows", 0, 0), ("tiled_4K", 1, 256), ("tiled_16K", 1, 1024), ("tiled_64K", 1, 4096),
-                            ("tiled_256K", 1, 16384), ("rows2", 0, 0)]:
+    for name, mode, t16 in [("rows", 0, 0), ("tiled_4K", 1, 256), ("tiled_4K_xcd", 2, 256), ("tiled_4K_b", 1, 256),
+                            ("tiled_4K_xcd_b", 2, 256)]:
         ts = []
         for _ in range(6):
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
