@@ -5,10 +5,10 @@
 // Coordinate-wise median (k_median): torch.median over the client axis is a SELECTION, so the
 // result is one of the inputs, bit for bit.  One lane owns one coordinate: it loads the K client
 // values (all loads in flight at once), maps them to order-preserving uint32 keys (unsigned order
-// == numeric order, -0.0 just below +0.0), pads to P2 = next power of two with low/high sentinels
-// that put the lower median at rank P2/2 - 1, and selects that rank with a pruned odd-even merge
-// network (median_nets.h: 283 min/max for P2 = 32, 2,299 for P2 = 128, vs 480 / 3,584 for a full
-// bitonic sort).  ATen's exact rules are kept: a NaN anywhere in the column returns the FIRST NaN;
+// == numeric order, -0.0 just below +0.0), pads to B = K rounded up to 8 with low/high sentinels
+// that put the lower median at rank (B-1)/2, and selects that rank with a pruned odd-even merge
+// network (median_nets.h: 283 min/max for B = 32, 1,233 for B = 72, 2,299 for B = 128, vs 480 /
+// 3,584 / 3,584 for a full bitonic sort of the next power of two).  ATen's exact rules are kept: a NaN anywhere in the column returns the FIRST NaN;
 // among equal values the client index decides, which only matters for +-0 -- both cases (a NaN
 // seen, or a zero selected) take a short in-order rescan of the column.
 // K <= 128 runs the network; larger K and float64 a rank-counting kernel (O(K^2) per coordinate).
@@ -27,7 +27,6 @@ using namespace fa_detail;
 
 namespace {
 
-constexpr int kMaxP2 = 128;  // largest column one lane selects from (median_nets.h)
 
 // Raw element loads in the global address space (global_load_*: vmcnt only).  Generic (flat)
 // loads also count in lgkmcnt, so every s_waitcnt for the next scalar pointer load drained them and
@@ -111,11 +110,11 @@ __device__ __forceinline__ void store_rare(const void* const* in, int k, int64_t
 }
 
 // One lane per coordinate.  Loads: the column's K client pointers first (scalar loads), then all
-// P2 element loads (clamped, unconditional) before any is consumed.  Keys: the K real keys, then
-// L = P2/2 - 1 - (K-1)/2 low sentinels (0, below every non-NaN key) and high sentinels
-// (0xFFFFFFFF) for the rest, so the lower median of the reals is rank P2/2 - 1 of all P2 keys --
-// which the pruned network select_mid<P2> (median_nets.h) computes.
-template <int DT, int P2>
+// B element loads (clamped, unconditional) before any is consumed.  Keys: the K real keys, then
+// L = (B-1)/2 - (K-1)/2 low sentinels (0, below every non-NaN key) and high sentinels
+// (0xFFFFFFFF) for the rest, so the lower median of the reals is rank (B-1)/2 of all B keys --
+// which the pruned network select_mid<B> (median_nets.h) computes.  B = K rounded up to 8.
+template <int DT, int B>
 __global__ void __launch_bounds__(kBlock)
 k_median(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k) {
   const int64_t tile = blockIdx.x;
@@ -124,21 +123,21 @@ k_median(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict_
   const bool live = e < sg.numel;
   const int64_t ec = live ? e : sg.numel - 1;
   const void* const* in = ptrs + sg.ptr_base;
-  const void* p[P2];
+  const void* p[B];
 #pragma unroll
-  for (int i = 0; i < P2; ++i) p[i] = in[min(i, k - 1)];
-  float x[P2];
+  for (int i = 0; i < B; ++i) p[i] = in[min(i, k - 1)];
+  float x[B];
 #pragma unroll
-  for (int i = 0; i < P2; ++i) x[i] = MedT<DT>::load(p[i], ec);  // clamped: every load unconditional
-  const int lo_end = k + P2 / 2 - 1 - ((k - 1) >> 1);              // sentinels [k, lo_end) are low
-  unsigned key[P2];
+  for (int i = 0; i < B; ++i) x[i] = MedT<DT>::load(p[i], ec);  // clamped: every load unconditional
+  const int lo_end = k + (B - 1) / 2 - ((k - 1) >> 1);          // sentinels [k, lo_end) are low
+  unsigned key[B];
   bool nan = false;
 #pragma unroll
-  for (int i = 0; i < P2; ++i) {
+  for (int i = 0; i < B; ++i) {
     nan = nan || (i < k && x[i] != x[i]);
     key[i] = i < k ? fkey(x[i]) : (i < lo_end ? 0u : 0xFFFFFFFFu);
   }
-  const unsigned kr = select_mid<P2>(key);
+  const unsigned kr = select_mid<B>(key);
   if (!live) return;
   const int r = (k - 1) >> 1;
   if (nan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, nan, sg.out);
@@ -188,12 +187,13 @@ void launch_median(int k, dim3 grid, hipStream_t st, const MSeg* ds, int nseg, c
   if constexpr (DT == FA_DTYPE_F64) {
     hipLaunchKernelGGL((k_median_rank<DT>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);
   } else {
-    if (k <= 4) { hipLaunchKernelGGL((k_median<DT, 4>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); return; }
-    if (k <= 8) { hipLaunchKernelGGL((k_median<DT, 8>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); return; }
-    if (k <= 16) { hipLaunchKernelGGL((k_median<DT, 16>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); return; }
-    if (k <= 32) { hipLaunchKernelGGL((k_median<DT, 32>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); return; }
-    if (k <= 64) { hipLaunchKernelGGL((k_median<DT, 64>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); return; }
-    if (k <= kMaxP2) { hipLaunchKernelGGL((k_median<DT, 128>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); return; }
+    switch ((k + 7) / 8) {  // bucket B = K rounded up to 8 (median_nets.h)
+#define FA_MB(Q) case Q: hipLaunchKernelGGL((k_median<DT, 8 * Q>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); return;
+      FA_MB(1) FA_MB(2) FA_MB(3) FA_MB(4) FA_MB(5) FA_MB(6) FA_MB(7) FA_MB(8)
+      FA_MB(9) FA_MB(10) FA_MB(11) FA_MB(12) FA_MB(13) FA_MB(14) FA_MB(15) FA_MB(16)
+#undef FA_MB
+      default: break;
+    }
     hipLaunchKernelGGL((k_median_rank<DT>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);
   }
 }
