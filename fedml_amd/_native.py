@@ -29,7 +29,7 @@ FA_OK, FA_ERR_INVALID, FA_ERR_DTYPE, FA_ERR_HIP, FA_ERR_NOMEM = 0, -1, -2, -3, -
 EXPORTED_SYMBOLS = (
     "fa_abi_version", "fa_ctx_create", "fa_ctx_destroy", "fa_weighted_sum",
     "fa_weighted_sum_multi", "fa_weighted_sum_tiled", "fa_weighted_sum_grouped", "fa_weighted_sum_grouped_tiled",
-    "fa_fedavg_sgd", "fa_fedavg_sgd_tiled", "fa_mix", "fa_mix_tiled", "fa_ctx_set_variant",
+    "fa_fedavg_sgd", "fa_fedavg_sgd_tiled", "fa_fedavg_rmsprop", "fa_mix", "fa_mix_tiled", "fa_ctx_set_variant",
     "fa_ctx_set_mix_band", "fa_stream_create_cu_masked", "fa_stream_destroy", "fa_strerror", "fa_last_error",
     # include/fedagg_finite.h
     "fa_finite_sum", "fa_finite_sum_tiled", "fa_finite_quantize", "fa_lcc_decode",
@@ -90,6 +90,10 @@ def _declare(L):
     L.fa_fedavg_sgd.argtypes = [_vp, ctypes.c_int32, _P_i64, ctypes.c_int32, _P_vp, _P_d, _P_vp, _P_vp,
                                 ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                 ctypes.c_int, ctypes.c_int, _vp]
+    L.fa_fedavg_rmsprop.restype = ctypes.c_int
+    L.fa_fedavg_rmsprop.argtypes = [_vp, ctypes.c_int32, _P_i64, ctypes.c_int32, _P_vp, _P_d, _P_vp, _P_vp, _P_vp,
+                                    ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                    ctypes.c_double, ctypes.c_int, _vp]
     L.fa_fedavg_sgd_tiled.restype = ctypes.c_int
     L.fa_fedavg_sgd_tiled.argtypes = [_vp, ctypes.c_int64, ctypes.c_int32, _P_vp, ctypes.c_int64, _P_d, _vp, _vp,
                                       ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,

@@ -470,11 +470,36 @@ __device__ __forceinline__ float sgd_update(float p, float avg, float& buf, floa
   return __fmaf_rn(g, neg_lr, p);
 }
 
-template <int U, bool NT>
+// torch.optim.RMSprop (centered=False) on CPU tensors, reachable from the reference's FedOpt as
+// server_optimizer="rmsprop" (OptRepo passes lr and momentum).  ATen's CPU op sequence:
+// square_avg.mul_(alpha).addcmul_(g, g, value=1-alpha) -> fma((1-alpha)*g, g, sq*alpha);
+// avg = sqrt(square_avg) + eps; momentum: buf = buf*m + g/avg (addcdiv), p += -lr*buf (FMA);
+// else p = p + (-lr*g)/avg.  ATen's sqrt there is MKL-VML (not correctly rounded): parity is
+// within 1e-6 relative, not bit-exact.  State starts at zero (torch initialises it so).
+struct RmsArgs { float alpha, one_m_alpha, eps; };
+
+__device__ __forceinline__ float rmsprop_update(float p, float avg, float& sq, float& buf, float neg_lr, float mom,
+                                                float wd, const RmsArgs& ra, int flags) {
+  float g = __fsub_rn(p, avg);
+  if (flags & SGD_WD) g = __fmaf_rn(p, wd, g);
+  sq = __fmaf_rn(__fmul_rn(ra.one_m_alpha, g), g, __fmul_rn(sq, ra.alpha));
+  // correctly rounded float sqrt: the float32 __fsqrt_rn lowers to v_sqrt_f32 (~1 ulp) on gfx950;
+  // the float64 sqrt is correctly rounded and float64 -> float32 rounding of a sqrt is innocuous
+  const float den = __fadd_rn(__double2float_rn(__dsqrt_rn((double)sq)), ra.eps);
+  if (flags & SGD_MOMENTUM) {
+    buf = __fadd_rn(__fmul_rn(buf, mom), __fdiv_rn(g, den));
+    return __fmaf_rn(buf, neg_lr, p);
+  }
+  return __fadd_rn(p, __fdiv_rn(__fmul_rn(neg_lr, g), den));
+}
+
+// OPT 0: SGD (bufs = momentum); OPT 1: RMSprop (bufs = momentum, bufs2 = square_avg)
+template <int U, bool NT, int OPT = 0>
 __global__ void __launch_bounds__(kBlock)
 k_fedavg_sgd(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
              const void* const* __restrict__ ptrs, int k, void* const* __restrict__ bufs, float neg_lr,
-             float mom, float damp1, float wd, int flags, int64_t sstr) {
+             float mom, float damp1, float wd, int flags, int64_t sstr, void* const* __restrict__ bufs2,
+             RmsArgs ra) {
   using B = WsumBody<FA_DTYPE_F32, FA_MODE_MUL_W, U, 1, NT>;
   using T = typename B::T;
   constexpr int V = T::V;
@@ -484,6 +509,7 @@ k_fedavg_sgd(const Seg* __restrict__ segs, int nseg, const double* __restrict__ 
   const Seg sg = segs[s];
   float* param = (float*)sg.out;
   float* mbuf = (float*)bufs[s];
+  float* sqb = OPT == 1 ? (float*)bufs2[s] : nullptr;
   const int64_t tl = tile - sg.tile_start;
   const int64_t base = tl * TILE;
   const void* const* in = ptrs + sg.ptr_base;
@@ -496,8 +522,9 @@ k_fedavg_sgd(const Seg* __restrict__ segs, int nseg, const double* __restrict__ 
     const int64_t boff = tl * sst + (int64_t)threadIdx.x * V * 4;
     // the parameter and momentum loads are issued first: their latency hides under the client stream
     u32x4 p4 = ld16<true>(param + e0);
-    u32x4 b4 = {0, 0, 0, 0};
+    u32x4 b4 = {0, 0, 0, 0}, q4 = {0, 0, 0, 0};
     if (read_buf) b4 = ld16<true>(mbuf + e0);
+    if (OPT == 1 && !(flags & SGD_FIRST)) q4 = ld16<true>(sqb + e0);
     float acc[1][V];
 #pragma unroll
     for (int v = 0; v < V; ++v) acc[0][v] = -0.0f;
@@ -509,11 +536,18 @@ k_fedavg_sgd(const Seg* __restrict__ segs, int nseg, const double* __restrict__ 
 #pragma unroll
     for (int v = 0; v < V; ++v) {
       float b = __uint_as_float(b4[v]);
-      p4[v] = __float_as_uint(sgd_update(__uint_as_float(p4[v]), acc[0][v], b, neg_lr, mom, damp1, wd, flags));
+      if constexpr (OPT == 1) {
+        float q = __uint_as_float(q4[v]);
+        p4[v] = __float_as_uint(rmsprop_update(__uint_as_float(p4[v]), acc[0][v], q, b, neg_lr, mom, wd, ra, flags));
+        q4[v] = __float_as_uint(q);
+      } else {
+        p4[v] = __float_as_uint(sgd_update(__uint_as_float(p4[v]), acc[0][v], b, neg_lr, mom, damp1, wd, flags));
+      }
       b4[v] = __float_as_uint(b);
     }
     __builtin_nontemporal_store(p4, (__attribute__((address_space(1))) u32x4*)(param + e0));
     if (flags & SGD_MOMENTUM) __builtin_nontemporal_store(b4, (__attribute__((address_space(1))) u32x4*)(mbuf + e0));
+    if constexpr (OPT == 1) __builtin_nontemporal_store(q4, (__attribute__((address_space(1))) u32x4*)(sqb + e0));
   } else {
     const int64_t end = min(base + TILE, sg.numel);
     for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
@@ -523,7 +557,13 @@ k_fedavg_sgd(const Seg* __restrict__ segs, int nseg, const double* __restrict__ 
         acc = accum<FA_DTYPE_F32, FA_MODE_MUL_W>(
             acc, term<FA_DTYPE_F32, FA_MODE_MUL_W>(T::ld1(in[i], pe), T::coef(coef[i]), d));
       float b = read_buf ? mbuf[e] : 0.f;
-      param[e] = sgd_update(param[e], acc, b, neg_lr, mom, damp1, wd, flags);
+      if constexpr (OPT == 1) {
+        float q = (flags & SGD_FIRST) ? 0.f : sqb[e];
+        param[e] = rmsprop_update(param[e], acc, q, b, neg_lr, mom, wd, ra, flags);
+        sqb[e] = q;
+      } else {
+        param[e] = sgd_update(param[e], acc, b, neg_lr, mom, damp1, wd, flags);
+      }
       if (flags & SGD_MOMENTUM) mbuf[e] = b;
     }
   }
@@ -1155,8 +1195,10 @@ namespace {
 int fedavg_sgd_impl(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, int32_t k,
                     const void* const* d_in, const double* coef, void* const* d_param, void* const* d_momentum,
                     double lr, double momentum, double dampening, double weight_decay, int nesterov,
-                    int first_step, void* hip_stream, int64_t sstr) {
+                    int first_step, void* hip_stream, int64_t sstr, int opt = 0,
+                    void* const* d_square_avg = nullptr, double alpha = 0.0, double eps = 0.0) {
   if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (opt == 1 && !d_square_avg) return fail(FA_ERR_INVALID, "fa_fedavg_rmsprop: square_avg buffers are NULL");
   if (k <= 0 || num_segments <= 0 || !seg_numel || !d_in || !coef || !d_param)
     return fail(FA_ERR_INVALID, "fa_fedavg_sgd: invalid arguments");
   if (momentum != 0.0 && !d_momentum) return fail(FA_ERR_INVALID, "fa_fedavg_sgd: momentum buffers are NULL");
@@ -1180,7 +1222,7 @@ int fedavg_sgd_impl(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel,
   const size_t coef_bytes = align16(sizeof(double) * k);
   const size_t buf_bytes = align16(sizeof(void*) * nseg);
   const size_t ptr_bytes = sizeof(void*) * (size_t)nseg * k;
-  const size_t bytes = seg_bytes + coef_bytes + buf_bytes + ptr_bytes;
+  const size_t bytes = seg_bytes + coef_bytes + 2 * buf_bytes + ptr_bytes;
   DeviceGuard g(ctx->device);
   if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
   hipStream_t st = (hipStream_t)hip_stream;
@@ -1191,14 +1233,17 @@ int fedavg_sgd_impl(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel,
   Seg* hs = (Seg*)h;
   double* hc = (double*)(h + seg_bytes);
   void** hb = (void**)(h + seg_bytes + coef_bytes);
-  const void** hp = (const void**)(h + seg_bytes + coef_bytes + buf_bytes);
+  void** hq = (void**)(h + seg_bytes + coef_bytes + buf_bytes);
+  const void** hp = (const void**)(h + seg_bytes + coef_bytes + 2 * buf_bytes);
   for (int i = 0; i < k; ++i) hc[i] = coef[i];
   int j = 0;
   int64_t t0 = 0;
   for (int s = 0; s < num_segments; ++s) {
     const int64_t n = seg_numel[s];
     if (n == 0) continue;
-    bool aligned = al16(d_param[s]) && (momentum == 0.0 || al16(d_momentum[s]));
+    if (opt == 1 && !d_square_avg[s]) return fail(FA_ERR_INVALID, "segment %d: square_avg NULL", s);
+    bool aligned = al16(d_param[s]) && (momentum == 0.0 || al16(d_momentum[s])) &&
+                   (opt != 1 || al16(d_square_avg[s]));
     for (int i = 0; i < k; ++i) {
       const void* p = d_in[(int64_t)s * k + i];
       hp[(int64_t)j * k + i] = p;
@@ -1207,6 +1252,7 @@ int fedavg_sgd_impl(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel,
     if (sstr && !aligned) return fail(FA_ERR_INVALID, "tiled inputs, parameter and momentum must be 16-byte aligned");
     hs[j] = Seg{n, t0, d_param[s], j * k, aligned ? 1 : 0};
     hb[j] = momentum != 0.0 ? d_momentum[s] : d_param[s];  // never dereferenced without momentum
+    hq[j] = opt == 1 ? d_square_avg[s] : d_param[s];       // never dereferenced for SGD
     t0 += (n + tile_elems - 1) / tile_elems;
     ++j;
   }
@@ -1215,10 +1261,19 @@ int fedavg_sgd_impl(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel,
   char* dv = (char*)slot->dev;
   const int flags = (momentum != 0.0 ? SGD_MOMENTUM : 0) | (nesterov ? SGD_NESTEROV : 0) |
                     (weight_decay != 0.0 ? SGD_WD : 0) | (first_step ? SGD_FIRST : 0);
-  hipLaunchKernelGGL((k_fedavg_sgd<8, true>), dim3((unsigned)tiles), dim3(kBlock), 0, st, (const Seg*)dv, nseg,
-                     (const double*)(dv + seg_bytes), (const void* const*)(dv + seg_bytes + coef_bytes + buf_bytes), k,
-                     (void* const*)(dv + seg_bytes + coef_bytes), (float)(-lr), (float)momentum,
-                     (float)(1.0 - dampening), (float)weight_decay, flags, sstr);
+  const RmsArgs ra{(float)alpha, (float)(1.0 - alpha), (float)eps};
+  const Seg* ds = (const Seg*)dv;
+  const double* dc = (const double*)(dv + seg_bytes);
+  void* const* db = (void* const*)(dv + seg_bytes + coef_bytes);
+  void* const* dq = (void* const*)(dv + seg_bytes + coef_bytes + buf_bytes);
+  const void* const* dp = (const void* const*)(dv + seg_bytes + coef_bytes + 2 * buf_bytes);
+  if (opt == 1)
+    hipLaunchKernelGGL((k_fedavg_sgd<8, true, 1>), dim3((unsigned)tiles), dim3(kBlock), 0, st, ds, nseg, dc, dp, k,
+                       db, (float)(-lr), (float)momentum, 1.0f, (float)weight_decay, flags, sstr, dq, ra);
+  else
+    hipLaunchKernelGGL((k_fedavg_sgd<8, true, 0>), dim3((unsigned)tiles), dim3(kBlock), 0, st, ds, nseg, dc, dp, k,
+                       db, (float)(-lr), (float)momentum, (float)(1.0 - dampening), (float)weight_decay, flags, sstr,
+                       dq, ra);
   FA_HIP(hipGetLastError());
   return release(slot, st);
 }
@@ -1230,6 +1285,14 @@ int fa_fedavg_sgd(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, i
                   int first_step, void* hip_stream) {
   return fedavg_sgd_impl(ctx, num_segments, seg_numel, k, d_in, coef, d_param, d_momentum, lr, momentum,
                          dampening, weight_decay, nesterov, first_step, hip_stream, 0);
+}
+
+int fa_fedavg_rmsprop(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, int32_t k,
+                      const void* const* d_in, const double* coef, void* const* d_param,
+                      void* const* d_square_avg, void* const* d_momentum, double lr, double alpha, double eps,
+                      double weight_decay, double momentum, int first_step, void* hip_stream) {
+  return fedavg_sgd_impl(ctx, num_segments, seg_numel, k, d_in, coef, d_param, d_momentum, lr, momentum, 0.0,
+                         weight_decay, 0, first_step, hip_stream, 0, 1, d_square_avg, alpha, eps);
 }
 
 int fa_fedavg_sgd_tiled(fa_ctx* ctx, int64_t n, int32_t k, const void* const* d_in, int64_t tile_stride,

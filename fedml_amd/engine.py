@@ -317,6 +317,48 @@ class AggEngine:
             float(weight_decay), int(bool(nesterov)), int(bool(first_step)), self._stream(stream))
         N.check(rc, "fa_fedavg_sgd")
 
+    def fedavg_rmsprop(self, segments: Sequence[Sequence[torch.Tensor]], coef: Sequence[float],
+                       params: Sequence[torch.Tensor], square_avgs: Sequence[torch.Tensor],
+                       momentum_bufs: Optional[Sequence[torch.Tensor]], lr: float, alpha: float = 0.99,
+                       eps: float = 1e-8, weight_decay: float = 0.0, momentum: float = 0.0,
+                       first_step: bool = True, stream=None) -> None:
+        """FedAvg + torch.optim.RMSprop server step in one pass (fa_fedavg_rmsprop); params, square
+        averages and momentum buffers (fp32, contiguous, on this device) are updated in place."""
+        k = len(segments[0]) if segments else 0
+        if k == 0:
+            raise ValueError("fedavg_rmsprop: no client tensors")
+        if len(coef) != k or len(params) != len(segments) or len(square_avgs) != len(params):
+            raise ValueError("fedavg_rmsprop: one coefficient per client, one parameter and state per segment")
+        in_ptrs, numels = [], []
+        for s, (seg, p, q) in enumerate(zip(segments, params, square_avgs)):
+            for t, what in ((p, "parameter"), (q, "square_avg")):
+                if t.dtype != torch.float32 or t.shape != p.shape:
+                    raise TypeError(f"fedavg_rmsprop: {what} {s} must be float32 of shape {tuple(p.shape)}")
+                _require_device(t, self.device, f"{what} {s}")
+            if len(seg) != k:
+                raise ValueError(f"segment {s}: {len(seg)} clients, expected {k}")
+            for i, t in enumerate(seg):
+                if t.dtype != torch.float32 or t.shape != p.shape:
+                    raise ValueError(f"segment {s} client {i}: must be float32 of shape {tuple(p.shape)}")
+                _require_device(t, self.device, f"segment {s} client {i}")
+                in_ptrs.append(t.data_ptr())
+            numels.append(p.numel())
+        mptr = None
+        if momentum != 0.0:
+            if momentum_bufs is None or len(momentum_bufs) != len(params):
+                raise ValueError("fedavg_rmsprop: momentum needs one buffer per parameter")
+            for b, p in zip(momentum_bufs, params):
+                if b.dtype != torch.float32 or b.shape != p.shape:
+                    raise ValueError("fedavg_rmsprop: momentum buffer dtype/shape mismatch")
+                _require_device(b, self.device, "momentum buffer")
+            mptr = N.ptr_array([b.data_ptr() for b in momentum_bufs])
+        rc = self._lib.fa_fedavg_rmsprop(
+            self._ctx, len(params), N.i64_array(numels), k, N.ptr_array(in_ptrs), N.f64_array(coef),
+            N.ptr_array([p.data_ptr() for p in params]), N.ptr_array([q.data_ptr() for q in square_avgs]), mptr,
+            float(lr), float(alpha), float(eps), float(weight_decay), float(momentum), int(bool(first_step)),
+            self._stream(stream))
+        N.check(rc, "fa_fedavg_rmsprop")
+
     def fedavg_sgd_tiled(self, buf: torch.Tensor, rows: Sequence[int], coef: Sequence[float], param: torch.Tensor,
                          momentum_buf: Optional[torch.Tensor], lr: float, momentum: float = 0.0,
                          dampening: float = 0.0, weight_decay: float = 0.0, nesterov: bool = False,

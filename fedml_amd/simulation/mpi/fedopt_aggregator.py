@@ -12,9 +12,12 @@ Reference semantics, reproduced bit-for-bit (fixtures g10_*):
 The MI355X path runs the average, the pseudo-gradient and the SGD update of every parameter in ONE
 kernel pass (``fa_fedavg_sgd``: reads the K client tensors, the parameter and its momentum buffer,
 writes the parameter and the buffer in place), instead of FedAvg + state_dict copies + a separate
-optimizer pass.  Supported server optimizer: ``sgd`` (momentum, dampening, nesterov, weight decay
-as torch.optim.SGD).  The reference instantiates its optimizer with ``momentum=`` for any name,
-which in practice limits it to SGD-like optimizers; others raise NotImplementedError here.
+optimizer pass.  Server optimizers: ``sgd`` (momentum, dampening, nesterov, weight decay as
+torch.optim.SGD; bit-exact) and ``rmsprop`` (torch.optim.RMSprop defaults alpha = 0.99, eps = 1e-8,
+centered = False; within 1e-6 relative -- the reference's CPU sqrt is MKL-VML, not correctly
+rounded).  The reference instantiates its optimizer with ``lr=`` and ``momentum=`` for any name
+(FedOptAggregator.py:49-54), so those two are the only ones it can construct (Adam, Adagrad, ...
+raise TypeError there); others raise NotImplementedError here.
 """
 from __future__ import annotations
 
@@ -34,8 +37,10 @@ class FedOptAggregator:
         self.aggregator = server_aggregator
         self.args = args
         name = str(getattr(args, "server_optimizer", "sgd")).lower()
-        if name != "sgd":
-            raise NotImplementedError(f"server_optimizer={name!r}: the fused FedOpt step implements 'sgd'")
+        if name not in ("sgd", "rmsprop"):
+            raise NotImplementedError(f"server_optimizer={name!r}: the fused FedOpt step implements 'sgd' and "
+                                      "'rmsprop' (the optimizers the reference can construct with momentum=)")
+        self.opt_name = name
         self.lr = float(args.server_lr)
         self.momentum = float(getattr(args, "server_momentum", 0.0) or 0.0)
         self.dampening = float(getattr(args, "server_dampening", 0.0) or 0.0)
@@ -45,6 +50,7 @@ class FedOptAggregator:
         self.sample_num_dict: Dict[int, int] = {}
         self.flag_client_model_uploaded_dict = {i: False for i in range(worker_num)}
         self.momentum_buffer: Dict[str, torch.Tensor] = {}
+        self.square_avg: Dict[str, torch.Tensor] = {}  # rmsprop state
 
     def get_global_model_params(self):
         return self.aggregator.get_model_params()
@@ -80,19 +86,26 @@ class FedOptAggregator:
         # global parameters: fused FedAvg + pseudo-gradient + SGD step, in place
         gparams = [p.data if on_gpu else p.data.to(eng.device) for _, p in named]
         segs = [[d[k].to(eng.device).contiguous() for d in dicts] for k, _ in named]
-        first = [k not in self.momentum_buffer for k, _ in named]
-        if self.momentum != 0.0:
-            for (k, p), g in zip(named, gparams):
-                if k not in self.momentum_buffer:
-                    self.momentum_buffer[k] = torch.empty_like(g)
+        first = [k not in (self.square_avg if self.opt_name == "rmsprop" else self.momentum_buffer) for k, _ in named]
+        rms = self.opt_name == "rmsprop"
+        for (k, p), g in zip(named, gparams):
+            if self.momentum != 0.0 and k not in self.momentum_buffer:
+                self.momentum_buffer[k] = torch.empty_like(g)
+            if rms and k not in self.square_avg:
+                self.square_avg[k] = torch.empty_like(g)
         for flag in (True, False):
             idx = [j for j, f in enumerate(first) if f == flag]
             if not idx:
                 continue
-            eng.fedavg_sgd([segs[j] for j in idx], w, [gparams[j] for j in idx],
-                           [self.momentum_buffer[named[j][0]] for j in idx] if self.momentum != 0.0 else None,
-                           self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov,
-                           first_step=flag)
+            mbufs = [self.momentum_buffer[named[j][0]] for j in idx] if self.momentum != 0.0 else None
+            if rms:
+                eng.fedavg_rmsprop([segs[j] for j in idx], w, [gparams[j] for j in idx],
+                                   [self.square_avg[named[j][0]] for j in idx], mbufs, self.lr,
+                                   weight_decay=self.weight_decay, momentum=self.momentum, first_step=flag)
+            else:
+                eng.fedavg_sgd([segs[j] for j in idx], w, [gparams[j] for j in idx], mbufs,
+                               self.lr, self.momentum, self.dampening, self.weight_decay, self.nesterov,
+                               first_step=flag)
         if not on_gpu:
             with torch.no_grad():
                 for (_, p), g in zip(named, gparams):

@@ -170,6 +170,23 @@ int fa_fedavg_sgd(fa_ctx *ctx, int32_t num_segments, const int64_t *seg_numel, i
                   double weight_decay, int nesterov, int first_step, void *hip_stream);
 /* fa_fedavg_sgd for ONE flat parameter over tile-interleaved inputs (addressing as
  * fa_weighted_sum_tiled); d_param / d_momentum are flat, 16-byte aligned. */
+/*
+ * FedOpt with server_optimizer = "rmsprop" (torch.optim.RMSprop, centered=False; the reference's
+ * OptRepo passes lr and momentum, alpha = 0.99 and eps = 1e-8 are torch's defaults): per element
+ *   g  = param - avg;  g = fma(param, weight_decay, g) if weight_decay != 0
+ *   sq = fma((1 - alpha) * g, g, sq * alpha);  den = sqrt(sq) + eps
+ *   momentum: m = m * momentum + g / den;  param = fma(m, -lr, param)
+ *   else:     param = param + (-lr * g) / den
+ * d_square_avg[s] (and d_momentum[s] when momentum != 0) updated in place; first_step treats them
+ * as zero (torch's initial state).  The reference's CPU sqrt is MKL-VML (not correctly rounded),
+ * so this is within 1e-6 relative of it, not bit-exact.
+ */
+int fa_fedavg_rmsprop(fa_ctx *ctx, int32_t num_segments, const int64_t *seg_numel, int32_t k,
+                      const void *const *d_in, const double *coef, void *const *d_param,
+                      void *const *d_square_avg, void *const *d_momentum, double lr, double alpha,
+                      double eps, double weight_decay, double momentum, int first_step,
+                      void *hip_stream);
+
 int fa_fedavg_sgd_tiled(fa_ctx *ctx, int64_t n, int32_t k, const void *const *d_in,
                         int64_t tile_stride, const double *coef, void *d_param, void *d_momentum,
                         double lr, double momentum, double dampening, double weight_decay,

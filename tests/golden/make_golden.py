@@ -554,7 +554,7 @@ def cases_fedopt():
             ("_instantiate_opt", "get_model_params", "get_global_model_params", "set_global_model_params",
              "add_local_trained_result", "check_whether_all_receive", "aggregate", "set_model_global_grads")}
 
-    for opt_name, lr, mom in (("sgd", 0.7, 0.9), ("sgd", 1.0, 0.0)):
+    for opt_name, lr, mom in (("sgd", 0.7, 0.9), ("sgd", 1.0, 0.0), ("rmsprop", 0.01, 0.9), ("rmsprop", 0.05, 0.0)):
         torch.manual_seed(5)
         model = torch.nn.Sequential(torch.nn.Linear(33, 17), torch.nn.BatchNorm1d(17), torch.nn.Linear(17, 5))
         with torch.no_grad():

@@ -256,10 +256,13 @@ def test_arena_fused_fedavg_seq_golden():
     assert_dict_bits(cpu(got), expected_dicts(meta, arr)[0], "fused fedavg_seq")
 
 
-@pytest.mark.parametrize("name", ["g10_fedopt_sgd_lr0.7_m0.9", "g10_fedopt_sgd_lr1.0_m0.0"])
+@pytest.mark.parametrize("name", ["g10_fedopt_sgd_lr0.7_m0.9", "g10_fedopt_sgd_lr1.0_m0.0",
+                                  "g10_fedopt_rmsprop_lr0.01_m0.9", "g10_fedopt_rmsprop_lr0.05_m0.0"])
 @pytest.mark.parametrize("where", ["cuda", "cpu"])
 def test_fedopt_fused_server_step_golden(name, where):
-    """FedOptAggregator (fused FedAvg + SGD step) == the reference's FedOptAggregator, 3 rounds."""
+    """FedOptAggregator (fused FedAvg + optimizer step) == the reference's FedOptAggregator, 3 rounds:
+    bit-exact for SGD; for RMSprop within 1e-6 relative (normwise per tensor) -- the reference's
+    CPU sqrt is MKL-VML, not correctly rounded -- and the buffers (plain averages) bit-exact."""
     from golden_io import np_to_tensor
     from refcases import fedopt_expected
     from fedml_amd.simulation.mpi.fedopt_aggregator import FedOptAggregator
@@ -287,5 +290,70 @@ def test_fedopt_fused_server_step_golden(name, where):
             fo.add_local_trained_result(i, OrderedDict((k, np_to_tensor(arr[f"r{r}_x{i}__{k}"], dt))
                                                        for k, dt in zip(meta["keys"], meta["dtypes"])), rd["n"][i])
         assert fo.check_whether_all_receive()
-        got = fo.aggregate()
-        assert_dict_bits(cpu(got), exp, f"{name} round {r}")
+        got = cpu(fo.aggregate())
+        if meta["server_optimizer"] == "sgd":
+            assert_dict_bits(got, exp, f"{name} round {r}")
+            continue
+        params = set(meta["params"])
+        for k in exp:
+            if k in params:
+                rel = float((got[k].double() - exp[k].double()).norm() / exp[k].double().norm())
+                assert rel <= 1e-6, (name, r, k, rel)
+            else:
+                assert_dict_bits(OrderedDict([(k, got[k])]), OrderedDict([(k, exp[k])]), f"{name} round {r}")
+
+
+def _rmsprop_cr(p, avg, sq, buf, lr, alpha, eps, wd, momentum):
+    """torch.optim.RMSprop's CPU op sequence (rmsprop.py _single_tensor_rmsprop, ATen's contracted
+    addcmul / addcdiv) with a CORRECTLY ROUNDED sqrt, float32 via exact float64 emulation."""
+    f, d = (lambda x: x.float()), (lambda x: x.double())
+    g = p - avg
+    if wd:
+        g = f(d(p) * wd32(wd) + d(g))
+    s1 = torch.tensor(1 - alpha, dtype=torch.float32)
+    sq = f(d(s1 * g) * d(g) + d(sq * torch.tensor(alpha, dtype=torch.float32)))
+    den = f(d(sq).sqrt()) + torch.tensor(eps, dtype=torch.float32)
+    nlr = torch.tensor(-lr, dtype=torch.float32)
+    if momentum:
+        buf = buf * torch.tensor(momentum, dtype=torch.float32) + g / den
+        p = f(d(buf) * d(nlr) + d(p))
+    else:
+        p = p + (nlr * g) / den
+    return p, sq, buf
+
+
+def wd32(wd):
+    return float(torch.tensor(wd, dtype=torch.float32))
+
+
+@pytest.mark.parametrize("momentum,wd", [(0.0, 0.0), (0.9, 0.0), (0.5, 1e-3)])
+def test_fedavg_rmsprop_vs_torch_optimizer(momentum, wd):
+    """fa_fedavg_rmsprop over 4 rounds, 1 M parameters: bit-exact to torch.optim.RMSprop's op
+    sequence with a correctly rounded sqrt, and within 1e-6 relative (normwise) of
+    torch.optim.RMSprop itself on this host's CPU (whose sqrt is MKL-VML, not correctly rounded)."""
+    from oracle import orc
+    from fedml_amd.engine import get_engine
+    eng = get_engine(0)
+    g = torch.Generator().manual_seed(11)
+    n, K, lr, alpha, eps = 1 << 20, 6, 0.01, 0.99, 1e-8
+    p_cpu = torch.nn.Parameter(torch.randn(n, generator=g))
+    opt = torch.optim.RMSprop([p_cpu], lr=lr, momentum=momentum, weight_decay=wd)
+    p_dev = p_cpu.detach().clone().cuda()
+    p_cr, sq_cr, buf_cr = p_cpu.detach().clone(), torch.zeros(n), torch.zeros(n)
+    sq = torch.empty(n, device="cuda:0")
+    buf = torch.empty(n, device="cuda:0")
+    for r in range(4):
+        xs = [p_cr + 0.1 * torch.randn(n, generator=g) for _ in range(K)]
+        w = [(i + 1) / (K * (K + 1) / 2) for i in range(K)]
+        avg = orc.weighted_sum(xs, 0, w)
+        opt.zero_grad()
+        p_cpu.grad = p_cpu.detach() - avg
+        opt.step()
+        p_cr, sq_cr, buf_cr = _rmsprop_cr(p_cr, avg, sq_cr, buf_cr, lr, alpha, eps, wd, momentum)
+        eng.fedavg_rmsprop([[x.cuda() for x in xs]], w, [p_dev], [sq], [buf] if momentum else None, lr,
+                           weight_decay=wd, momentum=momentum, first_step=(r == 0))
+        got = p_dev.cpu()
+        assert torch.equal(got.view(torch.int32), p_cr.view(torch.int32)), r
+        exp = p_cpu.detach()
+        rel = float((got.double() - exp.double()).norm() / exp.double().norm())
+        assert rel <= 1e-6, (r, rel)

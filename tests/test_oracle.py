@@ -33,7 +33,7 @@ class _Orc:
 
 
 GENERIC = aggregation_cases()
-FEDOPT = [p for p in CASES if "fedopt" in p]
+FEDOPT = [p for p in CASES if "fedopt_sgd" in p]  # the C oracle restates SGD (RMSprop: GPU test, 1e-6)
 
 
 @pytest.mark.parametrize("path", GENERIC, ids=lambda p: os.path.basename(p)[:-4])
