@@ -13,7 +13,10 @@ One process per GPU (torch.distributed, backend "nccl" = RCCL).  Rank r holds cl
                       cross-rank summation order is RCCL's, so the result matches the sequential
                       reference normwise (~1e-7), not bit-for-bit;
     "all_reduce"      the same, result on every rank;
-    "reduce_scatter"  the same, result sharded (rank r owns elements [r*P/G, (r+1)*P/G));
+    "reduce_scatter"  the same, result sharded: rank r owns elements [r*S, min((r+1)*S, P)) with
+                      S = P/G rounded up to whole tiles -- the least xGMI traffic (each link
+                      carries 1/G of a partial per direction), and the global model is already
+                      partitioned for a sharded broadcast;
     "ordered"         gather the G partials to ``dst`` and sum them there IN RANK ORDER with the
                       engine's SUM mode: bit-identical to the reference's two-level reduces --
                       fedavg_seq (worker partials, then an ordered sum; FedAVGAggregator.py:201-236)
@@ -168,9 +171,10 @@ class GroupReducer:
         works = []
         gathered = []
         if self.collective == "reduce_scatter":
-            if n % self.world or (n // self.world) % align:
-                raise ValueError("reduce_scatter needs P divisible by the world size (and shards of whole tiles)")
-            S = n // self.world
+            # shards of S elements (whole tiles), the last one zero-padded past n: rank r owns the
+            # global model's elements [r*S, min((r+1)*S, n))
+            S = -(-n // (self.world * align)) * align
+            stage = out if out.numel() >= S * self.world else torch.empty(S * self.world, dtype=out.dtype, device=dev)
             shard = torch.empty(S, dtype=out.dtype, device=dev)
             # chunk-major staging: chunk [a, b) of every rank's shard is laid out contiguously
             # (rank-major inside the chunk), which is what reduce_scatter_tensor consumes
@@ -178,17 +182,21 @@ class GroupReducer:
                 L = b - a
                 base = self.world * a
                 for r in range(self.world):
-                    lo = r * S + a
-                    local(out[base + r * L: base + (r + 1) * L], lo, lo + L)
+                    lo, hi = r * S + a, min(r * S + b, n)
+                    dstv = stage[base + r * L: base + (r + 1) * L]
+                    if hi > lo:
+                        local(dstv[:hi - lo], lo, hi)
+                    if hi - lo < L:
+                        dstv[max(hi - lo, 0):].zero_()
                 if self.world > 1:
-                    works.append(dist.reduce_scatter_tensor(shard[a:b], out[base: base + self.world * L],
+                    works.append(dist.reduce_scatter_tensor(shard[a:b], stage[base: base + self.world * L],
                                                             op=dist.ReduceOp.SUM, group=self.group,
                                                             async_op=True))
                 else:
-                    shard[a:b].copy_(out[base: base + L])
+                    shard[a:b].copy_(stage[base: base + L])
             for w in works:
                 w.wait()
-            return shard
+            return shard[:max(0, min(S, n - self.rank * S))]
         for a, b in chunk_bounds(n, self.chunks, align):
             part = out[a:b]
             local(part, a, b)

@@ -137,6 +137,37 @@ def test_reduce_scatter_gloo_world2():
     _spawn(_case_reduce_scatter)
 
 
+def _case_reduce_scatter_ragged(rank, world):
+    """P not divisible by the world size: padded shards, rank r owns [r*S, min((r+1)*S, P))."""
+    from oracle import orc
+    from fedml_amd.distributed.group_reduce import GroupReducer
+    K, P = 4, 4001
+    xs, counts = _clients(K, P, seed=6)
+    N = sum(counts)
+    mine = [rank * 2, rank * 2 + 1]
+    exp = orc.weighted_sum([orc.weighted_sum([xs[2 * r], xs[2 * r + 1]], 0, [counts[2 * r] / N, counts[2 * r + 1] / N])
+                            for r in range(world)], 2)
+    for chunks in (1, 3):
+        red = GroupReducer(collective="reduce_scatter", chunks=chunks, local_sum=_oracle_sum)
+        shard = red.fedavg([xs[i] for i in mine], [counts[i] / N for i in mine])
+        S = -(-P // world)
+        assert _bits(shard, exp[rank * S:min((rank + 1) * S, P)]), chunks
+    # tiled, shards of whole 1024-element tiles, P = 10 tiles + 77
+    P2 = 1024 * 10 + 77
+    xs2 = [x[:P2].contiguous() for x in _clients(K, P2, seed=7)[0]]
+    exp2 = orc.weighted_sum([orc.weighted_sum([xs2[2 * r], xs2[2 * r + 1]], 0,
+                                              [counts[2 * r] / N, counts[2 * r + 1] / N]) for r in range(world)], 2)
+    red = GroupReducer(collective="reduce_scatter", chunks=2, local_sum=_oracle_sum)
+    shard = red.fedavg_tiled(_OracleTiledEngine(), _tiled_buf([xs2[i] for i in mine]), [0, 1],
+                             [counts[i] / N for i in mine], P2)
+    S = -(-P2 // (world * 1024)) * 1024
+    assert _bits(shard, exp2[rank * S:min((rank + 1) * S, P2)])
+
+
+def test_reduce_scatter_ragged_gloo_world2():
+    _spawn(_case_reduce_scatter_ragged)
+
+
 # ------------------------------------------------------------------------------ gossip
 def _case_gossip(rank, world):
     from oracle import orc
