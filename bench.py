@@ -235,7 +235,9 @@ def wl_metric(args, eng, rank, world, timer):
         xs = None
     else:
         xs = make_arena_rows(mine, P) if args.layout == "arena" else make_flat_clients(mine, P)
-    out = torch.empty(P, device="cuda")
+    # reduce_scatter stages every rank's whole-tile shard: room for them, allocated once
+    S = -(-P // (world * 1024)) * 1024
+    out = torch.empty(max(P, S * world) if world > 1 and args.collective == "reduce_scatter" else P, device="cuda")
     if world > 1:
         from fedml_amd.distributed.group_reduce import GroupReducer
 
@@ -247,6 +249,10 @@ def wl_metric(args, eng, rank, world, timer):
             def weighted_sum_tiled(self, *a, **kw):
                 with timer:
                     return eng.weighted_sum_tiled(*a, **kw)
+
+            def weighted_sum_tiled_multi(self, *a, **kw):
+                with timer:
+                    return eng.weighted_sum_tiled_multi(*a, **kw)
         red = GroupReducer(collective=args.collective, chunks=args.chunks, local_sum=timed_sum,
                            stream=masked_stream(eng, args))
 

@@ -1172,6 +1172,15 @@ int grouped_impl(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t k, const v
 }
 }  // namespace
 
+int fa_weighted_sum_tiled_multi(fa_ctx* ctx, int dtype, int mode, int32_t num_segments, const int64_t* seg_numel,
+                                int32_t k, const void* const* d_in, int64_t tile_stride, const double* coef,
+                                double divisor, void* const* d_out, void* hip_stream) {
+  if (tile_stride <= 0 || tile_stride % FA_TILE_BYTES)
+    return fail(FA_ERR_INVALID, "tile_stride must be a positive multiple of %d (got %lld)", FA_TILE_BYTES,
+                (long long)tile_stride);
+  return wsum_impl(ctx, dtype, mode, num_segments, seg_numel, k, d_in, coef, divisor, d_out, hip_stream, tile_stride);
+}
+
 int fa_weighted_sum_grouped(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t k, const void* const* d_in,
                             const double* coef, double divisor, int32_t num_groups, const int32_t* group_ptr,
                             int group_mode, const double* group_coef, const double* group_divisor,

@@ -140,7 +140,13 @@ class GroupReducer:
             if a % E:
                 raise ValueError("fedavg_tiled: chunk does not start on a tile boundary")
             engine.weighted_sum_tiled(buf, rows, MUL_W, w, n=b - a, t0=a // E, out=part)
-        return self._run_n(n, buf.dtype, buf.device, local, out, MUL_W, align=E)
+
+        local_multi = None
+        if hasattr(engine, "weighted_sum_tiled_multi"):  # reduce_scatter: a chunk's G slices, one launch
+            def local_multi(pieces):
+                engine.weighted_sum_tiled_multi(buf, rows, MUL_W, w, 1.0, [(lo, hi) for _, lo, hi in pieces],
+                                                [p for p, _, _ in pieces])
+        return self._run_n(n, buf.dtype, buf.device, local, out, MUL_W, align=E, local_multi=local_multi)
 
     def sum(self, xs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None):
         """Plain global sum (FedAvg_seq / FedDyn branches)."""
@@ -152,22 +158,22 @@ class GroupReducer:
     def _run(self, flat, local, out, mode):
         return self._run_n(flat[0].numel(), flat[0].dtype, flat[0].device, local, out, mode)
 
-    def _run_n(self, n, dtype, dev, local, out, mode, align: int = 1):
+    def _run_n(self, n, dtype, dev, local, out, mode, align: int = 1, local_multi=None):
         if out is None:
             out = torch.empty(n, dtype=torch.float32 if dtype == torch.int64 and mode != SUM else dtype, device=dev)
         if self.stream is None:
-            return self._run_body(n, dev, local, out, align)
+            return self._run_body(n, dev, local, out, align, local_multi)
         caller = torch.cuda.current_stream(dev)
         self.stream.wait_stream(caller)      # inputs / out were produced on the caller's stream
         out.record_stream(self.stream)
         with torch.cuda.stream(self.stream):
-            res = self._run_body(n, dev, local, out, align)
+            res = self._run_body(n, dev, local, out, align, local_multi)
         caller.wait_stream(self.stream)      # the result is consumed on the caller's stream
         if res is not out:
             res.record_stream(caller)        # allocated on self.stream, used on the caller's
         return res
 
-    def _run_body(self, n, dev, local, out, align):
+    def _run_body(self, n, dev, local, out, align, local_multi=None):
         works = []
         gathered = []
         if self.collective == "reduce_scatter":
@@ -181,13 +187,19 @@ class GroupReducer:
             for a, b in chunk_bounds(S, self.chunks, align):
                 L = b - a
                 base = self.world * a
+                pieces = []
                 for r in range(self.world):
                     lo, hi = r * S + a, min(r * S + b, n)
                     dstv = stage[base + r * L: base + (r + 1) * L]
                     if hi > lo:
-                        local(dstv[:hi - lo], lo, hi)
+                        pieces.append((dstv[:hi - lo], lo, hi))
                     if hi - lo < L:
                         dstv[max(hi - lo, 0):].zero_()
+                if local_multi is not None:  # every rank's slice of the chunk in ONE launch
+                    local_multi(pieces)
+                else:
+                    for dstv, lo, hi in pieces:
+                        local(dstv, lo, hi)
                 if self.world > 1:
                     works.append(dist.reduce_scatter_tensor(shard[a:b], stage[base: base + self.world * L],
                                                             op=dist.ReduceOp.SUM, group=self.group,

@@ -225,6 +225,35 @@ class AggEngine:
         N.check(rc, "fa_weighted_sum_tiled")
         return out
 
+    def weighted_sum_tiled_multi(self, buf: torch.Tensor, rows: Sequence[int], mode: int,
+                                 coef: Optional[Sequence[float]], divisor: float,
+                                 ranges: Sequence[Tuple[int, int]], outs: Sequence[torch.Tensor],
+                                 stream=None) -> None:
+        """Several element ranges [lo, hi) (tile-aligned starts) of a tiled arena group reduced in ONE
+        launch (fa_weighted_sum_tiled_multi) into ``outs`` (flat, hi - lo elements each)."""
+        ntile, cap, E = buf.shape
+        k = len(rows)
+        if mode != SUM and (coef is None or len(coef) != k):
+            raise ValueError("weighted_sum_tiled_multi: need one coefficient per row")
+        odt = out_dtype(buf.dtype, mode)
+        if len(ranges) != len(outs) or not ranges:
+            raise ValueError("weighted_sum_tiled_multi: one output per range")
+        ptrs, numels = [], []
+        for (lo, hi), o in zip(ranges, outs):
+            if lo % E:
+                raise ValueError("weighted_sum_tiled_multi: ranges must start on a tile")
+            n, p, stride = self._tiled_args(buf, rows, lo // E, hi - lo, "weighted_sum_tiled_multi")
+            if o.dtype != odt or o.numel() != n:
+                raise ValueError(f"weighted_sum_tiled_multi: output must be {odt} with {n} elements")
+            _require_device(o, self.device, "output")
+            ptrs.extend(p)
+            numels.append(n)
+        rc = self._lib.fa_weighted_sum_tiled_multi(
+            self._ctx, DTYPE_CODE[buf.dtype], int(mode), len(ranges), N.i64_array(numels), k,
+            N.ptr_array(ptrs), cap * N.TILE_BYTES, N.f64_array(coef) if coef is not None else None, float(divisor),
+            N.ptr_array([o.data_ptr() for o in outs]), self._stream(stream))
+        N.check(rc, "fa_weighted_sum_tiled_multi")
+
     def weighted_sum_grouped_tiled(self, buf: torch.Tensor, rows: Sequence[int], mode: int,
                                    coef: Optional[Sequence[float]], divisor: float, group_ptr: Sequence[int],
                                    group_mode: int, group_coef: Optional[Sequence[float]] = None,

@@ -125,6 +125,14 @@ int fa_weighted_sum_multi(fa_ctx *ctx, int dtype, int mode, int32_t num_segments
 int fa_weighted_sum_tiled(fa_ctx *ctx, int dtype, int mode, int64_t n, int32_t k,
                           const void *const *d_in, int64_t tile_stride, const double *coef,
                           double divisor, void *d_out, void *hip_stream);
+/* Several element ranges of one tiled arena in ONE launch (e.g. the per-rank slices of a
+ * reduce-scatter chunk): segment s has seg_numel[s] elements, client i's input at d_in[s*k + i]
+ * (= base + (t0_s * capacity + r_i) * FA_TILE_BYTES for a range starting at tile t0_s), output
+ * d_out[s]; every segment shares tile_stride.  Same arithmetic as fa_weighted_sum_tiled. */
+int fa_weighted_sum_tiled_multi(fa_ctx *ctx, int dtype, int mode, int32_t num_segments,
+                                const int64_t *seg_numel, int32_t k, const void *const *d_in,
+                                int64_t tile_stride, const double *coef, double divisor,
+                                void *const *d_out, void *hip_stream);
 
 /*
  * Two-level (grouped) reduction in one pass, one flat vector per client:

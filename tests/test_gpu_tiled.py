@@ -123,6 +123,27 @@ def test_tiled_chunks_and_row_subset(eng):
     assert bits_equal(out.cpu(), exp)
 
 
+@pytest.mark.parametrize("variant", [0, 4, 6])
+def test_tiled_multi_ranges_one_launch(eng, variant):
+    """fa_weighted_sum_tiled_multi: several tile-aligned ranges (a reduce-scatter chunk's per-rank
+    slices, the last one ragged) in one launch == the whole reduction, every kernel variant."""
+    cap, n = 9, 1024 * 50 + 333
+    xs = _inputs(torch.float32, cap, n, 21)
+    buf = tiled_buf(xs)
+    rows = [8, 2, 4, 0]
+    w = [0.4, 0.1, 0.3, 0.2]
+    exp = eng.weighted_sum([xs[r].cuda() for r in rows], MUL_W, w).cpu()
+    ranges = [(0, 7 * 1024), (13 * 1024, 20 * 1024 + 5), (26 * 1024, n), (7 * 1024, 13 * 1024)]
+    outs = [torch.empty(hi - lo, device="cuda:0") for lo, hi in ranges]
+    try:
+        eng.set_variant(variant)
+        eng.weighted_sum_tiled_multi(buf, rows, MUL_W, w, 1.0, ranges, outs)
+    finally:
+        eng.set_variant(0)
+    for (lo, hi), o in zip(ranges, outs):
+        assert bits_equal(o.cpu(), exp[lo:hi]), (lo, hi)
+
+
 def test_tiled_rejects_bad_arguments(eng):
     from fedml_amd import _native as N
     buf = torch.zeros(4, 3, 1024, device="cuda:0")
