@@ -1002,7 +1002,11 @@ int wsum_impl(fa_ctx* ctx, int dtype, int mode, int32_t num_segments, const int6
   if (mode != FA_MODE_SUM && !coef) return fail(FA_ERR_INVALID, "coef is NULL for a weighted mode");
 
   // count non-empty segments and tiles
-  const int64_t tile_elems = (int64_t)kBlock * V * kVariants[ctx->variant].S;
+  // variant 0 = automatic: few clients per launch (K <= 16, e.g. one GPU's share at N = 8) leave a
+  // lane only 2 load groups, so two 16-byte vectors per lane (U = 8, S = 2, variant 5) keep more
+  // bytes in flight: measured K = 16 x 125 M tiled 1.46 -> 1.37 ms; K >= 32 keeps (8, 1)
+  const int variant = ctx->variant ? ctx->variant : (k <= 16 ? 5 : 0);
+  const int64_t tile_elems = (int64_t)kBlock * V * kVariants[variant].S;
   int nseg = 0;
   int64_t tiles = 0;
   for (int s = 0; s < num_segments; ++s) {
@@ -1058,11 +1062,11 @@ int wsum_impl(fa_ctx* ctx, int dtype, int mode, int32_t num_segments, const int6
   const void* const* dp = (const void* const*)(d + seg_bytes + coef_bytes);
 
   switch (dtype) {
-    case FA_DTYPE_F32: rc = dispatch_mode<FA_DTYPE_F32>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor, sstr); break;
-    case FA_DTYPE_BF16: rc = dispatch_mode<FA_DTYPE_BF16>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor, sstr); break;
-    case FA_DTYPE_F16: rc = dispatch_mode<FA_DTYPE_F16>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor, sstr); break;
-    case FA_DTYPE_F64: rc = dispatch_mode<FA_DTYPE_F64>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor, sstr); break;
-    case FA_DTYPE_I64: rc = dispatch_mode<FA_DTYPE_I64>(mode, ctx->variant, tiles, st, ds, nseg, dc, dp, k, divisor, sstr); break;
+    case FA_DTYPE_F32: rc = dispatch_mode<FA_DTYPE_F32>(mode, variant, tiles, st, ds, nseg, dc, dp, k, divisor, sstr); break;
+    case FA_DTYPE_BF16: rc = dispatch_mode<FA_DTYPE_BF16>(mode, variant, tiles, st, ds, nseg, dc, dp, k, divisor, sstr); break;
+    case FA_DTYPE_F16: rc = dispatch_mode<FA_DTYPE_F16>(mode, variant, tiles, st, ds, nseg, dc, dp, k, divisor, sstr); break;
+    case FA_DTYPE_F64: rc = dispatch_mode<FA_DTYPE_F64>(mode, variant, tiles, st, ds, nseg, dc, dp, k, divisor, sstr); break;
+    case FA_DTYPE_I64: rc = dispatch_mode<FA_DTYPE_I64>(mode, variant, tiles, st, ds, nseg, dc, dp, k, divisor, sstr); break;
   }
   if (rc) return rc;
   FA_HIP(hipGetLastError());
