@@ -17,6 +17,8 @@
 #include <algorithm>
 #include <climits>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 
 #include "fa_internal.h"
@@ -267,38 +269,66 @@ int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t*
 // Krum's pairwise squared distances (krum_defense.py:52-66): D[i][j] = sum_e (x_i[e] - x_j[e])^2
 // over the clients' weight vectors, float32 inputs, every pair (i < j) in ONE pass over the data.
 // A workgroup stages a chunk of coordinates of all K clients in LDS (transposed [e][client],
-// so 4 clients of one coordinate are one 16-byte LDS read), and each thread owns up to TPT 4x4
-// client-pair tiles (upper triangle) -- 16 differences per 2 LDS reads -- over a slice of the
-// chunk's coordinates (pair_split).  Sums: float32 within a chunk slice (<= kPE terms), float64
-// across chunks.
+// so 4 clients of one coordinate are one 16-byte LDS read), and each thread owns one 4x4
+// client-pair tile (upper triangle) -- 16 differences per 2 LDS reads, packed fp32 -- over a slice
+// of the chunk's coordinates (pair_split).  Software pipeline: chunk i is computed from one LDS
+// buffer while chunk i + 1 (already in registers) is written to the other and chunk i + 2 is loaded
+// from HBM -- one barrier per chunk, HBM latency behind the pair loop (K = 8 / 32 / 128: 0.22 /
+// 0.90 / 10.2 ms -> 0.12 / 0.62 / 6.9 ms over the single-buffered, load-then-compute form whose
+// waves sat 60% of their cycles in s_waitcnt / barriers).  Sums: float32 over runs of <= kPE
+// coordinates, float64 across runs.
 // Per-block float64 partials of the upper triangle go to a scratch buffer and a second kernel
-// adds them in block order (deterministic).  VALU-bound for large K (K^2/2 pair updates per
-// coordinate against 4K bytes).
+// adds them in block order (deterministic).
 namespace {
 
-constexpr int kPE = 64;       // nominal coordinates per LDS chunk (see pair_split)
+constexpr int kPE = 64;       // longest float32 run (coordinates); small-K esplit cap
 constexpr int kMaxPairK = 128;
+constexpr int kMaxPairThreads = 1024;
+constexpr int kNP = 8;             // coordinates of one client staged per thread and chunk
 
-// Work split of k_pairdist: ntiles 4x4 pair tiles; with ntiles <= kBlock every thread owns one
-// tile and one of `esplit` coordinate slices (esplit = kBlock / ntiles, so e.g. K = 32 keeps 252 of
-// 256 threads busy, not 144 as with a power-of-two split), `pe` = esplit * ceil(kPE / esplit)
-// coordinates per chunk; otherwise TPT tiles per thread over kPE coordinates.
-struct PairSplit { int kp, nb, ntiles, tpt, esplit, pe, nblocks; };
+// Work split of k_pairdist: ntiles 4x4 pair tiles (upper triangle), one per thread, times `esplit`
+// coordinate slices: a workgroup is ntiles * esplit threads (<= 1024; K <= 128 -> ntiles <= 528).
+// Staging: nthreads / kp threads per client, kNP coordinates each, so a chunk is
+// pe = (nthreads / kp) * kNP coordinates.  ntiles <= 128: esplit = 256 / ntiles (e.g. K = 32 keeps
+// 252 of 256 threads busy); larger: see below (measured, K = 100: 3 x 325 threads, 72-coordinate
+// chunks, 3.9 ms vs 5.1 ms with 325 threads and 24-coordinate chunks).
+struct PairSplit { int kp, nb, ntiles, esplit, nthreads, pe, nblocks; };
 PairSplit pair_split(int k) {
   PairSplit q;
   q.kp = (k + 3) & ~3;
   q.nb = q.kp / 4;
   q.ntiles = q.nb * (q.nb + 1) / 2;
-  q.tpt = (q.ntiles + kBlock - 1) / kBlock;
-  q.esplit = q.tpt == 1 ? std::min(kPE, kBlock / q.ntiles) : 1;
-  // coordinates per slice: as many as a <= 32 KiB chunk holds, 8..kPE (measured sweep, K = 8 / 32:
-  // 0.29 / 0.92 ms; larger chunks cost resident workgroups, smaller ones more barriers and float64
-  // conversions per coordinate)
-  const int per = std::max(8, std::min(kPE, (32 << 10) / (q.esplit * (q.kp + 4) * 4)));
+  if (q.ntiles <= 128) {
+    q.esplit = std::min(kPE, kBlock / q.ntiles);
+  } else {
+    // chunks of >= 64 coordinates (pe grows with the staging threads per client, nthreads / kp),
+    // then the fewest threads that keep >= 90% of the last wave's lanes; no such split (K > 112):
+    // the largest chunk
+    int best = -1, best_pe = -1;
+    for (int e = 1; e * q.ntiles <= kMaxPairThreads; ++e) {
+      const int th = e * q.ntiles, pe = (th / q.kp) * kNP;
+      const bool full = (double)th / (64.0 * ((th + 63) / 64)) >= 0.9;
+      if (pe >= 64 && full) { best = e; break; }
+      if (pe > best_pe) { best_pe = pe; q.esplit = e; }
+    }
+    if (best > 0) q.esplit = best;
+  }
+  // measurement override (tools/krum_split.sh sweeps): FA_PAIR_SPLIT="esplit"
+  static const char* ov = getenv("FA_PAIR_SPLIT");
+  const int oe = ov ? atoi(ov) : 0;
+  if (oe >= 1 && oe * q.ntiles <= kMaxPairThreads && (oe == 1 || 16 * 8 * q.ntiles <= 65536)) q.esplit = oe;
+  q.nthreads = q.ntiles * q.esplit;
+  if (q.nthreads < q.kp) {  // every client needs a staging thread (small K: more slices)
+    q.esplit = (q.kp + q.ntiles - 1) / q.ntiles;
+    q.nthreads = q.ntiles * q.esplit;
+  }
+  // chunk: kNP coordinates per staging thread, nthreads / kp staging threads per client
+  q.pe = (q.nthreads / q.kp) * kNP;
   q.nblocks = 1024;  // workgroups (each writes all pair partials once)
-  q.pe = q.esplit * per;
   return q;
 }
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 struct PSeg {
   int64_t numel;
@@ -309,126 +339,153 @@ struct PSeg {
 };
 static_assert(sizeof(PSeg) == 32, "PSeg layout");
 
-template <int TPT>
-__global__ void __launch_bounds__(kBlock)
+// waves_per_eu(5): <= 102 VGPRs, so two 10-wave groups share a CU (with 1024-thread bounds alone the
+// compiler took 100 -> 4 waves/SIMD -> one group per CU, idle across every barrier)
+template <bool VEC>
+__global__ void __launch_bounds__(kMaxPairThreads) __attribute__((amdgpu_waves_per_eu(5)))
 k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int kp,
            int64_t nchunks, int ntiles, int esplit, int pe, double* __restrict__ partial) {
-  extern __shared__ float lds[];              // [pe][kp + 4]
+  extern __shared__ float lds[];              // [2][pe][kp + 4]
   const int stride = kp + 4;
   const int nb = kp / 4;
-  const int t = threadIdx.x;
-  // work split: TPT == 1 -> tile t % ntiles, coordinate slice t / ntiles (esplit slices);
-  //             TPT  > 1 -> tiles t, t + kBlock, ... (esplit == 1)
-  const int es = TPT == 1 ? t / ntiles : 0;
-  const bool active = es < esplit;
-  const int tile0 = TPT == 1 ? t % ntiles : t;
-  int bi[TPT], bj[TPT];
-  bool tv[TPT];
+  const int t = threadIdx.x;                     // blockDim.x == ntiles * esplit
+  const int es = t / ntiles;                     // coordinate slice
+  const int tile = t % ntiles;
+  int bi = 0, rem = tile;  // tile -> (bi, bj), bi <= bj, row-major upper triangle
+  while (rem >= nb - bi) { rem -= nb - bi; ++bi; }
+  const int bj = bi + rem;
+  double accd[16];
+  f32x2 acc[8];
+  int run = 0;  // coordinates summed in acc since the last flush
 #pragma unroll
-  for (int q = 0; q < TPT; ++q) {
-    const int tile = tile0 + q * kBlock;
-    tv[q] = active && tile < ntiles;
-    int r = 0, rem = tv[q] ? tile : 0;  // tile -> (bi, bj), bi <= bj, row-major upper triangle
-    while (rem >= nb - r) { rem -= nb - r; ++r; }
-    bi[q] = r;
-    bj[q] = r + rem;
-  }
-  double accd[TPT][16];
+  for (int u = 0; u < 16; ++u) accd[u] = 0.0;
 #pragma unroll
-  for (int q = 0; q < TPT; ++q)
+  for (int u = 0; u < 8; ++u) acc[u] = f32x2{0.0f, 0.0f};
+  auto flush = [&]() {
 #pragma unroll
-    for (int u = 0; u < 16; ++u) accd[q][u] = 0.0;
-  const int per = pe / esplit;  // coordinates of a chunk per slice
-  const int se0 = t % pe, sc0 = t / pe, sde = kBlock % pe, sdc = kBlock / pe;  // staging walk
-  for (int64_t ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    const PSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, ch) : 0];
-    const int64_t e0 = (ch - sg.tile_start) * pe;
-    const void* const* in = ptrs + sg.ptr_base;
-    __syncthreads();  // the previous chunk is consumed
-    // stage: client c, coordinate e -> lds[e * stride + c]; clients >= k and coordinates past the
-    // segment end are zero (they add 0 to every sum).
-    {
-      // element idx = c * pe + e, idx = t, t + kBlock, ...: (e, c) advanced by carry, no division
-      int e = se0, c = sc0;
-      while (c < kp) {
-        int eu[8], cu[8];
-        float v[8];
+    for (int u = 0; u < 8; ++u) {
+      accd[2 * u] += (double)acc[u].x;
+      accd[2 * u + 1] += (double)acc[u].y;
+      acc[u] = f32x2{0.0f, 0.0f};
+    }
+    run = 0;
+  };
+  const int e_lo = (int)((int64_t)es * pe / esplit), e_hi = (int)((int64_t)(es + 1) * pe / esplit);
+  // staging role: client sc, kNP consecutive coordinates from se of every chunk (pe = (nthreads / kp)
+  // * kNP, so the row (t / kp) < nthreads / kp of a staging thread is exactly se < pe).  The loads of
+  // chunk ch + gridDim.x are issued before chunk ch is computed, so HBM latency hides behind the
+  // pair loop; the registers are written to LDS (transposed, [e][client]) after the next barrier.
+  const int sc = t % kp, se = (t / kp) * kNP;
+  const bool sact = se < pe && sc < k;
+  const bool swr = se < pe;            // clients k..kp-1 are staged as zeros
+  float v[kNP];
+  int cseg = -1;
+  const float* src = nullptr;
+  int64_t snum = 0;
+  auto load = [&](int64_t ch) {
+    const int si = nseg > 1 ? find_seg(segs, nseg, ch) : 0;
+    const PSeg sg = segs[si];
+    if (si != cseg) {  // one pointer load per segment, not per chunk
+      cseg = si;
+      src = sact ? (const float*)ptrs[sg.ptr_base + sc] : nullptr;
+      snum = sg.numel;
+    }
+    const int64_t b0 = (ch - sg.tile_start) * pe + se;
+    if (!sact) {
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          eu[u] = e;
-          cu[u] = c;
-          e += sde;
-          c += sdc;
-          if (e >= pe) { e -= pe; ++c; }
+      for (int u = 0; u < kNP; ++u) v[u] = 0.0f;
+    } else if (b0 + kNP <= snum) {  // whole run: one base address, immediate offsets
+      const __attribute__((address_space(1))) float* g = (const __attribute__((address_space(1))) float*)(src + b0);
+      if constexpr (VEC) {
+        typedef float f32x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+        for (int u = 0; u < kNP / 4; ++u) {
+          const f32x4 q = ((const __attribute__((address_space(1))) f32x4*)g)[u];
+          v[4 * u] = q.x;
+          v[4 * u + 1] = q.y;
+          v[4 * u + 2] = q.z;
+          v[4 * u + 3] = q.w;
         }
+      } else {
 #pragma unroll
-        for (int u = 0; u < 8; ++u)  // 8 clamped, unconditional loads in flight per lane
-          v[u] = gld<float>(in[min(cu[u], k - 1)], min(e0 + eu[u], sg.numel - 1));
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-          if (cu[u] < kp) lds[eu[u] * stride + cu[u]] = (e0 + eu[u] < sg.numel && cu[u] < k) ? v[u] : 0.0f;
+        for (int u = 0; u < kNP; ++u) v[u] = g[u];
       }
+    } else {  // the segment's last run: coordinates past the end add 0 to every sum
+#pragma unroll
+      for (int u = 0; u < kNP; ++u) v[u] = b0 + u < snum ? gld<float>(src, b0 + u) : 0.0f;
+    }
+  };
+  // two LDS buffers: chunk i is computed from buffer i & 1 while chunk i + 1 is written to the other
+  // (and chunk i + 2 loads into registers) -- one barrier per chunk
+  const int bufsz = pe * stride;
+  auto put = [&](int buf) {
+    if (swr) {
+#pragma unroll
+      for (int u = 0; u < kNP; ++u) lds[buf * bufsz + (se + u) * stride + sc] = v[u];
+    }
+  };
+  const int64_t g = gridDim.x;
+  if ((int64_t)blockIdx.x < nchunks) {
+    load(blockIdx.x);
+    put(0);
+    if (blockIdx.x + g < nchunks) load(blockIdx.x + g);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int64_t ch = blockIdx.x; ch < nchunks; ch += g, cur ^= 1) {
+    const float* lb = lds + cur * bufsz;
+    // packed fp32 (v_pk_add_f32 / v_pk_fma_f32): pair (x, y), (x, y+1) per instruction -- the same
+    // per-element IEEE sub and fused multiply-add as the scalar form, half the VALU issue slots
+    for (int e = e_lo; e < e_hi; ++e) {
+      const float4 a = *(const float4*)&lb[e * stride + 4 * bi];
+      const float4 b = *(const float4*)&lb[e * stride + 4 * bj];
+      const float av[4] = {a.x, a.y, a.z, a.w};
+      const f32x2 b01 = {b.x, b.y}, b23 = {b.z, b.w};
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const f32x2 ax = {av[x], av[x]};
+        const f32x2 d0 = ax - b01, d1 = ax - b23;
+        acc[2 * x] = __builtin_elementwise_fma(d0, d0, acc[2 * x]);
+        acc[2 * x + 1] = __builtin_elementwise_fma(d1, d1, acc[2 * x + 1]);
+      }
+    }
+    run += e_hi - e_lo;
+    if (run + (e_hi - e_lo) > kPE) flush();  // float runs of <= kPE coordinates, then float64
+    if (ch + g < nchunks) {
+      put(cur ^ 1);  // buffer cur ^ 1 was last read before the previous barrier
+      if (ch + 2 * g < nchunks) load(ch + 2 * g);
     }
     __syncthreads();
-    if (active) {
-      float acc[TPT][16];
-#pragma unroll
-      for (int q = 0; q < TPT; ++q)
-#pragma unroll
-        for (int u = 0; u < 16; ++u) acc[q][u] = 0.0f;
-      for (int e = es * per; e < (es + 1) * per; ++e) {
-#pragma unroll
-        for (int q = 0; q < TPT; ++q) {
-          if (!tv[q]) continue;
-          const float4 a = *(const float4*)&lds[e * stride + 4 * bi[q]];
-          const float4 b = *(const float4*)&lds[e * stride + 4 * bj[q]];
-          const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-          for (int x = 0; x < 4; ++x)
-#pragma unroll
-            for (int y = 0; y < 4; ++y) {
-              const float d = __fsub_rn(av[x], bv[y]);
-              acc[q][x * 4 + y] = __fmaf_rn(d, d, acc[q][x * 4 + y]);
-            }
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < TPT; ++q)
-#pragma unroll
-        for (int u = 0; u < 16; ++u) accd[q][u] += (double)acc[q][u];
-    }
   }
-  // reduce the esplit slices of each tile through LDS (reused as double scratch), then write the
-  // block's upper-triangle partials: pair (i, j), i < j -> index i*k - i*(i+1)/2 + (j - i - 1)
-  __syncthreads();
-  double* red = (double*)lds;  // [ntiles * 16] doubles, fits: kPE*(kp+4)*4 >= 16*8*ntiles? see host
+  flush();
+  // write the block's upper-triangle partials: pair (i, j), i < j -> index i*k - i*(i+1)/2 + (j-i-1);
+  // with esplit > 1 the slices of a tile are first added in slice order through LDS (reused as
+  // [ntiles * 16] doubles, sized by the host)
   const int64_t npairs = (int64_t)k * (k - 1) / 2;
   double* out = partial + (int64_t)blockIdx.x * npairs;
-  if (TPT == 1) {
-    for (int s = 0; s < esplit; ++s) {
-      if (active && es == s) {
+  if (esplit == 1) {
 #pragma unroll
-        for (int u = 0; u < 16; ++u) red[tile0 * 16 + u] = (s == 0 ? 0.0 : red[tile0 * 16 + u]) + accd[0][u];
-      }
-      __syncthreads();
+    for (int u = 0; u < 16; ++u) {
+      const int i = 4 * bi + u / 4, j = 4 * bj + u % 4;
+      if (i < j && j < k) out[(int64_t)i * k - (int64_t)i * (i + 1) / 2 + (j - i - 1)] = accd[u];
     }
-    for (int idx = t; idx < ntiles * 16; idx += kBlock) {
-      const int tile = idx / 16, u = idx % 16;
-      int r = 0, rem = tile;
-      while (rem >= nb - r) { rem -= nb - r; ++r; }
-      const int i = 4 * r + u / 4, j = 4 * (r + rem) + u % 4;
-      if (i < j && j < k) out[(int64_t)i * k - (int64_t)i * (i + 1) / 2 + (j - i - 1)] = red[idx];
-    }
-  } else {
+    return;
+  }
+  __syncthreads();
+  double* red = (double*)lds;
+  for (int s = 0; s < esplit; ++s) {
+    if (es == s) {
 #pragma unroll
-    for (int q = 0; q < TPT; ++q) {
-      if (!tv[q]) continue;
-#pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int i = 4 * bi[q] + u / 4, j = 4 * bj[q] + u % 4;
-        if (i < j && j < k) out[(int64_t)i * k - (int64_t)i * (i + 1) / 2 + (j - i - 1)] = accd[q][u];
-      }
+      for (int u = 0; u < 16; ++u) red[tile * 16 + u] = (s == 0 ? 0.0 : red[tile * 16 + u]) + accd[u];
     }
+    __syncthreads();
+  }
+  for (int idx = t; idx < ntiles * 16; idx += (int)blockDim.x) {
+    const int tl = idx / 16, u = idx % 16;
+    int r = 0, rm = tl;
+    while (rm >= nb - r) { rm -= nb - r; ++r; }
+    const int i = 4 * r + u / 4, j = 4 * (r + rm) + u % 4;
+    if (i < j && j < k) out[(int64_t)i * k - (int64_t)i * (i + 1) / 2 + (j - i - 1)] = red[idx];
   }
 }
 
@@ -473,8 +530,8 @@ int fa_pairwise_sqdist(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_num
   if (k < 2 || k > kMaxPairK || num_segments <= 0 || !seg_numel || !d_in || !d_dist)
     return fail(FA_ERR_INVALID, "fa_pairwise_sqdist: invalid arguments (2 <= k <= %d)", kMaxPairK);
   const PairSplit q = pair_split(k);
-  const int kp = q.kp, ntiles = q.ntiles, tpt = q.tpt, esplit = q.esplit, pe = q.pe;
-  if (tpt > 3) return fail(FA_ERR_INVALID, "fa_pairwise_sqdist: k too large");
+  const int kp = q.kp, ntiles = q.ntiles, esplit = q.esplit, pe = q.pe;
+  if (q.nthreads > kMaxPairThreads) return fail(FA_ERR_INVALID, "fa_pairwise_sqdist: k too large");
   int nseg = 0;
   int64_t nchunks = 0;
   for (int s = 0; s < num_segments; ++s) {
@@ -518,16 +575,19 @@ int fa_pairwise_sqdist(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_num
   rc = stage(slot, seg_bytes + ptr_bytes, st);
   if (rc) return rc;
   const char* dv = (const char*)slot->dev;
-  size_t lds = sizeof(float) * (size_t)pe * (kp + 4);
-  lds = std::max(lds, sizeof(double) * 16 * (size_t)ntiles);
-  const dim3 grid((unsigned)nblocks), blk(kBlock);
-#define FA_PD(T)                                                                                     \
-  hipLaunchKernelGGL((k_pairdist<T>), grid, blk, lds, st, (const PSeg*)dv, nseg,                       \
-                     (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit, pe, (double*)d_scratch)
-  if (tpt == 1) FA_PD(1);
-  else if (tpt == 2) FA_PD(2);
-  else FA_PD(3);
-#undef FA_PD
+  size_t lds = 2 * sizeof(float) * (size_t)pe * (kp + 4);
+  if (esplit > 1) lds = std::max(lds, sizeof(double) * 16 * (size_t)ntiles);
+  bool vec = true;  // 16-byte loads: every client segment 16-byte aligned (chunk starts are multiples of 16)
+  for (int i = 0; i < j * k; ++i) vec = vec && ((uintptr_t)hp[i] % 16 == 0);
+  if (vec)
+    hipLaunchKernelGGL((k_pairdist<true>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), lds, st,
+                       (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit,
+                       pe, (double*)d_scratch);
+  else
+    hipLaunchKernelGGL((k_pairdist<false>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), lds, st,
+                       (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit,
+                       pe, (double*)d_scratch);
+  const dim3 blk(kBlock);
   hipLaunchKernelGGL(k_pairdist_reduce, dim3((unsigned)((npairs + 7) / 8)), blk, 0,
                      st, (const double*)d_scratch, nblocks, k, (double*)d_dist);
   FA_HIP(hipGetLastError());

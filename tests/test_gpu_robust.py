@@ -104,13 +104,35 @@ def test_median_multi_segment(eng):
         assert bits_equal(o.cpu(), orc.coord_median(c) if c[0].numel() else torch.empty(0))
 
 
-@pytest.mark.parametrize("k", [2, 3, 5, 16, 31, 64, 97, 128])
+@pytest.mark.parametrize("k", [2, 3, 5, 8, 16, 31, 48, 64, 80, 97, 100, 128])
 def test_pairwise_sqdist_vs_oracle(eng, k):
     from oracle import orc
     g = torch.Generator().manual_seed(k)
     sizes = [70001, 5, 64, 1000]
     xs = [[torch.randn(s, generator=g) * (1 + (i % 3)) for s in sizes] for i in range(k)]
     D = eng.pairwise_sqdist([[xs[i][s].to(DEV) for i in range(k)] for s in range(len(sizes))]).cpu()
+    ref = orc.pairwise_sqdist([torch.cat(x) for x in xs])
+    assert torch.equal(D, D.T) and torch.all(D.diag() == 0)
+    np.testing.assert_allclose(D.numpy(), ref.numpy(), rtol=1e-6)
+
+
+@pytest.mark.parametrize("k,off", [(4, 1), (8, 3), (33, 1), (100, 2), (128, 1)])
+def test_pairwise_sqdist_unaligned_views(eng, k, off):
+    """Client vectors at 4-byte (not 16-byte) offsets take the scalar staging loads; one segment
+    whose length ends mid-chunk, another spanning many chunks (double-buffered pipeline)."""
+    from oracle import orc
+    g = torch.Generator().manual_seed(100 + k)
+    sizes = [4099, 123_457]
+    xs = [[torch.randn(s, generator=g) for s in sizes] for _ in range(k)]
+    segs = []
+    for s in range(len(sizes)):
+        views = []
+        for i in range(k):
+            buf = torch.zeros(sizes[s] + off + 5, device=DEV)
+            buf[off:off + sizes[s]] = xs[i][s].to(DEV)
+            views.append(buf[off:off + sizes[s]])
+        segs.append(views)
+    D = eng.pairwise_sqdist(segs).cpu()
     ref = orc.pairwise_sqdist([torch.cat(x) for x in xs])
     assert torch.equal(D, D.T) and torch.all(D.diag() == 0)
     np.testing.assert_allclose(D.numpy(), ref.numpy(), rtol=1e-6)
