@@ -372,9 +372,9 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
   };
   const int e_lo = (int)((int64_t)es * pe / esplit), e_hi = (int)((int64_t)(es + 1) * pe / esplit);
   // staging role: client sc, kNP consecutive coordinates from se of every chunk (pe = (nthreads / kp)
-  // * kNP, so the row (t / kp) < nthreads / kp of a staging thread is exactly se < pe).  The loads of
-  // chunk ch + gridDim.x are issued before chunk ch is computed, so HBM latency hides behind the
-  // pair loop; the registers are written to LDS (transposed, [e][client]) after the next barrier.
+  // * kNP, so the row (t / kp) < nthreads / kp of a staging thread is exactly se < pe).  Registers
+  // hold the next chunk while the current one is computed (see the pipeline below); they go to LDS
+  // transposed, [e][client].
   const int sc = t % kp, se = (t / kp) * kNP;
   const bool sact = se < pe && sc < k;
   const bool swr = se < pe;            // clients k..kp-1 are staged as zeros
@@ -424,15 +424,18 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
       for (int u = 0; u < kNP; ++u) lds[buf * bufsz + (se + u) * stride + sc] = v[u];
     }
   };
-  const int64_t g = gridDim.x;
-  if ((int64_t)blockIdx.x < nchunks) {
-    load(blockIdx.x);
+  // each workgroup takes a contiguous run of chunks: a 128-byte line split between two chunks is then
+  // fetched once, by one workgroup (grid-strided chunks put the halves on different CUs / XCDs: K = 32
+  // read 1.43x its bytes)
+  const int64_t c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
+  if (c0 < c1) {
+    load(c0);
     put(0);
-    if (blockIdx.x + g < nchunks) load(blockIdx.x + g);
+    if (c0 + 1 < c1) load(c0 + 1);
   }
   __syncthreads();
   int cur = 0;
-  for (int64_t ch = blockIdx.x; ch < nchunks; ch += g, cur ^= 1) {
+  for (int64_t ch = c0; ch < c1; ++ch, cur ^= 1) {
     const float* lb = lds + cur * bufsz;
     // packed fp32 (v_pk_add_f32 / v_pk_fma_f32): pair (x, y), (x, y+1) per instruction -- the same
     // per-element IEEE sub and fused multiply-add as the scalar form, half the VALU issue slots
@@ -451,9 +454,9 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
     }
     run += e_hi - e_lo;
     if (run + (e_hi - e_lo) > kPE) flush();  // float runs of <= kPE coordinates, then float64
-    if (ch + g < nchunks) {
+    if (ch + 1 < c1) {
       put(cur ^ 1);  // buffer cur ^ 1 was last read before the previous barrier
-      if (ch + 2 * g < nchunks) load(ch + 2 * g);
+      if (ch + 2 < c1) load(ch + 2);
     }
     __syncthreads();
   }
