@@ -38,16 +38,22 @@ __device__ __forceinline__ T gld(const void* p, int64_t e) {
   return ((const __attribute__((address_space(1))) T*)p)[e];
 }
 
+// non-temporal: each client element is read once (K = 16 / 32 medians 6% / 3% faster)
+template <typename T>
+__device__ __forceinline__ T gld_nt(const void* p, int64_t e) {
+  return __builtin_nontemporal_load((const __attribute__((address_space(1))) T*)p + e);
+}
+
 template <int DT> struct MedT;
 template <> struct MedT<FA_DTYPE_F32> {
   using S = unsigned;
-  __device__ static float load(const void* p, int64_t e) { return gld<float>(p, e); }
+  __device__ static float load(const void* p, int64_t e) { return gld_nt<float>(p, e); }
   __device__ static void store(void* p, int64_t e, float v) { ((float*)p)[e] = v; }
   __device__ static void store_bits(void* p, int64_t e, const void* src) { ((unsigned*)p)[e] = ((const unsigned*)src)[e]; }
 };
 template <> struct MedT<FA_DTYPE_BF16> {
   __device__ static float load(const void* p, int64_t e) {
-    return __uint_as_float((unsigned)gld<unsigned short>(p, e) << 16);
+    return __uint_as_float((unsigned)gld_nt<unsigned short>(p, e) << 16);
   }
   __device__ static void store(void* p, int64_t e, float v) {
     ((unsigned short*)p)[e] = (unsigned short)(__float_as_uint(v) >> 16);  // exact: v came from bf16
@@ -58,7 +64,7 @@ template <> struct MedT<FA_DTYPE_BF16> {
 };
 template <> struct MedT<FA_DTYPE_F16> {
   __device__ static float load(const void* p, int64_t e) {
-    return (float)__builtin_bit_cast(_Float16, gld<unsigned short>(p, e));
+    return (float)__builtin_bit_cast(_Float16, gld_nt<unsigned short>(p, e));
   }
   __device__ static void store(void* p, int64_t e, float v) {
     ((unsigned short*)p)[e] = __builtin_bit_cast(unsigned short, (_Float16)v);  // exact: v came from f16
