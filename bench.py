@@ -66,6 +66,8 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     p.add_argument("--check-samples", type=int, default=65536)
     p.add_argument("--pinned", action="store_true", help="host config: client updates already in pinned memory")
+    p.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "fp16"],
+                   help="median config: element type of the client vectors")
     p.add_argument("--layout", default=None, choices=["arena", "tiled", "tensors"],
                    help="arena: client updates as rows of one ClientArena allocation (fedml_amd/arena.py); "
                         "tiled: tile-interleaved ClientArena (4-KiB tiles of all clients contiguous); "
@@ -865,8 +867,17 @@ def wl_median(args, eng, rank, world, timer):
         raise SystemExit("median config: single GPU")
     K = args.clients or 32
     P = args.params or RESNET18_P
+    dt = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}[args.dtype]
     xs = _robust_inputs(K, P)
-    out = torch.empty(P, device="cuda")
+    if dt != torch.float32:
+        Ppad = -(-P // 64) * 64
+        arena = torch.empty((K, Ppad), dtype=dt, device="cuda")
+        for i, x in enumerate(xs):
+            arena[i, :P].copy_(x)
+        xs = [arena[i, :P] for i in range(K)]
+    es = xs[0].element_size()
+    ibits = {4: torch.int32, 2: torch.int16}[es]
+    out = torch.empty(P, dtype=dt, device="cuda")
 
     def step():
         with timer:
@@ -879,7 +890,7 @@ def wl_median(args, eng, rank, world, timer):
         gi = torch.Generator(device="cuda").manual_seed(99)
         idx = torch.randint(0, P, (args.check_samples,), generator=gi, device="cuda")
         exp = orc.coord_median([x.index_select(0, idx).cpu() for x in xs])
-        ok = torch.equal(out.index_select(0, idx).cpu().view(torch.int32), exp.view(torch.int32))
+        ok = torch.equal(out.index_select(0, idx).cpu().view(ibits), exp.view(ibits))
         return f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on {args.check_samples} sampled coordinates"
 
     def cpu(budget_s):
@@ -891,8 +902,8 @@ def wl_median(args, eng, rank, world, timer):
         return {"value": round((K * Pc * 4 + Pc * 4) / best / 1e9, 2), "unit": "GB/s", "cores": th, "kind": "port",
                 "sample": sample}
 
-    return dict(name=f"coord_median_K{K}_P{P}_fp32", dtype="fp32", step=step, parity=parity,
-                bytes_total=K * P * 4 + P * 4, launch_bytes=K * P * 4 + P * 4, clients=K, params=P, cpu_K=K, cpu=cpu,
+    return dict(name=f"coord_median_K{K}_P{P}_{args.dtype}", dtype=args.dtype, step=step, parity=parity,
+                bytes_total=(K * P + P) * es, launch_bytes=(K * P + P) * es, clients=K, params=P, cpu_K=K, cpu=cpu,
                 data="synthetic N(0,1) client weight vectors, resident in HBM (rows 256-byte aligned)")
 
 

@@ -122,6 +122,35 @@ __device__ __forceinline__ void store_rare(const void* const* in, int k, int64_t
 // L = (B-1)/2 - (K-1)/2 low sentinels (0, below every non-NaN key) and high sentinels
 // (0xFFFFFFFF) for the rest, so the lower median of the reals is rank (B-1)/2 of all B keys --
 // which the pruned network select_mid<B> (median_nets.h) computes.  B = K rounded up to 8.
+// One coordinate: all B element loads (clamped to the column's last coordinate when !live, so every
+// load is unconditional) before any is consumed, keys + sentinels, the network, the rare-case rescan
+// (k_median_pk's odd last coordinate).
+template <int DT, int B>
+__device__ __forceinline__ void median_col(const void* const* in, int k, int64_t e, int64_t ec, bool live,
+                                           void* out) {
+  const void* p[B];
+#pragma unroll
+  for (int i = 0; i < B; ++i) p[i] = in[min(i, k - 1)];
+  float x[B];
+#pragma unroll
+  for (int i = 0; i < B; ++i) x[i] = MedT<DT>::load(p[i], ec);  // clamped: every load unconditional
+  const int lo_end = k + (B - 1) / 2 - ((k - 1) >> 1);          // sentinels [k, lo_end) are low
+  unsigned key[B];
+  bool nan = false;
+#pragma unroll
+  for (int i = 0; i < B; ++i) {
+    nan = nan || (i < k && x[i] != x[i]);
+    key[i] = i < k ? fkey(x[i]) : (i < lo_end ? 0u : 0xFFFFFFFFu);
+  }
+  const unsigned kr = select_mid<B>(key);
+  if (!live) return;
+  const int r = (k - 1) >> 1;
+  if (nan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, nan, out);
+  else MedT<DT>::store(out, e, fkey_inv(kr));
+}
+
+// (B > 64: median_col's body written out -- called through median_col, B = 128 took 256 VGPRs,
+// 1 wave/SIMD, 1.6 -> 2.2 ms; B <= 64 the other way round)
 template <int DT, int B>
 __global__ void __launch_bounds__(kBlock)
 k_median(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k) {
@@ -131,6 +160,10 @@ k_median(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict_
   const bool live = e < sg.numel;
   const int64_t ec = live ? e : sg.numel - 1;
   const void* const* in = ptrs + sg.ptr_base;
+  if constexpr (B <= 64) {  // measured faster through median_col up to 64 (K = 64: 0.74 -> 0.64 ms)
+    median_col<DT, B>(in, k, e, ec, live, sg.out);
+    return;
+  }
   const void* p[B];
 #pragma unroll
   for (int i = 0; i < B; ++i) p[i] = in[min(i, k - 1)];
@@ -150,6 +183,60 @@ k_median(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict_
   const int r = (k - 1) >> 1;
   if (nan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, nan, sg.out);
   else MedT<DT>::store(sg.out, e, fkey_inv(kr));
+}
+
+// 16-bit types, two coordinates per lane: one 4-byte load per client, the two 16-bit keys packed in
+// one register and the same network on v_pk_min_u16 / v_pk_max_u16 (half the loads and min/max
+// instructions of one coordinate per lane).  Needs 4-byte aligned client and output pointers (the
+// host checks); a column pair cut by the segment end takes the one-coordinate path.
+__device__ __forceinline__ unsigned k16(unsigned u) { return u ^ ((u & 0x8000u) ? 0xFFFFu : 0x8000u); }
+__device__ __forceinline__ unsigned k16_inv(unsigned k) { return (k & 0x8000u) ? (k & 0x7FFFu) : (~k & 0xFFFFu); }
+template <int DT> __device__ __forceinline__ bool nan16(unsigned u) {
+  return (u & 0x7FFFu) > (DT == FA_DTYPE_BF16 ? 0x7F80u : 0x7C00u);
+}
+
+template <int DT, int B>
+__global__ void __launch_bounds__(kBlock)
+k_median_pk(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k) {
+  const int64_t tile = blockIdx.x;
+  const MSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
+  const int64_t e = ((tile - sg.tile_start) * kBlock + threadIdx.x) * 2;
+  if (e >= sg.numel) return;
+  const void* const* in = ptrs + sg.ptr_base;
+  if (e + 1 == sg.numel) {  // odd segment length: the last coordinate alone
+    median_col<DT, B>(in, k, e, e, true, sg.out);
+    return;
+  }
+  const void* p[B];
+#pragma unroll
+  for (int i = 0; i < B; ++i) p[i] = in[min(i, k - 1)];
+  unsigned w[B];
+#pragma unroll
+  for (int i = 0; i < B; ++i) w[i] = gld_nt<unsigned>(p[i], e >> 1);
+  const int lo_end = k + (B - 1) / 2 - ((k - 1) >> 1);
+  fa_u16x2 key[B];
+  bool nan0 = false, nan1 = false;
+#pragma unroll
+  for (int i = 0; i < B; ++i) {
+    const unsigned lo = w[i] & 0xFFFFu, hi = w[i] >> 16;
+    nan0 = nan0 || (i < k && nan16<DT>(lo));
+    nan1 = nan1 || (i < k && nan16<DT>(hi));
+    const unsigned short sent = i < lo_end ? (unsigned short)0 : (unsigned short)0xFFFF;
+    key[i] = i < k ? fa_u16x2{(unsigned short)k16(lo), (unsigned short)k16(hi)} : fa_u16x2{sent, sent};
+  }
+  const fa_u16x2 kr = select_mid<B>(key);
+  const int r = (k - 1) >> 1;
+  const unsigned k0 = kr.x, k1 = kr.y;
+  const bool rare0 = nan0 || k0 == 0x8000u || k0 == 0x7FFFu;  // NaN seen / a zero selected
+  const bool rare1 = nan1 || k1 == 0x8000u || k1 == 0x7FFFu;
+  if (!rare0 && !rare1) {
+    ((unsigned*)sg.out)[e >> 1] = k16_inv(k0) | (k16_inv(k1) << 16);
+    return;
+  }
+  if (rare0) store_rare<DT>(in, k, e, r, nan0, sg.out);
+  else ((unsigned short*)sg.out)[e] = (unsigned short)k16_inv(k0);
+  if (rare1) store_rare<DT>(in, k, e + 1, r, nan1, sg.out);
+  else ((unsigned short*)sg.out)[e + 1] = (unsigned short)k16_inv(k1);
 }
 
 // Any K (and float64): rank counting, ATen's order (value, client index), NaN first.
@@ -191,12 +278,20 @@ k_median_rank(const MSeg* __restrict__ segs, int nseg, const void* const* __rest
 }
 
 template <int DT>
-void launch_median(int k, dim3 grid, hipStream_t st, const MSeg* ds, int nseg, const void* const* dp) {
+void launch_median(int k, bool packed, dim3 grid, hipStream_t st, const MSeg* ds, int nseg, const void* const* dp) {
   if constexpr (DT == FA_DTYPE_F64) {
     hipLaunchKernelGGL((k_median_rank<DT>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);
   } else {
     switch ((k + 7) / 8) {  // bucket B = K rounded up to 8 (median_nets.h)
-#define FA_MB(Q) case Q: hipLaunchKernelGGL((k_median<DT, 8 * Q>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); return;
+#define FA_MB(Q)                                                                                       \
+  case Q:                                                                                            \
+    if constexpr (DT != FA_DTYPE_F32 && Q <= 8)  /* packed: K <= 64 (see fa_coord_median) */  \
+      if (packed) {                                                                                  \
+        hipLaunchKernelGGL((k_median_pk<DT, 8 * Q>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);     \
+        return;                                                                                      \
+      }                                                                                              \
+    hipLaunchKernelGGL((k_median<DT, 8 * Q>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);            \
+    return;
       FA_MB(1) FA_MB(2) FA_MB(3) FA_MB(4) FA_MB(5) FA_MB(6) FA_MB(7) FA_MB(8)
       FA_MB(9) FA_MB(10) FA_MB(11) FA_MB(12) FA_MB(13) FA_MB(14) FA_MB(15) FA_MB(16)
 #undef FA_MB
@@ -218,7 +313,16 @@ int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t*
     return fail(FA_ERR_INVALID, "fa_coord_median: invalid arguments");
   if (dtype != FA_DTYPE_F32 && dtype != FA_DTYPE_BF16 && dtype != FA_DTYPE_F16 && dtype != FA_DTYPE_F64)
     return fail(FA_ERR_DTYPE, "fa_coord_median: dtype %d not supported (F32, BF16, F16, F64)", dtype);
-  const int64_t tile_elems = kBlock;  // coordinates per tile (one lane each)
+  // bf16 / f16 with 4-byte aligned pointers, K <= 64: two coordinates per lane (k_median_pk;
+  // bf16 K = 16 / 32 / 64: 0.127 / 0.251 / 0.655 -> 0.106 / 0.205 / 0.572 ms.  K = 128 took 2.44 ms
+  // packed vs 1.51 ms one per lane: 128 live keys + 128 pointers exceed the register file)
+  bool packed = (dtype == FA_DTYPE_BF16 || dtype == FA_DTYPE_F16) && k <= 64;
+  for (int s = 0; s < num_segments && packed; ++s) {
+    if (seg_numel[s] <= 0) continue;
+    packed = d_out[s] && (uintptr_t)d_out[s] % 4 == 0;
+    for (int i = 0; i < k && packed; ++i) packed = (uintptr_t)d_in[(int64_t)s * k + i] % 4 == 0;
+  }
+  const int64_t tile_elems = packed ? 2 * kBlock : kBlock;  // coordinates per tile
   int nseg = 0;
   int64_t tiles = 0;
   for (int s = 0; s < num_segments; ++s) {
@@ -260,10 +364,10 @@ int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t*
   const void* const* dp = (const void* const*)(dv + seg_bytes);
   const dim3 grid((unsigned)tiles);
   switch (dtype) {
-    case FA_DTYPE_F32: launch_median<FA_DTYPE_F32>(k, grid, st, ds, nseg, dp); break;
-    case FA_DTYPE_BF16: launch_median<FA_DTYPE_BF16>(k, grid, st, ds, nseg, dp); break;
-    case FA_DTYPE_F16: launch_median<FA_DTYPE_F16>(k, grid, st, ds, nseg, dp); break;
-    default: launch_median<FA_DTYPE_F64>(k, grid, st, ds, nseg, dp); break;
+    case FA_DTYPE_F32: launch_median<FA_DTYPE_F32>(k, packed, grid, st, ds, nseg, dp); break;
+    case FA_DTYPE_BF16: launch_median<FA_DTYPE_BF16>(k, packed, grid, st, ds, nseg, dp); break;
+    case FA_DTYPE_F16: launch_median<FA_DTYPE_F16>(k, packed, grid, st, ds, nseg, dp); break;
+    default: launch_median<FA_DTYPE_F64>(k, packed, grid, st, ds, nseg, dp); break;
   }
   FA_HIP(hipGetLastError());
   return release(slot, st);

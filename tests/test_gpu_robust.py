@@ -83,6 +83,31 @@ def test_median_vs_oracle_dtypes(eng, dtype, k):
     assert bits_equal(got, orc.coord_median(xs))
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("k", [1, 2, 8, 9, 17, 33, 63, 64, 65])
+@pytest.mark.parametrize("off", [0, 1])
+def test_median_16bit_packed_and_unaligned(eng, dtype, k, off):
+    """bf16 / f16: 4-byte aligned columns take the two-coordinates-per-lane kernel (K <= 64), views
+    at a 2-byte offset the one-per-lane kernel; odd / tiny segment lengths (the last coordinate of an
+    odd segment alone), NaN, +-0, ties, +-Inf -- bit-exact either way."""
+    from oracle import orc
+    g = torch.Generator().manual_seed(7 * k + off)
+    sizes = [1, 2, 3, 257, 4096, 3001]
+    cols = [_column_data(g, k, n, dtype, zeros=0.15) for n in sizes]
+    segs = []
+    for c in cols:
+        views = []
+        for x in c:
+            buf = torch.zeros(x.numel() + off + 3, dtype=dtype, device=DEV)
+            buf[off:off + x.numel()] = x.to(DEV)
+            views.append(buf[off:off + x.numel()])
+        segs.append(views)
+    outs = eng.coord_median(segs)
+    for c, o in zip(cols, outs):
+        exp = orc.coord_median(c)
+        assert torch.equal(o.cpu().view(torch.int16), exp.view(torch.int16))
+
+
 def test_median_all_zero_columns(eng):
     """Columns of only +-0 in every sign pattern: ATen returns the zero of rank (K-1)/2 by index."""
     from oracle import orc

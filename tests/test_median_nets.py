@@ -1,5 +1,5 @@
 """CPU check of the generated selection networks (fedml_amd/csrc/median_nets.h, tools/
-gen_median_nets.py): every select_mid<B> returns the lower median of B keys, on random keys with
+gen_median_nets.py): every MidNet<B> returns the lower median of B keys, on random keys with
 many ties, and the committed header is what the generator produces."""
 from __future__ import annotations
 
@@ -18,7 +18,8 @@ HDR = os.path.join(ROOT, "fedml_amd", "csrc", "median_nets.h")
 def _networks():
     src = open(HDR).read()
     out = {}
-    for m in re.finditer(r"select_mid<(\d+)>\(const unsigned \(&x\)\[\d+\]\) \{\n(.*?)\n\}", src, re.S):
+    for m in re.finditer(r"struct MidNet<(\d+)> \{\n.*?static K run\(const K \(&x\)\[\d+\]\) \{\n(.*?)\n  \}\n\};",
+                         src, re.S):
         out[int(m.group(1))] = [l.strip() for l in m.group(2).split("\n")]
     return out
 
@@ -27,7 +28,7 @@ def _run(stmts, x):
     env = {}
     val = lambda t: x[int(t[2:-1])] if t.startswith("x[") else env[t]
     for s in stmts:
-        m = re.match(r"const unsigned (n\d+) = (min|max)\(([^,]+), ([^)]+)\);", s)
+        m = re.match(r"const K (n\d+) = k(min|max)\(([^,]+), ([^)]+)\);", s)
         if m:
             a, b = val(m.group(3)), val(m.group(4))
             env[m.group(1)] = min(a, b) if m.group(2) == "min" else max(a, b)
