@@ -35,6 +35,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
+from . import _host
 from .engine import MUL_N_DIV_N, MUL_W, SUM, AggEngine, get_engine, out_dtype
 
 _ALIGN_ELEMS = 64
@@ -62,6 +63,22 @@ class ArenaLayout:
             self.where[name] = (dt, off, tuple(int(s) for s in shape), n)
             self.group_numel[dt] = off + _pad(max(n, 1))
             self.keys.append(name)
+        # per dtype group: (key positions, element offsets, shapes) for _host.carve
+        self.group_keys: Dict[torch.dtype, Tuple[List[int], List[int], List[Tuple[int, ...]]]] = {}
+        for pos, name in enumerate(self.keys):
+            dt, off, shape, _ = self.where[name]
+            g = self.group_keys.setdefault(dt, ([], [], []))
+            g[0].append(pos)
+            g[1].append(off)
+            g[2].append(shape)
+
+    def carve(self, outs: Dict[torch.dtype, torch.Tensor]) -> "OrderedDict[str, torch.Tensor]":
+        """Per-key views of the flat per-dtype-group outputs, in key order (built in C++)."""
+        views: List[Optional[torch.Tensor]] = [None] * len(self.keys)
+        for dt, (pos, offs, shapes) in self.group_keys.items():
+            for p_, v in zip(pos, _host.carve(outs[dt], offs, shapes)):
+                views[p_] = v
+        return OrderedDict(zip(self.keys, views))
 
     @classmethod
     def from_state_dict(cls, sd) -> "ArenaLayout":
@@ -232,6 +249,15 @@ class ClientArena:
             raise IndexError("list index out of range")
         self._wait_ingest()
         outs: Dict[torch.dtype, torch.Tensor] = {}
+        pair = self._pair_groups()
+        if pair is not None:  # a float group + the int64 counters: one launch (fa_weighted_sum_pair)
+            fdt = pair
+            gn = self.layout.group_numel
+            outs[fdt], outs[torch.int64] = self.engine.weighted_sum_pair(
+                self.bufs[fdt], self.bufs[torch.int64], clients, mode, coef, divisor, n=gn[fdt],
+                n_i64=gn[torch.int64], out=out.get(fdt) if out is not None else None,
+                out_i64=out.get(torch.int64) if out is not None else None)
+            return self.layout.carve(outs)
         for dt, buf in self.bufs.items():
             o = out[dt] if out is not None else None
             if self.tiled:
@@ -239,11 +265,15 @@ class ClientArena:
                                                           n=self.layout.group_numel[dt], out=o)
             else:
                 outs[dt] = self.engine.weighted_sum_rows(buf, clients, mode, coef, divisor, out=o)
-        res = OrderedDict()
-        for k in self.layout.keys:
-            dt, off, shape, n = self.layout.where[k]
-            res[k] = outs[dt][off:off + n].view(shape)
-        return res
+        return self.layout.carve(outs)
+
+    def _pair_groups(self) -> Optional[torch.dtype]:
+        """The float dtype when the arena holds exactly one float group and one int64 group."""
+        dts = list(self.bufs)
+        if len(dts) != 2 or torch.int64 not in dts:
+            return None
+        fdt = dts[0] if dts[1] == torch.int64 else dts[1]
+        return fdt if fdt in (torch.float32, torch.bfloat16, torch.float16, torch.float64) else None
 
     def aggregate_grouped(self, groups: Sequence[Sequence[int]], mode: int, coef: Optional[Sequence[float]],
                           divisor: float, group_mode: int, group_coef: Optional[Sequence[float]] = None,
@@ -264,11 +294,7 @@ class ClientArena:
             else:
                 outs[dt] = self.engine.weighted_sum_grouped([buf[i] for i in order], mode, coef, divisor, gptr,
                                                             group_mode, group_coef, group_divisor)
-        res = OrderedDict()
-        for k in self.layout.keys:
-            dt, off, shape, n = self.layout.where[k]
-            res[k] = outs[dt][off:off + n].view(shape)
-        return res
+        return self.layout.carve(outs)
 
     def hierarchical(self, groups: Sequence[Sequence[int]], counts: Sequence[int], formula: str = "sp"):
         """Hierarchical FedAvg of a round in one pass: group FedAvg (weights n_i / N_g), then

@@ -308,17 +308,17 @@ struct WsumBody {
   }
 };
 
+// One workgroup's tile of an ordered weighted reduction (the body of k_wsum and k_wsum_pair).
 template <int DT, int MODE, int U, int S, bool NT, bool PF>
-__global__ void __launch_bounds__(kBlock)
-k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
-       const void* const* __restrict__ ptrs, int k, double divisor, int64_t sstr) {
+__device__ __forceinline__ void wsum_tile(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
+                                          const void* const* __restrict__ ptrs, int k, double divisor,
+                                          int64_t sstr, int64_t tile) {
   using B = WsumBody<DT, MODE, U, S, NT>;
   using T = typename B::T;
   using A = typename B::A;
   constexpr int V = T::V;
   constexpr int64_t TILE = (int64_t)kBlock * V * S;
 
-  const int64_t tile = blockIdx.x;
   const Seg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
   const int64_t tl = tile - sg.tile_start;
   const int64_t base = tl * TILE;
@@ -372,6 +372,30 @@ k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
       T::st1(sg.out, e, acc);
     }
   }
+}
+
+template <int DT, int MODE, int U, int S, bool NT, bool PF>
+__global__ void __launch_bounds__(kBlock)
+k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
+       const void* const* __restrict__ ptrs, int k, double divisor, int64_t sstr) {
+  wsum_tile<DT, MODE, U, S, NT, PF>(segs, nseg, coef, ptrs, k, divisor, sstr, blockIdx.x);
+}
+
+// A float dtype group and the state_dict's int64 group (BatchNorm num_batches_tracked counters,
+// promoted to fp32 by the reference's `x * w`) in ONE launch: the int64 tiles take the first
+// workgroups, so their latency-bound ordered loop (~10 us as a launch of its own for ResNet-18-GN's
+// 20 counters) overlaps the float group's stream instead of following it with a second launch and
+// a second descriptor copy.  Same per-element arithmetic as two k_wsum launches.
+template <int DT, int MODE, int U, int S, bool PF>
+__global__ void __launch_bounds__(kBlock)
+k_wsum_pair(const Seg* __restrict__ segs0, const void* const* __restrict__ ptrs0, int64_t sstr0,
+            const Seg* __restrict__ segs1, const void* const* __restrict__ ptrs1, int64_t sstr1, int64_t tiles1,
+            const double* __restrict__ coef, int k, double divisor) {
+  const int64_t t = blockIdx.x;
+  if (t < tiles1)
+    wsum_tile<FA_DTYPE_I64, MODE, 8, 1, true, false>(segs1, 1, coef, ptrs1, k, divisor, sstr1, t);
+  else
+    wsum_tile<DT, MODE, U, S, true, PF>(segs0, 1, coef, ptrs0, k, divisor, sstr0, t - tiles1);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1096,6 +1120,106 @@ int fa_weighted_sum_tiled(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t k
                 (long long)tile_stride);
   void* outs[1] = {d_out};
   return wsum_impl(ctx, dtype, mode, 1, &n, k, d_in, coef, divisor, outs, hip_stream, tile_stride);
+}
+
+extern "C++" {
+namespace {
+template <int DT, int MODE>
+void launch_pair(bool k16, int64_t tiles, hipStream_t st, const Seg* s0, const void* const* p0, int64_t sstr0,
+                 const Seg* s1, const void* const* p1, int64_t sstr1, int64_t tiles1, const double* coef, int k,
+                 double divisor) {
+  if (k16)  // variant 5 (automatic choice for K <= 16, see wsum_impl)
+    hipLaunchKernelGGL((k_wsum_pair<DT, MODE, 8, 2, false>), dim3((unsigned)tiles), dim3(kBlock), 0, st, s0, p0,
+                       sstr0, s1, p1, sstr1, tiles1, coef, k, divisor);
+  else
+    hipLaunchKernelGGL((k_wsum_pair<DT, MODE, 8, 1, false>), dim3((unsigned)tiles), dim3(kBlock), 0, st, s0, p0,
+                       sstr0, s1, p1, sstr1, tiles1, coef, k, divisor);
+}
+
+template <int DT>
+void pair_modes(int mode, bool k16, int64_t tiles, hipStream_t st, const Seg* s0, const void* const* p0,
+                int64_t sstr0, const Seg* s1, const void* const* p1, int64_t sstr1, int64_t tiles1,
+                const double* coef, int k, double divisor) {
+  switch (mode) {
+    case FA_MODE_MUL_W: launch_pair<DT, FA_MODE_MUL_W>(k16, tiles, st, s0, p0, sstr0, s1, p1, sstr1, tiles1, coef, k, divisor); break;
+    case FA_MODE_MUL_N_DIV_N: launch_pair<DT, FA_MODE_MUL_N_DIV_N>(k16, tiles, st, s0, p0, sstr0, s1, p1, sstr1, tiles1, coef, k, divisor); break;
+    default: launch_pair<DT, FA_MODE_SUM>(k16, tiles, st, s0, p0, sstr0, s1, p1, sstr1, tiles1, coef, k, divisor); break;
+  }
+}
+}  // namespace
+}  // extern "C++"
+
+int fa_weighted_sum_pair(fa_ctx* ctx, int dtype, int mode, int64_t n, int64_t n_i64, int32_t k,
+                         const void* const* d_in, const void* const* d_in_i64, int64_t tile_stride,
+                         int64_t tile_stride_i64, const double* coef, double divisor, void* d_out,
+                         void* d_out_i64, void* hip_stream) {
+  if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (k <= 0) return fail(FA_ERR_INVALID, "k must be > 0 (got %d)", k);
+  if (n < 0 || n_i64 < 0) return fail(FA_ERR_INVALID, "n must be >= 0");
+  if (!d_in || !d_in_i64 || !d_out || !d_out_i64) return fail(FA_ERR_INVALID, "fa_weighted_sum_pair: NULL table");
+  if (dtype != FA_DTYPE_F32 && dtype != FA_DTYPE_BF16 && dtype != FA_DTYPE_F16 && dtype != FA_DTYPE_F64)
+    return fail(FA_ERR_DTYPE, "fa_weighted_sum_pair: dtype %d not supported (F32, BF16, F16, F64)", dtype);
+  if (mode < FA_MODE_MUL_W || mode > FA_MODE_SUM) return fail(FA_ERR_DTYPE, "unknown mode %d", mode);
+  if (mode != FA_MODE_SUM && !coef) return fail(FA_ERR_INVALID, "coef is NULL for a weighted mode");
+  const int64_t strides[2] = {tile_stride, tile_stride_i64};
+  for (int g = 0; g < 2; ++g)
+    if (strides[g] < 0 || strides[g] % FA_TILE_BYTES)
+      return fail(FA_ERR_INVALID, "tile_stride must be 0 (row-major) or a positive multiple of %d (got %lld)",
+                  FA_TILE_BYTES, (long long)strides[g]);
+  if (n == 0 || n_i64 == 0) {  // one group: the ordinary launch
+    if (n == 0 && n_i64 == 0) return FA_OK;
+    return n ? wsum_impl(ctx, dtype, mode, 1, &n, k, d_in, coef, divisor, &d_out, hip_stream, tile_stride)
+             : wsum_impl(ctx, FA_DTYPE_I64, mode, 1, &n_i64, k, d_in_i64, coef, divisor, &d_out_i64, hip_stream,
+                         tile_stride_i64);
+  }
+  const bool k16 = k <= 16;
+  const int64_t te0 = (int64_t)kBlock * elems_per_vec(dtype) * (k16 ? 2 : 1);
+  const int64_t te1 = (int64_t)kBlock * elems_per_vec(FA_DTYPE_I64);
+  const int64_t tiles0 = (n + te0 - 1) / te0, tiles1 = (n_i64 + te1 - 1) / te1;
+  if (tiles0 + tiles1 > 0x7FFFFFFFll) return fail(FA_ERR_INVALID, "too many tiles");
+  bool al[2] = {al16(d_out), al16(d_out_i64)};
+  for (int i = 0; i < k; ++i) {
+    if (!d_in[i] || !d_in_i64[i]) return fail(FA_ERR_INVALID, "client %d: input NULL", i);
+    al[0] = al[0] && al16(d_in[i]);
+    al[1] = al[1] && al16(d_in_i64[i]);
+  }
+  for (int g = 0; g < 2; ++g)
+    if (strides[g] && !al[g]) return fail(FA_ERR_INVALID, "tiled inputs and the output must be 16-byte aligned");
+  const size_t seg_bytes = align16(sizeof(Seg) * 2);
+  const size_t coef_bytes = align16(sizeof(double) * k);
+  const size_t ptr_bytes = sizeof(void*) * 2 * (size_t)k;
+  const size_t bytes = seg_bytes + coef_bytes + ptr_bytes;
+  DeviceGuard g(ctx->device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
+  hipStream_t st = (hipStream_t)hip_stream;
+  fa_ctx::Slot* slot = nullptr;
+  int rc = acquire_slot(ctx, bytes, &slot);
+  if (rc) return rc;
+  char* h = (char*)slot->host;
+  Seg* hs = (Seg*)h;
+  hs[0] = Seg{n, 0, d_out, 0, al[0] ? 1 : 0};
+  hs[1] = Seg{n_i64, 0, d_out_i64, 0, al[1] ? 1 : 0};
+  double* hc = (double*)(h + seg_bytes);
+  for (int i = 0; i < k; ++i) hc[i] = coef ? coef[i] : 0.0;
+  memcpy(h + seg_bytes + coef_bytes, d_in, sizeof(void*) * k);
+  memcpy(h + seg_bytes + coef_bytes + sizeof(void*) * k, d_in_i64, sizeof(void*) * k);
+  rc = stage(slot, bytes, st);
+  if (rc) return rc;
+  char* d = (char*)slot->dev;
+  const Seg* ds = (const Seg*)d;
+  const double* dc = (const double*)(d + seg_bytes);
+  const void* const* dp = (const void* const*)(d + seg_bytes + coef_bytes);
+  const int64_t tiles = tiles0 + tiles1;
+#define FA_P(DT) pair_modes<DT>(mode, k16, tiles, st, ds, dp, tile_stride, ds + 1, dp + k, tile_stride_i64, tiles1, dc, k, divisor)
+  switch (dtype) {
+    case FA_DTYPE_F32: FA_P(FA_DTYPE_F32); break;
+    case FA_DTYPE_BF16: FA_P(FA_DTYPE_BF16); break;
+    case FA_DTYPE_F16: FA_P(FA_DTYPE_F16); break;
+    case FA_DTYPE_F64: FA_P(FA_DTYPE_F64); break;
+  }
+#undef FA_P
+  FA_HIP(hipGetLastError());
+  return release(slot, st);
 }
 
 namespace {

@@ -225,6 +225,56 @@ class AggEngine:
         N.check(rc, "fa_weighted_sum_tiled")
         return out
 
+    def weighted_sum_pair(self, buf: torch.Tensor, buf_i64: torch.Tensor, rows: Sequence[int], mode: int,
+                          coef: Optional[Sequence[float]] = None, divisor: float = 1.0, n: Optional[int] = None,
+                          n_i64: Optional[int] = None, out: Optional[torch.Tensor] = None,
+                          out_i64: Optional[torch.Tensor] = None, stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """A float arena group and the int64 arena group of the same clients in ONE launch
+        (fa_weighted_sum_pair).  Both groups are row-major [capacity, numel] or both tiled
+        [tiles, capacity, E]; returns the two flat outputs (same bits as two separate launches)."""
+        if buf_i64.dtype != torch.int64 or buf.dtype not in (torch.float32, torch.bfloat16, torch.float16,
+                                                             torch.float64):
+            raise TypeError("weighted_sum_pair: a float group and an int64 group")
+        if buf.dim() != buf_i64.dim() or buf.dim() not in (2, 3):
+            raise ValueError("weighted_sum_pair: both groups row-major (2-D) or both tiled (3-D)")
+        k = len(rows)
+        if mode != SUM and (coef is None or len(coef) != k):
+            raise ValueError("weighted_sum_pair: need one coefficient per row")
+        tabs = []
+        for b, nn in ((buf, n), (buf_i64, n_i64)):
+            if b.dim() == 3:
+                nn, ptrs, stride = self._tiled_args(b, rows, 0, nn, "weighted_sum_pair")
+            else:
+                if not b.is_contiguous():
+                    raise ValueError("weighted_sum_pair: buf must be contiguous")
+                _require_device(b, self.device, "arena")
+                if k == 0:
+                    raise ValueError("weighted_sum_pair: no rows")
+                if min(rows) < 0 or max(rows) >= b.shape[0]:
+                    raise IndexError("weighted_sum_pair: row out of range")
+                ncol = b.shape[1]
+                nn = ncol if nn is None else int(nn)
+                if not 0 <= nn <= ncol:
+                    raise ValueError("weighted_sum_pair: n exceeds the row")
+                rs = ncol * b.element_size()
+                ptrs, stride = N.ptr_array([b.data_ptr() + r * rs for r in rows]), 0
+            tabs.append((nn, ptrs, stride))
+        outs = []
+        for b, o, (nn, _, _) in ((buf, out, tabs[0]), (buf_i64, out_i64, tabs[1])):
+            odt = out_dtype(b.dtype, mode)
+            if o is None:
+                o = torch.empty(nn, dtype=odt, device=self.device)
+            elif o.dtype != odt or o.numel() != nn:
+                raise ValueError(f"weighted_sum_pair: output must be {odt} with {nn} elements")
+            _require_device(o, self.device, "output")
+            outs.append(o)
+        rc = self._lib.fa_weighted_sum_pair(
+            self._ctx, DTYPE_CODE[buf.dtype], int(mode), tabs[0][0], tabs[1][0], k, tabs[0][1], tabs[1][1],
+            tabs[0][2], tabs[1][2], N.f64_array(coef) if coef is not None else None, float(divisor),
+            outs[0].data_ptr(), outs[1].data_ptr(), self._stream(stream))
+        N.check(rc, "fa_weighted_sum_pair")
+        return outs[0], outs[1]
+
     def weighted_sum_tiled_multi(self, buf: torch.Tensor, rows: Sequence[int], mode: int,
                                  coef: Optional[Sequence[float]], divisor: float,
                                  ranges: Sequence[Tuple[int, int]], outs: Sequence[torch.Tensor],

@@ -134,6 +134,18 @@ int fa_weighted_sum_tiled_multi(fa_ctx *ctx, int dtype, int mode, int32_t num_se
                                 int64_t tile_stride, const double *coef, double divisor,
                                 void *const *d_out, void *hip_stream);
 
+/* A state_dict's float group (dtype F32, BF16, F16 or F64; n elements, inputs d_in[i]) and its
+ * int64 group (n_i64 elements, inputs d_in_i64[i]: BatchNorm num_batches_tracked counters, which
+ * the reference's `x * w` promotes to float32, agg_operator.py:37-44) reduced in ONE launch; both
+ * share k, mode, coef and divisor.  tile_stride / tile_stride_i64: 0 = one flat row per client
+ * (as fa_weighted_sum), else the tiled-arena stride (as fa_weighted_sum_tiled).  Outputs: d_out
+ * (same dtype as the inputs) and d_out_i64 (float32 for MUL_W / MUL_N_DIV_N,
+ * int64 for SUM).  Bit-identical to the two separate launches. */
+int fa_weighted_sum_pair(fa_ctx *ctx, int dtype, int mode, int64_t n, int64_t n_i64, int32_t k,
+                         const void *const *d_in, const void *const *d_in_i64, int64_t tile_stride,
+                         int64_t tile_stride_i64, const double *coef, double divisor, void *d_out,
+                         void *d_out_i64, void *hip_stream);
+
 /*
  * Two-level (grouped) reduction in one pass, one flat vector per client:
  *   clients [group_ptr[g], group_ptr[g+1]) form group g (group_ptr[0] = 0, group_ptr[G] = k,

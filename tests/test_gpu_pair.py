@@ -1,0 +1,106 @@
+"""GPU parity of fa_weighted_sum_pair: a float group and the int64 (BatchNorm counter) group of the
+same clients in ONE launch -- bit-identical to the two separate launches for every float dtype x
+mode x layout (row-major / tiled) x kernel shape (K <= 16 and K > 16), ragged lengths, row subsets,
+and through ClientArena on the reference's mixed-dtype golden fixtures (agg_operator.py:37-44 with
+int64 -> float32 promotion; FedAVGAggregator.py:99-116 for (x*n)/N)."""
+from __future__ import annotations
+
+import os
+from collections import OrderedDict
+
+import pytest
+import torch
+
+from golden_io import GOLDEN_DIR, client_dicts, expected_dicts, load_case
+from refcases import MUL_N_DIV_N, MUL_W, SUM, assert_dict_bits, bits_equal
+
+pytestmark = pytest.mark.gpu
+
+E_BYTES = 4096
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from fedml_amd.engine import get_engine
+    return get_engine(0)
+
+
+def _tiled(rows2d, cap_rows):
+    """[cap, n] CPU rows -> [tiles, cap, E] device buffer (zero padded)."""
+    cap, n = rows2d.shape
+    E = E_BYTES // rows2d.element_size()
+    nt = max(1, -(-n // E))
+    flat = torch.zeros((cap, nt * E), dtype=rows2d.dtype)
+    flat[:, :n] = rows2d
+    return flat.view(cap, nt, E).transpose(0, 1).contiguous().to("cuda:0")
+
+
+def _data(dt, cap, n, n64, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(cap, n, generator=g, dtype=torch.float64).mul_(3).to(dt)
+    c = torch.randint(0, 1 << 40, (cap, n64), generator=g, dtype=torch.int64)
+    c[:, :3] = torch.tensor([0, 1, -7])  # small counters as BatchNorm holds them
+    return x, c
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
+@pytest.mark.parametrize("mode", [MUL_W, MUL_N_DIV_N, SUM])
+@pytest.mark.parametrize("k", [5, 20])
+@pytest.mark.parametrize("layout", ["rows", "tiled"])
+def test_pair_matches_separate_launches(eng, dt, mode, k, layout):
+    cap = k + 3
+    n, n64 = 3 * 1024 * 8 + 77, 1029  # ragged: a partial tail tile in both groups
+    x, c = _data(dt, cap, n, n64, seed=k * 31 + mode)
+    rows = [cap - 1 - 2 * j if j < 2 else j - 2 for j in range(k)]  # out of order, not the first k rows
+    counts = [50 + 13 * j for j in range(k)]
+    N = sum(counts)
+    coef = None if mode == SUM else ([ci / N for ci in counts] if mode == MUL_W else [float(ci) for ci in counts])
+    div = float(N) if mode == MUL_N_DIV_N else 1.0
+    if layout == "rows":
+        bx, bc = x.to("cuda:0"), c.to("cuda:0")
+        ref_x = eng.weighted_sum_rows(bx, rows, mode, coef, div)
+        ref_c = eng.weighted_sum_rows(bc, rows, mode, coef, div)
+        got_x, got_c = eng.weighted_sum_pair(bx, bc, rows, mode, coef, div)
+    else:
+        bx, bc = _tiled(x, cap), _tiled(c, cap)
+        ref_x = eng.weighted_sum_tiled(bx, rows, mode, coef, div, n=n)
+        ref_c = eng.weighted_sum_tiled(bc, rows, mode, coef, div, n=n64)
+        got_x, got_c = eng.weighted_sum_pair(bx, bc, rows, mode, coef, div, n=n, n_i64=n64)
+    assert got_x.dtype == ref_x.dtype and got_c.dtype == ref_c.dtype
+    assert got_c.dtype == (torch.int64 if mode == SUM else torch.float32)
+    assert bits_equal(got_x.cpu(), ref_x.cpu())
+    assert bits_equal(got_c.cpu(), ref_c.cpu())
+
+
+def test_pair_rejects_bad_groups(eng):
+    a = torch.zeros(4, 100, device="cuda:0")
+    c = torch.zeros(4, 10, dtype=torch.int64, device="cuda:0")
+    with pytest.raises(TypeError):
+        eng.weighted_sum_pair(a, a, [0, 1], SUM)
+    with pytest.raises(ValueError):
+        eng.weighted_sum_pair(a, c.view(4, 10, 1), [0, 1], SUM)
+    with pytest.raises(ValueError):
+        eng.weighted_sum_pair(a, c, [0, 1], MUL_W, [0.5])
+    with pytest.raises(ValueError):  # the int64 group's SUM output is int64
+        eng.weighted_sum_pair(a, c, [0, 1], SUM, out_i64=torch.empty(10, device="cuda:0"))
+
+
+@pytest.mark.parametrize("name", ["g3_fedavg_mixed_K5", "g3_fedavg_mixed_K2", "g4_mpi_xn_div_N_int64_K5"])
+@pytest.mark.parametrize("tiled", [False, True])
+def test_arena_pair_golden(eng, name, tiled):
+    """ClientArena with one float + one int64 group aggregates in one pair launch; same bits as the
+    reference on its fixtures (FedAvg x*w and the MPI (x*n)/N)."""
+    from fedml_amd.arena import ClientArena
+    meta, arr = load_case(os.path.join(GOLDEN_DIR, name + ".npz"))
+    cl = client_dicts(meta, arr)
+    arena = ClientArena.for_model(cl[0], capacity=len(cl) + 2, device="cuda:0", tiled=tiled)
+    assert arena._pair_groups() == torch.float32
+    for i, d in enumerate(cl):
+        arena.write(i + 1, d)
+    rows = list(range(1, len(cl) + 1))
+    n = meta["n"]
+    if name.startswith("g4"):
+        got = arena.aggregate(MUL_N_DIV_N, [float(v) for v in n], float(sum(n)), clients=rows)
+    else:
+        got = arena.fedavg(n, clients=rows)
+    assert_dict_bits(OrderedDict((k, v.cpu()) for k, v in got.items()), expected_dicts(meta, arr)[0], name)
