@@ -381,6 +381,24 @@ k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
   wsum_tile<DT, MODE, U, S, NT, PF>(segs, nseg, coef, ptrs, k, divisor, sstr, blockIdx.x);
 }
 
+// Descriptor tables (segments | coefficients | pointers) small enough to travel as the kernel's
+// argument: the launch then needs no staged host->device copy (one ~2.5 us blit plus its dependency
+// gap on the stream per launch -- a visible share of a 0.26 ms cfg2 round or of a multi-GPU step's
+// eight chunk launches).  The tables are read with scalar loads from the kernarg segment, exactly
+// as from the staged buffer.
+constexpr int kInlineBytes = 3072;
+struct InlineDesc {
+  alignas(16) char raw[kInlineBytes];
+};
+
+template <int DT, int MODE, int U, int S, bool NT, bool PF>
+__global__ void __launch_bounds__(kBlock)
+k_wsum_inl(const InlineDesc dsc, int nseg, int coef_off, int ptr_off, int k, double divisor, int64_t sstr) {
+  const char* b = dsc.raw;
+  wsum_tile<DT, MODE, U, S, NT, PF>((const Seg*)b, nseg, (const double*)(b + coef_off),
+                                    (const void* const*)(b + ptr_off), k, divisor, sstr, blockIdx.x);
+}
+
 // A float dtype group and the state_dict's int64 group (BatchNorm num_batches_tracked counters,
 // promoted to fp32 by the reference's `x * w`) in ONE launch: the int64 tiles take the first
 // workgroups, so their latency-bound ordered loop (~10 us as a launch of its own for ResNet-18-GN's
@@ -396,6 +414,22 @@ k_wsum_pair(const Seg* __restrict__ segs0, const void* const* __restrict__ ptrs0
     wsum_tile<FA_DTYPE_I64, MODE, 8, 1, true, false>(segs1, 1, coef, ptrs1, k, divisor, sstr1, t);
   else
     wsum_tile<DT, MODE, U, S, true, PF>(segs0, 1, coef, ptrs0, k, divisor, sstr0, t - tiles1);
+}
+
+// k_wsum_pair with its tables as the kernel argument (layout: Seg[2] | coef[k] | ptrs0[k] | ptrs1[k])
+template <int DT, int MODE, int U, int S, bool PF>
+__global__ void __launch_bounds__(kBlock)
+k_wsum_pair_inl(const InlineDesc dsc, int coef_off, int ptr_off, int64_t sstr0, int64_t sstr1, int64_t tiles1,
+                int k, double divisor) {
+  const char* b = dsc.raw;
+  const Seg* sg = (const Seg*)b;
+  const double* coef = (const double*)(b + coef_off);
+  const void* const* p = (const void* const*)(b + ptr_off);
+  const int64_t t = blockIdx.x;
+  if (t < tiles1)
+    wsum_tile<FA_DTYPE_I64, MODE, 8, 1, true, false>(sg + 1, 1, coef, p + k, k, divisor, sstr1, t);
+  else
+    wsum_tile<DT, MODE, U, S, true, PF>(sg, 1, coef, p, k, divisor, sstr0, t - tiles1);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -815,6 +849,28 @@ void launch_wsum(int64_t tiles, hipStream_t st, const Seg* segs, int nseg, const
                      nseg, coef, ptrs, k, divisor, sstr);
 }
 
+// tables as the kernel argument: only the automatic shapes (variant 0: U = 8, S = 1; 5: U = 8, S = 2)
+template <int DT, int MODE>
+void launch_wsum_inl(int variant, int64_t tiles, hipStream_t st, const InlineDesc& dsc, int nseg, int coef_off,
+                     int ptr_off, int k, double divisor, int64_t sstr) {
+  if (variant == 5)
+    hipLaunchKernelGGL((k_wsum_inl<DT, MODE, 8, 2, true, false>), dim3((unsigned)tiles), dim3(kBlock), 0, st, dsc,
+                       nseg, coef_off, ptr_off, k, divisor, sstr);
+  else
+    hipLaunchKernelGGL((k_wsum_inl<DT, MODE, 8, 1, true, false>), dim3((unsigned)tiles), dim3(kBlock), 0, st, dsc,
+                       nseg, coef_off, ptr_off, k, divisor, sstr);
+}
+
+template <int DT>
+void dispatch_inl(int mode, int variant, int64_t tiles, hipStream_t st, const InlineDesc& dsc, int nseg,
+                  int coef_off, int ptr_off, int k, double divisor, int64_t sstr) {
+  switch (mode) {
+    case FA_MODE_MUL_W: launch_wsum_inl<DT, FA_MODE_MUL_W>(variant, tiles, st, dsc, nseg, coef_off, ptr_off, k, divisor, sstr); break;
+    case FA_MODE_MUL_N_DIV_N: launch_wsum_inl<DT, FA_MODE_MUL_N_DIV_N>(variant, tiles, st, dsc, nseg, coef_off, ptr_off, k, divisor, sstr); break;
+    default: launch_wsum_inl<DT, FA_MODE_SUM>(variant, tiles, st, dsc, nseg, coef_off, ptr_off, k, divisor, sstr); break;
+  }
+}
+
 template <int DT, int MODE>
 void dispatch_variant(int variant, int64_t tiles, hipStream_t st, const Seg* segs, int nseg,
                       const double* coef, const void* const* ptrs, int k, double divisor, int64_t sstr) {
@@ -1013,6 +1069,15 @@ int fa_stream_destroy(void* stream) {
 namespace {
 // fa_weighted_sum_multi / fa_weighted_sum_tiled.  sstr = 0: flat inputs; otherwise (one segment)
 // tile-interleaved inputs whose FA_TILE_BYTES slots are sstr bytes apart.
+// FA_INLINE_DESC=0 forces the staged-table launches (A/B measurement)
+bool inline_enabled() {
+  static const int on = [] {
+    const char* e = getenv("FA_INLINE_DESC");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 int wsum_impl(fa_ctx* ctx, int dtype, int mode, int32_t num_segments, const int64_t* seg_numel, int32_t k,
               const void* const* d_in, const double* coef, double divisor, void* const* d_out,
               void* hip_stream, int64_t sstr) {
@@ -1053,11 +1118,16 @@ int wsum_impl(fa_ctx* ctx, int dtype, int mode, int32_t num_segments, const int6
   DeviceGuard g(ctx->device);
   if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
   hipStream_t st = (hipStream_t)hip_stream;
+  const bool inl = bytes <= (size_t)kInlineBytes && (variant == 0 || variant == 5) && inline_enabled();
+  InlineDesc dsc;
   fa_ctx::Slot* slot = nullptr;
-  int rc = acquire_slot(ctx, bytes, &slot);
-  if (rc) return rc;
+  int rc = FA_OK;
+  if (!inl) {
+    rc = acquire_slot(ctx, bytes, &slot);
+    if (rc) return rc;
+  }
 
-  char* h = (char*)slot->host;
+  char* h = inl ? dsc.raw : (char*)slot->host;
   Seg* hs = (Seg*)h;
   double* hc = (double*)(h + seg_bytes);
   const void** hp = (const void**)(h + seg_bytes + coef_bytes);
@@ -1077,6 +1147,18 @@ int wsum_impl(fa_ctx* ctx, int dtype, int mode, int32_t num_segments, const int6
     hs[j] = Seg{n, t0, d_out[s], j * k, aligned ? 1 : 0};
     t0 += (n + tile_elems - 1) / tile_elems;
     ++j;
+  }
+  if (inl) {
+    const int co = (int)seg_bytes, po = (int)(seg_bytes + coef_bytes);
+    switch (dtype) {
+      case FA_DTYPE_F32: dispatch_inl<FA_DTYPE_F32>(mode, variant, tiles, st, dsc, nseg, co, po, k, divisor, sstr); break;
+      case FA_DTYPE_BF16: dispatch_inl<FA_DTYPE_BF16>(mode, variant, tiles, st, dsc, nseg, co, po, k, divisor, sstr); break;
+      case FA_DTYPE_F16: dispatch_inl<FA_DTYPE_F16>(mode, variant, tiles, st, dsc, nseg, co, po, k, divisor, sstr); break;
+      case FA_DTYPE_F64: dispatch_inl<FA_DTYPE_F64>(mode, variant, tiles, st, dsc, nseg, co, po, k, divisor, sstr); break;
+      case FA_DTYPE_I64: dispatch_inl<FA_DTYPE_I64>(mode, variant, tiles, st, dsc, nseg, co, po, k, divisor, sstr); break;
+    }
+    FA_HIP(hipGetLastError());
+    return FA_OK;
   }
   rc = stage(slot, bytes, st);
   if (rc) return rc;
@@ -1146,6 +1228,26 @@ void pair_modes(int mode, bool k16, int64_t tiles, hipStream_t st, const Seg* s0
     default: launch_pair<DT, FA_MODE_SUM>(k16, tiles, st, s0, p0, sstr0, s1, p1, sstr1, tiles1, coef, k, divisor); break;
   }
 }
+template <int DT, int MODE>
+void launch_pair_inl(bool k16, int64_t tiles, hipStream_t st, const InlineDesc& dsc, int co, int po, int64_t sstr0,
+                     int64_t sstr1, int64_t tiles1, int k, double divisor) {
+  if (k16)
+    hipLaunchKernelGGL((k_wsum_pair_inl<DT, MODE, 8, 2, false>), dim3((unsigned)tiles), dim3(kBlock), 0, st, dsc, co,
+                       po, sstr0, sstr1, tiles1, k, divisor);
+  else
+    hipLaunchKernelGGL((k_wsum_pair_inl<DT, MODE, 8, 1, false>), dim3((unsigned)tiles), dim3(kBlock), 0, st, dsc, co,
+                       po, sstr0, sstr1, tiles1, k, divisor);
+}
+
+template <int DT>
+void pair_modes_inl(int mode, bool k16, int64_t tiles, hipStream_t st, const InlineDesc& dsc, int co, int po,
+                    int64_t sstr0, int64_t sstr1, int64_t tiles1, int k, double divisor) {
+  switch (mode) {
+    case FA_MODE_MUL_W: launch_pair_inl<DT, FA_MODE_MUL_W>(k16, tiles, st, dsc, co, po, sstr0, sstr1, tiles1, k, divisor); break;
+    case FA_MODE_MUL_N_DIV_N: launch_pair_inl<DT, FA_MODE_MUL_N_DIV_N>(k16, tiles, st, dsc, co, po, sstr0, sstr1, tiles1, k, divisor); break;
+    default: launch_pair_inl<DT, FA_MODE_SUM>(k16, tiles, st, dsc, co, po, sstr0, sstr1, tiles1, k, divisor); break;
+  }
+}
 }  // namespace
 }  // extern "C++"
 
@@ -1192,10 +1294,15 @@ int fa_weighted_sum_pair(fa_ctx* ctx, int dtype, int mode, int64_t n, int64_t n_
   DeviceGuard g(ctx->device);
   if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
   hipStream_t st = (hipStream_t)hip_stream;
+  const bool inl = bytes <= (size_t)kInlineBytes && inline_enabled();
+  InlineDesc dsc;
   fa_ctx::Slot* slot = nullptr;
-  int rc = acquire_slot(ctx, bytes, &slot);
-  if (rc) return rc;
-  char* h = (char*)slot->host;
+  int rc = FA_OK;
+  if (!inl) {
+    rc = acquire_slot(ctx, bytes, &slot);
+    if (rc) return rc;
+  }
+  char* h = inl ? dsc.raw : (char*)slot->host;
   Seg* hs = (Seg*)h;
   hs[0] = Seg{n, 0, d_out, 0, al[0] ? 1 : 0};
   hs[1] = Seg{n_i64, 0, d_out_i64, 0, al[1] ? 1 : 0};
@@ -1203,13 +1310,24 @@ int fa_weighted_sum_pair(fa_ctx* ctx, int dtype, int mode, int64_t n, int64_t n_
   for (int i = 0; i < k; ++i) hc[i] = coef ? coef[i] : 0.0;
   memcpy(h + seg_bytes + coef_bytes, d_in, sizeof(void*) * k);
   memcpy(h + seg_bytes + coef_bytes + sizeof(void*) * k, d_in_i64, sizeof(void*) * k);
+  const int64_t tiles = tiles0 + tiles1;
+  if (inl) {
+    const int co = (int)seg_bytes, po = (int)(seg_bytes + coef_bytes);
+    switch (dtype) {
+      case FA_DTYPE_F32: pair_modes_inl<FA_DTYPE_F32>(mode, k16, tiles, st, dsc, co, po, tile_stride, tile_stride_i64, tiles1, k, divisor); break;
+      case FA_DTYPE_BF16: pair_modes_inl<FA_DTYPE_BF16>(mode, k16, tiles, st, dsc, co, po, tile_stride, tile_stride_i64, tiles1, k, divisor); break;
+      case FA_DTYPE_F16: pair_modes_inl<FA_DTYPE_F16>(mode, k16, tiles, st, dsc, co, po, tile_stride, tile_stride_i64, tiles1, k, divisor); break;
+      case FA_DTYPE_F64: pair_modes_inl<FA_DTYPE_F64>(mode, k16, tiles, st, dsc, co, po, tile_stride, tile_stride_i64, tiles1, k, divisor); break;
+    }
+    FA_HIP(hipGetLastError());
+    return FA_OK;
+  }
   rc = stage(slot, bytes, st);
   if (rc) return rc;
   char* d = (char*)slot->dev;
   const Seg* ds = (const Seg*)d;
   const double* dc = (const double*)(d + seg_bytes);
   const void* const* dp = (const void* const*)(d + seg_bytes + coef_bytes);
-  const int64_t tiles = tiles0 + tiles1;
 #define FA_P(DT) pair_modes<DT>(mode, k16, tiles, st, ds, dp, tile_stride, ds + 1, dp + k, tile_stride_i64, tiles1, dc, k, divisor)
   switch (dtype) {
     case FA_DTYPE_F32: FA_P(FA_DTYPE_F32); break;

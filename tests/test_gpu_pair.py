@@ -104,3 +104,37 @@ def test_arena_pair_golden(eng, name, tiled):
     else:
         got = arena.fedavg(n, clients=rows)
     assert_dict_bits(OrderedDict((k, v.cpu()) for k, v in got.items()), expected_dicts(meta, arr)[0], name)
+
+
+_INLINE_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+from fedml_amd.engine import get_engine
+eng = get_engine(0)
+g = torch.Generator().manual_seed(5)
+outs = []
+for k in (3, 16, 40, 128):
+    x = torch.randn(k, 20000 + k, generator=g).cuda()
+    c = torch.randint(0, 1000, (k, 37), generator=g).cuda()
+    w = [1.0 / (i + 2) for i in range(k)]
+    outs.append(eng.weighted_sum_rows(x, list(range(k)), 0, w))
+    outs.extend(eng.weighted_sum_pair(x, c, list(range(k))[::-1], 1, [float(i + 1) for i in range(k)], 7.0))
+torch.save([o.cpu() for o in outs], sys.argv[2])
+"""
+
+
+def test_inline_descriptors_match_staged(tmp_path):
+    """Tables passed as the kernel argument (default for small tables) and staged through a device
+    copy (FA_INLINE_DESC=0) give the same bits."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for flag in ("1", "0"):
+        path = str(tmp_path / f"out{flag}.pt")
+        env = dict(os.environ, FA_INLINE_DESC=flag)
+        subprocess.run([sys.executable, "-c", _INLINE_SCRIPT, root, path], env=env, check=True, timeout=120)
+        res[flag] = torch.load(path, weights_only=True)
+    assert len(res["1"]) == len(res["0"]) == 12
+    for a, b in zip(res["1"], res["0"]):
+        assert bits_equal(a, b)
