@@ -63,6 +63,8 @@ def test_invalid_arguments_return_codes_without_device():
     assert rc == N.FA_ERR_INVALID
     rc = L.fa_lcc_decode(None, 1, 1, 1, None, None, 7, 1, None, None)
     assert rc == N.FA_ERR_INVALID
+    rc = L.fa_weighted_sum_pair(None, N.F32, N.MUL_W, 10, 1, 2, None, None, 0, 0, None, 1.0, None, None, None)
+    assert rc == N.FA_ERR_INVALID and b"ctx" in L.fa_last_error()
 
 
 @pytest.mark.skipif(gpu_available(), reason="checks the no-device error path")
