@@ -552,17 +552,16 @@ __device__ __forceinline__ float rmsprop_update(float p, float avg, float& sq, f
 }
 
 // OPT 0: SGD (bufs = momentum); OPT 1: RMSprop (bufs = momentum, bufs2 = square_avg)
-template <int U, bool NT, int OPT = 0>
-__global__ void __launch_bounds__(kBlock)
-k_fedavg_sgd(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
-             const void* const* __restrict__ ptrs, int k, void* const* __restrict__ bufs, float neg_lr,
-             float mom, float damp1, float wd, int flags, int64_t sstr, void* const* __restrict__ bufs2,
-             RmsArgs ra) {
+template <int U, bool NT, int OPT>
+__device__ __forceinline__ void fedavg_sgd_tile(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
+                                                const void* const* __restrict__ ptrs, int k,
+                                                void* const* __restrict__ bufs, float neg_lr, float mom, float damp1,
+                                                float wd, int flags, int64_t sstr, void* const* __restrict__ bufs2,
+                                                RmsArgs ra, int64_t tile) {
   using B = WsumBody<FA_DTYPE_F32, FA_MODE_MUL_W, U, 1, NT>;
   using T = typename B::T;
   constexpr int V = T::V;
   constexpr int64_t TILE = (int64_t)kBlock * V;
-  const int64_t tile = blockIdx.x;
   const int s = nseg > 1 ? find_seg(segs, nseg, tile) : 0;
   const Seg sg = segs[s];
   float* param = (float*)sg.out;
@@ -625,6 +624,28 @@ k_fedavg_sgd(const Seg* __restrict__ segs, int nseg, const double* __restrict__ 
       if (flags & SGD_MOMENTUM) mbuf[e] = b;
     }
   }
+}
+
+template <int U, bool NT, int OPT = 0>
+__global__ void __launch_bounds__(kBlock)
+k_fedavg_sgd(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
+             const void* const* __restrict__ ptrs, int k, void* const* __restrict__ bufs, float neg_lr,
+             float mom, float damp1, float wd, int flags, int64_t sstr, void* const* __restrict__ bufs2,
+             RmsArgs ra) {
+  fedavg_sgd_tile<U, NT, OPT>(segs, nseg, coef, ptrs, k, bufs, neg_lr, mom, damp1, wd, flags, sstr, bufs2, ra,
+                              blockIdx.x);
+}
+
+// the same with its tables (Seg[nseg] | coef[k] | bufs[nseg] | bufs2[nseg] | ptrs[nseg * k]) as the
+// kernel argument (see InlineDesc)
+template <int U, bool NT, int OPT = 0>
+__global__ void __launch_bounds__(kBlock)
+k_fedavg_sgd_inl(const InlineDesc dsc, int nseg, int coef_off, int buf_off, int buf2_off, int ptr_off, int k,
+                 float neg_lr, float mom, float damp1, float wd, int flags, int64_t sstr, RmsArgs ra) {
+  const char* b = dsc.raw;
+  fedavg_sgd_tile<U, NT, OPT>((const Seg*)b, nseg, (const double*)(b + coef_off), (const void* const*)(b + ptr_off),
+                              k, (void* const*)(b + buf_off), neg_lr, mom, damp1, wd, flags, sstr,
+                              (void* const*)(b + buf2_off), ra, blockIdx.x);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1481,10 +1502,15 @@ int fedavg_sgd_impl(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel,
   DeviceGuard g(ctx->device);
   if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
   hipStream_t st = (hipStream_t)hip_stream;
+  const bool inl = bytes <= (size_t)kInlineBytes && inline_enabled();
+  InlineDesc dsc;
   fa_ctx::Slot* slot = nullptr;
-  int rc = acquire_slot(ctx, bytes, &slot);
-  if (rc) return rc;
-  char* h = (char*)slot->host;
+  int rc = FA_OK;
+  if (!inl) {
+    rc = acquire_slot(ctx, bytes, &slot);
+    if (rc) return rc;
+  }
+  char* h = inl ? dsc.raw : (char*)slot->host;
   Seg* hs = (Seg*)h;
   double* hc = (double*)(h + seg_bytes);
   void** hb = (void**)(h + seg_bytes + coef_bytes);
@@ -1511,12 +1537,25 @@ int fedavg_sgd_impl(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel,
     t0 += (n + tile_elems - 1) / tile_elems;
     ++j;
   }
-  rc = stage(slot, bytes, st);
-  if (rc) return rc;
-  char* dv = (char*)slot->dev;
   const int flags = (momentum != 0.0 ? SGD_MOMENTUM : 0) | (nesterov ? SGD_NESTEROV : 0) |
                     (weight_decay != 0.0 ? SGD_WD : 0) | (first_step ? SGD_FIRST : 0);
   const RmsArgs ra{(float)alpha, (float)(1.0 - alpha), (float)eps};
+  if (inl) {
+    const int co = (int)seg_bytes, bo = (int)(seg_bytes + coef_bytes), qo = (int)(seg_bytes + coef_bytes + buf_bytes),
+              po = (int)(seg_bytes + coef_bytes + 2 * buf_bytes);
+    if (opt == 1)
+      hipLaunchKernelGGL((k_fedavg_sgd_inl<8, true, 1>), dim3((unsigned)tiles), dim3(kBlock), 0, st, dsc, nseg, co, bo,
+                         qo, po, k, (float)(-lr), (float)momentum, 1.0f, (float)weight_decay, flags, sstr, ra);
+    else
+      hipLaunchKernelGGL((k_fedavg_sgd_inl<8, true, 0>), dim3((unsigned)tiles), dim3(kBlock), 0, st, dsc, nseg, co, bo,
+                         qo, po, k, (float)(-lr), (float)momentum, (float)(1.0 - dampening), (float)weight_decay,
+                         flags, sstr, ra);
+    FA_HIP(hipGetLastError());
+    return FA_OK;
+  }
+  rc = stage(slot, bytes, st);
+  if (rc) return rc;
+  char* dv = (char*)slot->dev;
   const Seg* ds = (const Seg*)dv;
   const double* dc = (const double*)(dv + seg_bytes);
   void* const* db = (void* const*)(dv + seg_bytes + coef_bytes);

@@ -119,13 +119,21 @@ for k in (3, 16, 40, 128):
     w = [1.0 / (i + 2) for i in range(k)]
     outs.append(eng.weighted_sum_rows(x, list(range(k)), 0, w))
     outs.extend(eng.weighted_sum_pair(x, c, list(range(k))[::-1], 1, [float(i + 1) for i in range(k)], 7.0))
+    segs = [[x[i, :5000] for i in range(k)], [x[i, 5000:] for i in range(k)]]
+    params = [torch.randn(5000, generator=g).cuda(), torch.randn(x.shape[1] - 5000, generator=g).cuda()]
+    bufs = [torch.randn(p.numel(), generator=g).cuda() for p in params]
+    sq = [torch.rand(p.numel(), generator=g).cuda() for p in params]
+    eng.fedavg_sgd(segs, w, params, bufs, 0.5, momentum=0.9, first_step=False)
+    eng.fedavg_rmsprop(segs, w, [p.clone() for p in params], sq, None, 0.01)
+    outs.extend(params + bufs + sq)
 torch.save([o.cpu() for o in outs], sys.argv[2])
 """
 
 
 def test_inline_descriptors_match_staged(tmp_path):
     """Tables passed as the kernel argument (default for small tables) and staged through a device
-    copy (FA_INLINE_DESC=0) give the same bits."""
+    copy (FA_INLINE_DESC=0) give the same bits: weighted sums, the pair launch, fused FedOpt SGD and
+    RMSprop steps."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -135,6 +143,6 @@ def test_inline_descriptors_match_staged(tmp_path):
         env = dict(os.environ, FA_INLINE_DESC=flag)
         subprocess.run([sys.executable, "-c", _INLINE_SCRIPT, root, path], env=env, check=True, timeout=120)
         res[flag] = torch.load(path, weights_only=True)
-    assert len(res["1"]) == len(res["0"]) == 12
+    assert len(res["1"]) == len(res["0"]) == 36
     for a, b in zip(res["1"], res["0"]):
         assert bits_equal(a, b)
