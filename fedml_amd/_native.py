@@ -28,7 +28,7 @@ FA_OK, FA_ERR_INVALID, FA_ERR_DTYPE, FA_ERR_HIP, FA_ERR_NOMEM = 0, -1, -2, -3, -
 
 EXPORTED_SYMBOLS = (
     "fa_abi_version", "fa_ctx_create", "fa_ctx_destroy", "fa_weighted_sum",
-    "fa_weighted_sum_multi", "fa_weighted_sum_tiled", "fa_weighted_sum_tiled_multi", "fa_weighted_sum_pair", "fa_weighted_sum_grouped", "fa_weighted_sum_grouped_tiled",
+    "fa_weighted_sum_multi", "fa_weighted_sum_tiled", "fa_weighted_sum_tiled_multi", "fa_weighted_sum_pair", "fa_weighted_sum_pair_multi", "fa_weighted_sum_grouped", "fa_weighted_sum_grouped_tiled",
     "fa_fedavg_sgd", "fa_fedavg_sgd_tiled", "fa_fedavg_rmsprop", "fa_mix", "fa_mix_tiled", "fa_ctx_set_variant",
     "fa_ctx_set_mix_band", "fa_stream_create_cu_masked", "fa_stream_destroy", "fa_strerror", "fa_last_error",
     # include/fedagg_finite.h
@@ -85,6 +85,10 @@ def _declare(L):
     L.fa_weighted_sum_pair.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int64, ctypes.c_int32,
                                        _P_vp, _P_vp, ctypes.c_int64, ctypes.c_int64, _P_d, ctypes.c_double, _vp, _vp,
                                        _vp]
+    L.fa_weighted_sum_pair_multi.restype = ctypes.c_int
+    L.fa_weighted_sum_pair_multi.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int32, _P_i64, ctypes.c_int32,
+                                             _P_i64, ctypes.c_int32, _P_vp, _P_vp, _P_d, ctypes.c_double, _P_vp,
+                                             _P_vp, _vp]
     L.fa_weighted_sum_grouped_tiled.restype = ctypes.c_int
     L.fa_weighted_sum_grouped_tiled.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int32,
                                                 _P_vp, ctypes.c_int64, _P_d, ctypes.c_double, ctypes.c_int32,

@@ -406,30 +406,30 @@ k_wsum_inl(const InlineDesc dsc, int nseg, int coef_off, int ptr_off, int k, dou
 // a second descriptor copy.  Same per-element arithmetic as two k_wsum launches.
 template <int DT, int MODE, int U, int S, bool PF>
 __global__ void __launch_bounds__(kBlock)
-k_wsum_pair(const Seg* __restrict__ segs0, const void* const* __restrict__ ptrs0, int64_t sstr0,
-            const Seg* __restrict__ segs1, const void* const* __restrict__ ptrs1, int64_t sstr1, int64_t tiles1,
-            const double* __restrict__ coef, int k, double divisor) {
+k_wsum_pair(const Seg* __restrict__ segs0, int nseg0, const void* const* __restrict__ ptrs0, int64_t sstr0,
+            const Seg* __restrict__ segs1, int nseg1, const void* const* __restrict__ ptrs1, int64_t sstr1,
+            int64_t tiles1, const double* __restrict__ coef, int k, double divisor) {
   const int64_t t = blockIdx.x;
   if (t < tiles1)
-    wsum_tile<FA_DTYPE_I64, MODE, 8, 1, true, false>(segs1, 1, coef, ptrs1, k, divisor, sstr1, t);
+    wsum_tile<FA_DTYPE_I64, MODE, 8, 1, true, false>(segs1, nseg1, coef, ptrs1, k, divisor, sstr1, t);
   else
-    wsum_tile<DT, MODE, U, S, true, PF>(segs0, 1, coef, ptrs0, k, divisor, sstr0, t - tiles1);
+    wsum_tile<DT, MODE, U, S, true, PF>(segs0, nseg0, coef, ptrs0, k, divisor, sstr0, t - tiles1);
 }
 
-// k_wsum_pair with its tables as the kernel argument (layout: Seg[2] | coef[k] | ptrs0[k] | ptrs1[k])
+// k_wsum_pair with its tables as the kernel argument (layout of PairTables)
 template <int DT, int MODE, int U, int S, bool PF>
 __global__ void __launch_bounds__(kBlock)
-k_wsum_pair_inl(const InlineDesc dsc, int coef_off, int ptr_off, int64_t sstr0, int64_t sstr1, int64_t tiles1,
-                int k, double divisor) {
+k_wsum_pair_inl(const InlineDesc dsc, int nseg0, int nseg1, int seg1_off, int coef_off, int ptr0_off, int ptr1_off,
+                int64_t sstr0, int64_t sstr1, int64_t tiles1, int k, double divisor) {
   const char* b = dsc.raw;
-  const Seg* sg = (const Seg*)b;
   const double* coef = (const double*)(b + coef_off);
-  const void* const* p = (const void* const*)(b + ptr_off);
   const int64_t t = blockIdx.x;
   if (t < tiles1)
-    wsum_tile<FA_DTYPE_I64, MODE, 8, 1, true, false>(sg + 1, 1, coef, p + k, k, divisor, sstr1, t);
+    wsum_tile<FA_DTYPE_I64, MODE, 8, 1, true, false>((const Seg*)(b + seg1_off), nseg1, coef,
+                                                     (const void* const*)(b + ptr1_off), k, divisor, sstr1, t);
   else
-    wsum_tile<DT, MODE, U, S, true, PF>(sg, 1, coef, p, k, divisor, sstr0, t - tiles1);
+    wsum_tile<DT, MODE, U, S, true, PF>((const Seg*)b, nseg0, coef, (const void* const*)(b + ptr0_off), k, divisor,
+                                        sstr0, t - tiles1);
 }
 
 // --------------------------------------------------------------------------------------------
@@ -1227,47 +1227,143 @@ int fa_weighted_sum_tiled(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t k
 
 extern "C++" {
 namespace {
-template <int DT, int MODE>
-void launch_pair(bool k16, int64_t tiles, hipStream_t st, const Seg* s0, const void* const* p0, int64_t sstr0,
-                 const Seg* s1, const void* const* p1, int64_t sstr1, int64_t tiles1, const double* coef, int k,
-                 double divisor) {
-  if (k16)  // variant 5 (automatic choice for K <= 16, see wsum_impl)
-    hipLaunchKernelGGL((k_wsum_pair<DT, MODE, 8, 2, false>), dim3((unsigned)tiles), dim3(kBlock), 0, st, s0, p0,
-                       sstr0, s1, p1, sstr1, tiles1, coef, k, divisor);
+// Tables of a pair launch: Seg0[nseg0] | Seg1[nseg1] | coef[k] | ptrs0[nseg0*k] | ptrs1[nseg1*k]
+struct PairTables { int seg1, coef, ptr0, ptr1; size_t bytes; };
+
+struct PairArgs {
+  int nseg0, nseg1;
+  int64_t sstr0, sstr1, tiles1;
+  int k;
+  double divisor;
+};
+
+template <int DT, int MODE, int S>
+void launch_pair(int64_t tiles, hipStream_t st, const char* dev, const InlineDesc* dsc, const PairTables& L,
+                 const PairArgs& a) {
+  if (dsc)
+    hipLaunchKernelGGL((k_wsum_pair_inl<DT, MODE, 8, S, false>), dim3((unsigned)tiles), dim3(kBlock), 0, st, *dsc,
+                       a.nseg0, a.nseg1, L.seg1, L.coef, L.ptr0, L.ptr1, a.sstr0, a.sstr1, a.tiles1, a.k, a.divisor);
   else
-    hipLaunchKernelGGL((k_wsum_pair<DT, MODE, 8, 1, false>), dim3((unsigned)tiles), dim3(kBlock), 0, st, s0, p0,
-                       sstr0, s1, p1, sstr1, tiles1, coef, k, divisor);
+    hipLaunchKernelGGL((k_wsum_pair<DT, MODE, 8, S, false>), dim3((unsigned)tiles), dim3(kBlock), 0, st,
+                       (const Seg*)dev, a.nseg0, (const void* const*)(dev + L.ptr0), a.sstr0,
+                       (const Seg*)(dev + L.seg1), a.nseg1, (const void* const*)(dev + L.ptr1), a.sstr1, a.tiles1,
+                       (const double*)(dev + L.coef), a.k, a.divisor);
 }
 
 template <int DT>
-void pair_modes(int mode, bool k16, int64_t tiles, hipStream_t st, const Seg* s0, const void* const* p0,
-                int64_t sstr0, const Seg* s1, const void* const* p1, int64_t sstr1, int64_t tiles1,
-                const double* coef, int k, double divisor) {
+void pair_modes(int mode, bool k16, int64_t tiles, hipStream_t st, const char* dev, const InlineDesc* dsc,
+                const PairTables& L, const PairArgs& a) {
+#define FA_PM(MODE) (k16 ? launch_pair<DT, MODE, 2>(tiles, st, dev, dsc, L, a) : launch_pair<DT, MODE, 1>(tiles, st, dev, dsc, L, a))
   switch (mode) {
-    case FA_MODE_MUL_W: launch_pair<DT, FA_MODE_MUL_W>(k16, tiles, st, s0, p0, sstr0, s1, p1, sstr1, tiles1, coef, k, divisor); break;
-    case FA_MODE_MUL_N_DIV_N: launch_pair<DT, FA_MODE_MUL_N_DIV_N>(k16, tiles, st, s0, p0, sstr0, s1, p1, sstr1, tiles1, coef, k, divisor); break;
-    default: launch_pair<DT, FA_MODE_SUM>(k16, tiles, st, s0, p0, sstr0, s1, p1, sstr1, tiles1, coef, k, divisor); break;
+    case FA_MODE_MUL_W: FA_PM(FA_MODE_MUL_W); break;
+    case FA_MODE_MUL_N_DIV_N: FA_PM(FA_MODE_MUL_N_DIV_N); break;
+    default: FA_PM(FA_MODE_SUM); break;
   }
-}
-template <int DT, int MODE>
-void launch_pair_inl(bool k16, int64_t tiles, hipStream_t st, const InlineDesc& dsc, int co, int po, int64_t sstr0,
-                     int64_t sstr1, int64_t tiles1, int k, double divisor) {
-  if (k16)
-    hipLaunchKernelGGL((k_wsum_pair_inl<DT, MODE, 8, 2, false>), dim3((unsigned)tiles), dim3(kBlock), 0, st, dsc, co,
-                       po, sstr0, sstr1, tiles1, k, divisor);
-  else
-    hipLaunchKernelGGL((k_wsum_pair_inl<DT, MODE, 8, 1, false>), dim3((unsigned)tiles), dim3(kBlock), 0, st, dsc, co,
-                       po, sstr0, sstr1, tiles1, k, divisor);
+#undef FA_PM
 }
 
-template <int DT>
-void pair_modes_inl(int mode, bool k16, int64_t tiles, hipStream_t st, const InlineDesc& dsc, int co, int po,
-                    int64_t sstr0, int64_t sstr1, int64_t tiles1, int k, double divisor) {
-  switch (mode) {
-    case FA_MODE_MUL_W: launch_pair_inl<DT, FA_MODE_MUL_W>(k16, tiles, st, dsc, co, po, sstr0, sstr1, tiles1, k, divisor); break;
-    case FA_MODE_MUL_N_DIV_N: launch_pair_inl<DT, FA_MODE_MUL_N_DIV_N>(k16, tiles, st, dsc, co, po, sstr0, sstr1, tiles1, k, divisor); break;
-    default: launch_pair_inl<DT, FA_MODE_SUM>(k16, tiles, st, dsc, co, po, sstr0, sstr1, tiles1, k, divisor); break;
+// A float dtype group (nseg0 segments) and the int64 group (nseg1 segments) of the same k clients in
+// one launch; the int64 tiles first.  sstr = 0: one flat vector per segment and client, else the
+// tiled-arena stride.
+int pair_impl(fa_ctx* ctx, int dtype, int mode, int32_t nseg0, const int64_t* numel0, int32_t nseg1,
+              const int64_t* numel1, int32_t k, const void* const* d_in0, const void* const* d_in1, int64_t sstr0,
+              int64_t sstr1, const double* coef, double divisor, void* const* d_out0, void* const* d_out1,
+              void* hip_stream) {
+  if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (k <= 0) return fail(FA_ERR_INVALID, "k must be > 0 (got %d)", k);
+  if (nseg0 < 0 || nseg1 < 0 || (nseg0 && (!numel0 || !d_in0 || !d_out0)) || (nseg1 && (!numel1 || !d_in1 || !d_out1)))
+    return fail(FA_ERR_INVALID, "fa_weighted_sum_pair: NULL table");
+  if (dtype != FA_DTYPE_F32 && dtype != FA_DTYPE_BF16 && dtype != FA_DTYPE_F16 && dtype != FA_DTYPE_F64)
+    return fail(FA_ERR_DTYPE, "fa_weighted_sum_pair: dtype %d not supported (F32, BF16, F16, F64)", dtype);
+  if (mode < FA_MODE_MUL_W || mode > FA_MODE_SUM) return fail(FA_ERR_DTYPE, "unknown mode %d", mode);
+  if (mode != FA_MODE_SUM && !coef) return fail(FA_ERR_INVALID, "coef is NULL for a weighted mode");
+  const int64_t strides[2] = {sstr0, sstr1};
+  for (int g = 0; g < 2; ++g)
+    if (strides[g] < 0 || strides[g] % FA_TILE_BYTES)
+      return fail(FA_ERR_INVALID, "tile_stride must be 0 (row-major) or a positive multiple of %d (got %lld)",
+                  FA_TILE_BYTES, (long long)strides[g]);
+  const bool k16 = k <= 16;
+  const int nsg[2] = {nseg0, nseg1};
+  const int64_t* numel[2] = {numel0, numel1};
+  const void* const* din[2] = {d_in0, d_in1};
+  void* const* dout[2] = {d_out0, d_out1};
+  const int64_t te[2] = {(int64_t)kBlock * elems_per_vec(dtype) * (k16 ? 2 : 1),
+                         (int64_t)kBlock * elems_per_vec(FA_DTYPE_I64)};
+  int live[2] = {0, 0};
+  int64_t tiles[2] = {0, 0};
+  for (int g = 0; g < 2; ++g)
+    for (int s = 0; s < nsg[g]; ++s) {
+      if (numel[g][s] < 0) return fail(FA_ERR_INVALID, "group %d segment %d has negative numel", g, s);
+      if (numel[g][s] == 0) continue;
+      if (!dout[g][s]) return fail(FA_ERR_INVALID, "group %d segment %d: output is NULL", g, s);
+      for (int i = 0; i < k; ++i)
+        if (!din[g][(int64_t)s * k + i]) return fail(FA_ERR_INVALID, "group %d segment %d client %d: input NULL", g, s, i);
+      ++live[g];
+      tiles[g] += (numel[g][s] + te[g] - 1) / te[g];
+    }
+  if (live[0] == 0 || live[1] == 0) {  // one group: the ordinary launch
+    if (live[0]) return wsum_impl(ctx, dtype, mode, nseg0, numel0, k, d_in0, coef, divisor, d_out0, hip_stream, sstr0);
+    if (live[1]) return wsum_impl(ctx, FA_DTYPE_I64, mode, nseg1, numel1, k, d_in1, coef, divisor, d_out1, hip_stream, sstr1);
+    return FA_OK;
   }
+  if (tiles[0] + tiles[1] > 0x7FFFFFFFll) return fail(FA_ERR_INVALID, "too many tiles");
+  PairTables L;
+  L.seg1 = (int)(sizeof(Seg) * live[0]);
+  L.coef = (int)align16(sizeof(Seg) * (live[0] + live[1]));
+  L.ptr0 = L.coef + (int)align16(sizeof(double) * k);
+  L.ptr1 = L.ptr0 + (int)(sizeof(void*) * live[0] * k);
+  L.bytes = (size_t)L.ptr1 + sizeof(void*) * live[1] * (size_t)k;
+  DeviceGuard dg(ctx->device);
+  if (!dg.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
+  hipStream_t st = (hipStream_t)hip_stream;
+  const bool inl = L.bytes <= (size_t)kInlineBytes && inline_enabled();
+  InlineDesc dsc;
+  fa_ctx::Slot* slot = nullptr;
+  int rc = FA_OK;
+  if (!inl) {
+    rc = acquire_slot(ctx, L.bytes, &slot);
+    if (rc) return rc;
+  }
+  char* h = inl ? dsc.raw : (char*)slot->host;
+  double* hc = (double*)(h + L.coef);
+  for (int i = 0; i < k; ++i) hc[i] = coef ? coef[i] : 0.0;
+  for (int g = 0; g < 2; ++g) {
+    Seg* hs = (Seg*)(h + (g ? L.seg1 : 0));
+    const void** hp = (const void**)(h + (g ? L.ptr1 : L.ptr0));
+    int j = 0;
+    int64_t t0 = 0;
+    for (int s = 0; s < nsg[g]; ++s) {
+      const int64_t n = numel[g][s];
+      if (n == 0) continue;
+      bool aligned = al16(dout[g][s]);
+      for (int i = 0; i < k; ++i) {
+        const void* q = din[g][(int64_t)s * k + i];
+        hp[(int64_t)j * k + i] = q;
+        aligned = aligned && al16(q);
+      }
+      if (strides[g] && !aligned) return fail(FA_ERR_INVALID, "tiled inputs and the output must be 16-byte aligned");
+      hs[j] = Seg{n, t0, dout[g][s], j * k, aligned ? 1 : 0};
+      t0 += (n + te[g] - 1) / te[g];
+      ++j;
+    }
+  }
+  const char* dev = nullptr;
+  if (!inl) {
+    rc = stage(slot, L.bytes, st);
+    if (rc) return rc;
+    dev = (const char*)slot->dev;
+  }
+  const PairArgs a{live[0], live[1], sstr0, sstr1, tiles[1], k, divisor};
+  const int64_t total = tiles[0] + tiles[1];
+  const InlineDesc* dp = inl ? &dsc : nullptr;
+  switch (dtype) {
+    case FA_DTYPE_F32: pair_modes<FA_DTYPE_F32>(mode, k16, total, st, dev, dp, L, a); break;
+    case FA_DTYPE_BF16: pair_modes<FA_DTYPE_BF16>(mode, k16, total, st, dev, dp, L, a); break;
+    case FA_DTYPE_F16: pair_modes<FA_DTYPE_F16>(mode, k16, total, st, dev, dp, L, a); break;
+    case FA_DTYPE_F64: pair_modes<FA_DTYPE_F64>(mode, k16, total, st, dev, dp, L, a); break;
+  }
+  FA_HIP(hipGetLastError());
+  return inl ? FA_OK : release(slot, st);
 }
 }  // namespace
 }  // extern "C++"
@@ -1276,89 +1372,19 @@ int fa_weighted_sum_pair(fa_ctx* ctx, int dtype, int mode, int64_t n, int64_t n_
                          const void* const* d_in, const void* const* d_in_i64, int64_t tile_stride,
                          int64_t tile_stride_i64, const double* coef, double divisor, void* d_out,
                          void* d_out_i64, void* hip_stream) {
-  if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
-  if (k <= 0) return fail(FA_ERR_INVALID, "k must be > 0 (got %d)", k);
   if (n < 0 || n_i64 < 0) return fail(FA_ERR_INVALID, "n must be >= 0");
-  if (!d_in || !d_in_i64 || !d_out || !d_out_i64) return fail(FA_ERR_INVALID, "fa_weighted_sum_pair: NULL table");
-  if (dtype != FA_DTYPE_F32 && dtype != FA_DTYPE_BF16 && dtype != FA_DTYPE_F16 && dtype != FA_DTYPE_F64)
-    return fail(FA_ERR_DTYPE, "fa_weighted_sum_pair: dtype %d not supported (F32, BF16, F16, F64)", dtype);
-  if (mode < FA_MODE_MUL_W || mode > FA_MODE_SUM) return fail(FA_ERR_DTYPE, "unknown mode %d", mode);
-  if (mode != FA_MODE_SUM && !coef) return fail(FA_ERR_INVALID, "coef is NULL for a weighted mode");
-  const int64_t strides[2] = {tile_stride, tile_stride_i64};
-  for (int g = 0; g < 2; ++g)
-    if (strides[g] < 0 || strides[g] % FA_TILE_BYTES)
-      return fail(FA_ERR_INVALID, "tile_stride must be 0 (row-major) or a positive multiple of %d (got %lld)",
-                  FA_TILE_BYTES, (long long)strides[g]);
-  if (n == 0 || n_i64 == 0) {  // one group: the ordinary launch
-    if (n == 0 && n_i64 == 0) return FA_OK;
-    return n ? wsum_impl(ctx, dtype, mode, 1, &n, k, d_in, coef, divisor, &d_out, hip_stream, tile_stride)
-             : wsum_impl(ctx, FA_DTYPE_I64, mode, 1, &n_i64, k, d_in_i64, coef, divisor, &d_out_i64, hip_stream,
-                         tile_stride_i64);
-  }
-  const bool k16 = k <= 16;
-  const int64_t te0 = (int64_t)kBlock * elems_per_vec(dtype) * (k16 ? 2 : 1);
-  const int64_t te1 = (int64_t)kBlock * elems_per_vec(FA_DTYPE_I64);
-  const int64_t tiles0 = (n + te0 - 1) / te0, tiles1 = (n_i64 + te1 - 1) / te1;
-  if (tiles0 + tiles1 > 0x7FFFFFFFll) return fail(FA_ERR_INVALID, "too many tiles");
-  bool al[2] = {al16(d_out), al16(d_out_i64)};
-  for (int i = 0; i < k; ++i) {
-    if (!d_in[i] || !d_in_i64[i]) return fail(FA_ERR_INVALID, "client %d: input NULL", i);
-    al[0] = al[0] && al16(d_in[i]);
-    al[1] = al[1] && al16(d_in_i64[i]);
-  }
-  for (int g = 0; g < 2; ++g)
-    if (strides[g] && !al[g]) return fail(FA_ERR_INVALID, "tiled inputs and the output must be 16-byte aligned");
-  const size_t seg_bytes = align16(sizeof(Seg) * 2);
-  const size_t coef_bytes = align16(sizeof(double) * k);
-  const size_t ptr_bytes = sizeof(void*) * 2 * (size_t)k;
-  const size_t bytes = seg_bytes + coef_bytes + ptr_bytes;
-  DeviceGuard g(ctx->device);
-  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
-  hipStream_t st = (hipStream_t)hip_stream;
-  const bool inl = bytes <= (size_t)kInlineBytes && inline_enabled();
-  InlineDesc dsc;
-  fa_ctx::Slot* slot = nullptr;
-  int rc = FA_OK;
-  if (!inl) {
-    rc = acquire_slot(ctx, bytes, &slot);
-    if (rc) return rc;
-  }
-  char* h = inl ? dsc.raw : (char*)slot->host;
-  Seg* hs = (Seg*)h;
-  hs[0] = Seg{n, 0, d_out, 0, al[0] ? 1 : 0};
-  hs[1] = Seg{n_i64, 0, d_out_i64, 0, al[1] ? 1 : 0};
-  double* hc = (double*)(h + seg_bytes);
-  for (int i = 0; i < k; ++i) hc[i] = coef ? coef[i] : 0.0;
-  memcpy(h + seg_bytes + coef_bytes, d_in, sizeof(void*) * k);
-  memcpy(h + seg_bytes + coef_bytes + sizeof(void*) * k, d_in_i64, sizeof(void*) * k);
-  const int64_t tiles = tiles0 + tiles1;
-  if (inl) {
-    const int co = (int)seg_bytes, po = (int)(seg_bytes + coef_bytes);
-    switch (dtype) {
-      case FA_DTYPE_F32: pair_modes_inl<FA_DTYPE_F32>(mode, k16, tiles, st, dsc, co, po, tile_stride, tile_stride_i64, tiles1, k, divisor); break;
-      case FA_DTYPE_BF16: pair_modes_inl<FA_DTYPE_BF16>(mode, k16, tiles, st, dsc, co, po, tile_stride, tile_stride_i64, tiles1, k, divisor); break;
-      case FA_DTYPE_F16: pair_modes_inl<FA_DTYPE_F16>(mode, k16, tiles, st, dsc, co, po, tile_stride, tile_stride_i64, tiles1, k, divisor); break;
-      case FA_DTYPE_F64: pair_modes_inl<FA_DTYPE_F64>(mode, k16, tiles, st, dsc, co, po, tile_stride, tile_stride_i64, tiles1, k, divisor); break;
-    }
-    FA_HIP(hipGetLastError());
-    return FA_OK;
-  }
-  rc = stage(slot, bytes, st);
-  if (rc) return rc;
-  char* d = (char*)slot->dev;
-  const Seg* ds = (const Seg*)d;
-  const double* dc = (const double*)(d + seg_bytes);
-  const void* const* dp = (const void* const*)(d + seg_bytes + coef_bytes);
-#define FA_P(DT) pair_modes<DT>(mode, k16, tiles, st, ds, dp, tile_stride, ds + 1, dp + k, tile_stride_i64, tiles1, dc, k, divisor)
-  switch (dtype) {
-    case FA_DTYPE_F32: FA_P(FA_DTYPE_F32); break;
-    case FA_DTYPE_BF16: FA_P(FA_DTYPE_BF16); break;
-    case FA_DTYPE_F16: FA_P(FA_DTYPE_F16); break;
-    case FA_DTYPE_F64: FA_P(FA_DTYPE_F64); break;
-  }
-#undef FA_P
-  FA_HIP(hipGetLastError());
-  return release(slot, st);
+  void* o0[1] = {d_out};
+  void* o1[1] = {d_out_i64};
+  return pair_impl(ctx, dtype, mode, 1, &n, 1, &n_i64, k, d_in, d_in_i64, tile_stride, tile_stride_i64, coef,
+                   divisor, d_out ? o0 : nullptr, d_out_i64 ? o1 : nullptr, hip_stream);
+}
+
+int fa_weighted_sum_pair_multi(fa_ctx* ctx, int dtype, int mode, int32_t num_segments, const int64_t* seg_numel,
+                               int32_t num_segments_i64, const int64_t* seg_numel_i64, int32_t k,
+                               const void* const* d_in, const void* const* d_in_i64, const double* coef,
+                               double divisor, void* const* d_out, void* const* d_out_i64, void* hip_stream) {
+  return pair_impl(ctx, dtype, mode, num_segments, seg_numel, num_segments_i64, seg_numel_i64, k, d_in, d_in_i64, 0,
+                   0, coef, divisor, d_out, d_out_i64, hip_stream);
 }
 
 namespace {

@@ -480,6 +480,28 @@ class AggEngine:
             N.ctypes.cast(out_ptrs.data_ptr(), N._P_vp), self._stream(stream))
         N.check(rc, "fa_weighted_sum_multi")
 
+    def weighted_sum_table_pair(self, dtype_code: int, mode: int, numel0: torch.Tensor, in0: torch.Tensor,
+                                out0: torch.Tensor, numel1: torch.Tensor, in1: torch.Tensor, out1: torch.Tensor,
+                                k: int, coef: Optional[Sequence[float]] = None, divisor: float = 1.0,
+                                stream=None) -> None:
+        """A float group and the int64 group of a state_dict (prebuilt host tables as in
+        weighted_sum_table) in ONE launch (fa_weighted_sum_pair_multi)."""
+        for nm, it, ot in ((numel0, in0, out0), (numel1, in1, out1)):
+            T = nm.numel()
+            assert nm.dtype == torch.int64 and nm.is_contiguous()
+            assert it.dtype == torch.int64 and it.numel() == T * k and it.is_contiguous()
+            assert ot.dtype == torch.int64 and ot.numel() == T and ot.is_contiguous()
+        if mode != SUM and (coef is None or len(coef) != k):
+            raise ValueError("weighted_sum: need one coefficient per client")
+        c = N.f64_array(coef if coef is not None else [0.0] * k)
+        cast = N.ctypes.cast
+        rc = self._lib.fa_weighted_sum_pair_multi(
+            self._ctx, int(dtype_code), int(mode), numel0.numel(), cast(numel0.data_ptr(), N._P_i64),
+            numel1.numel(), cast(numel1.data_ptr(), N._P_i64), k, cast(in0.data_ptr(), N._P_vp),
+            cast(in1.data_ptr(), N._P_vp), c, float(divisor), cast(out0.data_ptr(), N._P_vp),
+            cast(out1.data_ptr(), N._P_vp), self._stream(stream))
+        N.check(rc, "fa_weighted_sum_pair_multi")
+
     # ------------------------------------------------------------------ mixing / gossip
     def mix(self, xs: Sequence[torch.Tensor], row_ptr: Sequence[int], cols: Sequence[int],
             vals: Sequence[float], post_scale: Optional[Sequence[float]] = None,

@@ -78,6 +78,16 @@ def _aggregate_device(keys, ptrs, numel, codes, shapes, dev, k, mode, coef, divi
     for t, c in enumerate(code_list):
         groups.setdefault(c, []).append(t)
     table = ptrs.view(len(keys), k)
+    if len(groups) == 2 and 4 in groups and min(groups) in (0, 1, 2, 3):
+        # a float group + the int64 BatchNorm counters: one launch (fa_weighted_sum_pair_multi)
+        fc = min(groups)
+        tabs = []
+        for c in (fc, 4):
+            sel = torch.tensor(groups[c], dtype=torch.int64)
+            tabs += [numel.index_select(0, sel).contiguous(), table.index_select(0, sel).reshape(-1).contiguous(),
+                     optrs.index_select(0, sel).contiguous()]
+        eng.weighted_sum_table_pair(fc, mode, *tabs, k=k, coef=coef, divisor=divisor)
+        return OrderedDict(zip(keys, views))
     for c, idx in groups.items():
         if len(idx) == len(keys):
             eng.weighted_sum_table(c, mode, numel, k, ptrs, optrs, coef, divisor)

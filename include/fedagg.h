@@ -145,6 +145,15 @@ int fa_weighted_sum_pair(fa_ctx *ctx, int dtype, int mode, int64_t n, int64_t n_
                          const void *const *d_in, const void *const *d_in_i64, int64_t tile_stride,
                          int64_t tile_stride_i64, const double *coef, double divisor, void *d_out,
                          void *d_out_i64, void *hip_stream);
+/* The same for a whole state_dict held as separate tensors (fa_weighted_sum_multi's tables, one
+ * per group): num_segments float tensors (seg_numel[s], d_in[s*k + i], d_out[s]) and
+ * num_segments_i64 int64 tensors (seg_numel_i64, d_in_i64, d_out_i64), one launch.  Replaces the
+ * same per-key loop (agg_operator.py:37-44) over a model with BatchNorm counters. */
+int fa_weighted_sum_pair_multi(fa_ctx *ctx, int dtype, int mode, int32_t num_segments,
+                               const int64_t *seg_numel, int32_t num_segments_i64,
+                               const int64_t *seg_numel_i64, int32_t k, const void *const *d_in,
+                               const void *const *d_in_i64, const double *coef, double divisor,
+                               void *const *d_out, void *const *d_out_i64, void *hip_stream);
 
 /*
  * Two-level (grouped) reduction in one pass, one flat vector per client:

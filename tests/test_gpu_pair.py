@@ -146,3 +146,35 @@ def test_inline_descriptors_match_staged(tmp_path):
     assert len(res["1"]) == len(res["0"]) == 36
     for a, b in zip(res["1"], res["0"]):
         assert bits_equal(a, b)
+
+
+@pytest.mark.parametrize("fdt", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
+@pytest.mark.parametrize("mode", [MUL_W, MUL_N_DIV_N, SUM])
+@pytest.mark.parametrize("k", [3, 17])
+def test_state_dict_pair_multi_vs_oracle(fdt, mode, k):
+    """Device state_dicts with BatchNorm counters (the drop-in agg() path): the float keys and the
+    int64 keys aggregate in one fa_weighted_sum_pair_multi launch; every key equals the oracle."""
+    from oracle import orc
+    from fedml_amd.ml.aggregator.state_dict_agg import aggregate
+    g = torch.Generator().manual_seed(k + 7 * mode)
+    spec = [("conv.w", (16, 3, 3, 3)), ("bn.w", (16,)), ("bn.n", ()), ("fc.w", (10, 1000)), ("bn2.n", ()),
+            ("big", (70001,)), ("cnt", (5,)), ("tail", (3,))]
+    dicts = []
+    for _ in range(k):
+        d = OrderedDict()
+        for name, shape in spec:
+            if name.endswith(".n") or name == "cnt":
+                d[name] = torch.randint(0, 5000, shape, generator=g, dtype=torch.int64).cuda()
+            else:
+                d[name] = torch.randn(shape, generator=g, dtype=torch.float64).to(fdt).cuda()
+        dicts.append(d)
+    counts = [60 + 31 * i for i in range(k)]
+    N = sum(counts)
+    coef = None if mode == SUM else ([c / N for c in counts] if mode == MUL_W else [float(c) for c in counts])
+    div = float(N) if mode == MUL_N_DIV_N else 1.0
+    got = aggregate(dicts, mode, coef, div)
+    assert list(got) == [n for n, _ in spec]
+    for name, shape in spec:
+        exp = orc.weighted_sum([d[name].cpu() for d in dicts], mode, coef, div)
+        assert got[name].shape == torch.Size(shape) and got[name].dtype == exp.dtype, name
+        assert bits_equal(got[name].cpu(), exp), name
