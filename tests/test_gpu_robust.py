@@ -108,6 +108,29 @@ def test_median_16bit_packed_and_unaligned(eng, dtype, k, off):
         assert torch.equal(o.cpu().view(torch.int16), exp.view(torch.int16))
 
 
+@pytest.mark.parametrize("k", [1, 2, 5, 8, 17, 32, 33])
+@pytest.mark.parametrize("off", [0, 1])
+def test_median_f32_ragged_and_unaligned(eng, k, off):
+    """fp32 columns at 8-byte and 4-byte offsets, odd / tiny segment lengths, NaN, +-0, ties, +-Inf,
+    K across the network buckets -- bit-exact."""
+    from oracle import orc
+    g = torch.Generator().manual_seed(11 * k + off)
+    sizes = [1, 2, 3, 257, 4096, 3001]
+    cols = [_column_data(g, k, n, torch.float32, zeros=0.15) for n in sizes]
+    segs = []
+    for c in cols:
+        views = []
+        for x in c:
+            buf = torch.zeros(x.numel() + off + 3, dtype=torch.float32, device=DEV)
+            buf[off:off + x.numel()] = x.to(DEV)
+            views.append(buf[off:off + x.numel()])
+        segs.append(views)
+    outs = eng.coord_median(segs)
+    for c, o in zip(cols, outs):
+        exp = orc.coord_median(c)
+        assert torch.equal(o.cpu().view(torch.int32), exp.view(torch.int32))
+
+
 def test_median_all_zero_columns(eng):
     """Columns of only +-0 in every sign pattern: ATen returns the zero of rank (K-1)/2 by index."""
     from oracle import orc
