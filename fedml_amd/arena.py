@@ -241,7 +241,8 @@ class ClientArena:
     def aggregate(self, mode: int, coef: Optional[Sequence[float]] = None, divisor: float = 1.0,
                   clients: Optional[Sequence[int]] = None,
                   out: Optional[Dict[torch.dtype, torch.Tensor]] = None) -> "OrderedDict[str, torch.Tensor]":
-        """Ordered reduction over the given client rows (default: all), one launch per dtype group.
+        """Ordered reduction over the given client rows (default: all), one launch per dtype group
+        (one launch in all for a float group + the int64 counter group, fa_weighted_sum_pair).
         ``out`` (optional): preallocated flat output per INPUT dtype group (reused across rounds).
         Returns per-key views of the result in the model's key order."""
         clients = list(range(self.capacity)) if clients is None else list(clients)
