@@ -1065,7 +1065,9 @@ def main():
                                    "resident in HBM"),
             "config": {"workload": wl["name"], "clients": wl["clients"], "params_per_client": wl["params"],
                        "parallelism": f"client-groups x{world}" +
-                                      (f", {args.collective} over RCCL in {args.chunks} chunks"
+                                      (f", {args.collective} over "
+                                       f"{'gloo (one-GPU rehearsal)' if os.environ.get('FEDML_AMD_BENCH_REHEARSAL') else 'RCCL'}"
+                                       f" in {args.chunks} chunks"
                                        + (f", local partials on {args.cu_mask} CUs" if args.cu_mask else "")
                                        if world > 1 else ""),
                        "kernel_variant": args.variant, "layout": args.layout},
