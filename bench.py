@@ -58,10 +58,13 @@ def parse():
     p.add_argument("--cu-mask", type=int, default=192,
                    help="N > 1: run the local partials on a stream restricted to this many CUs (0 = off), "
                         "leaving the rest to RCCL's kernels (fa_stream_create_cu_masked)")
-    p.add_argument("--collective", default="reduce_scatter", choices=["reduce", "reduce_scatter", "all_reduce", "ordered"],
-                   help="group -> global exchange for N > 1 (fedml_amd/distributed/group_reduce.py): reduce_scatter "
-                        "leaves the global model partitioned over the GPUs with the least xGMI traffic per link; "
-                        "reduce = the reference NCCL simulator's reduce to rank 0; all_reduce = replicated")
+    p.add_argument("--collective", default="ordered",
+                   choices=["ordered", "ordered_all", "reduce", "reduce_scatter", "all_reduce"],
+                   help="group -> global exchange for N > 1 (fedml_amd/distributed/group_reduce.py): ordered = the "
+                        "full global model on rank 0, summed in rank order by the other ranks (bit-exact); "
+                        "ordered_all = the same on every rank; reduce = RCCL's reduce to rank 0 (the reference "
+                        "NCCL simulator's call); reduce_scatter = the global model left SHARDED over the GPUs "
+                        "(no rank holds all of it); all_reduce = RCCL all-reduce")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     p.add_argument("--check-samples", type=int, default=65536)
@@ -174,10 +177,28 @@ def make_tiled_arena(idx, P, dtype=torch.float32):
     return arena
 
 
-def tiled_gather(buf, row, idx):
-    """Logical elements ``idx`` of client row ``row`` of a tiled arena group [tiles, capacity, E]."""
-    _, cap, E = buf.shape
-    return buf.view(-1).index_select(0, (idx // E) * (cap * E) + row * E + idx % E)
+def sample_tiles(P, count, seed, E=1024):
+    """``count`` distinct 4-KiB tiles (E fp32 elements) of a P-element vector, sorted: the parity
+    sample.  Whole tiles are taken by slicing -- torch's index_select/gather kernels fault on
+    tensors of more than 2^31 elements on this ROCm build (tools/diag_large.py), and a tiled
+    arena group at the metric size holds 16 * 10^9."""
+    nt = -(-P // E)
+    g = torch.Generator().manual_seed(seed)
+    return sorted(torch.randperm(nt, generator=g)[:min(count, nt)].tolist())
+
+
+def flat_pick(x, tiles, P, E=1024):
+    """Elements of the sampled tiles of a flat (or tile-row) device vector, as one CPU tensor."""
+    return torch.cat([x[t * E:min((t + 1) * E, P)] for t in tiles]).cpu()
+
+
+def tiled_pick(buf, tiles, P):
+    """The sampled tiles of EVERY client row of a tiled arena group [tiles, capacity, E]:
+    returns a CPU tensor [capacity, m] (m = sampled elements), row r = flat_pick of client r."""
+    E = buf.shape[2]
+    blk = torch.stack([buf[t] for t in tiles]).cpu()  # [nt, cap, E], each buf[t] one contiguous run
+    cols = [blk[j, :, :min(E, P - t * E)] for j, t in enumerate(tiles)]
+    return torch.cat(cols, dim=1)
 
 
 def load_layout(name):
@@ -228,8 +249,50 @@ class Timed:
         d = [a.elapsed_time(b) for a, b in self.pairs]
         return float(np.mean(d)) if d else None
 
+    def per_step_ms(self, steps):
+        """Summed kernel time per step (several timed launches per step)."""
+        d = [a.elapsed_time(b) for a, b in self.pairs]
+        return float(np.sum(d)) / steps if d else None
+
 
 # ----------------------------------------------------------------------------- workloads
+def reducer(args, eng, timer, **kw):
+    """The N > 1 group -> global exchange (fedml_amd/distributed/group_reduce.py) with the bench's
+    HIP-event timing on the local partials (the owners' rank-ordered sum of the "ordered"
+    exchange is left out of that average: it is not the dominant kernel)."""
+    from fedml_amd.distributed.group_reduce import GroupReducer
+
+    def untimed_sum(xs_, mode, coef, div, o):
+        return eng.weighted_sum(xs_, mode, coef, div, out=o)
+    return GroupReducer(collective=args.collective, chunks=args.chunks, stream=masked_stream(eng, args),
+                        combine_sum=untimed_sum, **kw)
+
+
+def count_bad(got, exp):
+    """Mismatching elements (bitwise; NaN payloads compared as bits)."""
+    ib = {4: torch.int32, 2: torch.int16, 8: torch.int64}[got.element_size()]
+    return int((got.view(ib) != exp.view(ib)).sum())
+
+
+def sum_over_ranks(v, world):
+    if world == 1:
+        return v
+    import torch.distributed as dist
+    t = torch.tensor([float(v)], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t)
+    return float(t.item())
+
+
+def collective_note(args, world):
+    if world == 1:
+        return ""
+    return {"ordered": "the whole global model on rank 0, rank-ordered sum (bit-exact)",
+            "ordered_all": "the whole global model on every rank, rank-ordered sum (bit-exact)",
+            "reduce": "the whole global model on rank 0 (RCCL reduce order)",
+            "all_reduce": "the whole global model on every rank (RCCL order)",
+            "reduce_scatter": "the global model SHARDED over the ranks, every shard checked"}[args.collective]
+
+
 def wl_metric(args, eng, rank, world, timer):
     """Flat FedAvg K x P fp32 (the metric).  Returns a workload dict."""
     from fedml_amd.engine import MUL_W
@@ -246,12 +309,9 @@ def wl_metric(args, eng, rank, world, timer):
         xs = None
     else:
         xs = make_arena_rows(mine, P) if args.layout == "arena" else make_flat_clients(mine, P)
-    # reduce_scatter stages every rank's whole-tile shard: room for them, allocated once
-    S = -(-P // (world * 1024)) * 1024
-    out = torch.empty(max(P, S * world) if world > 1 and args.collective == "reduce_scatter" else P, device="cuda")
+    out = torch.empty(P, device="cuda")
+    res = {}
     if world > 1:
-        from fedml_amd.distributed.group_reduce import GroupReducer
-
         def timed_sum(xs_, mode, coef, div, o):
             with timer:
                 return eng.weighted_sum(xs_, mode, coef, div, out=o)
@@ -264,10 +324,7 @@ def wl_metric(args, eng, rank, world, timer):
             def weighted_sum_tiled_multi(self, *a, **kw):
                 with timer:
                     return eng.weighted_sum_tiled_multi(*a, **kw)
-        red = GroupReducer(collective=args.collective, chunks=args.chunks, local_sum=timed_sum,
-                           stream=masked_stream(eng, args))
-
-        res = {}
+        red = reducer(args, eng, timer, local_sum=timed_sum)
 
         def step():
             if tiled:
@@ -282,50 +339,58 @@ def wl_metric(args, eng, rank, world, timer):
                     eng.weighted_sum_tiled(buf, rows, MUL_W, w, n=P, out=out)
                 else:
                     eng.weighted_sum(xs, MUL_W, w, out=out)
+            res["g"] = out
         launches = 1
 
     def parity():
+        """The oracle's ordered FedAvg on 64 sampled 4-KiB tiles of the model.  N > 1: the oracle's
+        ordered partial of every rank's clients (regenerated from their seeds), summed in rank
+        order, vs the global model -- on rank 0 (ordered / reduce / all_reduce), or on every rank
+        for its shard (reduce_scatter); RCCL's own summation order (reduce, all_reduce,
+        reduce_scatter) is held to 1e-6 normwise, the rank-ordered exchanges to bit-exactness."""
         if args.check_samples <= 0:
             return None
         from oracle import orc
-        gi = torch.Generator(device="cuda").manual_seed(99)
-        idx = torch.randint(0, P, (args.check_samples,), generator=gi, device="cuda")
-        if world > 1:
-            return parity_multi(idx)
-        if tiled:
-            sampled = [tiled_gather(buf, r, idx).cpu() for r in rows]
-        else:
-            sampled = [x.index_select(0, idx).cpu() for x in xs]
-        exp = orc.weighted_sum(sampled, MUL_W, w)
-        ok = torch.equal(out.index_select(0, idx).cpu().view(torch.int32), exp.view(torch.int32))
-        return f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on {args.check_samples} sampled elements"
+        tiles = sample_tiles(P, max(1, args.check_samples // 1024), 99)
+        if world == 1:
+            sampled = list(tiled_pick(buf, tiles, P)[rows]) if tiled else [flat_pick(x, tiles, P) for x in xs]
+            exp = orc.weighted_sum(sampled, MUL_W, w)
+            bad = count_bad(flat_pick(out, tiles, P), exp)
+            return f"{'bit-exact' if bad == 0 else f'{bad} MISMATCHES'} vs oracle on {exp.numel()} sampled elements"
+        return parity_multi(tiles)
 
-    def parity_multi(idx):
-        """N > 1, rank 0: the oracle's ordered partial of every rank's clients (their updates
-        regenerated from the seeds), summed in rank order, vs rank 0's result -- the whole global
-        model (reduce / all_reduce / ordered) or its shard (reduce_scatter: the sampled elements
-        that fall in it).  RCCL's cross-rank summation order is its own, so the bar is 1e-6
-        normwise (exact for two ranks and for the 'ordered' collective)."""
-        if rank != 0:
-            return None
-        from oracle import orc
-        got_full = res["g"]
-        if args.collective == "reduce_scatter":
-            idx = idx[idx < got_full.numel()]  # rank 0's shard is the global model's first elements
-        parts = []
-        for r in range(world):
-            ids = split(K, r, world)
-            cols = []
-            for i in ids:
-                g = torch.Generator(device="cuda").manual_seed(1000 + i)
-                cols.append(torch.randn(P, generator=g, device="cuda").index_select(0, idx).cpu())
-            parts.append(orc.weighted_sum(cols, MUL_W, [counts[i] / N for i in ids]))
-        exp = orc.weighted_sum(parts, 2)
-        got = got_full.index_select(0, idx).cpu()
-        if torch.equal(got.view(torch.int32), exp.view(torch.int32)):
-            return f"bit-exact vs oracle (rank-ordered partials) on {idx.numel()} sampled elements"
-        rel = float((got.double() - exp.double()).norm() / exp.double().norm())
-        return f"{'within' if rel <= 1e-6 else 'OUTSIDE'} 1e-6 normwise vs oracle (rel {rel:.2e}) on {idx.numel()} sampled elements"
+    def parity_multi(tiles):
+        if args.collective == "reduce_scatter":  # rank r's shard [r*S, min((r+1)*S, P))
+            S = -(-P // (world * 1024)) * 1024
+            lo, hi = rank * S, min(P, (rank + 1) * S)
+            tiles = [t for t in tiles if lo <= t * 1024 < hi]
+        elif rank != 0 and args.collective != "ordered_all" and args.collective != "all_reduce":
+            tiles = []
+        bad = cnt = 0
+        rel = 0.0
+        if tiles:
+            from oracle import orc
+            parts = []
+            for r in range(world):
+                ids = split(K, r, world)
+                cols = []
+                for i in ids:
+                    g = torch.Generator(device="cuda").manual_seed(1000 + i)
+                    cols.append(flat_pick(torch.randn(P, generator=g, device="cuda"), tiles, P))
+                parts.append(orc.weighted_sum(cols, MUL_W, [counts[i] / N for i in ids]))
+            exp = orc.weighted_sum(parts, 2)
+            g_ = res["g"]
+            got = flat_pick(g_, [t - (rank * S // 1024) for t in tiles], g_.numel()) \
+                if args.collective == "reduce_scatter" else flat_pick(g_, tiles, P)
+            bad, cnt = count_bad(got, exp), exp.numel()
+            rel = float((got.double() - exp.double()).norm() / exp.double().norm())
+        bad, cnt = sum_over_ranks(bad, world), sum_over_ranks(cnt, world)
+        rel = max_over_ranks(rel, world)
+        where = collective_note(args, world)
+        if bad == 0:
+            return f"bit-exact vs oracle (rank-ordered partials) on {int(cnt)} sampled elements of {where}"
+        return (f"{'within' if rel <= 1e-6 else 'OUTSIDE'} 1e-6 normwise vs oracle (rel {rel:.2e}, {int(bad)} "
+                f"elements differ in the last bits) on {int(cnt)} sampled elements of {where}")
 
     suffix = {"arena": "", "tiled": "_tiled", "tensors": "_tensors"}[args.layout]
     return dict(name=f"fedavg_flat_K{K}_P{P}_fp32" + suffix,
@@ -335,7 +400,9 @@ def wl_metric(args, eng, rank, world, timer):
 
 
 def wl_layout(args, eng, rank, world, timer):
-    """cfg2 / cfg3: a real state_dict layout, all keys of one dtype in one launch."""
+    """cfg2 / cfg3: a real state_dict layout, all keys of one dtype in one launch.  N > 1: each
+    rank aggregates its clients' arena (one launch per dtype group), and every dtype group's flat
+    partial goes through the pipelined group -> global exchange."""
     from fedml_amd.ml.aggregator.state_dict_agg import MUL_W, aggregate
     resnet = args.config == "resnet18"
     layout = load_layout("resnet18_gn" if resnet else "vit_b16_bf16")
@@ -346,10 +413,10 @@ def wl_layout(args, eng, rank, world, timer):
     w = [counts[i] / N for i in mine]
     dicts = make_layout_clients(mine, layout)
     arena = None
-    if args.layout in ("arena", "tiled"):
+    if args.layout in ("arena", "tiled") or world > 1:
         from fedml_amd.arena import ArenaLayout, ClientArena
         arena = ClientArena(ArenaLayout([(n, tuple(s), getattr(torch, dt)) for n, s, dt in layout]),
-                            capacity=len(mine), tiled=args.layout == "tiled")
+                            capacity=len(mine), tiled=args.layout == "tiled" or world > 1)
         for j, d in enumerate(dicts):
             arena.write(j, d)
         if not arena.tiled:
@@ -360,32 +427,71 @@ def wl_layout(args, eng, rank, world, timer):
     in_b = sum(int(np.prod(s)) * size[dt] for _, s, dt in layout)
     out_b = sum(int(np.prod(s)) * (2 if dt == "bfloat16" else 4) for _, s, dt in layout)
     res = {}
+    if world > 1:
+        class TimedEngine:
+            def weighted_sum_tiled(self, *a, **kw):
+                with timer:
+                    return eng.weighted_sum_tiled(*a, **kw)
+
+            def weighted_sum_tiled_multi(self, *a, **kw):
+                with timer:
+                    return eng.weighted_sum_tiled_multi(*a, **kw)
+        red = reducer(args, eng, timer)
+        te = TimedEngine()
+        rows = list(range(len(mine)))
+        outs = {dt: torch.empty(n, dtype=torch.float32 if dt == torch.int64 else dt, device="cuda")
+                for dt, n in arena.layout.group_numel.items()}
 
     def step():
+        if world > 1:
+            flat = {dt: red.fedavg_tiled(te, arena.bufs[dt], rows, w, n, out=outs[dt])
+                    for dt, n in arena.layout.group_numel.items()}
+            res["out"] = arena.layout.carve(flat) if args.collective != "reduce_scatter" else None
+            return
         with timer:
             res["out"] = arena.aggregate(MUL_W, w) if arena is not None else aggregate(dicts, MUL_W, w)
-        if world > 1:
-            import torch.distributed as dist
-            for t in res["out"].values():
-                dist.reduce(t, dst=0)
 
     def parity():
-        if world > 1:
-            return None
         from oracle import orc
+        if world > 1:
+            if args.collective == "reduce_scatter" or (rank != 0 and args.collective not in ("ordered_all", "all_reduce")):
+                bad = cnt = 0
+            else:  # every client's dict regenerated from its seed, oracle partial per rank, rank-ordered sum
+                bad = cnt = 0
+                keys = layout[:: max(1, len(layout) // 24)]
+                idxs = {name: torch.arange(0, int(np.prod(shape)), max(1, int(np.prod(shape)) // 512), device="cuda")
+                        for name, shape, _ in keys}
+                cols = {}  # (key, client) -> sampled elements
+                for i in range(K):
+                    d = make_layout_clients([i], layout)[0]
+                    for name, _, _ in keys:
+                        cols[name, i] = d[name].reshape(-1).index_select(0, idxs[name]).cpu()
+                    del d
+                for name, _, _ in keys:
+                    parts = [orc.weighted_sum([cols[name, i] for i in split(K, r, world)], MUL_W,
+                                              [counts[i] / N for i in split(K, r, world)]) for r in range(world)]
+                    exp = orc.weighted_sum(parts, 2)
+                    bad += count_bad(res["out"][name].reshape(-1).index_select(0, idxs[name]).cpu(), exp)
+                    cnt += exp.numel()
+            bad, cnt = sum_over_ranks(bad, world), sum_over_ranks(cnt, world)
+            if args.collective == "reduce_scatter":
+                return "not checked (reduce_scatter leaves the state_dict sharded)"
+            return (f"{'bit-exact' if bad == 0 else f'{int(bad)} elements differ (RCCL order)'} vs oracle "
+                    f"(rank-ordered partials) on a strided sample of 24 keys ({int(cnt)} elements) of "
+                    f"{collective_note(args, world)}")
         bad = 0
         for name, shape, dt in layout:
             n = int(np.prod(shape))
             idx = torch.arange(0, n, max(1, n // 512), device="cuda")
             exp = orc.weighted_sum([d[name].reshape(-1).index_select(0, idx).cpu() for d in dicts], MUL_W, w)
             got = res["out"][name].reshape(-1).index_select(0, idx).cpu()
-            ib = {torch.float32: torch.int32, torch.bfloat16: torch.int16}[got.dtype]
-            bad += int((got.view(ib) != exp.view(ib)).sum())
+            bad += count_bad(got, exp)
         return f"{'bit-exact' if bad == 0 else f'{bad} MISMATCHES'} vs oracle on a strided sample of every key"
 
     tag = ("resnet18gn" if resnet else "vitb16_bf16") + {"arena": "", "tiled": "_tiled", "tensors": "_tensors"}[args.layout]
     return dict(name=f"fedavg_{tag}_K{K}_P{P}", dtype="fp32" if resnet else "bf16", step=step, parity=parity,
-                bytes_total=K * in_b + out_b, launch_bytes=None, clients=K, params=P, cpu_K=None)
+                bytes_total=K * in_b + out_b, launch_bytes=None, clients=K, params=P, cpu_K=None,
+                step_bytes=len(mine) * in_b + out_b if world > 1 else None)
 
 
 def wl_dropin_cpu(args, eng, rank, world, timer):
@@ -432,17 +538,24 @@ def wl_dropin_cpu(args, eng, rank, world, timer):
 
     def cpu(budget_s):
         import oracle.torch_port as tp
-        torch.set_num_threads(min(16, os.cpu_count() or 1))
-        best, runs, t_end = float("inf"), 0, time.perf_counter() + budget_s
-        while runs < 3 or (time.perf_counter() < t_end and runs < 30):
-            lst = [(n, OrderedDict((k, v.clone()) for k, v in d.items())) for n, d in zip(counts, dicts)]
+        lists = []
+
+        def run():  # agg() rebinds client 0's dict: fresh shallow copies, made outside the timed call
+            tp.agg("FedAvg", lists.pop())
+
+        def one():
+            lists.append([(n, OrderedDict((k, v.clone()) for k, v in d.items())) for n, d in zip(counts, dicts)])
             t0 = time.perf_counter()
-            tp.agg("FedAvg", lst)
-            best = min(best, time.perf_counter() - t0)
-            runs += 1
-        return {"value": round((K * in_b + out_b) / best / 1e9, 2), "unit": "GB/s", "cores": torch.get_num_threads(),
-                "kind": "port", "sample": f"the same K={K} ResNet-18-GN CPU state_dicts, best of {runs} runs of "
-                                          "oracle/torch_port.agg('FedAvg') (agg_operator.py:35-44)"}
+            run()
+            return time.perf_counter() - t0
+        legs = {}
+        for th in cpu_thread_legs():
+            torch.set_num_threads(th)
+            ts = [one() for _ in range(5)]
+            legs[th] = (min(ts), len(ts))
+        return legs_record(legs, K * in_b + out_b,
+                           f"the same K={K} ResNet-18-GN CPU state_dicts, oracle/torch_port.agg('FedAvg') "
+                           "(agg_operator.py:35-44)")
 
     return dict(name=f"dropin_agg_cpu_resnet18gn_K{K}_P{P}", dtype="fp32", step=step, parity=parity, cpu=cpu,
                 bytes_total=K * in_b + out_b, launch_bytes=None, clients=K, params=P, cpu_K=K,
@@ -512,7 +625,7 @@ def wl_hier(args, eng, rank, world, timer):
     """cfg4: G groups x M clients (ResNet-18 size, flat fp32): group FedAvg (weights n_i/N_g), cloud
     term (G_g * N_g) / N (HierFedAvgCloudAggregator.py:140-157), ordered global sum over groups --
     one fused two-level kernel pass over this rank's clients (fa_weighted_sum_grouped); across
-    ranks (one or more groups each) the partials are SUM-reduced over RCCL."""
+    ranks (one or more groups each) the partials go through the group -> global exchange."""
     from fedml_amd.engine import MUL_N_DIV_N, MUL_W
     G, M = 8, (args.clients or 512) // 8
     P = args.params or RESNET18_P
@@ -531,18 +644,17 @@ def wl_hier(args, eng, rank, world, timer):
     w = [c / gn[j] for j, cs in enumerate(gcounts) for c in cs]
     gptr = [j * M for j in range(len(my_groups) + 1)]
     out = torch.empty(P, device="cuda")
+    res = {}
 
     def timed_grouped(xs_, mode, coef, div, gp, gm, gc, gd, o):
         with timer:
             return eng.weighted_sum_grouped(xs_, mode, coef, div, gp, gm, gc, gd, out=o)
 
     if world > 1:
-        from fedml_amd.distributed.group_reduce import GroupReducer
-        red = GroupReducer(collective=args.collective, chunks=args.chunks, local_grouped=timed_grouped,
-                           stream=masked_stream(eng, args))
+        red = reducer(args, eng, timer, local_grouped=timed_grouped)
 
         def step():
-            red.hierarchical_groups(xs, gcounts, N, out=out)
+            res["g"] = red.hierarchical_groups(xs, gcounts, N, out=out)
         launches = args.chunks
     else:
         def step():
@@ -552,23 +664,50 @@ def wl_hier(args, eng, rank, world, timer):
                                                    [float(N)] * len(gn), n=P, out=out)
             else:
                 timed_grouped(xs, MUL_W, w, 1.0, gptr, MUL_N_DIV_N, gn, [float(N)] * len(gn), out)
+            res["g"] = out
         launches = 1
 
+    def rank_partial(r, tiles):
+        """The oracle's local step of rank r: per group FedAvg, cloud term, ordered sum over its groups."""
+        from oracle import orc
+        terms = []
+        for g in split(G, r, world):
+            cols = []
+            for i in range(g * M, (g + 1) * M):
+                gen = torch.Generator(device="cuda").manual_seed(1000 + i)
+                cols.append(flat_pick(torch.randn(P, generator=gen, device="cuda"), tiles, P))
+            cg = counts[g * M:(g + 1) * M]
+            Gj = orc.weighted_sum(cols, 0, [c / sum(cg) for c in cg])
+            terms.append(orc.weighted_sum([Gj], 1, [sum(cg)], float(N)))
+        return orc.weighted_sum(terms, 2) if len(terms) > 1 else terms[0]
+
     def parity():
-        if world > 1 or args.check_samples <= 0:
+        if args.check_samples <= 0:
             return None
         from oracle import orc
-        gi = torch.Generator(device="cuda").manual_seed(98)
-        idx = torch.randint(0, P, (min(args.check_samples, 8192),), generator=gi, device="cuda")
-        sample = ([tiled_gather(buf, r, idx).cpu() for r in rows] if tiled else
-                  [x.index_select(0, idx).cpu() for x in xs])
-        terms = []
-        for j in range(len(my_groups)):
-            Gj = orc.weighted_sum(sample[gptr[j]:gptr[j + 1]], 0, w[gptr[j]:gptr[j + 1]])
-            terms.append(orc.weighted_sum([Gj], 1, [gn[j]], float(N)))
-        exp = orc.weighted_sum(terms, 2)
-        ok = torch.equal(out.index_select(0, idx).cpu().view(torch.int32), exp.view(torch.int32))
-        return f"{'bit-exact' if ok else 'MISMATCH'} vs oracle (group FedAvg -> cloud term -> ordered sum) on {idx.numel()} sampled elements"
+        tiles = sample_tiles(P, max(1, min(args.check_samples, 8192) // 1024), 98)
+        if world > 1 and (args.collective == "reduce_scatter" or
+                          (rank != 0 and args.collective not in ("ordered_all", "all_reduce"))):
+            tiles = []
+        bad = cnt = 0
+        if tiles:
+            if world == 1 and tiled:  # the arena's own rows (same values as regenerating them)
+                sample = list(tiled_pick(buf, tiles, P)[rows])
+                terms = []
+                for j in range(len(my_groups)):
+                    Gj = orc.weighted_sum(sample[gptr[j]:gptr[j + 1]], 0, w[gptr[j]:gptr[j + 1]])
+                    terms.append(orc.weighted_sum([Gj], 1, [gn[j]], float(N)))
+                exp = orc.weighted_sum(terms, 2)
+            else:
+                parts = [rank_partial(r, tiles) for r in range(world)]
+                exp = orc.weighted_sum(parts, 2) if world > 1 else parts[0]
+            bad, cnt = count_bad(flat_pick(res["g"], tiles, P), exp), exp.numel()
+        bad, cnt = sum_over_ranks(bad, world), sum_over_ranks(cnt, world)
+        if world > 1 and args.collective == "reduce_scatter":
+            return "not checked (reduce_scatter leaves the model sharded)"
+        return (f"{'bit-exact' if bad == 0 else f'{int(bad)} elements differ'} vs oracle (group FedAvg -> cloud "
+                f"term -> ordered sum{' per rank -> rank-ordered sum' if world > 1 else ''}) on {int(cnt)} sampled "
+                f"elements" + (f" of {collective_note(args, world)}" if world > 1 else ""))
 
     return dict(name=f"hier_fedavg_G{G}x{M}_P{P}_fp32" + ("_tiled" if tiled else ""), dtype="fp32", step=step, parity=parity,
                 bytes_total=G * M * P * 4 + P * 4, launch_bytes=(len(clients) * P * 4 + P * 4) / launches,
@@ -576,31 +715,39 @@ def wl_hier(args, eng, rank, world, timer):
 
 
 def wl_gossip(args, eng, rank, world, timer):
-    """cfg5: n = 256 nodes on a ring (W = 1/3), one synchronous DSGD step, models of ResNet-18 size."""
+    """cfg5: n = 256 nodes on a ring (W = 1/3), one synchronous DSGD step, models of ResNet-18 size.
+    Value = compulsory bytes (every model read once, every mixed model written once: 2 n P s) per
+    second; the survey's 4 n P s accounting counts a ring row's three reads
+    separately and would exceed the HBM peak."""
     from fedml_amd.core.distributed.topology.topology_manager import SymmetricTopologyManager, gossip_rows
     n = args.clients or 256
     P = args.params or RESNET18_P
     m = SymmetricTopologyManager(n, 2)
     m.generate_topology()
     W = m.topology
+    rp, cs, vs = gossip_rows(W)
+    tiled = False
+    res = {}
     if world > 1:
         from fedml_amd.distributed.gossip import DistributedGossip
 
-        def timed_mix(xs_, rp, cs, vs, ps, outs, outs2):
+        def timed_mix(xs_, rp_, cs_, vs_, ps, outs, outs2):
             with timer:
-                return eng.mix(xs_, rp, cs, vs, ps, outs, outs2)
+                return eng.mix(xs_, rp_, cs_, vs_, ps, outs, outs2)
         dg = DistributedGossip(W, local_mix=timed_mix)
+        masked_stream(eng, args)
         xs = (make_arena_rows if args.layout in ("arena", "tiled") else make_flat_clients)(dg.mine, P)
+        nodes = dg.mine
 
         def step():
-            dg.step(xs)
+            res["outs"], _ = dg.step(xs)
         rows = len(dg.mine)
     else:
-        rp, cs, vs = gossip_rows(W)
         tiled = args.layout == "tiled"
+        nodes = list(range(n))
         if tiled:  # both the models and the mixed models in tile-interleaved arenas (fa_mix_tiled)
             arena = make_tiled_arena(range(n), P)
-            buf, nodes = arena.bufs[torch.float32], list(range(n))
+            buf = arena.bufs[torch.float32]
             obuf = torch.empty_like(buf)
 
             def step():
@@ -613,32 +760,47 @@ def wl_gossip(args, eng, rank, world, timer):
             def step():
                 with timer:
                     eng.mix(xs, rp, cs, vs, outs=outs)
+                res["outs"] = outs
         rows = n
 
-        def parity():
-            if args.check_samples <= 0:
-                return None
-            from oracle import orc
-            gi = torch.Generator(device="cuda").manual_seed(97)
-            idx = torch.randint(0, P, (min(args.check_samples, 16384),), generator=gi, device="cuda")
-            if tiled:
-                sin = [tiled_gather(buf, r, idx).cpu() for r in nodes]
-                sout = [tiled_gather(obuf, r, idx).cpu() for r in nodes]
-            else:
-                sin = [x.index_select(0, idx).cpu() for x in xs]
-                sout = [o.index_select(0, idx).cpu() for o in outs]
-            exp, _ = orc.mix(sin, rp, cs, vs)
-            bad = sum(int((a.view(torch.int32) != b.view(torch.int32)).sum()) for a, b in zip(sout, exp))
-            return f"{'bit-exact' if bad == 0 else f'{bad} MISMATCHES'} vs oracle (DSGD rows) on {idx.numel()} sampled elements x {n} nodes"
-    # survey §8(d): B = sum_i (deg_i + 1) * P * s + n * P * s  (ring: 4 n P s); compulsory = 2 n P s
-    if world > 1:
-        def parity():
+    def parity():
+        """Every node of this rank (all n at N = 1) vs the oracle's DSGD rows on sampled tiles; the
+        input models are regenerated from their seeds (the in-neighbours of a rank's boundary
+        nodes live on the neighbouring ranks); mismatches summed over the ranks."""
+        if args.check_samples <= 0:
             return None
-        tiled = False
+        from oracle import orc
+        tiles = sample_tiles(P, max(1, min(args.check_samples, 16384) // 1024), 97)
+        if tiled:
+            sin = list(tiled_pick(buf, tiles, P)[:n])
+            sout = list(tiled_pick(obuf, tiles, P)[:n])
+        else:
+            need = sorted({cs[j] for i in nodes for j in range(rp[i], rp[i + 1])})
+            sin = {}
+            for i in need:
+                gen = torch.Generator(device="cuda").manual_seed(1000 + i)
+                sin[i] = flat_pick(torch.randn(P, generator=gen, device="cuda"), tiles, P)
+            hole = torch.zeros_like(next(iter(sin.values())))  # nodes no row of this rank reads
+            sin = [sin.get(i, hole) for i in range(n)]
+            sout = {i: flat_pick(o, tiles, P) for i, o in zip(nodes, res["outs"])}
+        # the oracle's rows of this rank's nodes only
+        prp, pcs, pvs = [0], [], []
+        for i in nodes:
+            pcs += cs[rp[i]:rp[i + 1]]
+            pvs += vs[rp[i]:rp[i + 1]]
+            prp.append(len(pcs))
+        exp, _ = orc.mix(sin, prp, pcs, pvs)
+        bad = sum(count_bad(sout[i], e) for i, e in zip(nodes, exp))
+        cnt = sum(e.numel() for e in exp)
+        bad, cnt = sum_over_ranks(bad, world), sum_over_ranks(cnt, world)
+        return (f"{'bit-exact' if bad == 0 else f'{int(bad)} MISMATCHES'} vs oracle (DSGD rows) on {int(cnt)} "
+                f"sampled elements over all {n} nodes" + (f" ({world} ranks, halo exchange)" if world > 1 else ""))
+
     return dict(name=f"gossip_ring_n{n}_P{P}_fp32" + ("_tiled" if tiled else ""), dtype="fp32", step=step,
-                parity=parity,
-                bytes_total=4 * n * P * 4, launch_bytes=2 * rows * P * 4, clients=n, params=P, cpu_K=None,
-                roofline_note="achieved uses compulsory bytes 2*rows*P*4 (each model read once, written once)")
+                parity=parity, bytes_total=2 * n * P * 4, launch_bytes=2 * rows * P * 4, clients=n, params=P,
+                cpu_K=None, step_bytes=2 * rows * P * 4 if world > 1 else None,
+                roofline_note="compulsory bytes 2*n*P*4 (each model read once, each mixed model written once); "
+                              "the survey's 4*n*P*4 accounting would be 2x these figures")
 
 
 def wl_host(args, eng, rank, world, timer):
@@ -715,8 +877,8 @@ def wl_fedopt(args, eng, rank, world, timer):
         p_dev = torch.randn(n, generator=torch.Generator(device="cuda").manual_seed(6), device="cuda")
         b_dev = torch.zeros(n, device="cuda")
         p_cpu, b_cpu = p_dev.cpu(), b_dev.cpu()
-        idx = torch.arange(n, device="cuda")
-        cols = [tiled_gather(buf, r, idx).cpu() for r in rows] if tiled else [x[:n].cpu() for x in xs]
+        cols = list(buf[:n // buf.shape[2]].cpu().permute(1, 0, 2).reshape(buf.shape[1], -1)[rows]) if tiled \
+            else [x[:n].cpu() for x in xs]
         avg = orc.weighted_sum(cols, 0, w)
         for first in (True, False):
             run(p_dev, b_dev, first, n)
@@ -734,21 +896,16 @@ def wl_fedopt(args, eng, rank, world, timer):
         model = torch.nn.Linear(1, 1, bias=False)
         model.weight = torch.nn.Parameter(torch.randn(Pc, generator=gc))
         opt = torch.optim.SGD(model.parameters(), lr=lr, momentum=mom)
-        torch.set_num_threads(min(16, os.cpu_count() or 1))
-        best, runs, t_end = float("inf"), 0, time.perf_counter() + budget_s
-        while runs < 3 or (time.perf_counter() < t_end and runs < 50):
-            lst = [(n_, {"w": d["w"].clone()}) for n_, d in cl]  # agg() rebinds client 0's dict
-            t0 = time.perf_counter()
+
+        def run():
+            lst = [(n_, {"w": d["w"]}) for n_, d in cl]  # fresh dicts: agg() rebinds client 0's entry
             avg = tp.agg("FedAvg", lst)["w"]
             opt.zero_grad()
             model.weight.grad = model.weight.data - avg       # set_model_global_grads (:118-131)
             opt.step()
-            best = min(best, time.perf_counter() - t0)
-            runs += 1
-        gbs = (Kc + 4) * Pc * 4 / best / 1e9
-        return {"value": round(gbs, 2), "unit": "GB/s", "cores": torch.get_num_threads(), "kind": "port",
-                "sample": f"K={Kc} x P={Pc} fp32 host-resident, best of {runs}: oracle/torch_port.agg('FedAvg') "
-                          f"+ pseudo-gradient + torch.optim.SGD(momentum={mom}) step"}
+        return legs_record(timed_legs(run, budget_s), (Kc + 4) * Pc * 4,
+                           f"K={Kc} x P={Pc} fp32 host-resident: oracle/torch_port.agg('FedAvg') + pseudo-gradient "
+                           f"+ torch.optim.SGD(momentum={mom}) step")
 
     return dict(name=f"fedopt_sgd_K{K}_P{P}_fp32" + ("_tiled" if tiled else ""), dtype="fp32", step=step, parity=parity, cpu=cpu,
                 bytes_total=(K + 4) * P * 4, launch_bytes=(K + 4) * P * 4, clients=K, params=P, cpu_K=K)
@@ -800,8 +957,8 @@ def wl_secagg(args, eng, rank, world, timer):
         from oracle import orc
         gi = torch.Generator(device="cuda").manual_seed(99)
         idx = torch.randint(0, P, (args.check_samples,), generator=gi, device="cuda")
-        cols_in = ([tiled_gather(tbuf, r, idx).cpu() for r in rows] if tiled else
-                   [x.index_select(0, idx).cpu() for x in xs])
+        cols_in = ([tbuf[:, r, :].reshape(-1)[:P].index_select(0, idx).cpu() for r in rows] if tiled else
+                   [x.index_select(0, idx).cpu() for x in xs])  # 1.5e9-element arena: one row at a time
         _, exp = orc.finite_sum(cols_in, p, MOD_END,
                                 mask=state["mask"].index_select(0, idx).cpu(), q_bits=q, scale=1 / K)
         ok = torch.equal(state["real"].index_select(0, idx).cpu().view(torch.int32), exp.view(torch.int32))
@@ -846,18 +1003,11 @@ def _robust_inputs(K, P):
     return [arena[i, :P] for i in range(K)]
 
 
-def _robust_cpu(fn, K, Pc, budget_s, what):
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
-    torch.set_num_threads(threads)
+def _robust_cpu(fn, K, Pc, budget_s, nbytes, what, digits=2):
     g = torch.Generator().manual_seed(0)
     xs = [torch.randn(Pc, generator=g) for _ in range(K)]
-    best, runs, t_end = float("inf"), 0, time.perf_counter() + budget_s
-    while runs < 2 or (time.perf_counter() < t_end and runs < 20):
-        t0 = time.perf_counter()
-        fn(xs)
-        best = min(best, time.perf_counter() - t0)
-        runs += 1
-    return best, runs, torch.get_num_threads(), f"K={K} x P={Pc} fp32 host-resident, best of {runs} runs of {what}"
+    return legs_record(timed_legs(lambda: fn(xs), budget_s, min_runs=2, max_runs=20), nbytes,
+                       f"K={K} x P={Pc} fp32 host-resident, {what}", digits=digits)
 
 
 def wl_median(args, eng, rank, world, timer):
@@ -896,11 +1046,8 @@ def wl_median(args, eng, rank, world, timer):
     def cpu(budget_s):
         from oracle import robust_port
         Pc = 1_000_000
-        best, runs, th, sample = _robust_cpu(robust_port.median_port, K, Pc, budget_s,
-                                             "oracle/robust_port.median_port (cat + torch.median, "
-                                             "coordinate_wise_median_defense.py:26-31)")
-        return {"value": round((K * Pc * 4 + Pc * 4) / best / 1e9, 2), "unit": "GB/s", "cores": th, "kind": "port",
-                "sample": sample}
+        return _robust_cpu(robust_port.median_port, K, Pc, budget_s, K * Pc * 4 + Pc * 4,
+                           "oracle/robust_port.median_port (cat + torch.median, coordinate_wise_median_defense.py:26-31)")
 
     return dict(name=f"coord_median_K{K}_P{P}_{args.dtype}", dtype=args.dtype, step=step, parity=parity,
                 bytes_total=(K * P + P) * es, launch_bytes=(K * P + P) * es, clients=K, params=P, cpu_K=K, cpu=cpu,
@@ -936,11 +1083,9 @@ def wl_krum(args, eng, rank, world, timer):
         from oracle import robust_port
         Pc = 1_000_000
         Kc = min(K, 16)
-        best, runs, th, sample = _robust_cpu(robust_port.krum_distances_port, Kc, Pc, budget_s,
-                                             "oracle/robust_port.krum_distances_port (one (v_i - v_j).norm() per "
-                                             "ordered pair, krum_defense.py:52-66)")
-        return {"value": round(Kc * Pc * 4 / best / 1e9, 3), "unit": "GB/s", "cores": th, "kind": "port",
-                "sample": sample}
+        return _robust_cpu(robust_port.krum_distances_port, Kc, Pc, budget_s, Kc * Pc * 4,
+                           "oracle/robust_port.krum_distances_port (one (v_i - v_j).norm() per ordered pair, "
+                           "krum_defense.py:52-66)", digits=3)
 
     pairs = K * (K - 1) // 2
     return dict(name=f"krum_pairdist_K{K}_P{P}_fp32", dtype="fp32", step=step, parity=parity,
@@ -951,30 +1096,54 @@ def wl_krum(args, eng, rank, world, timer):
 
 
 # ----------------------------------------------------------------------------- CPU baseline
+def cpu_thread_legs():
+    """the CPU baseline runs on ALL the host's cores (torch.set_num_threads(
+    os.cpu_count())), overriding the box's OMP_NUM_THREADS=16; a 16-thread leg (the process's CPU
+    share on a one-GPU box) is recorded beside it."""
+    allc = os.cpu_count() or 1
+    return [allc] + ([16] if allc > 16 else [])
+
+
+def timed_legs(fn, budget_s, min_runs=3, max_runs=50):
+    """Best-of wall time of fn() per thread leg: {threads: (best_s, runs)}."""
+    out = {}
+    for th in cpu_thread_legs():
+        torch.set_num_threads(th)
+        best, runs, t_end = float("inf"), 0, time.perf_counter() + budget_s / len(cpu_thread_legs())
+        while runs < min_runs or (time.perf_counter() < t_end and runs < max_runs):
+            t0 = time.perf_counter()
+            fn()
+            best = min(best, time.perf_counter() - t0)
+            runs += 1
+        out[th] = (best, runs)
+    return out
+
+
+def legs_record(legs, nbytes, sample, kind="port", digits=2):
+    """The all-core leg is the reported value (cores = os.cpu_count()); every leg's rate is kept."""
+    allc = max(legs)
+    rates = {th: round(nbytes / b / 1e9, digits) for th, (b, _) in legs.items()}
+    return {"value": rates[allc], "unit": "GB/s", "cores": allc, "kind": kind,
+            "value_by_threads": {str(th): r for th, r in sorted(rates.items())},
+            "sample": sample + f", best of {legs[allc][1]} runs per thread count"}
+
+
 def cpu_baseline(K, budget_s):
     """The reference's CPU cost: oracle/torch_port.py (op-for-op restatement of agg_operator.py's
-    FedAvg loop) on host-resident tensors, K clients x a bounded P, best of several runs."""
+    FedAvg loop) on host-resident tensors, K clients x a bounded P, best of several runs, on all
+    cores and on 16 threads."""
     from oracle import torch_port
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count()
-    torch.set_num_threads(threads)
     P = 4_000_000
     g = torch.Generator().manual_seed(0)
     xs = [torch.randn(P, generator=g) for _ in range(K)]
     counts = client_counts(K)
     raw = [(counts[i], {"w": xs[i]}) for i in range(K)]
-    best = float("inf")
-    t_end = time.perf_counter() + budget_s
-    runs = 0
-    while runs < 3 or (time.perf_counter() < t_end and runs < 50):
-        t0 = time.perf_counter()
-        torch_port.agg("FedAvg", raw)
-        best = min(best, time.perf_counter() - t0)
-        runs += 1
-    gbs = (K * P * 4 + P * 4) / best / 1e9
-    return {"value": round(gbs, 2), "unit": "GB/s", "cores": torch.get_num_threads(), "kind": "port",
-            "cpu_model": cpu_model(), "os_cpu_count": os.cpu_count(),
-            "sample": f"K={K} x P={P} fp32 host-resident, best of {runs} runs of oracle/torch_port.agg('FedAvg') "
-                      f"(op-for-op restatement of agg_operator.py:35-44)"}
+    legs = timed_legs(lambda: torch_port.agg("FedAvg", raw), budget_s)
+    rec = legs_record(legs, K * P * 4 + P * 4,
+                      f"K={K} x P={P} fp32 host-resident, oracle/torch_port.agg('FedAvg') "
+                      f"(op-for-op restatement of agg_operator.py:35-44)")
+    rec.update(cpu_model=cpu_model(), os_cpu_count=os.cpu_count())
+    return rec
 
 
 def cpu_model():
@@ -1038,7 +1207,9 @@ def main():
 
     kernel_ms = timer.avg_ms()
     launch_bytes = wl["launch_bytes"]
-    if launch_bytes is None and kernel_ms:  # layout configs: the whole aggregate() call per step
+    if wl.get("step_bytes"):  # several launches per step: this rank's bytes over the summed kernel time
+        kernel_ms, launch_bytes = timer.per_step_ms(args.steps), wl["step_bytes"]
+    elif launch_bytes is None and kernel_ms:  # layout configs: the whole aggregate() call per step
         launch_bytes = wl["bytes_total"] / world
     achieved = launch_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms else None
     parity = wl["parity"]()

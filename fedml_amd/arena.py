@@ -30,6 +30,7 @@ H2D per dtype group is issued on a copy stream, and the aggregation stream waits
 """
 from __future__ import annotations
 
+import weakref
 from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -95,6 +96,11 @@ class ArenaLayout:
 
 TILE_BYTES = 4096  # FA_TILE_BYTES (include/fedagg.h)
 
+# state_dicts adopted into arena rows (ClientArena.adopt): id(dict) -> (arena, row).  A later
+# aggregate() over such dicts is recognised (resident_rows) and runs as ONE launch per dtype group
+# over the arena rows instead of walking a (key, client) pointer table.
+_ADOPTED: Dict[int, Tuple["weakref.ref", int]] = {}
+
 
 def tile_elems(dt: torch.dtype) -> int:
     return TILE_BYTES // torch.empty((), dtype=dt).element_size()
@@ -122,6 +128,8 @@ class ClientArena:
         self._staging: List[Tuple[Dict[torch.dtype, torch.Tensor], Optional[torch.cuda.Event]]] = []
         self._next_stage = 0
         self._pending: List[torch.cuda.Event] = []
+        self._rows_adopted: Dict[int, int] = {}  # row -> id of the state_dict adopted into it
+        self._layout_codes = None
 
     @classmethod
     def for_model(cls, template_state_dict, capacity: int, device=None, **kw) -> "ClientArena":
@@ -187,6 +195,38 @@ class ClientArena:
             return
         self._write_host(i, state_dict)
 
+    def adopt(self, i: int, state_dict) -> None:
+        """On-arrival ingest (the reference moves an arriving update to the server device in place,
+        cross_silo/server/fedml_aggregator.py:57-66 -> ml_engine_adapter.py:234-254): copy the update
+        into row i and rebind the dict's entries to the row's device views, in place.  The compute
+        stream is ordered after the copy (a stream wait, no host block), so the rebound tensors
+        are safe to use on it at once.  Later aggregations over adopted dicts are recognised by
+        ``resident_rows`` and run over the arena rows."""
+        if self.tiled:
+            raise TypeError("adopt: a tiled arena's rows are not tensor views (use a client-major arena)")
+        self.write(i, state_dict)
+        self._wait_ingest()
+        for k, v in self.slot(i).items():
+            state_dict[k] = v
+        old = self._rows_adopted.get(i)  # the dict this row held before: no longer resident here
+        if old is not None and _ADOPTED.get(old, (None, -1))[1] == i:
+            _ADOPTED.pop(old, None)
+        self._rows_adopted[i] = id(state_dict)
+        _ADOPTED[id(state_dict)] = (weakref.ref(self), i)
+
+    def _ptr_table(self):
+        """Per key (layout order): device address of row 0's tensor and the row stride in bytes."""
+        t = getattr(self, "_ptr_tab", None)
+        if t is None:
+            base, stride = [], []
+            for k in self.layout.keys:
+                dt, off, _, _ = self.layout.where[k]
+                b = self.bufs[dt]
+                base.append(b.data_ptr() + off * b.element_size())
+                stride.append(b.stride(0) * b.element_size())
+            t = self._ptr_tab = (torch.tensor(base, dtype=torch.int64), torch.tensor(stride, dtype=torch.int64))
+        return t
+
     def _stage_slot(self):
         if len(self._staging) < 2:
             bufs = {dt: torch.zeros(n, dtype=dt, pin_memory=True) for dt, n in self.layout.group_numel.items()}
@@ -201,6 +241,9 @@ class ClientArena:
     def _write_host(self, i: int, state_dict) -> None:
         if self._copy_stream is None:
             self._copy_stream = torch.cuda.Stream(self.device)
+        # the H2D overwrites row i: it must not start before every kernel already queued on the
+        # compute stream (e.g. the previous round's aggregate() or read() of these rows) has run
+        self._copy_stream.wait_stream(torch.cuda.current_stream(self.device))
         if not self.tiled and all(state_dict[k].is_pinned() for k in self.layout.keys):
             # already page-locked (e.g. a transport that receives into pinned buffers): DMA directly
             slot = self.slot(i)
@@ -315,3 +358,36 @@ class ClientArena:
         """FedMLAggOperator.agg FedAvg branch (agg_operator.py:35-44) over the arena rows."""
         N = sum(counts)
         return self.aggregate(MUL_W, [c / N for c in counts], clients=clients)
+
+
+_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3, torch.int64: 4}
+
+
+def resident_rows(dicts, keys, ptrs: torch.Tensor, numel: torch.Tensor, codes: torch.Tensor):
+    """(arena, rows) when every dict of ``dicts`` was adopted by ONE client-major arena, lists
+    exactly the layout's keys in order, and still holds that arena's row views (``ptrs`` /
+    ``numel`` / ``codes``: the dicts' key-major device pointer table, element counts and dtype
+    codes, fedml_amd._host.gather); else None."""
+    first = _ADOPTED.get(id(dicts[0]))
+    if first is None:
+        return None
+    arena = first[0]()
+    if arena is None or list(keys) != arena.layout.keys:
+        return None
+    rows = []
+    for d in dicts:
+        e = _ADOPTED.get(id(d))
+        if e is None or e[0]() is not arena:
+            return None
+        rows.append(e[1])
+    base, stride = arena._ptr_table()
+    if arena._layout_codes is None:
+        arena._layout_codes = (torch.tensor([arena.layout.where[k][3] for k in arena.layout.keys], dtype=torch.int64),
+                               torch.tensor([_CODE[arena.layout.where[k][0]] for k in arena.layout.keys],
+                                            dtype=torch.int64))
+    if not (torch.equal(arena._layout_codes[0], numel) and torch.equal(arena._layout_codes[1], codes)):
+        return None
+    expect = base.view(-1, 1) + stride.view(-1, 1) * torch.tensor(rows, dtype=torch.int64).view(1, -1)
+    if not torch.equal(expect.view(-1), ptrs):
+        return None
+    return arena, rows

@@ -31,45 +31,79 @@ def _engine_mix(xs, row_ptr, cols, vals, post_scale, outs, outs2):
     return get_engine(xs[0].device.index).mix(xs, row_ptr, cols, vals, post_scale, outs, outs2)
 
 
-class DistributedGossip:
-    def __init__(self, W: np.ndarray, group=None, local_mix: Optional[Callable] = None):
+class GossipPlan:
+    """One rank's share of a distributed gossip step, as a pure function of (W, rank, world): the
+    nodes it owns, the halo it receives and sends, its interior / boundary rows and the ring-ordered
+    input list its mixing rows index.  DistributedGossip executes it; tests run every rank's local
+    problem on one device through the same plan."""
+
+    def __init__(self, W: np.ndarray, rank: int, world: int):
         self.W = np.asarray(W, dtype=np.float32)
         self.n = self.W.shape[0]
-        self.group = group
-        self.rank = dist.get_rank(group)
-        self.world = dist.get_world_size(group)
-        self.block = -(-self.n // self.world)
-        self.local_mix = local_mix or _engine_mix
-        self.mine = [i for i in range(self.n) if self.owner(i) == self.rank]
+        self.rank, self.world = rank, world
+        self.block = -(-self.n // world)
+        self.mine = [i for i in range(self.n) if self.owner(i) == rank]
         row_ptr, cols, vals = gossip_rows(self.W, self.mine)
         self._rows = [(cols[row_ptr[r]:row_ptr[r + 1]], vals[row_ptr[r]:row_ptr[r + 1]]) for r in range(len(self.mine))]
-        needed = sorted({c for cs, _ in self._rows for c in cs if self.owner(c) != self.rank})
-        self.halo_in = needed                               # remote models this rank receives
+        self.halo_in = sorted({c for cs, _ in self._rows for c in cs if self.owner(c) != rank})  # received
         # what this rank must send: for every other rank, its remote needs that live here
         self.halo_out: Dict[int, List[int]] = {}
-        for r in range(self.world):
-            if r == self.rank:
+        for r in range(world):
+            if r == rank:
                 continue
             theirs = [i for i in range(self.n) if self.owner(i) == r]
-            rp, cs, _ = gossip_rows(self.W, theirs)
-            want = sorted({c for c in cs if self.owner(c) == self.rank})
+            _, cs, _ = gossip_rows(self.W, theirs)
+            want = sorted({c for c in cs if self.owner(c) == rank})
             if want:
                 self.halo_out[r] = want
         local_set = set(self.mine)
         self.interior = [r for r, (cs, _) in enumerate(self._rows) if all(c in local_set for c in cs)]
         self.boundary = [r for r in range(len(self.mine)) if r not in set(self.interior)]
+        # inputs in ring order around this rank's block (left halo, own nodes, right halo): for a
+        # banded W the mixing rows then read inputs (row + const + {-1, 0, 1}) and take the
+        # sliding-window kernel
+        half = self.n // 2
+        self.inputs = sorted(list(self.mine) + list(self.halo_in), key=lambda v: (v - self.mine[0] + half) % self.n) \
+            if self.mine else []
+        self.index = {v: k for k, v in enumerate(self.inputs)}
 
     def owner(self, i: int) -> int:
         return min(i // self.block, self.world - 1)
 
-    def _csr(self, rows: Sequence[int], index: Dict[int, int]) -> Tuple[list, list, list]:
+    def csr(self, rows: Sequence[int]) -> Tuple[list, list, list]:
+        """CSR of the given local rows over ``self.inputs`` positions."""
         row_ptr, cols, vals = [0], [], []
         for r in rows:
             cs, vs = self._rows[r]
-            cols += [index[c] for c in cs]
+            cols += [self.index[c] for c in cs]
             vals += vs
             row_ptr.append(len(cols))
         return row_ptr, cols, vals
+
+    def mix_local(self, tensor_of: Dict[int, torch.Tensor], local_mix: Callable, rows: Sequence[int],
+                  outs: List[torch.Tensor], outs2: Optional[List[torch.Tensor]] = None,
+                  post_scale: Optional[Sequence[float]] = None):
+        """Mix the given local rows (indices into ``mine``) from node models ``tensor_of``."""
+        if not rows:
+            return
+        inputs = [tensor_of[v] for v in self.inputs]
+        rp, cs, vs = self.csr(rows)
+        ps = [post_scale[r] for r in rows] if post_scale is not None else None
+        local_mix(inputs, rp, cs, vs, ps, [outs[r] for r in rows], [outs2[r] for r in rows] if outs2 is not None else None)
+
+
+class DistributedGossip:
+    def __init__(self, W: np.ndarray, group=None, local_mix: Optional[Callable] = None):
+        self.group = group
+        self.plan = GossipPlan(W, dist.get_rank(group), dist.get_world_size(group))
+        p = self.plan
+        self.W, self.n, self.rank, self.world, self.block = p.W, p.n, p.rank, p.world, p.block
+        self.mine, self.halo_in, self.halo_out = p.mine, p.halo_in, p.halo_out
+        self.interior, self.boundary = p.interior, p.boundary
+        self.local_mix = local_mix or _engine_mix
+
+    def owner(self, i: int) -> int:
+        return self.plan.owner(i)
 
     def step(self, local_models: Sequence[torch.Tensor], post_scale: Optional[Sequence[float]] = None):
         """local_models[k] = flat model of node self.mine[k]; returns (new_models, scaled or None)."""
@@ -83,28 +117,13 @@ class DistributedGossip:
             for i in idxs:
                 ops.append(dist.P2POp(dist.isend, local_models[self.mine.index(i)], r, self.group))
         reqs = dist.batch_isend_irecv(ops) if ops else []
-        # inputs in ring order around this rank's block (left halo, own nodes, right halo): for a
-        # banded W the mixing rows then read inputs (row + const + {-1, 0, 1}) and take the
-        # sliding-window kernel
-        half = self.n // 2
-        nodes = sorted(list(self.mine) + list(self.halo_in), key=lambda v: (v - self.mine[0] + half) % self.n)
         tensor_of = {node: local_models[k] for k, node in enumerate(self.mine)}
         tensor_of.update(halo)
-        inputs = [tensor_of[v] for v in nodes]
-        index = {v: k for k, v in enumerate(nodes)}
         outs = [torch.empty_like(proto) for _ in self.mine]
         outs2 = [torch.empty_like(proto) for _ in self.mine] if post_scale is not None else None
-
-        def run(rows):
-            if not rows:
-                return
-            rp, cs, vs = self._csr(rows, index)
-            ps = [post_scale[r] for r in rows] if post_scale is not None else None
-            self.local_mix(inputs, rp, cs, vs, ps, [outs[r] for r in rows],
-                           [outs2[r] for r in rows] if outs2 is not None else None)
-
-        run(self.interior)       # overlaps the halo exchange
+        # the interior rows read only local models: they overlap the halo exchange
+        self.plan.mix_local(tensor_of, self.local_mix, self.interior, outs, outs2, post_scale)
         for q in reqs:
             q.wait()
-        run(self.boundary)
+        self.plan.mix_local(tensor_of, self.local_mix, self.boundary, outs, outs2, post_scale)
         return outs, outs2

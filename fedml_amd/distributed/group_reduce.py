@@ -8,22 +8,34 @@ One process per GPU (torch.distributed, backend "nccl" = RCCL).  Rank r holds cl
   formula's term ``(G_r * N_r) / N`` (HierFedAvgCloudAggregator.py:146-156) -- the exact per-element
   ops the reference applies before its cloud-side accumulation.
 * Global step (the exchange), ``collective``:
-    "reduce"          SUM-reduce to ``dst`` -- the reference's NCCL simulator pattern
+    "ordered"         (default) the full global model on ``dst``, summed IN RANK ORDER -- bit-identical
+                      to the reference's two-level reduces: fedavg_seq (worker partials, then an
+                      ordered sum; FedAVGAggregator.py:201-236), the hierarchical cloud step (ordered
+                      sum of the pre-scaled group terms) and the oracle's rank-ordered sum.  The
+                      summation is spread over the G-1 ranks other than ``dst`` ("owners"): chunk
+                      [a, b) is split into G-1 consecutive pieces, one per owner in rank order; an
+                      all-to-all sends every rank's partial of piece o to owner o (``dst`` owns
+                      nothing, so its links carry only its own partial out and the results in);
+                      owner o sums the G partials of its piece in rank order with the engine's SUM
+                      kernel; a second all-to-all, on a second communicator so that it runs beside
+                      the next chunk's first one, lands the summed pieces in ``out[a:b]`` on ``dst``
+                      -- they are consecutive, so no copy.  Per chunk every directed xGMI link
+                      carries at most (b - a)/(G - 1) elements, vs (b - a)/G * 2 into ``dst`` for a
+                      reduce-scatter + gather and (b - a) per ring link for a ring reduce;
+    "ordered_all"     the same, summed pieces delivered to EVERY rank (the reference's reduce followed
+                      by its broadcast of the global model, simulation/nccl/base_framework/
+                      common.py:196-228);
+    "reduce"          SUM-reduce to ``dst`` with RCCL's reduce -- the reference's NCCL simulator call
                       (simulation/nccl/base_framework/params.py:98-105, common.py:196-210); the
                       cross-rank summation order is RCCL's, so the result matches the sequential
                       reference normwise (~1e-7), not bit-for-bit;
     "all_reduce"      the same, result on every rank;
-    "reduce_scatter"  the same, result sharded: rank r owns elements [r*S, min((r+1)*S, P)) with
-                      S = P/G rounded up to whole tiles -- the least xGMI traffic (each link
-                      carries 1/G of a partial per direction), and the global model is already
-                      partitioned for a sharded broadcast;
-    "ordered"         gather the G partials to ``dst`` and sum them there IN RANK ORDER with the
-                      engine's SUM mode: bit-identical to the reference's two-level reduces --
-                      fedavg_seq (worker partials, then an ordered sum; FedAVGAggregator.py:201-236)
-                      and the hierarchical cloud step (ordered sum of the pre-scaled group terms).
-* Pipelining: P is cut into ``chunks``; chunk c's collective is issued (async, stream-ordered
-  behind chunk c's kernel) while chunk c+1's partial is computed, so the xGMI transfer hides
-  behind HBM streaming.
+    "reduce_scatter"  the same, result SHARDED: rank r owns elements [r*S, min((r+1)*S, P)) with
+                      S = P/G rounded up to whole tiles, and no rank holds the whole model (a
+                      sharded broadcast would follow); the least xGMI traffic of all.
+* Pipelining: P is cut into ``chunks``; chunk c's exchange is issued (async, stream-ordered behind
+  chunk c's kernel) while chunk c+1's partial is computed, so the xGMI transfer hides behind HBM
+  streaming.  ("ordered": the owners' sum of chunk c is queued after chunk c+1's partial.)
 
 The local reduction is injectable (``local_sum``) so the exchange logic can be tested with the
 gloo backend on CPU; in the product it is the HIP engine and there is no CPU path.
@@ -39,6 +51,9 @@ from ..engine import MUL_N_DIV_N, MUL_W, SUM
 
 LocalSum = Callable[..., torch.Tensor]  # (xs, mode, coef, divisor, out) -> out
 
+COLLECTIVES = ("ordered", "ordered_all", "reduce", "all_reduce", "reduce_scatter")
+_SECOND_GROUP: dict = {}  # process group -> a second communicator over the same ranks ("ordered")
+
 
 def _engine_local_sum(xs, mode, coef, divisor, out):
     from ..engine import get_engine
@@ -51,6 +66,13 @@ def _engine_local_grouped(xs, mode, coef, divisor, gptr, gmode, gcoef, gdiv, out
                                                              gdiv, out=out)
 
 
+def split_bounds(n: int, parts: int, align: int = 1) -> List[tuple]:
+    """Exactly ``parts`` consecutive ranges covering [0, n) (some may be empty); inner bounds are
+    multiples of ``align``."""
+    units = -(-n // align)
+    return [(min(n, units * j // parts * align), min(n, units * (j + 1) // parts * align)) for j in range(parts)]
+
+
 def chunk_bounds(n: int, chunks: int, align: int = 1) -> List[tuple]:
     """``chunks`` consecutive ranges covering [0, n); inner bounds are multiples of ``align``."""
     units = -(-n // align)
@@ -61,25 +83,34 @@ def chunk_bounds(n: int, chunks: int, align: int = 1) -> List[tuple]:
 class GroupReducer:
     """Group -> global reduction of flat parameter vectors over a process group."""
 
-    def __init__(self, group=None, collective: str = "reduce", dst: int = 0, chunks: int = 8,
+    def __init__(self, group=None, collective: str = "ordered", dst: int = 0, chunks: int = 8,
                  local_sum: Optional[LocalSum] = None, local_grouped: Optional[Callable] = None,
-                 stream: Optional[torch.cuda.Stream] = None):
-        if collective not in ("reduce", "all_reduce", "reduce_scatter", "ordered"):
+                 stream: Optional[torch.cuda.Stream] = None, combine_sum: Optional[LocalSum] = None):
+        if collective not in COLLECTIVES:
             raise ValueError(f"unknown collective {collective!r}")
         self.group = group
         self.collective = collective
         self.dst = dst
         self.chunks = chunks
         self.local_sum = local_sum or _engine_local_sum
+        # the owners' rank-ordered sum of the G partials ("ordered"): SUM mode of the same engine
+        self.combine_sum = combine_sum or self.local_sum
         # fused two-level local step (group partial + epilogue in one kernel pass); with an injected
         # local_sum and no local_grouped the levels run as separate passes (same arithmetic)
         self.local_grouped = local_grouped if local_grouped is not None else (
             _engine_local_grouped if local_sum is None else None)
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
+        if not 0 <= dst < self.world:
+            raise ValueError(f"dst {dst} outside the group of {self.world}")
         # optional stream for the local partials and the collectives' dependencies, e.g. a CU-masked
         # stream (AggEngine.cu_masked_stream) that leaves CUs free for RCCL's kernels
         self.stream = stream
+        self._group2 = None
+        if collective in ("ordered", "ordered_all") and self.world > 1:
+            self._group2 = _second_group(group)
+        self._bufs: dict = {}
+        self.owned = None  # "ordered": (lo, hi) pieces of the global model this rank summed, last call
 
     # -------------------------------------------------------------- public entry points
     def fedavg(self, xs: Sequence[torch.Tensor], weights: Sequence[float], out: Optional[torch.Tensor] = None):
@@ -173,59 +204,136 @@ class GroupReducer:
             res.record_stream(caller)        # allocated on self.stream, used on the caller's
         return res
 
+    def _scratch(self, name, numel, dtype, dev):
+        """Internal staging, kept across calls (never the caller's ``out``)."""
+        t = self._bufs.get(name)
+        if t is None or t.numel() < numel or t.dtype != dtype or t.device != dev:
+            t = self._bufs[name] = torch.empty(max(numel, 1), dtype=dtype, device=dev)
+        return t
+
     def _run_body(self, n, dev, local, out, align, local_multi=None):
-        works = []
-        gathered = []
+        if self.world == 1:
+            for a, b in chunk_bounds(n, self.chunks, align):
+                local(out[a:b], a, b)
+            return out
+        if self.collective in ("ordered", "ordered_all"):
+            return self._run_ordered(n, dev, local, out, align)
         if self.collective == "reduce_scatter":
-            # shards of S elements (whole tiles), the last one zero-padded past n: rank r owns the
-            # global model's elements [r*S, min((r+1)*S, n))
-            S = -(-n // (self.world * align)) * align
-            stage = out if out.numel() >= S * self.world else torch.empty(S * self.world, dtype=out.dtype, device=dev)
-            shard = torch.empty(S, dtype=out.dtype, device=dev)
-            # chunk-major staging: chunk [a, b) of every rank's shard is laid out contiguously
-            # (rank-major inside the chunk), which is what reduce_scatter_tensor consumes
-            for a, b in chunk_bounds(S, self.chunks, align):
-                L = b - a
-                base = self.world * a
-                pieces = []
-                for r in range(self.world):
-                    lo, hi = r * S + a, min(r * S + b, n)
-                    dstv = stage[base + r * L: base + (r + 1) * L]
-                    if hi > lo:
-                        pieces.append((dstv[:hi - lo], lo, hi))
-                    if hi - lo < L:
-                        dstv[max(hi - lo, 0):].zero_()
-                if local_multi is not None:  # every rank's slice of the chunk in ONE launch
-                    local_multi(pieces)
-                else:
-                    for dstv, lo, hi in pieces:
-                        local(dstv, lo, hi)
-                if self.world > 1:
-                    works.append(dist.reduce_scatter_tensor(shard[a:b], stage[base: base + self.world * L],
-                                                            op=dist.ReduceOp.SUM, group=self.group,
-                                                            async_op=True))
-                else:
-                    shard[a:b].copy_(stage[base: base + L])
-            for w in works:
-                w.wait()
-            return shard[:max(0, min(S, n - self.rank * S))]
+            return self._run_reduce_scatter(n, dev, local, out, align, local_multi)
+        works = []
         for a, b in chunk_bounds(n, self.chunks, align):
             part = out[a:b]
             local(part, a, b)
-            if self.world == 1:
-                continue
             if self.collective == "reduce":
                 works.append(dist.reduce(part, dst=self.dst, op=dist.ReduceOp.SUM, group=self.group,
                                          async_op=True))
-            elif self.collective == "all_reduce":
+            else:  # all_reduce
                 works.append(dist.all_reduce(part, op=dist.ReduceOp.SUM, group=self.group, async_op=True))
-            else:  # ordered
-                bufs = [torch.empty_like(part) for _ in range(self.world)] if self.rank == self.dst else None
-                works.append(dist.gather(part, bufs, dst=self.dst, group=self.group, async_op=True))
-                gathered.append((a, b, bufs))
         for w in works:
             w.wait()
-        if self.collective == "ordered" and self.rank == self.dst and self.world > 1:
-            for a, b, bufs in gathered:
-                self.local_sum(bufs, SUM, None, 1.0, out[a:b])
         return out
+
+    def _run_reduce_scatter(self, n, dev, local, out, align, local_multi):
+        # shards of S elements (whole tiles), the last one zero-padded past n: rank r owns the
+        # global model's elements [r*S, min((r+1)*S, n)); staging is internal
+        S = -(-n // (self.world * align)) * align
+        stage = self._scratch("rs_stage", S * self.world, out.dtype, dev)
+        shard = torch.empty(S, dtype=out.dtype, device=dev)
+        works = []
+        # chunk-major staging: chunk [a, b) of every rank's shard is laid out contiguously
+        # (rank-major inside the chunk), which is what reduce_scatter_tensor consumes
+        for a, b in chunk_bounds(S, self.chunks, align):
+            L = b - a
+            base = self.world * a
+            pieces = []
+            for r in range(self.world):
+                lo, hi = r * S + a, min(r * S + b, n)
+                dstv = stage[base + r * L: base + (r + 1) * L]
+                if hi > lo:
+                    pieces.append((dstv[:hi - lo], lo, hi))
+                if hi - lo < L:
+                    dstv[max(hi - lo, 0):].zero_()
+            if local_multi is not None:  # every rank's slice of the chunk in ONE launch
+                local_multi(pieces)
+            else:
+                for dstv, lo, hi in pieces:
+                    local(dstv, lo, hi)
+            works.append(dist.reduce_scatter_tensor(shard[a:b], stage[base: base + self.world * L],
+                                                    op=dist.ReduceOp.SUM, group=self.group, async_op=True))
+        for w in works:
+            w.wait()
+        return shard[:max(0, min(S, n - self.rank * S))]
+
+    def _run_ordered(self, n, dev, local, out, align):
+        """Rank-ordered global sum, summed by the owners (every rank but ``dst``), delivered to
+        ``dst`` (or to every rank, "ordered_all").  See the module docstring."""
+        world, me, dst = self.world, self.rank, self.dst
+        to_all = self.collective == "ordered_all"
+        owners = [r for r in range(world) if r != dst]
+        plan = []  # per chunk: (a, b, piece size per rank, piece start per rank)
+        for a, b in chunk_bounds(n, self.chunks, align):
+            sizes, starts = [0] * world, [a] * world
+            for o, (lo, hi) in zip(owners, split_bounds(b - a, len(owners), align)):
+                sizes[o], starts[o] = hi - lo, a + lo
+            plan.append((a, b, sizes, starts))
+        dt = out.dtype
+        send = self._scratch("send", n, dt, dev)
+        mine = sum(p[2][me] for p in plan)
+        recv = self._scratch("recv", world * mine, dt, dev)
+        own = self._scratch("own", mine, dt, dev)
+        offs, o = [], 0
+        for p in plan:
+            offs.append(o)
+            o += p[2][me]
+        first, second = [], []
+
+        def finish(c):
+            a, b, sizes, starts = plan[c]
+            L, o0 = sizes[me], offs[c]
+            first[c].wait()  # this chunk's G partials of my piece have landed (stream-ordered on device)
+            if L:
+                r0 = world * o0
+                self.combine_sum([recv[r0 + r * L: r0 + (r + 1) * L] for r in range(world)], SUM, None, 1.0,
+                                 own[o0:o0 + L])
+            if not to_all:  # deliver the summed pieces owner -> dst, consecutive in out[a:b]
+                osz = list(sizes) if me == dst else [0] * world
+                isz = [L if r == dst else 0 for r in range(world)]
+                second.append(dist.all_to_all_single(out[a:b] if me == dst else out[a:a], own[o0:o0 + L], osz,
+                                                     isz, group=self._group2, async_op=True))
+                return
+            # "ordered_all": every owner's piece to every rank (one buffer, G-1 sends: P2P)
+            ops = []
+            for r in range(world):
+                if r == me:
+                    if L:
+                        out[starts[me]:starts[me] + L].copy_(own[o0:o0 + L])
+                    continue
+                if sizes[r]:
+                    ops.append(dist.P2POp(dist.irecv, out[starts[r]:starts[r] + sizes[r]], r, self._group2))
+                if L:
+                    ops.append(dist.P2POp(dist.isend, own[o0:o0 + L], r, self._group2))
+            if ops:
+                second.extend(dist.batch_isend_irecv(ops))
+
+        for c, (a, b, sizes, starts) in enumerate(plan):
+            local(send[a:b], a, b)
+            L, o0 = sizes[me], offs[c]
+            first.append(dist.all_to_all_single(recv[world * o0: world * (o0 + L)], send[a:b], [L] * world,
+                                                list(sizes), group=self.group, async_op=True))
+            if c >= 1:  # software pipeline: chunk c-1's owner sum queues behind chunk c's partial
+                finish(c - 1)
+        finish(len(plan) - 1)
+        for w in second:
+            w.wait()
+        self.owned = [(p[3][me], p[3][me] + p[2][me]) for p in plan if p[2][me]]
+        return out
+
+
+def _second_group(group):
+    """A second communicator over ``group``'s ranks (created collectively, once per group)."""
+    key = group if group is not None else dist.group.WORLD  # a re-created default group is a new key
+    g2 = _SECOND_GROUP.get(key)
+    if g2 is None:
+        ranks = dist.get_process_group_ranks(group) if group is not None else list(range(dist.get_world_size()))
+        g2 = _SECOND_GROUP[key] = dist.new_group(ranks)
+    return g2

@@ -38,8 +38,31 @@ def _require_device(t: torch.Tensor, dev: torch.device, what: str):
         raise ValueError(f"{what}: tensor must be contiguous")
 
 
+class _LockedLib:
+    """The native library with every call made under the engine's lock.  One fa_ctx per device is
+    shared by every thread of the process (the engine is a per-device singleton), while the C ABI
+    allows one thread per context at a time (include/fedagg.h: the staging-slot ring); ctypes
+    releases the GIL during the call, so the lock is what serialises two receive threads."""
+
+    def __init__(self, lib, lock):
+        self._l = lib
+        self._lock = lock
+
+    def __getattr__(self, name):
+        fn = getattr(self._l, name)
+        lock = self._lock
+
+        def call(*a):
+            with lock:
+                return fn(*a)
+        call.__name__ = name
+        setattr(self, name, call)
+        return call
+
+
 class AggEngine:
-    """One native context bound to one HIP device."""
+    """One native context bound to one HIP device.  Thread-safe: native launches and the host
+    staging of ``state_dict_agg`` are serialised by ``self.lock`` (a re-entrant lock)."""
 
     _engines: Dict[int, "AggEngine"] = {}
     _elock = threading.Lock()
@@ -53,7 +76,8 @@ class AggEngine:
         h = N.ctypes.c_void_p()
         N.check(L.fa_ctx_create(self.device_index, N.ctypes.byref(h)), "fa_ctx_create")
         self._ctx = h
-        self._lib = L
+        self.lock = threading.RLock()
+        self._lib = _LockedLib(L, self.lock)
 
     @classmethod
     def get(cls, device: Optional[int] = None) -> "AggEngine":
@@ -714,13 +738,17 @@ class AggEngine:
         N.check(rc, "fa_coord_median")
         return results
 
+    MAX_PAIR_K = 128  # kMaxPairK (fedml_amd/csrc/robust.hip): clients per fa_pairwise_sqdist launch
+
     def pairwise_sqdist(self, segments: Sequence[Sequence[torch.Tensor]], stream=None) -> torch.Tensor:
         """K x K float64 matrix of squared Euclidean distances between the clients' float32 vectors
-        (segments[s][i] = client i's piece s), fa_pairwise_sqdist."""
+        (segments[s][i] = client i's piece s), fa_pairwise_sqdist.  K > 128 (one launch holds at
+        most 128 clients): clients in blocks of 64, one launch per pair of blocks (each launch the
+        union of two blocks, its cross distances kept) -- every distance is still one device pass
+        over the two clients' vectors, the same per-pair arithmetic as the single launch."""
         k = len(segments[0]) if segments else 0
         if k < 2:
             raise ValueError("pairwise_sqdist: need at least two clients")
-        in_ptrs, numels = [], []
         for s, seg in enumerate(segments):
             if len(seg) != k:
                 raise ValueError(f"segment {s}: {len(seg)} clients, expected {k}")
@@ -728,16 +756,31 @@ class AggEngine:
                 if t.dtype != torch.float32 or t.numel() != seg[0].numel():
                     raise ValueError(f"segment {s} client {i}: float32 of {seg[0].numel()} elements expected")
                 _require_device(t, self.device, f"segment {s} client {i}")
-                in_ptrs.append(t.data_ptr())
-            numels.append(seg[0].numel())
-        nl = N.i64_array(numels)
-        need = self._lib.fa_pairwise_sqdist_scratch_bytes(len(segments), nl, k)
-        scratch = getattr(self, "_pd_scratch", None)
-        if scratch is None or scratch.numel() < need:
-            scratch = self._pd_scratch = torch.empty(max(need, 1), dtype=torch.uint8, device=self.device)
-        d = torch.empty((k, k), dtype=torch.float64, device=self.device)
-        rc = self._lib.fa_pairwise_sqdist(self._ctx, len(segments), nl, k, N.ptr_array(in_ptrs), d.data_ptr(),
-                                          scratch.data_ptr(), scratch.numel(), self._stream(stream))
+        if k <= self.MAX_PAIR_K:
+            return self._pairwise_launch(segments, stream)
+        B = self.MAX_PAIR_K // 2
+        blocks = [list(range(lo, min(k, lo + B))) for lo in range(0, k, B)]
+        d = torch.zeros((k, k), dtype=torch.float64, device=self.device)
+        for a in range(len(blocks)):
+            for b in range(a + 1, len(blocks)):
+                ids = blocks[a] + blocks[b]
+                sub = self._pairwise_launch([[seg[i] for i in ids] for seg in segments], stream)
+                idx = torch.tensor(ids, device=self.device)
+                d.index_put_((idx.view(-1, 1), idx.view(1, -1)), sub)  # diagonal blocks rewritten, same values
+        return d
+
+    def _pairwise_launch(self, segments, stream=None) -> torch.Tensor:
+        k = len(segments[0])
+        in_ptrs = [t.data_ptr() for seg in segments for t in seg]
+        nl = N.i64_array([seg[0].numel() for seg in segments])
+        with self.lock:
+            need = self._lib.fa_pairwise_sqdist_scratch_bytes(len(segments), nl, k)
+            scratch = getattr(self, "_pd_scratch", None)
+            if scratch is None or scratch.numel() < need:
+                scratch = self._pd_scratch = torch.empty(max(need, 1), dtype=torch.uint8, device=self.device)
+            d = torch.empty((k, k), dtype=torch.float64, device=self.device)
+            rc = self._lib.fa_pairwise_sqdist(self._ctx, len(segments), nl, k, N.ptr_array(in_ptrs), d.data_ptr(),
+                                              scratch.data_ptr(), scratch.numel(), self._stream(stream))
         N.check(rc, "fa_pairwise_sqdist")
         return d
 

@@ -1,0 +1,83 @@
+"""On-arrival ingest of client updates into HBM.
+
+The reference server moves each client update to its device as it arrives
+(python/fedml/cross_silo/server/fedml_aggregator.py:57-66 -> ml/engine/ml_engine_adapter.py:234-254,
+one ``.to(device)`` per tensor, in place on the update's dict) and aggregates once every client
+has reported.  ``ArrivalIngest`` does the same move into a ClientArena row (fedml_amd/arena.py):
+the update is packed into pinned staging and copied H2D on a copy stream while the server waits
+for the next client, and the dict's entries are rebound to the row's device views.  The round's
+aggregation over those dicts is then recognised as arena-resident (arena.resident_rows) and runs
+as one launch per dtype group over the rows; only the LAST client's ingest, the kernel and the
+result's D2H remain after the last arrival.
+
+Rows are double-buffered by round parity, so round r+1's updates can be ingested while round r's
+result is still being read.  ``to_host`` copies the aggregated model into pinned buffers (also
+double-buffered) that a send path can pickle or post directly (fedml_server_manager.py:217-231).
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Dict, Optional
+
+import torch
+
+from ...arena import ArenaLayout, ClientArena
+
+
+class ArrivalIngest:
+    def __init__(self, capacity: int, device=None):
+        self.capacity = int(capacity)
+        self.device = device
+        self.arena: Optional[ClientArena] = None
+        self.parity = 0
+        self._host: Dict[int, "OrderedDict[str, torch.Tensor]"] = {}
+
+    @staticmethod
+    def wants(device) -> bool:
+        """The server device is a HIP device (the reference moves updates there on arrival)."""
+        return device is not None and torch.device(device).type == "cuda"
+
+    def add(self, index: int, state_dict) -> bool:
+        """Adopt client ``index``'s update into this round's row.  False if it cannot be adopted
+        (empty, unsupported dtype, or a layout other than the round's first update) -- the
+        caller then keeps the reference's per-tensor move."""
+        if not 0 <= index < self.capacity or len(state_dict) == 0:
+            return False
+        if self.arena is None:
+            try:
+                layout = ArenaLayout.from_state_dict(state_dict)
+            except TypeError:
+                return False
+            dev = torch.device(self.device) if self.device is not None else None
+            self.arena = ClientArena(layout, 2 * self.capacity, device=dev)
+        try:
+            self.arena.adopt(index + self.parity * self.capacity, state_dict)
+        except (TypeError, KeyError):
+            return False
+        return True
+
+    def round_done(self) -> None:
+        """The round's aggregation has been issued: the next round fills the other rows."""
+        self.parity ^= 1
+
+    def to_host(self, averaged) -> "OrderedDict[str, torch.Tensor]":
+        """The aggregated model in pinned host memory (one D2H per tensor on the current stream,
+        then a wait): the broadcast's send buffer.  Buffers alternate between two rounds."""
+        if not any(v.is_cuda for v in averaged.values()):
+            return averaged
+        bufs = self._host.get(self.parity)
+        if bufs is None or list(bufs.keys()) != list(averaged.keys()) or any(
+                bufs[k].shape != v.shape or bufs[k].dtype != v.dtype for k, v in averaged.items()):
+            bufs = self._host[self.parity] = OrderedDict(
+                (k, torch.empty(v.shape, dtype=v.dtype, pin_memory=True)) for k, v in averaged.items())
+        for k, v in averaged.items():
+            bufs[k].copy_(v, non_blocking=True)
+        torch.cuda.current_stream(next(iter(averaged.values())).device).synchronize()
+        return bufs
+
+
+def move_to_device(state_dict, device):
+    """The reference's per-tensor move (ml_engine_adapter.model_params_to_device), in place."""
+    for k in list(state_dict.keys()):
+        state_dict[k] = state_dict[k].to(device)
+    return state_dict

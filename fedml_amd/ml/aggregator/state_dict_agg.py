@@ -26,6 +26,7 @@ from typing import Dict, List, Optional, Sequence
 import torch
 
 from ... import _host
+from ...arena import resident_rows
 from ...engine import MUL_N_DIV_N, MUL_W, SUM, AggEngine, get_engine, out_dtype
 
 _NATIVE = (torch.float32, torch.bfloat16, torch.float16, torch.float64, torch.int64)
@@ -62,6 +63,10 @@ def aggregate(dicts: Sequence[Dict[str, torch.Tensor]], mode: int, coef: Optiona
         ptrs = None
     if ptrs is not None and int(codes.min()) >= 0:
         if dev.startswith("cuda"):
+            hit = resident_rows(dicts, keys, ptrs, numel, codes)
+            if hit is not None:  # updates adopted into arena rows on arrival: one launch per dtype group
+                arena, rows = hit
+                return arena.aggregate(mode, coef, divisor, clients=rows)
             return _aggregate_device(keys, ptrs, numel, codes, shapes, dev, len(dicts), mode, coef, divisor, engine)
         if dev == "cpu" and os.environ.get("FEDML_AMD_HOST_PATH", "packed") == "packed":
             return _aggregate_host(keys, ptrs, numel, codes, shapes, len(dicts), mode, coef, divisor, engine)
@@ -130,8 +135,15 @@ def _pack_threads() -> int:
 
 
 def _aggregate_host(keys, ptrs, numel, codes, shapes, k, mode, coef, divisor, engine):
-    """CPU state_dicts: pack -> pinned -> H2D (overlapped) -> one launch per dtype -> D2H."""
+    """CPU state_dicts: pack -> pinned -> H2D (overlapped) -> one launch per dtype -> D2H.
+    The pinned slots and device matrices are per-device state shared by every caller: the
+    engine's lock serialises concurrent rounds (e.g. two receive threads)."""
     eng = engine or get_engine(None)
+    with eng.lock:
+        return _aggregate_host_locked(eng, keys, ptrs, numel, codes, shapes, k, mode, coef, divisor)
+
+
+def _aggregate_host_locked(eng, keys, ptrs, numel, codes, shapes, k, mode, coef, divisor):
     st = _STAGING.get(eng.device_index)
     if st is None:
         st = _STAGING[eng.device_index] = _HostStaging(eng)

@@ -94,11 +94,11 @@ def _case_group_reduce(rank, world):
     parts = [orc.weighted_sum([xs[i] for i in range(r * per, (r + 1) * per)], 0,
                               [counts[i] / N for i in range(r * per, (r + 1) * per)]) for r in range(world)]
     exp = orc.weighted_sum(parts, 2)
-    for coll in ("reduce", "all_reduce", "ordered"):
+    for coll in ("reduce", "all_reduce", "ordered", "ordered_all"):
         for chunks in (1, 3, 8):
             red = GroupReducer(collective=coll, chunks=chunks, local_sum=_oracle_sum)
             got = red.fedavg([xs[i] for i in mine], w)
-            if rank == 0 or coll == "all_reduce":
+            if rank == 0 or coll in ("all_reduce", "ordered_all"):
                 assert _bits(got, exp), (coll, chunks)
     # hierarchical: group FedAvg, cloud term (G*N_r)/N, ordered sum over groups
     red = GroupReducer(collective="ordered", chunks=4, local_sum=_oracle_sum)
@@ -238,11 +238,11 @@ def _case_group_reduce_tiled(rank, world):
                               [counts[i] / N for i in range(r * per, (r + 1) * per)]) for r in range(world)]
     exp = orc.weighted_sum(parts, 2)
     buf = _tiled_buf([xs[i] for i in mine])
-    for coll in ("reduce", "all_reduce", "ordered"):
+    for coll in ("reduce", "all_reduce", "ordered", "ordered_all"):
         for chunks in (1, 3, 8):
             red = GroupReducer(collective=coll, chunks=chunks, local_sum=_oracle_sum)
             got = red.fedavg_tiled(_OracleTiledEngine(), buf, list(range(per)), [counts[i] / N for i in mine], P)
-            if rank == 0 or coll == "all_reduce":
+            if rank == 0 or coll in ("all_reduce", "ordered_all"):
                 assert _bits(got, exp), (coll, chunks)
     # reduce_scatter: shards of whole tiles
     P2 = 1024 * 8
@@ -259,3 +259,70 @@ def _case_group_reduce_tiled(rank, world):
 
 def test_group_reduce_tiled_gloo_world2():
     _spawn(_case_group_reduce_tiled)
+
+
+# ------------------------------------------------------------------------------ ordered, G > 2
+def _case_ordered_multi(rank, world):
+    """The owner-summed "ordered" exchange at G = 3 / 4: every chunk split over the G-1 owners (some
+    pieces empty at small n), rank-ordered sums, delivered to dst (0 or the last rank) or to all;
+    bit-identical to the oracle's rank-ordered sum of per-rank partials, flat and tiled, and for the
+    hierarchical cloud formula with one group per rank."""
+    from oracle import orc
+    from fedml_amd.distributed.group_reduce import GroupReducer
+    per = 3
+    K = per * world
+    for P in (1, 5, 1024 * 7 + 13, 40_001):
+        xs, counts = _clients(K, P, seed=P)
+        N = sum(counts)
+        ids = [list(range(r * per, (r + 1) * per)) for r in range(world)]
+        parts = [orc.weighted_sum([xs[i] for i in ids[r]], 0, [counts[i] / N for i in ids[r]]) for r in range(world)]
+        exp = orc.weighted_sum(parts, 2)
+        mine = ids[rank]
+        for coll, dst in (("ordered", 0), ("ordered", world - 1), ("ordered_all", 0)):
+            for chunks in (1, 4):
+                red = GroupReducer(collective=coll, dst=dst, chunks=chunks, local_sum=_oracle_sum)
+                out = torch.full((P,), float("nan"))
+                got = red.fedavg([xs[i] for i in mine], [counts[i] / N for i in mine], out=out)
+                if rank == dst or coll == "ordered_all":
+                    assert got is out and _bits(got, exp), (P, coll, dst, chunks)
+                owned = sum(hi - lo for lo, hi in red.owned)
+                assert owned == 0 if rank == dst else (owned > 0 or P < 1000), (rank, red.owned)
+        if P > 1024:
+            red = GroupReducer(collective="ordered", chunks=3, local_sum=_oracle_sum)
+            got = red.fedavg_tiled(_OracleTiledEngine(), _tiled_buf([xs[i] for i in mine]), list(range(per)),
+                                   [counts[i] / N for i in mine], P)
+            if rank == 0:
+                assert _bits(got, exp), P
+        # hierarchical cloud formula, one group per rank: bit-identical to the sequential cloud sum
+        red = GroupReducer(collective="ordered", chunks=2, local_sum=_oracle_sum)
+        got = red.hierarchical([xs[i] for i in mine], [counts[i] for i in mine], N)
+        terms = []
+        for r in range(world):
+            nr = sum(counts[i] for i in ids[r])
+            G = orc.weighted_sum([xs[i] for i in ids[r]], 0, [counts[i] / nr for i in ids[r]])
+            terms.append(orc.weighted_sum([G], 1, [nr], float(N)))
+        if rank == 0:
+            assert _bits(got, orc.weighted_sum(terms, 2)), P
+
+
+def test_ordered_gloo_world3():
+    _spawn(_case_ordered_multi, world=3)
+
+
+def test_ordered_gloo_world4():
+    _spawn(_case_ordered_multi, world=4)
+
+
+def _case_reduce_scatter_out_untouched(rank, world):
+    """reduce_scatter stages internally: a caller's ``out`` is never overwritten with partials."""
+    from fedml_amd.distributed.group_reduce import GroupReducer
+    xs, counts = _clients(2, 4000, seed=3)
+    out = torch.full((4000,), 7.0)
+    red = GroupReducer(collective="reduce_scatter", chunks=2, local_sum=_oracle_sum)
+    shard = red.fedavg([xs[rank]], [0.5], out=out)
+    assert torch.equal(out, torch.full((4000,), 7.0))
+    assert shard.numel() == 2000
+
+
+def test_reduce_scatter_out_untouched_gloo_world2():
+    _spawn(_case_reduce_scatter_out_untouched)
