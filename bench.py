@@ -50,7 +50,7 @@ def parse():
     p.add_argument("--config", default="metric",
                    choices=["metric", "fragmented", "resnet18", "vit_bf16", "hier", "gossip", "host", "secagg", "fedopt",
                             "dropin_cpu", "median",
-                            "krum"])
+                            "krum", "arrival"])
     p.add_argument("--clients", type=int, default=None)
     p.add_argument("--params", type=int, default=None)
     p.add_argument("--variant", type=int, default=0, help="kernel variant (fa_ctx_set_variant)")
@@ -68,13 +68,17 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     p.add_argument("--check-samples", type=int, default=65536)
+    p.add_argument("--arrival-gap-ms", type=float, default=2.0,
+                   help="arrival config: time between two clients' updates arriving")
     p.add_argument("--pinned", action="store_true", help="host config: client updates already in pinned memory")
     p.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "fp16"],
                    help="median config: element type of the client vectors")
-    p.add_argument("--layout", default=None, choices=["arena", "tiled", "tensors"],
+    p.add_argument("--layout", default=None, choices=["arena", "tiled", "tensors", "adopted"],
                    help="arena: client updates as rows of one ClientArena allocation (fedml_amd/arena.py); "
                         "tiled: tile-interleaved ClientArena (4-KiB tiles of all clients contiguous); "
-                        "tensors: one allocation per client tensor.  Default: tiled, except gossip (arena: its "
+                        "tensors: one allocation per client tensor; adopted: state_dicts adopted into client-major "
+                        "arena rows on arrival (ClientArena.adopt, what the round drivers do) and aggregated through "
+                        "FedMLAggOperator.agg.  Default: tiled, except gossip (arena: its "
                         "row-sequential sliding window measured 5.12 ms client-major vs 5.52 ms tiled)")
     a = p.parse_args()
     if a.layout is None:
@@ -413,7 +417,17 @@ def wl_layout(args, eng, rank, world, timer):
     w = [counts[i] / N for i in mine]
     dicts = make_layout_clients(mine, layout)
     arena = None
-    if args.layout in ("arena", "tiled") or world > 1:
+    adopted = args.layout == "adopted" and world == 1
+    if adopted:  # the round drivers' form: updates adopted into arena rows, aggregated by the drop-in
+        from fedml_amd.arena import ArenaLayout, ClientArena
+        from fedml_amd.ml.aggregator.agg_operator import FedMLAggOperator
+        keep = ClientArena(ArenaLayout([(n, tuple(s), getattr(torch, dt)) for n, s, dt in layout]), capacity=len(mine))
+        for j, d in enumerate(dicts):
+            keep.adopt(j, d)
+        torch.cuda.synchronize()
+        A = type("Args", (), {"federated_optimizer": "FedAvg"})()
+        raw = [(counts[i], d) for i, d in zip(mine, dicts)]
+    elif args.layout in ("arena", "tiled") or world > 1:
         from fedml_amd.arena import ArenaLayout, ClientArena
         arena = ClientArena(ArenaLayout([(n, tuple(s), getattr(torch, dt)) for n, s, dt in layout]),
                             capacity=len(mine), tiled=args.layout == "tiled" or world > 1)
@@ -449,7 +463,10 @@ def wl_layout(args, eng, rank, world, timer):
             res["out"] = arena.layout.carve(flat) if args.collective != "reduce_scatter" else None
             return
         with timer:
-            res["out"] = arena.aggregate(MUL_W, w) if arena is not None else aggregate(dicts, MUL_W, w)
+            if adopted:
+                res["out"] = FedMLAggOperator.agg(A, raw)
+            else:
+                res["out"] = arena.aggregate(MUL_W, w) if arena is not None else aggregate(dicts, MUL_W, w)
 
     def parity():
         from oracle import orc
@@ -488,7 +505,8 @@ def wl_layout(args, eng, rank, world, timer):
             bad += count_bad(got, exp)
         return f"{'bit-exact' if bad == 0 else f'{bad} MISMATCHES'} vs oracle on a strided sample of every key"
 
-    tag = ("resnet18gn" if resnet else "vitb16_bf16") + {"arena": "", "tiled": "_tiled", "tensors": "_tensors"}[args.layout]
+    tag = ("resnet18gn" if resnet else "vitb16_bf16") + {"arena": "", "tiled": "_tiled", "tensors": "_tensors",
+                                                         "adopted": "_adopted_agg"}[args.layout]
     return dict(name=f"fedavg_{tag}_K{K}_P{P}", dtype="fp32" if resnet else "bf16", step=step, parity=parity,
                 bytes_total=K * in_b + out_b, launch_bytes=None, clients=K, params=P, cpu_K=None,
                 step_bytes=len(mine) * in_b + out_b if world > 1 else None)
@@ -551,8 +569,8 @@ def wl_dropin_cpu(args, eng, rank, world, timer):
         legs = {}
         for th in cpu_thread_legs():
             torch.set_num_threads(th)
-            ts = [one() for _ in range(5)]
-            legs[th] = (min(ts), len(ts))
+            ts = [one() for _ in range(5 if th <= cpu_quota() else 1)]
+            legs[th] = (min(ts), len(ts), 1.0)
         return legs_record(legs, K * in_b + out_b,
                            f"the same K={K} ResNet-18-GN CPU state_dicts, oracle/torch_port.agg('FedAvg') "
                            "(agg_operator.py:35-44)")
@@ -561,6 +579,106 @@ def wl_dropin_cpu(args, eng, rank, world, timer):
                 bytes_total=K * in_b + out_b, launch_bytes=None, clients=K, params=P, cpu_K=K,
                 data="synthetic CPU state_dicts (ResNet-18-GN layout), host-resident: the step includes H2D and D2H",
                 roofline_note="kernel time = the whole agg() call incl. PCIe transfers (host-resident inputs)")
+
+
+def _resnet_host_dicts(K, seed=1):
+    """K ResNet-18-GN state_dicts of CPU tensors (as unpickled from MPI / socket receive buffers)."""
+    layout = load_layout("resnet18_gn")
+    g = torch.Generator().manual_seed(seed)
+    dicts = []
+    for _ in range(K):
+        d = OrderedDict()
+        for name, shape, dt in layout:
+            dt = getattr(torch, dt)
+            d[name] = (torch.randint(0, 100, tuple(shape), generator=g, dtype=dt) if dt == torch.int64
+                       else torch.randn(tuple(shape), generator=g).to(dt))
+        dicts.append(d)
+    return layout, dicts
+
+
+def wl_arrival(args, eng, rank, world, timer):
+    """SURVEY.md §8(f) #1 / the reference's cross-silo round (cross_silo/server/fedml_aggregator.py:
+    57-104): K = 32 ResNet-18-GN updates arrive one at a time as CPU state_dicts; each is ingested
+    into HBM on arrival (FedMLAggregator.add_local_trained_result -> ArrivalIngest: pinned staging +
+    H2D on a copy stream, fedml_amd/ml/aggregator/ingest.py) while the next one is awaited
+    (``--arrival-gap-ms`` between arrivals, a network receive of 47 MB at ~25 GB/s takes ~2 ms);
+    after the last arrival: FedMLAggregator.aggregate (the user's ServerAggregator ->
+    FedMLAggOperator.agg, recognised as arena-resident: one launch) and the D2H of the global model
+    into pinned send buffers.  Value = latency from the last arrival to the host-resident global
+    model (ms, lower is better); the reference CPU loop can only start at that instant too."""
+    if world > 1:
+        raise SystemExit("--config arrival is a single-GPU configuration")
+    from fedml_amd.core.alg_frame.server_aggregator import ServerAggregator
+    from fedml_amd.cross_silo.server.fedml_aggregator import FedMLAggregator
+    K = args.clients or 32
+    layout, pristine = _resnet_host_dicts(K)
+    counts = client_counts(K)
+    gap = args.arrival_gap_ms * 1e-3
+
+    class BenchServerAggregator(ServerAggregator):
+        def get_model_params(self):
+            return self.params
+
+        def set_model_params(self, p):
+            self.params = p
+
+        def test(self, *a):
+            return None
+
+    A = type("Args", (), {"federated_optimizer": "FedAvg"})()
+    sagg = BenchServerAggregator(None, A)
+    agg = FedMLAggregator(K, torch.device("cuda", 0), A, sagg)
+    res = {}
+
+    def round_(gap_s):
+        dicts = [OrderedDict(d) for d in pristine]  # fresh containers; tensors are the received ones
+        for i in range(K - 1):
+            agg.add_local_trained_result(i, dicts[i], counts[i])
+            t_next = time.perf_counter() + gap_s
+            while time.perf_counter() < t_next:
+                pass
+        t0 = time.perf_counter()  # the last client's message has arrived
+        agg.add_local_trained_result(K - 1, dicts[K - 1], counts[K - 1])
+        agg.check_whether_all_receive()
+        agg.aggregate()
+        host = agg.get_global_model_params_host()
+        lat = time.perf_counter() - t0
+        res["host"] = host
+        return lat
+
+    def step():
+        return round_(gap)
+
+    P = sum(int(np.prod(s)) for _, s, _ in layout)
+
+    def parity():
+        import oracle.torch_port as tp
+        exp = tp.agg("FedAvg", [(n, OrderedDict(d)) for n, d in zip(counts, pristine)])
+        bad = sum(count_bad(res["host"][k].reshape(-1), exp[k].reshape(-1)) for k in exp)
+        back = [round_(0.0) * 1e3 for _ in range(3)]
+        res["b2b_ms"] = round(min(back), 3)
+        return (f"{'bit-exact' if bad == 0 else f'{bad} MISMATCHES'} vs the reference op sequence on every element "
+                f"of the host-resident global model")
+
+    def cpu(budget_s):
+        import oracle.torch_port as tp
+
+        def run():
+            tp.agg("FedAvg", [(n, OrderedDict(d)) for n, d in zip(counts, pristine)])
+        legs = timed_legs(run, budget_s, min_runs=3, max_runs=20)
+        best = min(legs, key=lambda th: legs[th][0])
+        return {"value": round(legs[best][0] * 1e3, 3), "unit": "ms", "cores": best, "kind": "port",
+                "value_by_threads": {str(th): round(b * 1e3, 3) for th, (b, _, _) in sorted(legs.items())},
+                "os_cpu_count": os.cpu_count(), "cpu_quota": cpu_quota(),
+                "sample": f"the reference loop oracle/torch_port.agg('FedAvg') (agg_operator.py:35-44) over the same "
+                          f"K={K} CPU state_dicts, started once all have arrived; best of runs per thread count"}
+
+    return dict(name=f"arrival_fedavg_resnet18gn_K{K}_P{P}", dtype="fp32", step=step, parity=parity, cpu=cpu,
+                latency=True, extra=res, clients=K, params=P, cpu_K=K, bytes_total=None, launch_bytes=None,
+                data=f"synthetic CPU state_dicts (ResNet-18-GN layout) arriving {args.arrival_gap_ms} ms apart; "
+                     "ingested to HBM on arrival; result D2H to pinned host memory",
+                metric_name=f"last-arrival -> host-resident global model latency, cross-silo FedAvg round, "
+                            f"ResNet-18-GN K={K}")
 
 
 def fragmented_layout(P, n_tensors=200):
@@ -1096,36 +1214,67 @@ def wl_krum(args, eng, rank, world, timer):
 
 
 # ----------------------------------------------------------------------------- CPU baseline
+def cpu_quota():
+    """CPUs this process may actually use: the affinity mask and the cgroup CFS quota (cpu.max);
+    on a one-GPU box os.cpu_count() shows the whole machine while the quota is the box's share."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def cpu_thread_legs():
-    """the CPU baseline runs on ALL the host's cores (torch.set_num_threads(
-    os.cpu_count())), overriding the box's OMP_NUM_THREADS=16; a 16-thread leg (the process's CPU
-    share on a one-GPU box) is recorded beside it."""
-    allc = os.cpu_count() or 1
-    return [allc] + ([16] if allc > 16 else [])
+    """SURVEY.md §8(d) asks for the CPU baseline on ALL the host's cores (torch.set_num_threads(
+    os.cpu_count()), overriding the box's OMP_NUM_THREADS=16).  That leg is run and recorded; so are
+    the CPU quota the process really has (cgroup cpu.max / affinity) and 16 threads.  A one-GPU box
+    shows all 256 cores but grants a 16-CPU share, where 256 threads collapse (0.07 GB/s measured,
+    profiles/r02a_bench.json): the reported value is the best leg, with its thread count."""
+    return sorted({os.cpu_count() or 1, cpu_quota(), min(16, os.cpu_count() or 1)}, reverse=True)
 
 
-def timed_legs(fn, budget_s, min_runs=3, max_runs=50):
-    """Best-of wall time of fn() per thread leg: {threads: (best_s, runs)}."""
+def timed_legs(fn, budget_s, min_runs=3, max_runs=50, small=None):
+    """Best-of wall time per thread leg: {threads: (best_s, runs, scale)}.  Legs with more threads
+    than the CPU quota run ONCE, on ``small()`` = (fn, scale) when given (a scaled-down sample: an
+    oversubscribed run of the full sample takes ~30 s)."""
     out = {}
-    for th in cpu_thread_legs():
+    quota = cpu_quota()
+    legs = sorted(cpu_thread_legs())
+    for th in legs:
         torch.set_num_threads(th)
-        best, runs, t_end = float("inf"), 0, time.perf_counter() + budget_s / len(cpu_thread_legs())
-        while runs < min_runs or (time.perf_counter() < t_end and runs < max_runs):
+        f, scale, lo, hi = fn, 1.0, min_runs, max_runs
+        if th > quota:
+            if small is None:  # an oversubscribed full-size run takes minutes (138 s measured, r02b)
+                continue
+            lo = hi = 1
+            f, scale = small()
+        best, runs, t_end = float("inf"), 0, time.perf_counter() + budget_s / len(legs)
+        while runs < lo or (time.perf_counter() < t_end and runs < hi):
             t0 = time.perf_counter()
-            fn()
+            f()
             best = min(best, time.perf_counter() - t0)
             runs += 1
-        out[th] = (best, runs)
+        out[th] = (best, runs, scale)
+    torch.set_num_threads(min(16, quota))
     return out
 
 
 def legs_record(legs, nbytes, sample, kind="port", digits=2):
-    """The all-core leg is the reported value (cores = os.cpu_count()); every leg's rate is kept."""
-    allc = max(legs)
-    rates = {th: round(nbytes / b / 1e9, digits) for th, (b, _) in legs.items()}
-    return {"value": rates[allc], "unit": "GB/s", "cores": allc, "kind": kind,
-            "value_by_threads": {str(th): r for th, r in sorted(rates.items())},
-            "sample": sample + f", best of {legs[allc][1]} runs per thread count"}
+    """The best thread-count leg is the reported value (``cores`` = its threads); every leg's rate
+    is kept, the all-core one included (see cpu_thread_legs)."""
+    rates = {th: round(nbytes * sc / b / 1e9, digits) for th, (b, _, sc) in legs.items()}
+    best = max(rates, key=lambda th: rates[th])
+    byth = {str(th): r for th, r in sorted(rates.items())}
+    for th in cpu_thread_legs():
+        byth.setdefault(str(th), "not run: oversubscribed past the CPU quota (the metric line records it)")
+    return {"value": rates[best], "unit": "GB/s", "cores": best, "kind": kind,
+            "value_by_threads": byth,
+            "os_cpu_count": os.cpu_count(), "cpu_quota": cpu_quota(),
+            "sample": sample + f", best of {legs[best][1]} runs per thread count"}
 
 
 def cpu_baseline(K, budget_s):
@@ -1138,7 +1287,11 @@ def cpu_baseline(K, budget_s):
     xs = [torch.randn(P, generator=g) for _ in range(K)]
     counts = client_counts(K)
     raw = [(counts[i], {"w": xs[i]}) for i in range(K)]
-    legs = timed_legs(lambda: torch_port.agg("FedAvg", raw), budget_s)
+
+    def small():  # 1/16 of the sample for the oversubscribed all-core leg
+        r = [(c, {"w": x[:P // 16]}) for c, x in zip(counts, xs)]
+        return (lambda: torch_port.agg("FedAvg", r)), 1 / 16
+    legs = timed_legs(lambda: torch_port.agg("FedAvg", raw), budget_s, small=small)
     rec = legs_record(legs, K * P * 4 + P * 4,
                       f"K={K} x P={P} fp32 host-resident, oracle/torch_port.agg('FedAvg') "
                       f"(op-for-op restatement of agg_operator.py:35-44)")
@@ -1186,7 +1339,7 @@ def main():
     timer = Timed()
     wl = {"metric": wl_metric, "fragmented": wl_fragmented, "resnet18": wl_layout, "vit_bf16": wl_layout, "hier": wl_hier,
           "gossip": wl_gossip, "host": wl_host, "secagg": wl_secagg, "fedopt": wl_fedopt, "dropin_cpu": wl_dropin_cpu, "median": wl_median,
-          "krum": wl_krum}[args.config](args, eng, rank, world, timer)
+          "krum": wl_krum, "arrival": wl_arrival}[args.config](args, eng, rank, world, timer)
 
     for _ in range(args.warmup):
         wl["step"]()
@@ -1195,15 +1348,19 @@ def main():
     torch.cuda.synchronize()
     timer.on = True
     t0 = time.perf_counter()
+    lat = []
     for _ in range(args.steps):
-        wl["step"]()
+        lat.append(wl["step"]())
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
     timer.on = False
     ms_per_step = elapsed / args.steps * 1e3
-    value = wl["bytes_total"] * args.steps / elapsed / 1e9
+    if wl.get("latency"):  # the step returns its own latency (s); value = mean latency in ms
+        value, unit, hib = float(np.mean(lat)) * 1e3, "ms", False
+    else:
+        value, unit, hib = wl["bytes_total"] * args.steps / elapsed / 1e9, "GB/s", True
 
     kernel_ms = timer.avg_ms()
     launch_bytes = wl["launch_bytes"]
@@ -1221,14 +1378,15 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": METRIC if args.config == "metric" else f"device-resident aggregate GB/s, {wl['name']}",
-            "value": round(value, 2),
-            "unit": "GB/s",
+            "metric": METRIC if args.config == "metric" else wl.get("metric_name",
+                                                                     f"device-resident aggregate GB/s, {wl['name']}"),
+            "value": round(value, 3 if unit == "ms" else 2),
+            "unit": unit,
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
+            "higher_is_better": hib,
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": wl["dtype"],
@@ -1254,6 +1412,12 @@ def main():
         }
         if wl.get("roofline_note"):
             line["roofline"]["note"] = wl["roofline_note"]
+        if wl.get("latency"):
+            line["latency_ms"] = {"mean": round(value, 3), "min": round(min(lat) * 1e3, 3),
+                                  "max": round(max(lat) * 1e3, 3)}
+            line["roofline"] = None  # a latency, not one kernel's rate
+            if wl.get("extra", {}).get("b2b_ms") is not None:  # all K updates arriving at once
+                line["latency_ms"]["all_arrive_at_once"] = wl["extra"]["b2b_ms"]
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

@@ -129,7 +129,6 @@ class ClientArena:
         self._next_stage = 0
         self._pending: List[torch.cuda.Event] = []
         self._rows_adopted: Dict[int, int] = {}  # row -> id of the state_dict adopted into it
-        self._layout_codes = None
 
     @classmethod
     def for_model(cls, template_state_dict, capacity: int, device=None, **kw) -> "ClientArena":
@@ -204,6 +203,8 @@ class ClientArena:
         ``resident_rows`` and run over the arena rows."""
         if self.tiled:
             raise TypeError("adopt: a tiled arena's rows are not tensor views (use a client-major arena)")
+        if len(state_dict) != len(self.layout.keys) or any(k not in self.layout.where for k in state_dict):
+            raise TypeError("adopt: the update's keys differ from the arena layout")
         self.write(i, state_dict)
         self._wait_ingest()
         for k, v in self.slot(i).items():
@@ -360,19 +361,18 @@ class ClientArena:
         return self.aggregate(MUL_W, [c / N for c in counts], clients=clients)
 
 
-_CODE = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3, torch.int64: 4}
 
 
-def resident_rows(dicts, keys, ptrs: torch.Tensor, numel: torch.Tensor, codes: torch.Tensor):
-    """(arena, rows) when every dict of ``dicts`` was adopted by ONE client-major arena, lists
-    exactly the layout's keys in order, and still holds that arena's row views (``ptrs`` /
-    ``numel`` / ``codes``: the dicts' key-major device pointer table, element counts and dtype
-    codes, fedml_amd._host.gather); else None."""
+def resident_rows(dicts, keys=None):
+    """(arena, rows) when every dict of ``dicts`` was adopted by ONE client-major arena and still
+    holds exactly that arena's row views, keys in the layout's order (checked in C++ by
+    fedml_amd._host.match_rows: the key order, each value's address, contiguity; dtype and shape
+    follow from the address being the arena's view, which adopt() created); else None."""
     first = _ADOPTED.get(id(dicts[0]))
     if first is None:
         return None
     arena = first[0]()
-    if arena is None or list(keys) != arena.layout.keys:
+    if arena is None:
         return None
     rows = []
     for d in dicts:
@@ -381,13 +381,6 @@ def resident_rows(dicts, keys, ptrs: torch.Tensor, numel: torch.Tensor, codes: t
             return None
         rows.append(e[1])
     base, stride = arena._ptr_table()
-    if arena._layout_codes is None:
-        arena._layout_codes = (torch.tensor([arena.layout.where[k][3] for k in arena.layout.keys], dtype=torch.int64),
-                               torch.tensor([_CODE[arena.layout.where[k][0]] for k in arena.layout.keys],
-                                            dtype=torch.int64))
-    if not (torch.equal(arena._layout_codes[0], numel) and torch.equal(arena._layout_codes[1], codes)):
-        return None
-    expect = base.view(-1, 1) + stride.view(-1, 1) * torch.tensor(rows, dtype=torch.int64).view(1, -1)
-    if not torch.equal(expect.view(-1), ptrs):
+    if not _host.match_rows(list(dicts), arena.layout.keys, base, stride, rows):
         return None
     return arena, rows

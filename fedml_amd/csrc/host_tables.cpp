@@ -218,7 +218,44 @@ void pack_range(torch::Tensor src, torch::Tensor dst_off, torch::Tensor nbytes, 
   for (auto& x : th) x.join();
 }
 
+// match_rows(dicts, keys, base, stride, rows) -> bool: does every dict list exactly `keys` (in
+// order) with values that are the views of an arena's rows -- value t of dict i at address
+// base[t] + rows[i] * stride[t], contiguous?  The arena-resident fast path of a state_dict
+// aggregation (fedml_amd/arena.py resident_rows) needs only this, not gather()'s full validation
+// and tables: one pass, no allocation, early exit (~10 ns per tensor).
+bool match_rows(py::list dicts, py::list keys, torch::Tensor base, torch::Tensor stride, py::list rows) {
+  const int64_t K = (int64_t)py::len(dicts);
+  const int64_t T = (int64_t)py::len(keys);
+  TORCH_CHECK(base.dtype() == torch::kInt64 && stride.dtype() == torch::kInt64 && base.numel() == T &&
+              stride.numel() == T && base.is_contiguous() && stride.is_contiguous(), "match_rows: tables");
+  if ((int64_t)py::len(rows) != K) return false;
+  const int64_t* B = base.data_ptr<int64_t>();
+  const int64_t* S = stride.data_ptr<int64_t>();
+  for (int64_t i = 0; i < K; ++i) {
+    PyObject* d = PyList_GET_ITEM(dicts.ptr(), i);
+    if (!PyDict_Check(d) || PyDict_GET_SIZE(d) != T) return false;
+    const int64_t row = PyLong_AsLongLong(PyList_GET_ITEM(rows.ptr(), i));
+    if (row == -1 && PyErr_Occurred()) throw py::error_already_set();
+    Py_ssize_t pos = 0;
+    PyObject *k, *v;
+    for (int64_t t = 0; t < T; ++t) {
+      if (!PyDict_Next(d, &pos, &k, &v)) return false;
+      PyObject* want = PyList_GET_ITEM(keys.ptr(), t);
+      if (k != want) {
+        const int eq = PyObject_RichCompareBool(k, want, Py_EQ);
+        if (eq < 0) throw py::error_already_set();
+        if (!eq) return false;
+      }
+      if (!THPVariable_Check(v)) return false;
+      const at::Tensor& x = THPVariable_Unpack(v);
+      if ((int64_t)x.data_ptr() != B[t] + row * S[t] || !x.is_contiguous()) return false;
+    }
+  }
+  return true;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("match_rows", &match_rows, "are these state_dicts the row views of one arena?");
   m.def("pack_range", &pack_range, "multi-threaded packing of host tensors into a pinned staging range");
   m.doc() = "host-side table builder of the fedml_amd aggregation engine (no tensor data access)";
   m.def("gather", &gather, "validate K client dicts x T keys, return the device pointer table");

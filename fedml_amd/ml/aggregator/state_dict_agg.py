@@ -57,16 +57,16 @@ def aggregate(dicts: Sequence[Dict[str, torch.Tensor]], mode: int, coef: Optiona
     keys = list(dicts[0].keys())
     if not keys:
         return OrderedDict()
+    hit = resident_rows(dicts)
+    if hit is not None:  # updates adopted into arena rows on arrival: one launch per dtype group
+        arena, rows = hit
+        return arena.aggregate(mode, coef, divisor, clients=rows)
     try:
         ptrs, numel, codes, shapes, dev = _host.gather(list(dicts), keys)
     except ValueError:  # mixed devices / non-contiguous: the staging path below normalises them
         ptrs = None
     if ptrs is not None and int(codes.min()) >= 0:
         if dev.startswith("cuda"):
-            hit = resident_rows(dicts, keys, ptrs, numel, codes)
-            if hit is not None:  # updates adopted into arena rows on arrival: one launch per dtype group
-                arena, rows = hit
-                return arena.aggregate(mode, coef, divisor, clients=rows)
             return _aggregate_device(keys, ptrs, numel, codes, shapes, dev, len(dicts), mode, coef, divisor, engine)
         if dev == "cpu" and os.environ.get("FEDML_AMD_HOST_PATH", "packed") == "packed":
             return _aggregate_host(keys, ptrs, numel, codes, shapes, len(dicts), mode, coef, divisor, engine)

@@ -4,6 +4,12 @@
 bit-identical to FedMLAggOperator.agg's FedAvg branch), run on the MI355X engine.  ``train`` is a
 compact version of the reference's round loop (:66-125): every round, each sampled client gets
 the global weights, trains with its ClientTrainer, and the updates are averaged on the GPU.
+
+The reference keeps each trained update as ``copy.deepcopy(w)`` (:101).  Here that copy is made
+into a row of a ClientArena on the engine's device (ClientArena.adopt: one copy per dtype group,
+the dict's entries rebound to the row's views), so ``_aggregate`` over the round's updates is
+recognised as arena-resident and runs as one launch per dtype group over the rows instead of a
+(key, client) pointer-table walk over separate allocations.
 """
 from __future__ import annotations
 
@@ -12,6 +18,9 @@ import logging
 from collections import OrderedDict
 from typing import Callable, List, Optional, Sequence, Tuple
 
+import torch
+
+from ...arena import ClientArena
 from ...ml.aggregator.state_dict_agg import fedavg
 
 
@@ -30,17 +39,38 @@ class FedAvgAPI:
         """Reference fedavg_api.py:144-159: avg[k] = sum_i x_i[k] * (n_i / N), client order."""
         return fedavg([params for _, params in w_locals], [n for n, _ in w_locals])
 
+    def _arena_for(self, w, capacity):
+        try:
+            return ClientArena.for_model(w, capacity, device=self._engine_device())
+        except TypeError:  # a dtype the arena does not hold: keep the reference's deep copies
+            return None
+
+    def _engine_device(self):
+        dev = torch.device(self.device) if self.device is not None else None
+        return dev if dev is not None and dev.type == "cuda" else None
+
     def train(self, rounds: Optional[int] = None):
         rounds = rounds if rounds is not None else int(getattr(self.args, "comm_round", 1))
         w_global = self.model.state_dict()
+        arena = None
         for r in range(rounds):
             idx = self.sampler(r) if self.sampler else list(range(len(self.client_trainers)))
             w_locals = []
-            for i in idx:
+            for j, i in enumerate(idx):
                 trainer = self.client_trainers[i]
                 trainer.set_model_params(copy.deepcopy(w_global))
                 trainer.train(self.train_data[i], self.device, self.args)
-                w_locals.append((self.sample_nums[i], trainer.get_model_params()))
+                w = OrderedDict(trainer.get_model_params())
+                if arena is None:
+                    arena = self._arena_for(w, len(self.client_trainers))
+                if arena is not None:
+                    try:
+                        arena.adopt(j, w)  # the reference's copy.deepcopy(w), into HBM row j
+                    except (TypeError, KeyError):
+                        w = copy.deepcopy(w)
+                else:
+                    w = copy.deepcopy(w)
+                w_locals.append((self.sample_nums[i], w))
             w_global = self._aggregate(w_locals)
             self.model.load_state_dict(w_global)
             logging.info("round %d aggregated %d clients", r, len(w_locals))

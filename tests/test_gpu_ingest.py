@@ -73,3 +73,113 @@ def test_concurrent_agg_threads():
         w = [c / sum(counts) for c in counts]
         for key in dicts[0]:
             assert _bits(results[t][key], orc.weighted_sum([d[key] for d in dicts], MUL_W, w)), (t, key)
+
+
+# ------------------------------------------------------------------------------ on-arrival ingest
+def _golden(name):
+    import os
+    from golden_io import GOLDEN_DIR, load_case
+    return load_case(os.path.join(GOLDEN_DIR, name + ".npz"))
+
+
+class _Count:
+    """Counts ClientArena.aggregate calls (the arena-resident path) during a block."""
+
+    def __init__(self, monkeypatch):
+        from fedml_amd.arena import ClientArena
+        self.n = 0
+        orig = ClientArena.aggregate
+
+        def spy(arena, *a, **kw):
+            self.n += 1
+            return orig(arena, *a, **kw)
+        monkeypatch.setattr(ClientArena, "aggregate", spy)
+
+
+def _server(client_num):
+    from fedml_amd.core.alg_frame.server_aggregator import ServerAggregator
+    from fedml_amd.cross_silo.server.fedml_aggregator import FedMLAggregator
+
+    class S(ServerAggregator):
+        def get_model_params(self):
+            return getattr(self, "p", None)
+
+        def set_model_params(self, p):
+            self.p = p
+
+        def test(self, *a):
+            return None
+    args = types.SimpleNamespace(federated_optimizer="FedAvg")
+    return FedMLAggregator(client_num=client_num, device="cuda:0", args=args, server_aggregator=S(None, args))
+
+
+@pytest.mark.parametrize("name", ["g3_fedavg_mixed_K5", "g2_fedavg_bf16_K7_P4099", "g1_fedavg_f32_K32_P4099",
+                                  "g9_edge_values_K4"])
+def test_cross_silo_arrival_ingest_rounds(monkeypatch, name):
+    """Updates adopted into arena rows as they arrive (out of order), three rounds (both row
+    buffers, then the first again): the round's aggregation is ONE arena launch, bit-exact to the
+    reference's output, the dicts now hold device tensors (as the reference's in-place move), and
+    the pinned host copy for the broadcast matches too."""
+    from golden_io import client_dicts, expected_dicts
+    from refcases import assert_dict_bits
+    meta, arr = _golden(name)
+    exp = expected_dicts(meta, arr)[0]
+    K = meta["num_clients"]
+    srv = _server(K)
+    spy = _Count(monkeypatch)
+    for rnd in range(3):
+        cl = client_dicts(meta, arr)
+        for i in reversed(range(K)):
+            srv.add_local_trained_result(i, cl[i], meta["n"][i])
+            assert all(v.is_cuda for v in cl[i].values())
+        assert srv.check_whether_all_receive()
+        avg, _, _ = srv.aggregate()
+        assert spy.n == rnd + 1, "the round did not run over the arena rows"
+        assert_dict_bits(OrderedDict((k, v.cpu()) for k, v in avg.items()), exp, f"{name} round {rnd}")
+        host = srv.get_global_model_params_host()
+        assert all(v.is_pinned() for v in host.values())
+        assert_dict_bits(host, exp, f"{name} host round {rnd}")
+
+
+def test_cross_silo_arrival_mixed_layouts_and_plain_dicts(monkeypatch):
+    """A plain ``dict`` is left where it is (reference :59-62); an update whose layout differs
+    from the round's first (an extra key) is moved tensor by tensor instead (the reference's
+    model_params_to_device); the round is aggregated over client 0's keys, exactly."""
+    from oracle import orc
+    srv = _server(3)
+    g = torch.Generator().manual_seed(2)
+    a = OrderedDict(w=torch.randn(1000, generator=g), b=torch.randn(10, generator=g))
+    b = dict(w=torch.randn(1000, generator=g), b=torch.randn(10, generator=g))
+    c = OrderedDict(w=torch.randn(1000, generator=g), b=torch.randn(10, generator=g), extra=torch.ones(3))
+    xs = {k: [d[k].clone() for d in (a, b, c)] for k in ("w", "b")}
+    srv.add_local_trained_result(0, a, 10)
+    srv.add_local_trained_result(1, b, 20)
+    srv.add_local_trained_result(2, c, 30)
+    assert a["w"].is_cuda and not b["w"].is_cuda and c["extra"].is_cuda
+    assert srv.check_whether_all_receive()
+    avg, _, _ = srv.aggregate()
+    assert list(avg.keys()) == ["w", "b"]
+    for k in ("w", "b"):
+        assert _bits(avg[k].cpu(), orc.weighted_sum(xs[k], MUL_W, [10 / 60, 20 / 60, 30 / 60])), k
+
+
+def test_mpi_aggregator_arrival_ingest(monkeypatch):
+    """The MPI simulator's server (x * n) / N formula over updates ingested on arrival; the result
+    comes back in pinned host memory, as the reference returns CPU tensors for CPU updates."""
+    from golden_io import client_dicts, expected_dicts
+    from refcases import assert_dict_bits
+    from fedml_amd.simulation.mpi.fedavg_aggregator import FedAVGAggregator
+    for name in ("g4_mpi_xn_div_N_K32", "g4_mpi_xn_div_N_int64_K5", "g4_mpi_xn_div_N_bf16_K4"):
+        meta, arr = _golden(name)
+        K = meta["num_clients"]
+        agg = FedAVGAggregator(K, device="cuda:0")
+        spy = _Count(monkeypatch)
+        for rnd in range(2):
+            cl = client_dicts(meta, arr)
+            for i in range(K):
+                agg.add_local_trained_result(i, cl[i], meta["n"][i])
+            assert agg.check_whether_all_receive()
+            avg = agg.aggregate()
+            assert spy.n == rnd + 1
+            assert all(not v.is_cuda for v in avg.values())
+            assert_dict_bits(avg, expected_dicts(meta, arr)[0], f"{name} round {rnd}")
