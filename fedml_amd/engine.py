@@ -526,6 +526,29 @@ class AggEngine:
             cast(out1.data_ptr(), N._P_vp), self._stream(stream))
         N.check(rc, "fa_weighted_sum_pair_multi")
 
+    def promote_add(self, acc: torch.Tensor, t: torch.Tensor, out: Optional[torch.Tensor] = None,
+                    stream=None) -> torch.Tensor:
+        """``acc += t`` across dtypes, PyTorch's in-place semantics (fa_promote_add): computed in
+        promote_types(acc, t), rounded to acc's dtype.  acc a float tensor; returns ``out`` (default:
+        a new tensor like acc; ``out=acc`` updates in place)."""
+        if acc.dtype not in (torch.float32, torch.bfloat16, torch.float16, torch.float64):
+            raise TypeError(f"promote_add: accumulator dtype {acc.dtype} must be a float type")
+        if t.dtype not in DTYPE_CODE:
+            raise TypeError(f"promote_add: term dtype {t.dtype} not supported")
+        if t.numel() != acc.numel():
+            raise RuntimeError(f"promote_add: {t.numel()} elements vs {acc.numel()}")
+        _require_device(acc, self.device, "accumulator")
+        _require_device(t, self.device, "term")
+        if out is None:
+            out = torch.empty_like(acc)
+        elif out.dtype != acc.dtype or out.numel() != acc.numel():
+            raise ValueError("promote_add: out must be like acc")
+        _require_device(out, self.device, "output")
+        rc = self._lib.fa_promote_add(self._ctx, DTYPE_CODE[acc.dtype], DTYPE_CODE[t.dtype], acc.numel(),
+                                      acc.data_ptr(), t.data_ptr(), out.data_ptr(), self._stream(stream))
+        N.check(rc, "fa_promote_add")
+        return out
+
     # ------------------------------------------------------------------ mixing / gossip
     def mix(self, xs: Sequence[torch.Tensor], row_ptr: Sequence[int], cols: Sequence[int],
             vals: Sequence[float], post_scale: Optional[Sequence[float]] = None,

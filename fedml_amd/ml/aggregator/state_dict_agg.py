@@ -63,7 +63,7 @@ def aggregate(dicts: Sequence[Dict[str, torch.Tensor]], mode: int, coef: Optiona
         return arena.aggregate(mode, coef, divisor, clients=rows)
     try:
         ptrs, numel, codes, shapes, dev = _host.gather(list(dicts), keys)
-    except ValueError:  # mixed devices / non-contiguous: the staging path below normalises them
+    except (ValueError, TypeError):  # mixed devices or dtypes / non-contiguous: the staging path handles them
         ptrs = None
     if ptrs is not None and int(codes.min()) >= 0:
         if dev.startswith("cuda"):
@@ -211,16 +211,17 @@ def _aggregate_staged(dicts, keys, mode, coef, divisor, engine):
     groups: Dict[torch.dtype, List[str]] = {}
     post: Dict[str, torch.dtype] = {}
     staged: Dict[str, List[torch.Tensor]] = {}
+    mixed: Dict[str, List[torch.Tensor]] = {}
     for k in keys:
         col = [d[k] for d in dicts]  # KeyError on a missing key, like the reference
         dt = col[0].dtype
         for i, t in enumerate(col):
-            if t.dtype != dt:
-                raise TypeError(f"key {k!r}: client {i} has dtype {t.dtype}, client 0 has {dt} "
-                                "(mixed-dtype promotion is not part of the supported contract)")
             if t.shape != col[0].shape:
                 raise RuntimeError(f"key {k!r}: client {i} shape {tuple(t.shape)} != {tuple(col[0].shape)}")
         col = [_to_engine(t, eng) for t in col]
+        if any(t.dtype != dt for t in col):  # clients disagree on this key's dtype: promotion
+            mixed[k] = col
+            continue
         if dt in _SMALL_INT or dt == torch.bool:
             # exact widening: int64 arithmetic gives the same low bits (SUM) and the same fp32
             # conversion (weighted modes) as the narrower integer type
@@ -236,6 +237,10 @@ def _aggregate_staged(dicts, keys, mode, coef, divisor, engine):
         outs = eng.weighted_sum_multi([staged[k] for k in ks], mode, coef, divisor)
         for k, o in zip(ks, outs):
             results[k] = o
+    for k, col in mixed.items():
+        results[k] = _aggregate_mixed(k, col, mode, coef, divisor, eng)
+        if mode == SUM and col[0].dtype in _SMALL_INT:
+            post[k] = col[0].dtype
     for k in keys:
         r = results[k]
         if k in post:
@@ -245,6 +250,38 @@ def _aggregate_staged(dicts, keys, mode, coef, divisor, engine):
             r = r.cpu()
         out[k] = r
     return out
+
+
+def _aggregate_mixed(k, col, mode, coef, divisor, eng):
+    """One key whose clients disagree on its dtype, with the reference's in-place semantics
+    (agg_operator.py:37-44, 55-63): avg = t_0; avg += t_i, each += computed in
+    promote_types(avg, t_i) and rounded to avg's dtype (fa_promote_add).  t_i = x_i * w_i in x_i's
+    own dtype (a K = 1 launch of the ordinary kernel: the reference's ``x * w``), or x_i for the
+    plain-sum branch; integer sums stay in int64 (wrap-around), narrow integer types widened
+    exactly first.  Pinned by tests/golden/g19_* (generated from the reference)."""
+    def widen(t):
+        if t.dtype in _SMALL_INT:
+            return t.to(torch.int64)  # exact
+        if t.dtype == torch.bool or t.dtype not in _NATIVE:
+            raise TypeError(f"key {k!r}: dtype {t.dtype} cannot take part in a mixed-dtype aggregation")
+        return t
+    terms = []
+    for i, x in enumerate(col):
+        x = widen(x).reshape(-1)
+        if mode == SUM:
+            terms.append(x)
+        else:
+            terms.append(eng.weighted_sum([x], mode, [coef[i]], divisor))
+    acc = terms[0].clone() if mode == SUM else terms[0]
+    for i, t in enumerate(terms[1:], 1):
+        if acc.dtype == t.dtype:
+            acc = eng.weighted_sum([acc, t], SUM)
+        elif acc.dtype == torch.int64:  # the reference's `int_tensor += float_tensor`
+            raise RuntimeError(f"result type {t.dtype} can't be cast to the desired output type Long "
+                               f"(key {k!r}, client {i})")
+        else:
+            acc = eng.promote_add(acc, t, out=acc)
+    return acc.view(col[0].shape)
 
 
 def fedavg(dicts, counts, engine=None):

@@ -259,6 +259,19 @@ int fa_ctx_set_mix_band(fa_ctx *ctx, int enable);
 int fa_stream_create_cu_masked(int hip_device, int cu_count, void **out_stream);
 int fa_stream_destroy(void *stream);
 
+/*
+ * Cross-dtype accumulation step of the reference's per-key client loop, for clients that disagree
+ * on a key's dtype (python/fedml/ml/aggregator/agg_operator.py:37-44 and :55-63: `avg[k] += t` with
+ * t = x_i[k] * w_i, or x_i[k], of another dtype than avg[k]):
+ *   out[e] = A( C(acc[e]) + C(t[e]) ),  C = torch.promote_types(A, T), added in C's op-math
+ *   (float for bf16/f16/f32, double for f64) and rounded to C, then cast to A.
+ * Casts are c10's: int64 -> bf16/f16 and f64 -> bf16/f16 round through float32.  acc_dtype A is a
+ * float type (F32/BF16/F16/F64); t_dtype T any FA_DTYPE.  out may alias acc.  Asynchronous on
+ * hip_stream; 0 or a negative status.
+ */
+int fa_promote_add(fa_ctx *ctx, int acc_dtype, int t_dtype, int64_t n, const void *d_acc, const void *d_t,
+                   void *d_out, void *hip_stream);
+
 /* Static name of a status code. */
 const char *fa_strerror(int code);
 /* Detail of the calling thread's last error ("" if none). */

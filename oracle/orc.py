@@ -87,6 +87,22 @@ def weighted_sum(xs, mode: int, coef=None, divisor: float = 1.0) -> torch.Tensor
     return out
 
 
+def promote_add(acc, t):
+    """acc += t across dtypes with PyTorch's in-place semantics (see orc_promote_add); new tensor."""
+    L = lib()
+    if not getattr(L, "_promote_declared", False):
+        L.orc_promote_add.restype = ctypes.c_int
+        L.orc_promote_add.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p]
+        L._promote_declared = True
+    acc, t = acc.contiguous(), t.contiguous()
+    out = torch.empty_like(acc)
+    rc = L.orc_promote_add(_DT[acc.dtype], _DT[t.dtype], acc.numel(), acc.data_ptr(), t.data_ptr(), out.data_ptr())
+    if rc != 0:
+        raise RuntimeError(f"orc_promote_add failed: {rc}")
+    return out
+
+
 def mix(xs, row_ptr, cols, vals, post_scale=None):
     """CSR-ordered mixing rows (see orc_mix); returns (outs, outs2 or None)."""
     xs = [x.contiguous() for x in xs]

@@ -946,6 +946,54 @@ def layouts(ao):
         print(f"layout {k}: {len(v)} tensors, {numel} elements")
 
 
+def cases_promotion():
+    """G19: clients that DISAGREE on a key's dtype, through the reference's FedMLAggOperator.agg:
+    every ``avg[k] += x_i[k] * w_i`` (and the plain-sum branch's ``avg[k] += x_i[k]``) is an
+    in-place add across dtypes -- computed in the promoted type of (avg, term), rounded to avg's
+    dtype (agg_operator.py:37-44, 55-63)."""
+    ao = load_agg_operator()
+    agg = ao.FedMLAggOperator.agg
+    f32, f64, bf, f16, i64, i32, i16 = (torch.float32, torch.float64, torch.bfloat16, torch.float16, torch.int64,
+                                       torch.int32, torch.int16)
+
+    def clients_of(seed, spec):
+        """spec: [(key, shape, [dtype per client])]: wide-magnitude values so roundings matter."""
+        g = torch.Generator().manual_seed(seed)
+        K = len(spec[0][2])
+        out = [OrderedDict() for _ in range(K)]
+        for key, shape, dts in spec:
+            for i, dt in enumerate(dts):
+                if dt in (i64, i32, i16):
+                    lim = {i64: 2 ** 40, i32: 2 ** 30, i16: 2 ** 14}[dt]
+                    out[i][key] = torch.randint(-lim, lim, shape, generator=g, dtype=dt)
+                else:
+                    v = torch.randn(shape, generator=g, dtype=f64) * torch.exp2(
+                        torch.randint(-12, 12, shape, generator=g).double())
+                    out[i][key] = v.to(dt)
+        return out
+
+    cases = [
+        ("g19_promote_fedavg_K5", "FedAvg", [("w", (1000,), [f32, f64, bf, i64, f16]),
+                                             ("v", (7, 3), [bf, f32, f16, f64, i64]),
+                                             ("s", (), [i64, f32, f64, i64, bf])]),
+        ("g19_promote_fedavg_K3", "FedAvg", [("a", (513,), [f64, f32, f32]),
+                                             ("b", (257,), [f16, bf, f32]),
+                                             ("c", (129,), [bf, i64, i64]),
+                                             ("d", (65,), [f16, i64, f64])]),
+        ("g19_promote_sum_K4", "FedAvg_seq", [("w", (1000,), [f32, f64, bf, f16]),
+                                              ("n", (33,), [i64, i32, i64, i16]),
+                                              ("h", (17,), [bf, f32, i64, f16]),
+                                              ("q", (9,), [f16, i64, bf, f32])]),
+    ]
+    for name, opt, spec in cases:
+        clients = clients_of(len(WRITTEN) + 1900, spec)
+        n = gen_counts(19, len(clients))
+        out = agg(Args(federated_optimizer=opt), list(zip(n, dc(clients))))
+        meta = dict(kind="agg", optimizer=opt, n=n, ref="agg_operator.py:35-63 (in-place add across dtypes)",
+                    client_in_dtypes=[[dtype_name(c[k]) for k in c] for c in clients])
+        write(name, clients, [out], meta)
+
+
 def main():
     if len(sys.argv) > 1:  # regenerate only the named families, e.g. `make_golden.py secagg`
         for part in sys.argv[1:]:
@@ -960,6 +1008,7 @@ def main():
     cases_topology_and_mixing(stm, tu)
     cases_fedopt()
     cases_secagg()
+    cases_promotion()
     layouts(ao)
     total = sum(s for _, s in WRITTEN)
     for name, s in WRITTEN:

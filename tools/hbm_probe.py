@@ -39,6 +39,11 @@ for k in (8, 32, 128):
     for u in (8, 16):
         t = timeit(lambda: L.hbm_probe_multi(ptrs.data_ptr(), k, per, out.data_ptr(), u, s))
         res[f"multi_k{k}_u{u}_GBs"] = round(k * per / t / 1e9, 1)
+    # with the aggregation kernel's output: one 16-byte vector per lane (bytes counted: k reads + 1 write)
+    outw = torch.empty(per // 4, dtype=torch.float32, device="cuda")
+    t = timeit(lambda: L.hbm_probe_multi(ptrs.data_ptr(), k, per, outw.data_ptr(), -8, s))
+    res[f"multi_k{k}_wide_out_incl_write_GBs"] = round((k + 1) * per / t / 1e9, 1)
+    del outw
 # the metric's shape: 128 streams x 500 MB in ONE 64 GB allocation, with and without a 16-B/lane output
 if os.environ.get("PROBE_BIG", "1") == "1":
     del src
