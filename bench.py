@@ -50,7 +50,7 @@ def parse():
     p.add_argument("--config", default="metric",
                    choices=["metric", "fragmented", "resnet18", "vit_bf16", "hier", "gossip", "host", "secagg", "fedopt",
                             "dropin_cpu", "median",
-                            "krum", "arrival"])
+                            "krum", "arrival", "lr"])
     p.add_argument("--clients", type=int, default=None)
     p.add_argument("--params", type=int, default=None)
     p.add_argument("--variant", type=int, default=0, help="kernel variant (fa_ctx_set_variant)")
@@ -427,6 +427,7 @@ def wl_layout(args, eng, rank, world, timer):
         torch.cuda.synchronize()
         A = type("Args", (), {"federated_optimizer": "FedAvg"})()
         raw = [(counts[i], d) for i, d in zip(mine, dicts)]
+        res_keep = keep  # the arena stays alive (its rows back the dicts; residency needs the object)
     elif args.layout in ("arena", "tiled") or world > 1:
         from fedml_amd.arena import ArenaLayout, ClientArena
         arena = ClientArena(ArenaLayout([(n, tuple(s), getattr(torch, dt)) for n, s, dt in layout]),
@@ -440,7 +441,7 @@ def wl_layout(args, eng, rank, world, timer):
     size = {"int64": 8, "bfloat16": 2, "float32": 4}
     in_b = sum(int(np.prod(s)) * size[dt] for _, s, dt in layout)
     out_b = sum(int(np.prod(s)) * (2 if dt == "bfloat16" else 4) for _, s, dt in layout)
-    res = {}
+    res = {"arena": res_keep} if adopted else {}
     if world > 1:
         class TimedEngine:
             def weighted_sum_tiled(self, *a, **kw):
@@ -679,6 +680,76 @@ def wl_arrival(args, eng, rank, world, timer):
                      "ingested to HBM on arrival; result D2H to pinned host memory",
                 metric_name=f"last-arrival -> host-resident global model latency, cross-silo FedAvg round, "
                             f"ResNet-18-GN K={K}")
+
+
+def wl_lr(args, eng, rank, world, timer):
+    """cfg1 (BASELINE configs[0], the reference's quick_start): FedAvg of K = 2 logistic-regression
+    updates (784 -> 10 weight + bias, 62.8 KB per client) through the drop-in
+    FedMLAggOperator.agg.  A round this small is launch/latency-bound, so the value is the latency
+    of one agg() call (ms, lower is better) until the result is usable: ``--layout host`` (default
+    here): CPU state_dicts in, CPU tensors out, as the reference's MPI/CPU quick_start holds them;
+    ``tensors``: device dicts, device result (synchronised); ``adopted``: arena-resident updates.
+    CPU baseline: the reference's loop (oracle/torch_port.agg) on the same CPU dicts."""
+    if world > 1:
+        raise SystemExit("--config lr is a single-GPU configuration")
+    from fedml_amd.ml.aggregator.agg_operator import FedMLAggOperator
+    K = args.clients or 2
+    layout = [("linear.weight", (10, 784), "float32"), ("linear.bias", (10,), "float32")]
+    counts = client_counts(K)
+    g = torch.Generator().manual_seed(3)
+    host = [OrderedDict((n, torch.randn(s, generator=g)) for n, s, _ in layout) for _ in range(K)]
+    mode = args.layout if args.layout in ("tensors", "adopted") else "host"
+    if mode == "host":
+        dicts = host
+    else:
+        dicts = [OrderedDict((k, v.cuda()) for k, v in d.items()) for d in host]
+        if mode == "adopted":
+            from fedml_amd.arena import ClientArena
+            keep = ClientArena.for_model(dicts[0], K)
+            for j, d in enumerate(dicts):
+                keep.adopt(j, d)
+    A = type("Args", (), {"federated_optimizer": "FedAvg"})()
+    raw = list(zip(counts, dicts))
+    res = {"arena": keep} if mode == "adopted" else {}  # the adopting arena must stay alive
+
+    def step():
+        t0 = time.perf_counter()
+        out = FedMLAggOperator.agg(A, raw)
+        if mode != "host":
+            torch.cuda.current_stream().synchronize()
+        res["out"] = out
+        return time.perf_counter() - t0
+
+    def parity():
+        import oracle.torch_port as tp
+        exp = tp.agg("FedAvg", [(n, OrderedDict(d)) for n, d in zip(counts, host)])
+        bad = sum(count_bad(res["out"][k].cpu().reshape(-1), exp[k].reshape(-1)) for k in exp)
+        return f"{'bit-exact' if bad == 0 else f'{bad} MISMATCHES'} vs the reference op sequence on every element"
+
+    def cpu(budget_s):
+        import oracle.torch_port as tp
+        lat = {}
+        for th in sorted({1, min(16, cpu_quota())}):
+            torch.set_num_threads(th)
+            ts = []
+            for _ in range(2000):
+                lst = [(n, OrderedDict(d)) for n, d in zip(counts, host)]
+                t0 = time.perf_counter()
+                tp.agg("FedAvg", lst)
+                ts.append(time.perf_counter() - t0)
+            lat[th] = float(np.median(ts))
+        best = min(lat, key=lambda th: lat[th])
+        return {"value": round(lat[best] * 1e3, 4), "unit": "ms", "cores": best, "kind": "port",
+                "value_by_threads": {str(th): round(v * 1e3, 4) for th, v in sorted(lat.items())},
+                "sample": f"median of 2000 calls of oracle/torch_port.agg('FedAvg') (agg_operator.py:35-44) on the "
+                          f"same K={K} CPU state_dicts"}
+
+    P = sum(int(np.prod(s)) for _, s, _ in layout)
+    return dict(name=f"fedavg_lr_mnist_K{K}_P{P}_{mode}", dtype="fp32", step=step, parity=parity, cpu=cpu,
+                latency=True, stat="median", clients=K, params=P, cpu_K=K, bytes_total=None, launch_bytes=None,
+                data=f"synthetic LR-MNIST updates (784x10 + 10 fp32), {'CPU' if mode == 'host' else 'device'} "
+                     f"state_dicts{' adopted into arena rows' if mode == 'adopted' else ''}",
+                metric_name=f"FedMLAggOperator.agg latency per call, cfg1 LR-MNIST K={K} ({mode})")
 
 
 def fragmented_layout(P, n_tensors=200):
@@ -1339,7 +1410,7 @@ def main():
     timer = Timed()
     wl = {"metric": wl_metric, "fragmented": wl_fragmented, "resnet18": wl_layout, "vit_bf16": wl_layout, "hier": wl_hier,
           "gossip": wl_gossip, "host": wl_host, "secagg": wl_secagg, "fedopt": wl_fedopt, "dropin_cpu": wl_dropin_cpu, "median": wl_median,
-          "krum": wl_krum, "arrival": wl_arrival}[args.config](args, eng, rank, world, timer)
+          "krum": wl_krum, "arrival": wl_arrival, "lr": wl_lr}[args.config](args, eng, rank, world, timer)
 
     for _ in range(args.warmup):
         wl["step"]()
@@ -1357,8 +1428,9 @@ def main():
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
     timer.on = False
     ms_per_step = elapsed / args.steps * 1e3
-    if wl.get("latency"):  # the step returns its own latency (s); value = mean latency in ms
-        value, unit, hib = float(np.mean(lat)) * 1e3, "ms", False
+    if wl.get("latency"):  # the step returns its own latency (s); value = mean (or median) latency in ms
+        value = float(np.median(lat) if wl.get("stat") == "median" else np.mean(lat)) * 1e3
+        unit, hib = "ms", False
     else:
         value, unit, hib = wl["bytes_total"] * args.steps / elapsed / 1e9, "GB/s", True
 
@@ -1380,7 +1452,7 @@ def main():
         line = {
             "metric": METRIC if args.config == "metric" else wl.get("metric_name",
                                                                      f"device-resident aggregate GB/s, {wl['name']}"),
-            "value": round(value, 3 if unit == "ms" else 2),
+            "value": round(value, 4 if unit == "ms" else 2),
             "unit": unit,
             "n_gpus": world,
             "steps": args.steps,
@@ -1413,8 +1485,9 @@ def main():
         if wl.get("roofline_note"):
             line["roofline"]["note"] = wl["roofline_note"]
         if wl.get("latency"):
-            line["latency_ms"] = {"mean": round(value, 3), "min": round(min(lat) * 1e3, 3),
-                                  "max": round(max(lat) * 1e3, 3)}
+            line["latency_ms"] = {"mean": round(float(np.mean(lat)) * 1e3, 4),
+                                  "median": round(float(np.median(lat)) * 1e3, 4),
+                                  "min": round(min(lat) * 1e3, 4), "max": round(max(lat) * 1e3, 4)}
             line["roofline"] = None  # a latency, not one kernel's rate
             if wl.get("extra", {}).get("b2b_ms") is not None:  # all K updates arriving at once
                 line["latency_ms"]["all_arrive_at_once"] = wl["extra"]["b2b_ms"]

@@ -78,6 +78,11 @@ struct fa_ctx {
     bool pending = false;
   } slots[fa_detail::kSlots];
   int next = 0;
+  // fa_weighted_sum_host: one mapped pinned buffer the kernel reads and writes in place over PCIe
+  void* zc_host = nullptr;
+  void* zc_dev = nullptr;
+  size_t zc_cap = 0;
+  hipEvent_t zc_ev = nullptr;
 };
 
 namespace fa_detail {

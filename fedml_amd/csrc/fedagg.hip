@@ -30,6 +30,7 @@
 #include <cstring>
 #include <new>
 #include <type_traits>
+#include <vector>
 
 #include "fa_internal.h"
 
@@ -1037,6 +1038,8 @@ int fa_ctx_destroy(fa_ctx* c) {
     if (s.host) (void)hipHostFree(s.host);
     if (s.dev) (void)hipFree(s.dev);
   }
+  if (c->zc_ev) (void)hipEventDestroy(c->zc_ev);
+  if (c->zc_host) (void)hipHostFree(c->zc_host);
   delete c;
   return FA_OK;
 }
@@ -1205,6 +1208,71 @@ int fa_weighted_sum_multi(fa_ctx* ctx, int dtype, int mode, int32_t num_segments
                           const int64_t* seg_numel, int32_t k, const void* const* d_in,
                           const double* coef, double divisor, void* const* d_out, void* hip_stream) {
   return wsum_impl(ctx, dtype, mode, num_segments, seg_numel, k, d_in, coef, divisor, d_out, hip_stream, 0);
+}
+
+// Small host-resident rounds (the reference's quick_start: LR-MNIST, K = 2, 63 KB per client): the
+// launch/copy latencies dominate, so the inputs are packed into ONE mapped pinned buffer and the
+// kernel reads them -- and writes the result -- in place over PCIe (no H2D / D2H copies, one launch,
+// one event wait).  Same kernel, same bits as the device path.
+int fa_weighted_sum_host(fa_ctx* ctx, int dtype, int mode, int32_t num_segments, const int64_t* seg_numel,
+                         int32_t k, const void* const* h_in, const double* coef, double divisor, void* const* h_out,
+                         void* hip_stream) {
+  if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (k <= 0 || num_segments <= 0 || !seg_numel || !h_in || !h_out)
+    return fail(FA_ERR_INVALID, "fa_weighted_sum_host: invalid arguments");
+  const int V = elems_per_vec(dtype);
+  if (V == 0) return fail(FA_ERR_DTYPE, "unknown dtype %d", dtype);
+  if (num_segments > 4096 || k > 4096) return fail(FA_ERR_INVALID, "fa_weighted_sum_host: too many segments/clients");
+  const size_t in_es = dtype == FA_DTYPE_F32 ? 4 : (dtype == FA_DTYPE_BF16 || dtype == FA_DTYPE_F16) ? 2 : 8;
+  const size_t out_es = (dtype == FA_DTYPE_I64 && mode != FA_MODE_SUM) ? 4 : in_es;
+  size_t total = 0;
+  for (int s = 0; s < num_segments; ++s) {
+    if (seg_numel[s] < 0) return fail(FA_ERR_INVALID, "segment %d has negative numel", s);
+    total += (size_t)k * align16((size_t)seg_numel[s] * in_es) + align16((size_t)seg_numel[s] * out_es);
+  }
+  DeviceGuard g(ctx->device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
+  if (!ctx->zc_ev) FA_HIP(hipEventCreateWithFlags(&ctx->zc_ev, hipEventDisableTiming));
+  if (ctx->zc_cap < total) {
+    if (ctx->zc_host) FA_HIP(hipHostFree(ctx->zc_host));
+    ctx->zc_host = ctx->zc_dev = nullptr;
+    ctx->zc_cap = 0;
+    const size_t cap = std::max<size_t>(total, 1 << 20);
+    if (hipHostMalloc(&ctx->zc_host, cap, hipHostMallocMapped) != hipSuccess)
+      return fail(FA_ERR_NOMEM, "hipHostMalloc(%zu, mapped) failed", cap);
+    FA_HIP(hipHostGetDevicePointer(&ctx->zc_dev, ctx->zc_host, 0));
+    ctx->zc_cap = cap;
+  }
+  std::vector<const void*> din((size_t)num_segments * k);
+  std::vector<void*> dout(num_segments);
+  size_t off = 0;
+  char* hb = (char*)ctx->zc_host;
+  char* db = (char*)ctx->zc_dev;
+  for (int s = 0; s < num_segments; ++s) {
+    const size_t nb = (size_t)seg_numel[s] * in_es;
+    for (int i = 0; i < k; ++i) {
+      const void* src = h_in[(size_t)s * k + i];
+      if (!src && nb) return fail(FA_ERR_INVALID, "segment %d client %d: input NULL", s, i);
+      if (nb) memcpy(hb + off, src, nb);
+      din[(size_t)s * k + i] = db + off;
+      off += align16(nb);
+    }
+    dout[s] = db + off;
+    off += align16((size_t)seg_numel[s] * out_es);
+  }
+  int rc = wsum_impl(ctx, dtype, mode, num_segments, seg_numel, k, din.data(), coef, divisor, dout.data(),
+                     hip_stream, 0);
+  if (rc) return rc;
+  FA_HIP(hipEventRecord(ctx->zc_ev, (hipStream_t)hip_stream));
+  FA_HIP(hipEventSynchronize(ctx->zc_ev));
+  for (int s = 0; s < num_segments; ++s) {
+    const size_t nb = (size_t)seg_numel[s] * out_es;
+    if (nb) {
+      if (!h_out[s]) return fail(FA_ERR_INVALID, "segment %d: output NULL", s);
+      memcpy(h_out[s], hb + ((char*)dout[s] - db), nb);
+    }
+  }
+  return FA_OK;
 }
 
 int fa_weighted_sum(fa_ctx* ctx, int dtype, int mode, int64_t n, int32_t k, const void* const* d_in,

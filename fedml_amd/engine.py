@@ -504,6 +504,24 @@ class AggEngine:
             N.ctypes.cast(out_ptrs.data_ptr(), N._P_vp), self._stream(stream))
         N.check(rc, "fa_weighted_sum_multi")
 
+    def weighted_sum_host_table(self, dtype_code: int, mode: int, seg_numel: torch.Tensor, k: int,
+                                in_ptrs: torch.Tensor, out_ptrs: torch.Tensor, coef: Optional[Sequence[float]] = None,
+                                divisor: float = 1.0, stream=None) -> None:
+        """fa_weighted_sum_host from prebuilt tables of HOST pointers (int64 CPU tensors, as
+        weighted_sum_table): synchronous, the kernel reads and writes mapped pinned memory."""
+        T = seg_numel.numel()
+        assert in_ptrs.dtype == torch.int64 and in_ptrs.numel() == T * k and in_ptrs.is_contiguous()
+        assert out_ptrs.dtype == torch.int64 and out_ptrs.numel() == T and out_ptrs.is_contiguous()
+        assert seg_numel.dtype == torch.int64 and seg_numel.is_contiguous()
+        if mode != SUM and (coef is None or len(coef) != k):
+            raise ValueError("weighted_sum: need one coefficient per client")
+        c = N.f64_array(coef if coef is not None else [0.0] * k)
+        rc = self._lib.fa_weighted_sum_host(
+            self._ctx, int(dtype_code), int(mode), T, N.ctypes.cast(seg_numel.data_ptr(), N._P_i64), k,
+            N.ctypes.cast(in_ptrs.data_ptr(), N._P_vp), c, float(divisor),
+            N.ctypes.cast(out_ptrs.data_ptr(), N._P_vp), self._stream(stream))
+        N.check(rc, "fa_weighted_sum_host")
+
     def weighted_sum_table_pair(self, dtype_code: int, mode: int, numel0: torch.Tensor, in0: torch.Tensor,
                                 out0: torch.Tensor, numel1: torch.Tensor, in1: torch.Tensor, out1: torch.Tensor,
                                 k: int, coef: Optional[Sequence[float]] = None, divisor: float = 1.0,

@@ -69,6 +69,10 @@ def aggregate(dicts: Sequence[Dict[str, torch.Tensor]], mode: int, coef: Optiona
         if dev.startswith("cuda"):
             return _aggregate_device(keys, ptrs, numel, codes, shapes, dev, len(dicts), mode, coef, divisor, engine)
         if dev == "cpu" and os.environ.get("FEDML_AMD_HOST_PATH", "packed") == "packed":
+            nbytes = sum(n * _ELEM[c] for n, c in zip(numel.tolist(), codes.tolist())) * len(dicts)
+            if nbytes <= _SMALL_HOST_BYTES:
+                return _aggregate_host_small(keys, ptrs, numel, codes, shapes, len(dicts), mode, coef, divisor,
+                                             engine)
             return _aggregate_host(keys, ptrs, numel, codes, shapes, len(dicts), mode, coef, divisor, engine)
     return _aggregate_staged(dicts, keys, mode, coef, divisor, engine)
 
@@ -105,6 +109,32 @@ def _aggregate_device(keys, ptrs, numel, codes, shapes, dev, k, mode, coef, divi
 
 
 _ELEM = {0: 4, 1: 2, 2: 2, 3: 8, 4: 8}  # bytes per element of each dtype code
+_SMALL_HOST_BYTES = 4 << 20             # CPU rounds up to this size: zero-copy kernel (fa_weighted_sum_host)
+
+
+def _aggregate_host_small(keys, ptrs, numel, codes, shapes, k, mode, coef, divisor, engine):
+    """Small CPU state_dicts (cfg1's LR-MNIST: 63 KB a client): one synchronous zero-copy launch
+    per dtype group -- inputs packed into mapped pinned memory, read and the result written in
+    place by the kernel over PCIe, copied into fresh CPU tensors (fa_weighted_sum_host)."""
+    eng = engine or get_engine(None)
+    code_list = codes.tolist()
+    out_dt = [out_dtype(_CODE_DTYPE[c], mode) for c in code_list]
+    _, views, optrs = _host.alloc_outputs(shapes, out_dt, "cpu")
+    groups: Dict[int, List[int]] = {}
+    for t, c in enumerate(code_list):
+        groups.setdefault(c, []).append(t)
+    with eng.lock:
+        if len(groups) == 1:
+            c = code_list[0]
+            eng.weighted_sum_host_table(c, mode, numel, k, ptrs, optrs, coef, divisor)
+        else:
+            table = ptrs.view(len(keys), k)
+            for c, idx in groups.items():
+                sel = torch.tensor(idx, dtype=torch.int64)
+                eng.weighted_sum_host_table(c, mode, numel.index_select(0, sel).contiguous(), k,
+                                            table.index_select(0, sel).reshape(-1).contiguous(),
+                                            optrs.index_select(0, sel).contiguous(), coef, divisor)
+    return OrderedDict(zip(keys, views))
 _SLOT_BYTES = 64 << 20                  # pinned staging slot (two of them, ping-pong)
 
 

@@ -260,6 +260,19 @@ int fa_stream_create_cu_masked(int hip_device, int cu_count, void **out_stream);
 int fa_stream_destroy(void *stream);
 
 /*
+ * fa_weighted_sum_multi for HOST-resident inputs and outputs (h_in: nseg*k host pointers,
+ * key-major; h_out: nseg host pointers), SYNCHRONOUS: the inputs are packed into one mapped pinned
+ * buffer owned by ctx, the kernel reads them and writes the results in place over PCIe (no
+ * separate H2D/D2H copies), the call waits for it on hip_stream and copies the results out.
+ * Replaces the reference loop (agg_operator.py:37-44) for small CPU-resident rounds, where
+ * launch and copy latencies dominate (cfg1: LR-MNIST, K = 2, 63 KB per client).  Same
+ * arithmetic and bits as fa_weighted_sum_multi.
+ */
+int fa_weighted_sum_host(fa_ctx *ctx, int dtype, int mode, int32_t num_segments, const int64_t *seg_numel,
+                         int32_t k, const void *const *h_in, const double *coef, double divisor,
+                         void *const *h_out, void *hip_stream);
+
+/*
  * Cross-dtype accumulation step of the reference's per-key client loop, for clients that disagree
  * on a key's dtype (python/fedml/ml/aggregator/agg_operator.py:37-44 and :55-63: `avg[k] += t` with
  * t = x_i[k] * w_i, or x_i[k], of another dtype than avg[k]):
