@@ -31,7 +31,7 @@ EXPORTED_SYMBOLS = (
     "fa_weighted_sum_multi", "fa_weighted_sum_tiled", "fa_weighted_sum_tiled_multi", "fa_weighted_sum_pair", "fa_weighted_sum_pair_multi", "fa_weighted_sum_grouped", "fa_weighted_sum_grouped_tiled",
     "fa_fedavg_sgd", "fa_fedavg_sgd_tiled", "fa_fedavg_rmsprop", "fa_mix", "fa_mix_tiled", "fa_ctx_set_variant",
     "fa_ctx_set_mix_band", "fa_stream_create_cu_masked", "fa_stream_destroy", "fa_strerror", "fa_last_error",
-    "fa_promote_add", "fa_weighted_sum_host",
+    "fa_promote_add", "fa_weighted_sum_host", "fa_pushsum",
     # include/fedagg_finite.h
     "fa_finite_sum", "fa_finite_sum_tiled", "fa_finite_quantize", "fa_lcc_decode",
     # include/fedagg_robust.h
@@ -137,6 +137,9 @@ def _declare(L):
     L.fa_weighted_sum_host.restype = ctypes.c_int
     L.fa_weighted_sum_host.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int32, _P_i64, ctypes.c_int32,
                                        _P_vp, _P_d, ctypes.c_double, _P_vp, _vp]
+    L.fa_pushsum.restype = ctypes.c_int
+    L.fa_pushsum.argtypes = [_vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int32, _P_i32, _P_i32, _P_d, ctypes.c_int32,
+                             _P_vp, _vp, _P_vp, _P_vp, _vp, _vp]
     L.fa_promote_add.restype = ctypes.c_int
     L.fa_promote_add.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _vp, _vp, _vp, _vp]
     L.fa_strerror.restype = ctypes.c_char_p

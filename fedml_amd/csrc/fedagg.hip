@@ -820,6 +820,24 @@ k_mix_band(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict
   }
 }
 
+// PushSum's weight on the device (client_pushsum.py:127-156): omega'_r = the row's ordered sum
+// omega_r * W_rr + sum_j omega_j * W_jr in float32 -- the same CSR order and per-op rounding as the
+// models' mixing rows (the reference's omega is a numpy float32: `omega *= W[i][i]`, then `+=` of
+// each sender's `omega_j * W`, in receive order) -- and the row's post-scale 1/omega' (float32
+// division, `1.0 / self.omega`), written into the staged row table the mixing kernel reads next.
+__global__ void __launch_bounds__(kBlock)
+k_pushsum_omega(MixRow* __restrict__ rows, int nrows, const int32_t* __restrict__ cols,
+                const double* __restrict__ vals, const float* __restrict__ omega_in, float* __restrict__ omega_out) {
+  const int r = blockIdx.x * kBlock + threadIdx.x;
+  if (r >= nrows) return;
+  const MixRow row = rows[r];
+  float acc = -0.0f;
+  for (int j = row.begin; j < row.end; ++j)
+    acc = accum<FA_DTYPE_F32, FA_MODE_MUL_W>(acc, term<FA_DTYPE_F32, FA_MODE_MUL_W>(omega_in[cols[j]], (float)vals[j], 0.f));
+  omega_out[r] = acc;
+  rows[r].scale = (double)op_div(1.0f, acc);
+}
+
 // The band offset `off` for which every entry of row r is input (r + off + {-1,0,1}) mod num_in,
 // or INT_MIN if the CSR is not banded that way.
 int band_offset(int32_t rows, const int32_t* row_ptr, const int32_t* cols, int32_t num_in) {
@@ -1700,7 +1718,11 @@ namespace {
 int mix_impl(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_ptr,
              const int32_t* cols, const double* vals, int32_t num_in, const void* const* d_in,
              void* const* d_out, const double* post_scale, void* const* d_out2, void* hip_stream,
-             int64_t isst, int64_t osst) {
+             int64_t isst, int64_t osst, const float* d_omega_in = nullptr, float* d_omega_out = nullptr) {
+  static const double kOnes[1] = {1.0};
+  const bool dev_omega = d_omega_in != nullptr;
+  if (dev_omega && (!d_omega_out || !d_out2)) return fail(FA_ERR_INVALID, "fa_pushsum: omega_out / d_out2 NULL");
+  if (dev_omega) post_scale = kOnes;  // the scales come from k_pushsum_omega, on the device
   if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
   if (rows <= 0 || n < 0 || !row_ptr || !cols || !vals || !d_in || !d_out || num_in <= 0)
     return fail(FA_ERR_INVALID, "fa_mix: invalid arguments");
@@ -1721,7 +1743,7 @@ int mix_impl(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row
     if (!d_in[i]) return fail(FA_ERR_INVALID, "fa_mix: input %d NULL", i);
     aligned = aligned && al16(d_in[i]);
   }
-  if (n == 0) return FA_OK;
+  if (n == 0 && !dev_omega) return FA_OK;
   if ((isst || osst) && !aligned) return fail(FA_ERR_INVALID, "fa_mix_tiled: inputs and outputs must be 16-byte aligned");
   const int V = elems_per_vec(dtype);
   const int64_t tiles = (n + (int64_t)kBlock * V - 1) / ((int64_t)kBlock * V);
@@ -1743,7 +1765,7 @@ int mix_impl(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row
   MixRow* hr = (MixRow*)h;
   for (int r = 0; r < rows; ++r)
     hr[r] = MixRow{row_ptr[r], row_ptr[r + 1], d_out[r], post_scale ? d_out2[r] : nullptr,
-                   post_scale ? post_scale[r] : 1.0};
+                   post_scale && !dev_omega ? post_scale[r] : 1.0};
   memcpy(h + row_bytes, cols, sizeof(int32_t) * nnz);
   memcpy(h + row_bytes + col_bytes, vals, sizeof(double) * nnz);
   memcpy(h + row_bytes + col_bytes + val_bytes, d_in, ptr_bytes);
@@ -1756,6 +1778,13 @@ int mix_impl(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row
   const void* const* dptr = (const void* const*)(d + row_bytes + col_bytes + val_bytes);
   const dim3 grid((unsigned)tiles), blk(kBlock);
   const int al = aligned ? 1 : 0;
+  if (dev_omega)
+    hipLaunchKernelGGL(k_pushsum_omega, dim3((unsigned)((rows + kBlock - 1) / kBlock)), blk, 0, st, (MixRow*)drw, rows,
+                       dcol, dval, d_omega_in, d_omega_out);
+  if (n == 0) {
+    FA_HIP(hipGetLastError());
+    return release(slot, st);
+  }
   int maxdeg = 0;
   for (int r = 0; r < rows; ++r) maxdeg = std::max(maxdeg, row_ptr[r + 1] - row_ptr[r]);
   const int band = (aligned && ctx->mix_band) ? band_offset(rows, row_ptr, cols, num_in) : INT32_MIN;
@@ -1802,6 +1831,14 @@ int fa_mix(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_p
            const int32_t* cols, const double* vals, int32_t num_in, const void* const* d_in,
            void* const* d_out, const double* post_scale, void* const* d_out2, void* hip_stream) {
   return mix_impl(ctx, dtype, n, rows, row_ptr, cols, vals, num_in, d_in, d_out, post_scale, d_out2, hip_stream, 0, 0);
+}
+
+int fa_pushsum(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_ptr, const int32_t* cols,
+               const double* vals, int32_t num_in, const void* const* d_in, const float* d_omega_in,
+               void* const* d_out, void* const* d_out2, float* d_omega_out, void* hip_stream) {
+  if (!d_omega_in || !d_omega_out || !d_out2) return fail(FA_ERR_INVALID, "fa_pushsum: omega / z outputs NULL");
+  return mix_impl(ctx, dtype, n, rows, row_ptr, cols, vals, num_in, d_in, d_out, nullptr, d_out2, hip_stream, 0, 0,
+                  d_omega_in, d_omega_out);
 }
 
 int fa_mix_tiled(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row_ptr,

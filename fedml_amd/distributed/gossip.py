@@ -31,6 +31,11 @@ def _engine_mix(xs, row_ptr, cols, vals, post_scale, outs, outs2):
     return get_engine(xs[0].device.index).mix(xs, row_ptr, cols, vals, post_scale, outs, outs2)
 
 
+def _engine_pushsum(xs, row_ptr, cols, vals, omega_in, outs, outs2, omega_out):
+    from ..engine import get_engine
+    return get_engine(xs[0].device.index).pushsum(xs, row_ptr, cols, vals, omega_in, outs, outs2, omega_out)
+
+
 class GossipPlan:
     """One rank's share of a distributed gossip step, as a pure function of (W, rank, world): the
     nodes it owns, the halo it receives and sends, its interior / boundary rows and the ring-ordered
@@ -91,10 +96,25 @@ class GossipPlan:
         ps = [post_scale[r] for r in rows] if post_scale is not None else None
         local_mix(inputs, rp, cs, vs, ps, [outs[r] for r in rows], [outs2[r] for r in rows] if outs2 is not None else None)
 
+    def pushsum_local(self, tensor_of: Dict[int, torch.Tensor], omega_inputs: torch.Tensor, local_pushsum: Callable,
+                      rows: Sequence[int], outs: List[torch.Tensor], outs2: List[torch.Tensor],
+                      omega_out: torch.Tensor):
+        """PushSum rows with the weights on the device: ``omega_inputs`` (float32, ``self.inputs``
+        order) mixed by the same rows; omega' of local row r lands in omega_out[r]."""
+        if not rows:
+            return
+        inputs = [tensor_of[v] for v in self.inputs]
+        rp, cs, vs = self.csr(rows)
+        om = torch.empty(len(rows), dtype=torch.float32, device=omega_out.device)
+        local_pushsum(inputs, rp, cs, vs, omega_inputs, [outs[r] for r in rows], [outs2[r] for r in rows], om)
+        omega_out.index_copy_(0, torch.tensor(list(rows), device=omega_out.device), om)
+
 
 class DistributedGossip:
-    def __init__(self, W: np.ndarray, group=None, local_mix: Optional[Callable] = None):
+    def __init__(self, W: np.ndarray, group=None, local_mix: Optional[Callable] = None,
+                 local_pushsum: Optional[Callable] = None):
         self.group = group
+        self.local_pushsum = local_pushsum or _engine_pushsum
         self.plan = GossipPlan(W, dist.get_rank(group), dist.get_world_size(group))
         p = self.plan
         self.W, self.n, self.rank, self.world, self.block = p.W, p.n, p.rank, p.world, p.block
@@ -105,8 +125,13 @@ class DistributedGossip:
     def owner(self, i: int) -> int:
         return self.plan.owner(i)
 
-    def step(self, local_models: Sequence[torch.Tensor], post_scale: Optional[Sequence[float]] = None):
-        """local_models[k] = flat model of node self.mine[k]; returns (new_models, scaled or None)."""
+    def step(self, local_models: Sequence[torch.Tensor], post_scale: Optional[Sequence[float]] = None,
+             omega: Optional[torch.Tensor] = None):
+        """local_models[k] = flat model of node self.mine[k]; returns (new_models, scaled or None).
+
+        PushSum with the weights on the device: ``omega`` = float32 tensor of this rank's nodes'
+        weights; the halo carries the neighbours' weights with their models, omega' is mixed by the
+        same rows and 1/omega' applied on the device; returns (x', z', omega')."""
         assert len(local_models) == len(self.mine)
         proto = local_models[0]
         halo = {i: torch.empty_like(proto) for i in self.halo_in}
@@ -116,7 +141,18 @@ class DistributedGossip:
         for r, idxs in self.halo_out.items():
             for i in idxs:
                 ops.append(dist.P2POp(dist.isend, local_models[self.mine.index(i)], r, self.group))
+        if omega is not None:
+            assert omega.dtype == torch.float32 and omega.numel() == len(self.mine)
+            omega_halo = {i: torch.empty(1, dtype=torch.float32, device=omega.device) for i in self.halo_in}
+            for i in self.halo_in:
+                ops.append(dist.P2POp(dist.irecv, omega_halo[i], self.owner(i), self.group))
+            for r, idxs in self.halo_out.items():
+                for i in idxs:
+                    k = self.mine.index(i)
+                    ops.append(dist.P2POp(dist.isend, omega[k:k + 1], r, self.group))
         reqs = dist.batch_isend_irecv(ops) if ops else []
+        if omega is not None:
+            return self._pushsum_rest(local_models, halo, omega, omega_halo, reqs)
         tensor_of = {node: local_models[k] for k, node in enumerate(self.mine)}
         tensor_of.update(halo)
         outs = [torch.empty_like(proto) for _ in self.mine]
@@ -127,3 +163,24 @@ class DistributedGossip:
             q.wait()
         self.plan.mix_local(tensor_of, self.local_mix, self.boundary, outs, outs2, post_scale)
         return outs, outs2
+
+    def _pushsum_rest(self, local_models, halo, omega, omega_halo, reqs):
+        p = self.plan
+        proto = local_models[0]
+        tensor_of = {node: local_models[k] for k, node in enumerate(self.mine)}
+        tensor_of.update(halo)
+        outs = [torch.empty_like(proto) for _ in self.mine]
+        outs2 = [torch.empty_like(proto) for _ in self.mine]
+        omega_out = torch.empty(len(self.mine), dtype=torch.float32, device=omega.device)
+        # weights in the plan's input order: own nodes now, the halo's once received
+        om_in = torch.zeros(len(p.inputs), dtype=torch.float32, device=omega.device)
+        own_pos = torch.tensor([p.index[v] for v in self.mine], device=omega.device)
+        om_in.index_copy_(0, own_pos, omega)
+        p.pushsum_local(tensor_of, om_in, self.local_pushsum, self.interior, outs, outs2, omega_out)
+        for q in reqs:
+            q.wait()
+        if self.halo_in:
+            halo_pos = torch.tensor([p.index[v] for v in self.halo_in], device=omega.device)
+            om_in.index_copy_(0, halo_pos, torch.cat([omega_halo[i] for i in self.halo_in]))
+        p.pushsum_local(tensor_of, om_in, self.local_pushsum, self.boundary, outs, outs2, omega_out)
+        return outs, outs2, omega_out

@@ -600,6 +600,43 @@ class AggEngine:
         N.check(rc, "fa_mix")
         return list(outs), (list(outs2) if outs2 is not None else None)
 
+    def pushsum(self, xs: Sequence[torch.Tensor], row_ptr: Sequence[int], cols: Sequence[int], vals: Sequence[float],
+                omega_in: torch.Tensor, outs: Optional[Sequence[torch.Tensor]] = None,
+                outs2: Optional[Sequence[torch.Tensor]] = None, omega_out: Optional[torch.Tensor] = None,
+                stream=None) -> Tuple[List[torch.Tensor], List[torch.Tensor], torch.Tensor]:
+        """One PushSum step with the weights on the device (fa_pushsum): mixed models, their z = x /
+        omega', and omega' (float32, one per row), all computed on the GPU."""
+        if len(xs) == 0:
+            raise ValueError("pushsum: no inputs")
+        dt, shape = xs[0].dtype, xs[0].shape
+        for i, t in enumerate(xs):
+            if t.dtype != dt or t.shape != shape:
+                raise ValueError(f"pushsum: input {i} dtype/shape mismatch")
+            _require_device(t, self.device, f"pushsum input {i}")
+        rows = len(row_ptr) - 1
+        if omega_in.dtype != torch.float32 or omega_in.numel() != len(xs):
+            raise ValueError("pushsum: omega_in must be float32 with one weight per input")
+        _require_device(omega_in, self.device, "omega_in")
+        outs = list(outs) if outs is not None else [torch.empty(shape, dtype=dt, device=self.device) for _ in range(rows)]
+        outs2 = list(outs2) if outs2 is not None else [torch.empty(shape, dtype=dt, device=self.device) for _ in range(rows)]
+        if omega_out is None:
+            omega_out = torch.empty(rows, dtype=torch.float32, device=self.device)
+        elif omega_out.dtype != torch.float32 or omega_out.numel() != rows:
+            raise ValueError("pushsum: omega_out must be float32 with one weight per row")
+        _require_device(omega_out, self.device, "omega_out")
+        in_set = {t.data_ptr() for t in xs}
+        for o in outs + outs2:
+            _require_device(o, self.device, "pushsum output")
+            if o.data_ptr() in in_set:
+                raise ValueError("pushsum: outputs must not alias inputs")
+        rc = self._lib.fa_pushsum(
+            self._ctx, DTYPE_CODE.get(dt, -1), xs[0].numel(), rows, N.i32_array(row_ptr), N.i32_array(cols),
+            N.f64_array(vals), len(xs), N.ptr_array([t.data_ptr() for t in xs]), omega_in.data_ptr(),
+            N.ptr_array([o.data_ptr() for o in outs]), N.ptr_array([o.data_ptr() for o in outs2]),
+            omega_out.data_ptr(), self._stream(stream))
+        N.check(rc, "fa_pushsum")
+        return outs, outs2, omega_out
+
     def mix_tiled(self, buf_in: torch.Tensor, in_rows: Sequence[int], row_ptr: Sequence[int], cols: Sequence[int],
                   vals: Sequence[float], buf_out: torch.Tensor, out_rows: Sequence[int],
                   post_scale: Optional[Sequence[float]] = None, buf_out2: Optional[torch.Tensor] = None,

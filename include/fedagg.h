@@ -242,6 +242,17 @@ int fa_mix_tiled(fa_ctx *ctx, int dtype, int64_t n, int32_t rows, const int32_t 
                  int64_t in_tile_stride, void *const *d_out, int64_t out_tile_stride,
                  const double *post_scale, void *const *d_out2, void *hip_stream);
 
+/*
+ * One PushSum gossip step with the weights on the DEVICE (simulation/sp/decentralized/
+ * client_pushsum.py:127-156): fa_mix's rows for the models (x' = ordered CSR sum), the same rows
+ * over the float32 weights d_omega_in[num_in] (omega' -> d_omega_out[rows], float32 per-op rounding,
+ * the reference's numpy float32 chain), and z = x' * float32(1 / omega') into d_out2 -- the
+ * post-scale computed on the device, no host round trip for omega.  Asynchronous on hip_stream.
+ */
+int fa_pushsum(fa_ctx *ctx, int dtype, int64_t n, int32_t rows, const int32_t *row_ptr, const int32_t *cols,
+               const double *vals, int32_t num_in, const void *const *d_in, const float *d_omega_in,
+               void *const *d_out, void *const *d_out2, float *d_omega_out, void *hip_stream);
+
 /* Performance tuning only (results are identical for every variant): selects the weighted-sum
  * kernel's shape -- U clients per load group, S 16-byte vectors per lane, load cache policy,
  * double-buffered group prefetch.  0 = default; valid range [0, 9). */

@@ -326,3 +326,77 @@ def _case_reduce_scatter_out_untouched(rank, world):
 
 def test_reduce_scatter_out_untouched_gloo_world2():
     _spawn(_case_reduce_scatter_out_untouched)
+
+
+# ------------------------------------------------------------------------------ PushSum, device weights
+def _oracle_pushsum(xs, row_ptr, cols, vals, omega_in, outs, outs2, omega_out):
+    """The engine's fa_pushsum restated: omega' = the row's ordered float32 chain, z = x' * fp32(1/omega')."""
+    from oracle import orc
+    om = omega_in.numpy().astype(np.float32)
+    new = []
+    for r in range(len(row_ptr) - 1):
+        acc = np.float32(-0.0)
+        for j in range(row_ptr[r], row_ptr[r + 1]):
+            acc = np.float32(acc + np.float32(om[cols[j]] * np.float32(vals[j])))
+        new.append(acc)
+    post = [float(np.float32(1.0) / a) for a in new]
+    o, o2 = orc.mix(xs, row_ptr, cols, vals, post_scale=post)
+    for a, b in zip(outs, o):
+        a.copy_(b)
+    for a, b in zip(outs2, o2):
+        a.copy_(b)
+    omega_out.copy_(torch.tensor([float(a) for a in new], dtype=torch.float32))
+
+
+def _case_pushsum_device_omega(rank, world):
+    from oracle import orc
+    from fedml_amd.core.distributed.topology.topology_manager import SymmetricTopologyManager, gossip_rows
+    from fedml_amd.distributed.gossip import DistributedGossip
+    n, P = 12, 2001
+    m = SymmetricTopologyManager(n, 2)
+    m.generate_topology()
+    W = m.topology
+    xs, _ = _clients(n, P, seed=13)
+    om = np.array([1.0 + i / n for i in range(n)], dtype=np.float32)
+    # expected: the whole-ring step (host bookkeeping in numpy float32, reference order)
+    rp, cs, vs = gossip_rows(W)
+    full_om = torch.empty(n, dtype=torch.float32)
+    exp_x = [torch.empty(P) for _ in range(n)]
+    exp_z = [torch.empty(P) for _ in range(n)]
+    _oracle_pushsum(xs, rp, cs, vs, torch.from_numpy(om), exp_x, exp_z, full_om)
+    dg = DistributedGossip(W, local_mix=_oracle_mix, local_pushsum=_oracle_pushsum)
+    mine = dg.mine
+    x, z, om_out = dg.step([xs[i] for i in mine], omega=torch.from_numpy(om[mine].copy()))
+    for k, i in enumerate(mine):
+        assert _bits(x[k], exp_x[i]) and _bits(z[k], exp_z[i]), i
+        assert float(om_out[k]) == float(full_om[i]), i
+
+
+def test_pushsum_device_omega_gloo_world2():
+    _spawn(_case_pushsum_device_omega)
+
+
+def test_pushsum_device_omega_gloo_world3():
+    _spawn(_case_pushsum_device_omega, world=3)
+
+
+def test_oracle_pushsum_restatement_matches_reference():
+    """_oracle_pushsum (the device-weight step's restatement) reproduces the reference's PushSum
+    fixture: x', z' bit for bit, omega' equal to the reference's float32 omegas."""
+    sys.path[:0] = [os.path.join(ROOT, "tests", "golden")]
+    from golden_io import client_dicts, expected_dicts, load_case
+    from fedml_amd.core.distributed.topology.topology_manager import gossip_rows
+    meta, arr = load_case(os.path.join(ROOT, "tests", "golden", "g8_pushsum_ring_N8.npz"))
+    cl = client_dicts(meta, arr)
+    exp = expected_dicts(meta, arr)
+    rp, cs, vs = gossip_rows(arr["W"])
+    n = len(cl)
+    for key in meta["keys"]:
+        xs = [c[key].reshape(-1).float() for c in cl]
+        ox = [torch.empty_like(xs[0]) for _ in range(n)]
+        oz = [torch.empty_like(xs[0]) for _ in range(n)]
+        om = torch.empty(n, dtype=torch.float32)
+        _oracle_pushsum(xs, rp, cs, vs, torch.tensor(meta["omegas_in"], dtype=torch.float32), ox, oz, om)
+        assert om.tolist() == meta["omegas_out"]
+        for i in range(n):
+            assert _bits(oz[i], exp[i][key].reshape(-1).float()), (key, i)

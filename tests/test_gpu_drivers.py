@@ -357,3 +357,30 @@ def test_fedavg_rmsprop_vs_torch_optimizer(momentum, wd):
         exp = p_cpu.detach()
         rel = float((got.double() - exp.double()).norm() / exp.double().norm())
         assert rel <= 1e-6, (r, rel)
+
+
+def test_pushsum_step_device_omega():
+    """PushSum with the weights on the device (fa_pushsum): omega' mixed by the same rows in float32,
+    1/omega' and z on the GPU -- the reference's outputs (g8 fixture) bit for bit, then 3 more steps
+    on a 37-node ring equal to the host bookkeeping path."""
+    from fedml_amd.core.distributed.topology.topology_manager import SymmetricTopologyManager
+    from fedml_amd.simulation.sp.decentralized import pushsum_step
+    meta, arr = case("g8_pushsum_ring_N8")
+    cl = [on_gpu(c) for c in client_dicts(meta, arr)]
+    x, z, om = pushsum_step(cl, arr["W"], torch.tensor(meta["omegas_in"], dtype=torch.float32, device="cuda:0"))
+    assert om.is_cuda and om.cpu().tolist() == meta["omegas_out"]
+    for g, e in zip(z, expected_dicts(meta, arr)):
+        assert_dict_bits(cpu(g), e, "pushsum device omega")
+    m = SymmetricTopologyManager(37, 4)
+    m.generate_topology()
+    g = torch.Generator().manual_seed(4)
+    nodes = [OrderedDict(w=torch.randn(3001, generator=g).cuda(), b=torch.randn(7, generator=g).cuda()) for _ in range(37)]
+    om_host = [np.float32(1.0 + i / 37) for i in range(37)]
+    om_dev = torch.tensor([float(o) for o in om_host], dtype=torch.float32, device="cuda:0")
+    xa, xb = nodes, nodes
+    for step in range(3):
+        xa, za, om_host = pushsum_step(xa, m.topology, om_host)
+        xb, zb, om_dev = pushsum_step(xb, m.topology, om_dev)
+        assert [float(o) for o in om_host] == om_dev.cpu().tolist(), step
+        for a, b in zip(za, zb):
+            assert_dict_bits(cpu(a), cpu(b), f"step {step}")

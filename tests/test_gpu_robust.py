@@ -203,12 +203,37 @@ def test_krum_defense_golden(path, where):
 
 
 def test_robust_errors(eng):
-    from fedml_amd._native import FedAggNativeError
     x = torch.zeros(10, device=DEV)
-    with pytest.raises(FedAggNativeError):
-        eng.pairwise_sqdist([[x] * 129])
+    with pytest.raises(ValueError):
+        eng.pairwise_sqdist([[x]])
     with pytest.raises(TypeError):
         eng.coord_median([[x.long()]])
+
+
+@pytest.mark.parametrize("K", [129, 200, 256])
+def test_pairwise_more_than_128_clients(eng, K):
+    """K > 128: blocks of 64 clients, one launch per block pair; every distance within
+    1e-6 relative of the exact float64 oracle, symmetric, zero diagonal; Krum selects as the
+    reference's rule on those distances."""
+    from oracle import orc
+    g = torch.Generator().manual_seed(K)
+    xs = [torch.randn(5003, generator=g) * (1 + (i % 7)) for i in range(K)]
+    d = eng.pairwise_sqdist([[x.to(DEV) for x in xs]]).cpu()
+    ref = orc.pairwise_sqdist(xs)
+    off = ~torch.eye(K, dtype=torch.bool)
+    assert float(((d - ref).abs()[off] / ref[off]).max()) <= 1e-6
+    assert torch.equal(d, d.t()) and float(d.diagonal().abs().max()) == 0.0
+    from fedml_amd.core.security.defense.krum_defense import KrumDefense
+    raw = [(10, OrderedDict(w=x.to(DEV))) for x in xs]
+    dfn = KrumDefense(types.SimpleNamespace(byzantine_client_num=3, krum_param_m=4))
+    sel = dfn.defend_before_aggregation(raw)
+    # the reference's scores on the exact distances (krum_defense.py:52-66), float32 norms squared
+    exact = []
+    for i in range(K):
+        ds = sorted(float(np.float32(np.sqrt(ref[i, j].item()))) ** 2 for j in range(K) if j != i)
+        exact.append(sum(ds[:K - 3 - 2]))
+    want = torch.argsort(torch.Tensor(exact)).tolist()[:4]
+    assert [next(i for i, (_, c) in enumerate(raw) if c is sc) for _, sc in sel] == want
 
 
 def _reset_defender():
