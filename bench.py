@@ -569,8 +569,10 @@ def wl_dropin_cpu(args, eng, rank, world, timer):
             return time.perf_counter() - t0
         legs = {}
         for th in cpu_thread_legs():
+            if th > cpu_quota():  # oversubscribed: minutes per run (see cpu_thread_legs)
+                continue
             torch.set_num_threads(th)
-            ts = [one() for _ in range(5 if th <= cpu_quota() else 1)]
+            ts = [one() for _ in range(5)]
             legs[th] = (min(ts), len(ts), 1.0)
         return legs_record(legs, K * in_b + out_b,
                            f"the same K={K} ResNet-18-GN CPU state_dicts, oracle/torch_port.agg('FedAvg') "
@@ -1337,7 +1339,8 @@ def timed_legs(fn, budget_s, min_runs=3, max_runs=50, small=None):
 def legs_record(legs, nbytes, sample, kind="port", digits=2):
     """The best thread-count leg is the reported value (``cores`` = its threads); every leg's rate
     is kept, the all-core one included (see cpu_thread_legs)."""
-    rates = {th: round(nbytes * sc / b / 1e9, digits) for th, (b, _, sc) in legs.items()}
+    rates = {th: nbytes * sc / b / 1e9 for th, (b, _, sc) in legs.items()}
+    rates = {th: round(r, digits if r >= 1 else 5) for th, r in rates.items()}
     best = max(rates, key=lambda th: rates[th])
     byth = {str(th): r for th, r in sorted(rates.items())}
     for th in cpu_thread_legs():

@@ -182,6 +182,18 @@ class ClientArena:
                 raise TypeError(f"arena: key {k!r} is {t.dtype}{tuple(t.shape)}, layout says {dt}{shape}")
         first = state_dict[self.layout.keys[0]]
         if first.is_cuda:
+            if self.tiled and len(self.layout.keys) == 1 and first.is_contiguous():
+                # one key at offset 0: scatter it straight into the tiles (2 P s bytes, no row scratch)
+                dt = first.dtype
+                nt, _, E = self.bufs[dt].shape
+                x = first.reshape(-1)
+                full = x.numel() // E
+                tv = self.tile_view(dt, i)
+                if full:
+                    tv[:full].copy_(x[:full * E].view(full, E))
+                if x.numel() > full * E:
+                    tv[full, :x.numel() - full * E].copy_(x[full * E:])
+                return
             if self.tiled:  # pack the logical row, then one strided tile scatter per dtype group
                 rows = {dt: self._row_scratch(dt) for dt in self.bufs}
                 for k, v in self.layout.views(rows, None).items():
