@@ -44,16 +44,28 @@ __device__ __forceinline__ T gld_nt(const void* p, int64_t e) {
   return __builtin_nontemporal_load((const __attribute__((address_space(1))) T*)p + e);
 }
 
+// uniform base + 32-bit byte offset (zero-extended): selects the saddr form of global_load
+template <typename T>
+__device__ __forceinline__ T gld_nt_off(const void* p, unsigned off) {
+  return __builtin_nontemporal_load((const __attribute__((address_space(1))) T*)((const char*)p + off));
+}
+
 template <int DT> struct MedT;
 template <> struct MedT<FA_DTYPE_F32> {
   using S = unsigned;
+  static constexpr int kBytes = 4;
   __device__ static float load(const void* p, int64_t e) { return gld_nt<float>(p, e); }
+  __device__ static float load_off(const void* p, unsigned off) { return gld_nt_off<float>(p, off); }
   __device__ static void store(void* p, int64_t e, float v) { ((float*)p)[e] = v; }
   __device__ static void store_bits(void* p, int64_t e, const void* src) { ((unsigned*)p)[e] = ((const unsigned*)src)[e]; }
 };
 template <> struct MedT<FA_DTYPE_BF16> {
+  static constexpr int kBytes = 2;
   __device__ static float load(const void* p, int64_t e) {
     return __uint_as_float((unsigned)gld_nt<unsigned short>(p, e) << 16);
+  }
+  __device__ static float load_off(const void* p, unsigned off) {
+    return __uint_as_float((unsigned)gld_nt_off<unsigned short>(p, off) << 16);
   }
   __device__ static void store(void* p, int64_t e, float v) {
     ((unsigned short*)p)[e] = (unsigned short)(__float_as_uint(v) >> 16);  // exact: v came from bf16
@@ -63,8 +75,12 @@ template <> struct MedT<FA_DTYPE_BF16> {
   }
 };
 template <> struct MedT<FA_DTYPE_F16> {
+  static constexpr int kBytes = 2;
   __device__ static float load(const void* p, int64_t e) {
     return (float)__builtin_bit_cast(_Float16, gld_nt<unsigned short>(p, e));
+  }
+  __device__ static float load_off(const void* p, unsigned off) {
+    return (float)__builtin_bit_cast(_Float16, gld_nt_off<unsigned short>(p, off));
   }
   __device__ static void store(void* p, int64_t e, float v) {
     ((unsigned short*)p)[e] = __builtin_bit_cast(unsigned short, (_Float16)v);  // exact: v came from f16
@@ -147,6 +163,51 @@ __device__ __forceinline__ void median_col(const void* const* in, int k, int64_t
   const int r = (k - 1) >> 1;
   if (nan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, nan, out);
   else MedT<DT>::store(out, e, fkey_inv(kr));
+}
+
+// Branch-free form (r02), used whenever every segment's byte size fits in 32 bits: the generic
+// form below compiles `i < k ? key : sentinel` and `nan || ...` (k a runtime value) into an
+// exec-mask branch with its own s_waitcnt per client -- ~3,000 scalar and branch instructions ahead
+// of B = 128's 2,175 min/max -- and keeps a 64-bit VGPR address per client (B = 128: 158 VGPRs).
+// Here the sentinels are uniform bit masks (and/or, no branch), the NaN test an integer OR, and
+// every load is `uniform base (SGPRs) + ONE shared 32-bit byte offset` (global_load ... saddr).
+// Measured (r02j): K = 128 1.58 -> 1.45 ms, K = 96 1.11 -> 0.88, K = 64 0.62 -> 0.59, K = 32 0.278
+// -> 0.272 ms; bit-exact (same network, same keys).
+// EXACT (k == B, no sentinels): the masks are dropped at compile time (K = 128: 1.53 -> 1.45 ms).
+template <int DT, int B, bool EXACT, int W = (B > 64 ? 2 : (B > 56 ? 3 : (B > 32 ? 4 : 5)))>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W)))
+k_median_off(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k) {
+  if constexpr (EXACT) k = B;
+  const int64_t tile = blockIdx.x;
+  const MSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
+  const int64_t e = (tile - sg.tile_start) * kBlock + threadIdx.x;
+  const bool live = e < sg.numel;
+  const int64_t ec = live ? e : sg.numel - 1;
+  const void* const* in = ptrs + sg.ptr_base;
+  const unsigned boff = (unsigned)ec * (unsigned)MedT<DT>::kBytes;
+  const int lo_end = k + (B - 1) / 2 - ((k - 1) >> 1);  // sentinels [k, lo_end) low, [lo_end, B) high
+  unsigned key[B];
+#pragma unroll
+  for (int i = 0; i < B; ++i) key[i] = __float_as_uint(MedT<DT>::load_off(in[min(i, k - 1)], boff));
+  unsigned nanbits = 0;
+#pragma unroll
+  for (int i = 0; i < B; ++i) {
+    const unsigned kk = key[i] ^ ((unsigned)((int)key[i] >> 31) | 0x80000000u);  // fkey
+    if constexpr (EXACT) {
+      nanbits |= (unsigned)((key[i] & 0x7FFFFFFFu) > 0x7F800000u);
+      key[i] = kk;
+    } else {
+      const unsigned real = 0u - (unsigned)(i < k);        // uniform all-ones / zero
+      const unsigned sent = i < lo_end ? 0u : 0xFFFFFFFFu;  // uniform
+      nanbits |= real & (unsigned)((key[i] & 0x7FFFFFFFu) > 0x7F800000u);
+      key[i] = (kk & real) | (sent & ~real);
+    }
+  }
+  const unsigned kr = select_mid<B>(key);
+  if (!live) return;
+  const int r = (k - 1) >> 1;
+  if (nanbits || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, nanbits != 0, sg.out);
+  else MedT<DT>::store(sg.out, e, fkey_inv(kr));
 }
 
 // (B > 64: median_col's body written out -- called through median_col, B = 128 took 256 VGPRs,
@@ -277,8 +338,18 @@ k_median_rank(const MSeg* __restrict__ segs, int nseg, const void* const* __rest
   }
 }
 
+// FA_MEDIAN_FULL=0 forces the generic (branching, 64-bit address) form (A/B measurement)
+bool full_enabled() {
+  static const int on = [] {
+    const char* e = getenv("FA_MEDIAN_FULL");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 template <int DT>
-void launch_median(int k, bool packed, dim3 grid, hipStream_t st, const MSeg* ds, int nseg, const void* const* dp) {
+void launch_median(int k, bool packed, bool off32, dim3 grid, hipStream_t st, const MSeg* ds, int nseg,
+                   const void* const* dp) {
   if constexpr (DT == FA_DTYPE_F64) {
     hipLaunchKernelGGL((k_median_rank<DT>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);
   } else {
@@ -290,7 +361,12 @@ void launch_median(int k, bool packed, dim3 grid, hipStream_t st, const MSeg* ds
         hipLaunchKernelGGL((k_median_pk<DT, 8 * Q>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);     \
         return;                                                                                      \
       }                                                                                              \
-    hipLaunchKernelGGL((k_median<DT, 8 * Q>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);            \
+    if (off32 && full_enabled() && k == 8 * Q)                                                       \
+      hipLaunchKernelGGL((k_median_off<DT, 8 * Q, true>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); \
+    else if (off32 && full_enabled())                                                                \
+      hipLaunchKernelGGL((k_median_off<DT, 8 * Q, false>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); \
+    else                                                                                             \
+      hipLaunchKernelGGL((k_median<DT, 8 * Q>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);          \
     return;
       FA_MB(1) FA_MB(2) FA_MB(3) FA_MB(4) FA_MB(5) FA_MB(6) FA_MB(7) FA_MB(8)
       FA_MB(9) FA_MB(10) FA_MB(11) FA_MB(12) FA_MB(13) FA_MB(14) FA_MB(15) FA_MB(16)
@@ -363,11 +439,15 @@ int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t*
   const MSeg* ds = (const MSeg*)dv;
   const void* const* dp = (const void* const*)(dv + seg_bytes);
   const dim3 grid((unsigned)tiles);
+  // k_median_off addresses a client's element by a 32-bit byte offset: every segment must fit
+  const int64_t es = dtype == FA_DTYPE_F32 ? 4 : dtype == FA_DTYPE_F64 ? 8 : 2;
+  bool off32 = true;
+  for (int s = 0; s < num_segments; ++s) off32 = off32 && seg_numel[s] * es <= (int64_t)0xFFFFFFFFll;
   switch (dtype) {
-    case FA_DTYPE_F32: launch_median<FA_DTYPE_F32>(k, packed, grid, st, ds, nseg, dp); break;
-    case FA_DTYPE_BF16: launch_median<FA_DTYPE_BF16>(k, packed, grid, st, ds, nseg, dp); break;
-    case FA_DTYPE_F16: launch_median<FA_DTYPE_F16>(k, packed, grid, st, ds, nseg, dp); break;
-    default: launch_median<FA_DTYPE_F64>(k, packed, grid, st, ds, nseg, dp); break;
+    case FA_DTYPE_F32: launch_median<FA_DTYPE_F32>(k, packed, off32, grid, st, ds, nseg, dp); break;
+    case FA_DTYPE_BF16: launch_median<FA_DTYPE_BF16>(k, packed, off32, grid, st, ds, nseg, dp); break;
+    case FA_DTYPE_F16: launch_median<FA_DTYPE_F16>(k, packed, off32, grid, st, ds, nseg, dp); break;
+    default: launch_median<FA_DTYPE_F64>(k, packed, off32, grid, st, ds, nseg, dp); break;
   }
   FA_HIP(hipGetLastError());
   return release(slot, st);
