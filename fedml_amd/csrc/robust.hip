@@ -461,12 +461,10 @@ int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t*
 // A workgroup stages a chunk of coordinates of all K clients in LDS (transposed [e][client],
 // so 4 clients of one coordinate are one 16-byte LDS read), and each thread owns one 4x4
 // client-pair tile (upper triangle) -- 16 differences per 2 LDS reads, packed fp32 -- over a slice
-// of the chunk's coordinates (pair_split).  Software pipeline: chunk i is computed from one LDS
+// of `ce` coordinates of the chunk (pair_split).  Software pipeline: chunk i is computed from one LDS
 // buffer while chunk i + 1 (already in registers) is written to the other and chunk i + 2 is loaded
-// from HBM -- one barrier per chunk, HBM latency behind the pair loop (K = 8 / 32 / 128: 0.22 /
-// 0.90 / 10.2 ms -> 0.12 / 0.62 / 6.9 ms over the single-buffered, load-then-compute form whose
-// waves sat 60% of their cycles in s_waitcnt / barriers).  Sums: float32 over runs of <= kPE
-// coordinates, float64 across runs.
+// from HBM -- one barrier per chunk, HBM latency behind the pair loop.  Sums: float32 over runs of
+// <= kPE coordinates, float64 across runs.
 // Per-block float64 partials of the upper triangle go to a scratch buffer and a second kernel
 // adds them in block order (deterministic).
 namespace {
@@ -474,18 +472,27 @@ namespace {
 constexpr int kPE = 64;       // longest float32 run (coordinates); small-K esplit cap
 constexpr int kMaxPairK = 128;
 constexpr int kMaxPairThreads = 1024;
-constexpr int kNP = 8;             // coordinates of one client staged per thread and chunk
+constexpr int kNP = 8;        // split heuristic: staged coordinates per lane (chunks of >= 64 below)
+constexpr int kNPS = 16;      // k_pairdist: elements of one client staged per thread and chunk
+constexpr int kNPL = 8;       // k_pairdist_lane: coordinates of one client staged per lane and chunk
 
 // Work split of k_pairdist: ntiles 4x4 pair tiles (upper triangle), one per thread, times `esplit`
 // coordinate slices: a workgroup is ntiles * esplit threads (<= 1024; K <= 128 -> ntiles <= 528).
-// Staging: nthreads / kp threads per client, kNP coordinates each, so a chunk is
-// pe = (nthreads / kp) * kNP coordinates.  ntiles <= 128: esplit = 256 / ntiles (e.g. K = 32 keeps
-// 252 of 256 threads busy); larger: see below (measured, K = 100: 3 x 325 threads, 72-coordinate
-// chunks, 3.9 ms vs 5.1 ms with 325 threads and 24-coordinate chunks).
-struct PairSplit { int kp, nb, ntiles, esplit, nthreads, pe, nblocks; };
+// Staging: `rows` = nthreads / kp threads per client, np elements each; a chunk is pe = ce * esplit
+// coordinates, every slice exactly ce (a uniform trip count: the pair loop runs on a scalar
+// counter).  ntiles <= 128: esplit = 256 / ntiles (e.g. K = 32 keeps 252 of 256 threads busy);
+// larger: see below (measured, K = 100: 3 x 325 threads, 72-coordinate chunks, 3.9 ms vs 5.1 ms
+// with 325 threads and 24-coordinate chunks).  The LDS row stride is KPAD + 4 floats with KPAD the
+// next of 16 / 32 / 64 / 96 / 128 >= kp, a compile-time constant (immediate LDS offsets).
+// Staging: kp <= 32 -- k_pairdist_lane, a lane per client, 8 consecutive coordinates by two 16-byte
+// loads; larger K -- k_pairdist, `rows` lanes per client reading consecutive floats, 16 elements per
+// thread (r02: K = 64 / 100 / 128: 2.59 / 3.99 / 6.58 -> 2.0 / 3.7 / 6.38 ms; at K <= 32 the
+// per-element form's extra instructions cost more than its coalescing gains).
+struct PairSplit { int kp, kpad, nb, ntiles, esplit, nthreads, rows, ce, pe, nblocks; bool lane; };
 PairSplit pair_split(int k) {
   PairSplit q;
   q.kp = (k + 3) & ~3;
+  q.kpad = q.kp <= 64 ? 64 : q.kp <= 96 ? 96 : 128;  // k_pairdist (kp > 32)
   q.nb = q.kp / 4;
   q.ntiles = q.nb * (q.nb + 1) / 2;
   if (q.ntiles <= 128) {
@@ -512,8 +519,18 @@ PairSplit pair_split(int k) {
     q.esplit = (q.kp + q.ntiles - 1) / q.ntiles;
     q.nthreads = q.ntiles * q.esplit;
   }
-  // chunk: kNP coordinates per staging thread, nthreads / kp staging threads per client
-  q.pe = (q.nthreads / q.kp) * kNP;
+  q.rows = q.nthreads / q.kp;
+  q.lane = q.kp <= 32;
+  if (q.lane) {  // k_pairdist_lane: slices of pe / esplit coordinates, not necessarily equal
+    q.pe = q.rows * kNPL;
+    q.ce = 0;
+  } else {
+    // a slice is one float32 run at most, and every element of a chunk has a staging thread
+    q.ce = std::max(1, std::min(kPE, q.rows * kNPS / q.esplit));
+    // two LDS buffers of pe rows: at most 80 KB, so two workgroups share a CU
+    while (q.ce > 1 && 2 * sizeof(float) * (size_t)q.ce * q.esplit * (q.kpad + 4) > 80 * 1024) --q.ce;
+    q.pe = q.ce * q.esplit;
+  }
   q.nblocks = 1024;  // workgroups (each writes all pair partials once)
   return q;
 }
@@ -529,11 +546,12 @@ struct PSeg {
 };
 static_assert(sizeof(PSeg) == 32, "PSeg layout");
 
-// waves_per_eu(5): <= 102 VGPRs, so two 10-wave groups share a CU (with 1024-thread bounds alone the
-// compiler took 100 -> 4 waves/SIMD -> one group per CU, idle across every barrier)
+// K <= 32 (kp <= 32): the r01 form -- a lane per client stages 8 consecutive coordinates (two 16-byte
+// loads), slices of pe / esplit coordinates (pe = rows * 8); measured faster there than the
+// strided form below (K = 16 / 32: 0.20 / 0.59 vs 0.27 / 0.65 ms)
 template <bool VEC>
 __global__ void __launch_bounds__(kMaxPairThreads) __attribute__((amdgpu_waves_per_eu(5)))
-k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int kp,
+k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int kp,
            int64_t nchunks, int ntiles, int esplit, int pe, double* __restrict__ partial) {
   extern __shared__ float lds[];              // [2][pe][kp + 4]
   const int stride = kp + 4;
@@ -561,14 +579,14 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
     run = 0;
   };
   const int e_lo = (int)((int64_t)es * pe / esplit), e_hi = (int)((int64_t)(es + 1) * pe / esplit);
-  // staging role: client sc, kNP consecutive coordinates from se of every chunk (pe = (nthreads / kp)
-  // * kNP, so the row (t / kp) < nthreads / kp of a staging thread is exactly se < pe).  Registers
+  // staging role: client sc, kNPL consecutive coordinates from se of every chunk (pe = (nthreads / kp)
+  // * kNPL, so the row (t / kp) < nthreads / kp of a staging thread is exactly se < pe).  Registers
   // hold the next chunk while the current one is computed (see the pipeline below); they go to LDS
   // transposed, [e][client].
-  const int sc = t % kp, se = (t / kp) * kNP;
+  const int sc = t % kp, se = (t / kp) * kNPL;
   const bool sact = se < pe && sc < k;
   const bool swr = se < pe;            // clients k..kp-1 are staged as zeros
-  float v[kNP];
+  float v[kNPL];
   int cseg = -1;
   const float* src = nullptr;
   int64_t snum = 0;
@@ -583,13 +601,13 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
     const int64_t b0 = (ch - sg.tile_start) * pe + se;
     if (!sact) {
 #pragma unroll
-      for (int u = 0; u < kNP; ++u) v[u] = 0.0f;
-    } else if (b0 + kNP <= snum) {  // whole run: one base address, immediate offsets
+      for (int u = 0; u < kNPL; ++u) v[u] = 0.0f;
+    } else if (b0 + kNPL <= snum) {  // whole run: one base address, immediate offsets
       const __attribute__((address_space(1))) float* g = (const __attribute__((address_space(1))) float*)(src + b0);
       if constexpr (VEC) {
         typedef float f32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-        for (int u = 0; u < kNP / 4; ++u) {
+        for (int u = 0; u < kNPL / 4; ++u) {
           const f32x4 q = ((const __attribute__((address_space(1))) f32x4*)g)[u];
           v[4 * u] = q.x;
           v[4 * u + 1] = q.y;
@@ -598,11 +616,11 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
         }
       } else {
 #pragma unroll
-        for (int u = 0; u < kNP; ++u) v[u] = g[u];
+        for (int u = 0; u < kNPL; ++u) v[u] = g[u];
       }
     } else {  // the segment's last run: coordinates past the end add 0 to every sum
 #pragma unroll
-      for (int u = 0; u < kNP; ++u) v[u] = b0 + u < snum ? gld<float>(src, b0 + u) : 0.0f;
+      for (int u = 0; u < kNPL; ++u) v[u] = b0 + u < snum ? gld<float>(src, b0 + u) : 0.0f;
     }
   };
   // two LDS buffers: chunk i is computed from buffer i & 1 while chunk i + 1 is written to the other
@@ -611,7 +629,7 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
   auto put = [&](int buf) {
     if (swr) {
 #pragma unroll
-      for (int u = 0; u < kNP; ++u) lds[buf * bufsz + (se + u) * stride + sc] = v[u];
+      for (int u = 0; u < kNPL; ++u) lds[buf * bufsz + (se + u) * stride + sc] = v[u];
     }
   };
   // each workgroup takes a contiguous run of chunks: a 128-byte line split between two chunks is then
@@ -645,6 +663,157 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
     }
     run += e_hi - e_lo;
     if (run + (e_hi - e_lo) > kPE) flush();  // float runs of <= kPE coordinates, then float64
+    if (ch + 1 < c1) {
+      put(cur ^ 1);  // buffer cur ^ 1 was last read before the previous barrier
+      if (ch + 2 < c1) load(ch + 2);
+    }
+    __syncthreads();
+  }
+  flush();
+  // write the block's upper-triangle partials: pair (i, j), i < j -> index i*k - i*(i+1)/2 + (j-i-1);
+  // with esplit > 1 the slices of a tile are first added in slice order through LDS (reused as
+  // [ntiles * 16] doubles, sized by the host)
+  const int64_t npairs = (int64_t)k * (k - 1) / 2;
+  double* out = partial + (int64_t)blockIdx.x * npairs;
+  if (esplit == 1) {
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = 4 * bi + u / 4, j = 4 * bj + u % 4;
+      if (i < j && j < k) out[(int64_t)i * k - (int64_t)i * (i + 1) / 2 + (j - i - 1)] = accd[u];
+    }
+    return;
+  }
+  __syncthreads();
+  double* red = (double*)lds;
+  for (int s = 0; s < esplit; ++s) {
+    if (es == s) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) red[tile * 16 + u] = (s == 0 ? 0.0 : red[tile * 16 + u]) + accd[u];
+    }
+    __syncthreads();
+  }
+  for (int idx = t; idx < ntiles * 16; idx += (int)blockDim.x) {
+    const int tl = idx / 16, u = idx % 16;
+    int r = 0, rm = tl;
+    while (rm >= nb - r) { rm -= nb - r; ++r; }
+    const int i = 4 * r + u / 4, j = 4 * (r + rm) + u % 4;
+    if (i < j && j < k) out[(int64_t)i * k - (int64_t)i * (i + 1) / 2 + (j - i - 1)] = red[idx];
+  }
+}
+
+// waves_per_eu(5): <= 102 VGPRs, so two 10-wave groups share a CU (with 1024-thread bounds alone the
+// compiler took 100 -> 4 waves/SIMD -> one group per CU, idle across every barrier)
+template <int KPAD>
+__global__ void __launch_bounds__(kMaxPairThreads) __attribute__((amdgpu_waves_per_eu(5)))
+k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int kp,
+           int64_t nchunks, int ntiles, int esplit, int ce, int rows, double* __restrict__ partial) {
+  constexpr int S = KPAD + 4;                    // LDS row stride (floats), 16-byte rows
+  constexpr int NP = kNPS;
+  extern __shared__ float lds[];                 // [2][pe][S]
+  const int pe = ce * esplit;
+  const int nb = kp / 4;
+  const int t = threadIdx.x;                     // blockDim.x == ntiles * esplit
+  const int es = t / ntiles;                     // coordinate slice
+  const int tile = t % ntiles;
+  int bi = 0, rem = tile;  // tile -> (bi, bj), bi <= bj, row-major upper triangle
+  while (rem >= nb - bi) { rem -= nb - bi; ++bi; }
+  const int bj = bi + rem;
+  double accd[16];
+  f32x2 acc[8];
+  int run = 0;  // coordinates summed in acc since the last flush (uniform)
+#pragma unroll
+  for (int u = 0; u < 16; ++u) accd[u] = 0.0;
+#pragma unroll
+  for (int u = 0; u < 8; ++u) acc[u] = f32x2{0.0f, 0.0f};
+  auto flush = [&]() {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      accd[2 * u] += (double)acc[u].x;
+      accd[2 * u + 1] += (double)acc[u].y;
+      acc[u] = f32x2{0.0f, 0.0f};
+    }
+    run = 0;
+  };
+  // staging role: client sc = t / rows, elements sr, sr + rows, ... of every chunk -- consecutive
+  // lanes read consecutive floats of one client (rows * 4 contiguous bytes per client and load; a
+  // lane per client had made every load touch 64 lines: K = 64 staging alone took 2.6 ms), and their
+  // LDS stores [e][sc] fall on distinct banks (S = 4 mod 32: bank 4 * sr + sc).  Registers hold the
+  // next chunk while the current one is computed (see the pipeline below).
+  const int sc = t / rows, sr = t % rows;
+  const int sstep = rows;              // element step of a staging thread
+  const bool sact = sc < k;
+  const bool swr = sc < kp;            // clients k..kp-1 are staged as zeros
+  float v[NP];
+  int cseg = -1;
+  const float* src = nullptr;
+  int64_t snum = 0;
+  auto load = [&](int64_t ch) {
+    const int si = nseg > 1 ? find_seg(segs, nseg, ch) : 0;
+    const PSeg sg = segs[si];
+    if (si != cseg) {  // one pointer load per segment, not per chunk
+      cseg = si;
+      src = sact ? (const float*)ptrs[sg.ptr_base + sc] : nullptr;
+      snum = sg.numel;
+    }
+    const int64_t b0 = (ch - sg.tile_start) * pe;
+    // elements of this chunk inside the segment: all of them but in the segment's last chunk, where
+    // coordinates past the end add 0 to every sum
+    const int lim = sact ? (int)std::min<int64_t>(pe, snum - b0) : 0;
+    const __attribute__((address_space(1))) float* g =
+        (const __attribute__((address_space(1))) float*)(sact ? src + b0 + sr : nullptr);
+    const int n = lim > sr ? (lim - sr + sstep - 1) / sstep : 0;  // elements u < n are inside
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+      v[u] = u < n ? *g : 0.0f;
+      g += sstep;
+    }
+  };
+  // two LDS buffers: chunk i is computed from buffer i & 1 while chunk i + 1 is written to the other
+  // (and chunk i + 2 loads into registers) -- one barrier per chunk
+  const int bufsz = pe * S;
+  const int nput = swr && pe > sr ? std::min(NP, (pe - sr + sstep - 1) / sstep) : 0;
+  const int rstep = sstep * S;
+  auto put = [&](int buf) {
+    float* l = lds + buf * bufsz + sr * S + sc;
+#pragma unroll
+    for (int u = 0; u < NP; ++u) {
+      if (u < nput) *l = v[u];
+      l += rstep;
+    }
+  };
+  // each workgroup takes a contiguous run of chunks: a 128-byte line split between two chunks is then
+  // fetched once, by one workgroup (grid-strided chunks put the halves on different CUs / XCDs: K = 32
+  // read 1.43x its bytes)
+  const int64_t c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
+  if (c0 < c1) {
+    load(c0);
+    put(0);
+    if (c0 + 1 < c1) load(c0 + 1);
+  }
+  __syncthreads();
+  int cur = 0;
+  const int off_a = es * ce * S + 4 * bi, off_b = es * ce * S + 4 * bj;
+  for (int64_t ch = c0; ch < c1; ++ch, cur ^= 1) {
+    const float* pa = lds + cur * bufsz + off_a;
+    const float* pb = lds + cur * bufsz + off_b;
+    // packed fp32 (v_pk_add_f32 / v_pk_fma_f32): pair (x, y), (x, y+1) per instruction -- the same
+    // per-element IEEE sub and fused multiply-add as the scalar form, half the VALU issue slots
+#pragma unroll 2  // two coordinates' LDS reads in flight (K = 128: 7.0 -> 6.5 ms; 4 was slower)
+    for (int i = 0; i < ce; ++i) {
+      const float4 a = *(const float4*)(pa + i * S);
+      const float4 b = *(const float4*)(pb + i * S);
+      const float av[4] = {a.x, a.y, a.z, a.w};
+      const f32x2 b01 = {b.x, b.y}, b23 = {b.z, b.w};
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        const f32x2 ax = {av[x], av[x]};
+        const f32x2 d0 = ax - b01, d1 = ax - b23;
+        acc[2 * x] = __builtin_elementwise_fma(d0, d0, acc[2 * x]);
+        acc[2 * x + 1] = __builtin_elementwise_fma(d1, d1, acc[2 * x + 1]);
+      }
+    }
+    run += ce;
+    if (run + ce > kPE) flush();  // float runs of <= kPE coordinates, then float64
     if (ch + 1 < c1) {
       put(cur ^ 1);  // buffer cur ^ 1 was last read before the previous barrier
       if (ch + 2 < c1) load(ch + 2);
@@ -769,18 +938,32 @@ int fa_pairwise_sqdist(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_num
   rc = stage(slot, seg_bytes + ptr_bytes, st);
   if (rc) return rc;
   const char* dv = (const char*)slot->dev;
-  size_t lds = 2 * sizeof(float) * (size_t)pe * (kp + 4);
-  if (esplit > 1) lds = std::max(lds, sizeof(double) * 16 * (size_t)ntiles);
-  bool vec = true;  // 16-byte loads: every client segment 16-byte aligned (chunk starts are multiples of 16)
-  for (int i = 0; i < j * k; ++i) vec = vec && ((uintptr_t)hp[i] % 16 == 0);
-  if (vec)
-    hipLaunchKernelGGL((k_pairdist<true>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), lds, st,
-                       (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit,
-                       pe, (double*)d_scratch);
-  else
-    hipLaunchKernelGGL((k_pairdist<false>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), lds, st,
-                       (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit,
-                       pe, (double*)d_scratch);
+  if (q.lane) {
+    size_t lds = 2 * sizeof(float) * (size_t)pe * (kp + 4);
+    if (esplit > 1) lds = std::max(lds, sizeof(double) * 16 * (size_t)ntiles);
+    bool vec = true;  // 16-byte loads: every client segment 16-byte aligned (chunk starts are multiples of 8)
+    for (int i = 0; i < j * k; ++i) vec = vec && ((uintptr_t)hp[i] % 16 == 0);
+    if (vec)
+      hipLaunchKernelGGL((k_pairdist_lane<true>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), lds, st,
+                         (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit,
+                         pe, (double*)d_scratch);
+    else
+      hipLaunchKernelGGL((k_pairdist_lane<false>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), lds, st,
+                         (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit,
+                         pe, (double*)d_scratch);
+  } else {
+    size_t lds = 2 * sizeof(float) * (size_t)pe * (q.kpad + 4);
+    if (esplit > 1) lds = std::max(lds, sizeof(double) * 16 * (size_t)ntiles);
+#define FA_PD(KPAD) hipLaunchKernelGGL((k_pairdist<KPAD>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), lds, \
+      st, (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit, q.ce, q.rows, \
+      (double*)d_scratch)
+    switch (q.kpad) {
+      case 64: FA_PD(64); break;
+      case 96: FA_PD(96); break;
+      default: FA_PD(128); break;
+    }
+#undef FA_PD
+  }
   const dim3 blk(kBlock);
   hipLaunchKernelGGL(k_pairdist_reduce, dim3((unsigned)((npairs + 7) / 8)), blk, 0,
                      st, (const double*)d_scratch, nblocks, k, (double*)d_dist);
