@@ -72,6 +72,7 @@ struct fa_ctx {
   bool mix_band = true;  // banded (sliding-window) mixing kernel when the CSR allows it
   struct Slot {
     void* host = nullptr;
+    void* hmap = nullptr;  // device address of the mapped `host` buffer
     void* dev = nullptr;
     size_t cap = 0;
     hipEvent_t ev = nullptr;

@@ -1,0 +1,7 @@
+# full GPU suite + smoke (after the staging-copy change)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/r02q
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r02q/gpu_tests.log 2>&1 || { tail -40 gpurun_out/r02q/gpu_tests.log; exit 1; }
+tail -2 gpurun_out/r02q/gpu_tests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r02q/smoke.log 2>&1 || { tail -20 gpurun_out/r02q/smoke.log; exit 1; }
+tail -1 gpurun_out/r02q/smoke.log
