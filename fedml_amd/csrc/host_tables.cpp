@@ -152,6 +152,68 @@ py::tuple alloc_outputs(py::list shapes, py::list dtypes, const std::string& dev
   return py::make_tuple(arena, views, ptrs);
 }
 
+// plan_outputs(shapes, codes, int64_to_f32, device, ptrs, K) -> (arena, views, groups): the outputs
+// of a device round (alloc_outputs, output dtype = input dtype except int64 -> float32 when
+// int64_to_f32: the weighted modes' PyTorch promotion) and, per input dtype code in ascending
+// order, the launch tables (code, numel int64[Tg], in int64[Tg*K] key-major, out int64[Tg]) --
+// what the Python dispatcher had built with a per-key loop and index_select (~50 us a 122-key round).
+py::tuple plan_outputs(py::list shapes, torch::Tensor codes, bool int64_to_f32, const std::string& device,
+                       torch::Tensor ptrs, int64_t K) {
+  const int64_t T = (int64_t)py::len(shapes);
+  TORCH_CHECK(codes.dtype() == torch::kInt64 && codes.numel() == T && codes.is_contiguous(), "plan_outputs: codes");
+  TORCH_CHECK(ptrs.dtype() == torch::kInt64 && ptrs.numel() == T * K && ptrs.is_contiguous(), "plan_outputs: ptrs");
+  const int64_t* C = codes.data_ptr<int64_t>();
+  const int64_t* P = ptrs.data_ptr<int64_t>();
+  static const at::ScalarType kCode[5] = {at::kFloat, at::kBFloat16, at::kHalf, at::kDouble, at::kLong};
+  std::vector<int64_t> off(T), numel(T);
+  std::vector<at::ScalarType> sts(T);
+  std::vector<std::vector<int64_t>> shp(T);
+  int64_t total = 0;
+  for (int64_t t = 0; t < T; ++t) {
+    TORCH_CHECK(C[t] >= 0 && C[t] <= 4, "plan_outputs: dtype code ", C[t]);
+    shp[t] = shapes[t].cast<std::vector<int64_t>>();
+    sts[t] = (C[t] == 4 && int64_to_f32) ? at::kFloat : kCode[C[t]];
+    int64_t n = 1;
+    for (auto x : shp[t]) n *= x;
+    numel[t] = n;
+    off[t] = total;
+    total += (n * (int64_t)c10::elementSize(sts[t]) + 255) / 256 * 256;
+  }
+  auto arena = torch::empty({std::max<int64_t>(total, 256)}, torch::TensorOptions().dtype(torch::kUInt8).device(device));
+  const c10::Storage& storage = arena.storage();
+  const c10::DispatchKeySet keys = arena.key_set();
+  char* base = (char*)arena.data_ptr();
+  py::list views;
+  for (int64_t t = 0; t < T; ++t) {
+    at::Tensor v = at::detail::make_tensor<c10::TensorImpl>(c10::Storage(storage), keys,
+                                                            caffe2::TypeMeta::fromScalarType(sts[t]));
+    c10::TensorImpl* impl = v.unsafeGetTensorImpl();
+    impl->set_storage_offset(off[t] / (int64_t)c10::elementSize(sts[t]));
+    impl->set_sizes_contiguous(shp[t]);
+    views.append(py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(v))));
+  }
+  py::list groups;
+  for (int64_t c = 0; c <= 4; ++c) {
+    int64_t tg = 0;
+    for (int64_t t = 0; t < T; ++t) tg += C[t] == c;
+    if (!tg) continue;
+    auto nm = torch::empty({tg}, torch::kInt64);
+    auto in = torch::empty({tg * K}, torch::kInt64);
+    auto out = torch::empty({tg}, torch::kInt64);
+    int64_t *N = nm.data_ptr<int64_t>(), *I = in.data_ptr<int64_t>(), *O = out.data_ptr<int64_t>();
+    int64_t j = 0;
+    for (int64_t t = 0; t < T; ++t) {
+      if (C[t] != c) continue;
+      N[j] = numel[t];
+      std::memcpy(I + j * K, P + t * K, sizeof(int64_t) * (size_t)K);
+      O[j] = (int64_t)(base + off[t]);
+      ++j;
+    }
+    groups.append(py::make_tuple(c, nm, in, out));
+  }
+  return py::make_tuple(arena, views, groups);
+}
+
 // carve(flat, offsets, shapes) -> [views]: contiguous views of a flat 1-D tensor at the given
 // element offsets (the per-key outputs of an arena's dtype group), built directly on its storage
 // like alloc_outputs' (Python slicing + view costs ~3 us a key: a 122-key round's whole kernel time).
@@ -261,4 +323,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gather", &gather, "validate K client dicts x T keys, return the device pointer table");
   m.def("carve", &carve, "contiguous views of a flat tensor at element offsets");
   m.def("alloc_outputs", &alloc_outputs, "carve T aligned outputs out of one device allocation");
+  m.def("plan_outputs", &plan_outputs, "outputs of a device round plus its per-dtype launch tables");
 }

@@ -78,33 +78,17 @@ def aggregate(dicts: Sequence[Dict[str, torch.Tensor]], mode: int, coef: Optiona
 
 
 def _aggregate_device(keys, ptrs, numel, codes, shapes, dev, k, mode, coef, divisor, engine):
-    """Fast path: every tensor already on one HIP device, native dtypes; one launch per dtype."""
+    """Fast path: every tensor already on one HIP device, native dtypes; one launch per dtype.  The
+    outputs and the per-dtype launch tables come from one C++ call (_host.plan_outputs)."""
     eng = engine or get_engine(torch.device(dev).index)
-    code_list = codes.tolist()
-    out_dt = [out_dtype(_CODE_DTYPE[c], mode) for c in code_list]
-    _, views, optrs = _host.alloc_outputs(shapes, out_dt, dev)
-    groups: Dict[int, List[int]] = {}
-    for t, c in enumerate(code_list):
-        groups.setdefault(c, []).append(t)
-    table = ptrs.view(len(keys), k)
-    if len(groups) == 2 and 4 in groups and min(groups) in (0, 1, 2, 3):
+    _, views, groups = _host.plan_outputs(shapes, codes, mode != SUM, dev, ptrs, k)
+    if len(groups) == 2 and groups[1][0] == 4:
         # a float group + the int64 BatchNorm counters: one launch (fa_weighted_sum_pair_multi)
-        fc = min(groups)
-        tabs = []
-        for c in (fc, 4):
-            sel = torch.tensor(groups[c], dtype=torch.int64)
-            tabs += [numel.index_select(0, sel).contiguous(), table.index_select(0, sel).reshape(-1).contiguous(),
-                     optrs.index_select(0, sel).contiguous()]
-        eng.weighted_sum_table_pair(fc, mode, *tabs, k=k, coef=coef, divisor=divisor)
-        return OrderedDict(zip(keys, views))
-    for c, idx in groups.items():
-        if len(idx) == len(keys):
-            eng.weighted_sum_table(c, mode, numel, k, ptrs, optrs, coef, divisor)
-        else:
-            sel = torch.tensor(idx, dtype=torch.int64)
-            eng.weighted_sum_table(c, mode, numel.index_select(0, sel).contiguous(), k,
-                                   table.index_select(0, sel).reshape(-1).contiguous(),
-                                   optrs.index_select(0, sel).contiguous(), coef, divisor)
+        (fc, n0, i0, o0), (_, n1, i1, o1) = groups
+        eng.weighted_sum_table_pair(fc, mode, n0, i0, o0, n1, i1, o1, k=k, coef=coef, divisor=divisor)
+    else:
+        for c, nm, it, ot in groups:
+            eng.weighted_sum_table(c, mode, nm, k, it, ot, coef, divisor)
     return OrderedDict(zip(keys, views))
 
 
