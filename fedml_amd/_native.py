@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = (
     # include/fedagg_finite.h
     "fa_finite_sum", "fa_finite_sum_tiled", "fa_finite_quantize", "fa_lcc_decode",
     # include/fedagg_robust.h
-    "fa_coord_median", "fa_pairwise_sqdist", "fa_pairwise_sqdist_scratch_bytes",
+    "fa_coord_median", "fa_pairwise_sqdist", "fa_pairwise_sqdist_rt", "fa_pairwise_sqdist_scratch_bytes",
 )
 
 MOD_FIRST, MOD_EACH, MOD_END, REAL_F64 = 1, 2, 4, 8  # enum fa_finite_flags
@@ -132,6 +132,9 @@ def _declare(L):
     L.fa_coord_median.argtypes = [_vp, ctypes.c_int, ctypes.c_int32, _P_i64, ctypes.c_int32, _P_vp, _P_vp, _vp]
     L.fa_pairwise_sqdist.restype = ctypes.c_int
     L.fa_pairwise_sqdist.argtypes = [_vp, ctypes.c_int32, _P_i64, ctypes.c_int32, _P_vp, _vp, _vp, ctypes.c_size_t, _vp]
+    L.fa_pairwise_sqdist_rt.restype = ctypes.c_int
+    L.fa_pairwise_sqdist_rt.argtypes = [_vp, ctypes.c_int, ctypes.c_int32, _P_i64, ctypes.c_int32, _P_vp, _vp, _vp,
+                                        ctypes.c_size_t, _vp]
     L.fa_pairwise_sqdist_scratch_bytes.restype = ctypes.c_size_t
     L.fa_pairwise_sqdist_scratch_bytes.argtypes = [ctypes.c_int32, _P_i64, ctypes.c_int32]
     L.fa_weighted_sum_host.restype = ctypes.c_int

@@ -5,13 +5,16 @@ The reference computes every pairwise distance with a separate float32 ``(v_i - 
 (K(K-1) passes over the model on the CPU, :52-66).  Here ONE ``fa_pairwise_sqdist`` launch reads
 each client's weights once and produces all K(K-1)/2 squared distances; the score bookkeeping
 (ascending distances, sum of the K - f - 2 smallest, float32 ``argsort``) is the reference's,
-on the host, over K numbers.  Distances are rounded to the reference's float32 ``norm`` before
-squaring, so near-equal scores order the same way; the selection is checked against the
-reference (tests/golden/g18_*).
+on the host, over K numbers.  Distances are rounded to the reference's ``norm`` result before
+squaring -- float32, or the model's dtype for bfloat16 / float16 models, whose differences the
+reference also rounds to that dtype (``vectorize_weight`` keeps it; the device pass does the same,
+``fa_pairwise_sqdist_rt``) -- so near-equal scores order the same way; the selection is checked
+against the reference (tests/golden/g18_*, including bf16 / f16 models).  float64 models are
+measured in float32 (differences within 1e-6 relative of the reference's float64 norms).
 """
 from __future__ import annotations
 
-import math
+import functools
 from collections import OrderedDict
 from typing import Any, List, Tuple
 
@@ -45,10 +48,20 @@ class KrumDefense(object):
     def get_malicious_client_idxs(self):
         return []
 
+    @staticmethod
+    def vector_dtype(grads) -> torch.dtype:
+        """dtype of the reference's vectorize_weight result (torch.cat promotes the weight tensors;
+        core/security/common/utils.py:8-13), over every client."""
+        keys = [k for k in grads[0].keys() if is_weight_param(k)]
+        return functools.reduce(torch.promote_types, [g[k].dtype for g in grads for k in keys])
+
     def pairwise_sq_distances(self, grads) -> np.ndarray:
         """(K, K) squared distances of the clients' weight vectors (BatchNorm statistics skipped,
-        as vectorize_weight does), one device pass."""
+        as vectorize_weight does), one device pass; for bf16 / f16 models every difference is
+        rounded to that dtype as the reference's ``v_i - v_j`` does."""
         keys = [k for k in grads[0].keys() if is_weight_param(k)]
+        vdt = self.vector_dtype(grads)
+        diff_dt = vdt if vdt in (torch.bfloat16, torch.float16) else torch.float32
         dev = next((g[k].device for g in grads for k in keys if g[k].is_cuda), None)
         eng = get_engine(dev.index if dev is not None else None)
         segs = []
@@ -60,15 +73,21 @@ class KrumDefense(object):
                     t = t.to(eng.device)
                 col.append(t.to(torch.float32).contiguous().reshape(-1))
             segs.append(col)
-        return eng.pairwise_sqdist(segs).cpu().numpy()
+        return eng.pairwise_sqdist(segs, diff_dtype=diff_dt).cpu().numpy()
 
     def _compute_krum_score(self, grads):
         D = self.pairwise_sq_distances(grads)
         num_client = len(grads)
+        # the reference's compute_euclidean_distance(...).item() ** 2: the norm in the vector's dtype
+        # (computed in float, rounded to float32 / bf16 / f16; float64 models: float32 here), squared
+        vdt = self.vector_dtype(grads)
+        norms = torch.from_numpy(np.sqrt(D)).to(torch.float32)
+        if vdt in (torch.bfloat16, torch.float16):
+            norms = norms.to(vdt)
+        norms = norms.to(torch.float64).numpy()
         krum_scores = []
         for i in range(num_client):
-            # the reference's compute_euclidean_distance(...).item() ** 2: a float32 norm, squared
-            dists = [float(np.float32(math.sqrt(D[i, j]))) ** 2 for j in range(num_client) if i != j]
+            dists = [float(norms[i, j]) ** 2 for j in range(num_client) if i != j]
             dists.sort()
             krum_scores.append(sum(dists[0: num_client - self.byzantine_client_num - 2]))
         return krum_scores

@@ -546,10 +546,24 @@ struct PSeg {
 };
 static_assert(sizeof(PSeg) == 32, "PSeg layout");
 
+// The reference's difference `v_i - v_j` is computed in the vectorized model's dtype
+// (krum_defense.py:52-60: torch.cat of the weights, then `(v1 - v2).norm()`): for bfloat16 / float16
+// models every difference is the float32 difference rounded to that type (ATen's CPU sub: float
+// arithmetic, one rounding to the storage type), then squared and summed in float.  RT: 0 = float32
+// (no rounding), 1 = bfloat16, 2 = float16 (round to nearest even; overflow -> inf, NaN stays NaN).
+template <int RT>
+__device__ __forceinline__ f32x2 round_diff(f32x2 d) {
+  typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+  typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+  if constexpr (RT == 1) return __builtin_convertvector(__builtin_convertvector(d, bf16x2), f32x2);
+  else if constexpr (RT == 2) return __builtin_convertvector(__builtin_convertvector(d, f16x2), f32x2);
+  else return d;
+}
+
 // K <= 32 (kp <= 32): the r01 form -- a lane per client stages 8 consecutive coordinates (two 16-byte
 // loads), slices of pe / esplit coordinates (pe = rows * 8); measured faster there than the
 // strided form below (K = 16 / 32: 0.20 / 0.59 vs 0.27 / 0.65 ms)
-template <bool VEC>
+template <bool VEC, int RT>
 __global__ void __launch_bounds__(kMaxPairThreads) __attribute__((amdgpu_waves_per_eu(5)))
 k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int kp,
            int64_t nchunks, int ntiles, int esplit, int pe, double* __restrict__ partial) {
@@ -656,7 +670,7 @@ k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __re
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
         const f32x2 ax = {av[x], av[x]};
-        const f32x2 d0 = ax - b01, d1 = ax - b23;
+        const f32x2 d0 = round_diff<RT>(ax - b01), d1 = round_diff<RT>(ax - b23);
         acc[2 * x] = __builtin_elementwise_fma(d0, d0, acc[2 * x]);
         acc[2 * x + 1] = __builtin_elementwise_fma(d1, d1, acc[2 * x + 1]);
       }
@@ -703,7 +717,7 @@ k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __re
 
 // waves_per_eu(5): <= 102 VGPRs, so two 10-wave groups share a CU (with 1024-thread bounds alone the
 // compiler took 100 -> 4 waves/SIMD -> one group per CU, idle across every barrier)
-template <int KPAD>
+template <int KPAD, int RT>
 __global__ void __launch_bounds__(kMaxPairThreads) __attribute__((amdgpu_waves_per_eu(5)))
 k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int kp,
            int64_t nchunks, int ntiles, int esplit, int ce, int rows, double* __restrict__ partial) {
@@ -807,7 +821,7 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
 #pragma unroll
       for (int x = 0; x < 4; ++x) {
         const f32x2 ax = {av[x], av[x]};
-        const f32x2 d0 = ax - b01, d1 = ax - b23;
+        const f32x2 d0 = round_diff<RT>(ax - b01), d1 = round_diff<RT>(ax - b23);
         acc[2 * x] = __builtin_elementwise_fma(d0, d0, acc[2 * x]);
         acc[2 * x + 1] = __builtin_elementwise_fma(d1, d1, acc[2 * x + 1]);
       }
@@ -889,7 +903,17 @@ extern "C" {
 int fa_pairwise_sqdist(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, int32_t k,
                        const void* const* d_in, void* d_dist, void* d_scratch, size_t scratch_bytes,
                        void* hip_stream) {
+  return fa_pairwise_sqdist_rt(ctx, FA_DTYPE_F32, num_segments, seg_numel, k, d_in, d_dist, d_scratch,
+                               scratch_bytes, hip_stream);
+}
+
+int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, const int64_t* seg_numel, int32_t k,
+                          const void* const* d_in, void* d_dist, void* d_scratch, size_t scratch_bytes,
+                          void* hip_stream) {
   if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (diff_dtype != FA_DTYPE_F32 && diff_dtype != FA_DTYPE_BF16 && diff_dtype != FA_DTYPE_F16)
+    return fail(FA_ERR_INVALID, "fa_pairwise_sqdist_rt: diff_dtype must be F32, BF16 or F16 (got %d)", diff_dtype);
+  const int rt = diff_dtype == FA_DTYPE_BF16 ? 1 : diff_dtype == FA_DTYPE_F16 ? 2 : 0;
   if (k < 2 || k > kMaxPairK || num_segments <= 0 || !seg_numel || !d_in || !d_dist)
     return fail(FA_ERR_INVALID, "fa_pairwise_sqdist: invalid arguments (2 <= k <= %d)", kMaxPairK);
   const PairSplit q = pair_split(k);
@@ -943,25 +967,28 @@ int fa_pairwise_sqdist(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_num
     if (esplit > 1) lds = std::max(lds, sizeof(double) * 16 * (size_t)ntiles);
     bool vec = true;  // 16-byte loads: every client segment 16-byte aligned (chunk starts are multiples of 8)
     for (int i = 0; i < j * k; ++i) vec = vec && ((uintptr_t)hp[i] % 16 == 0);
-    if (vec)
-      hipLaunchKernelGGL((k_pairdist_lane<true>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), lds, st,
-                         (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit,
-                         pe, (double*)d_scratch);
-    else
-      hipLaunchKernelGGL((k_pairdist_lane<false>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), lds, st,
-                         (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit,
-                         pe, (double*)d_scratch);
+#define FA_PDL(V, R) hipLaunchKernelGGL((k_pairdist_lane<V, R>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), \
+      lds, st, (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit, pe,      \
+      (double*)d_scratch)
+    if (vec) {
+      if (rt == 1) FA_PDL(true, 1); else if (rt == 2) FA_PDL(true, 2); else FA_PDL(true, 0);
+    } else {
+      if (rt == 1) FA_PDL(false, 1); else if (rt == 2) FA_PDL(false, 2); else FA_PDL(false, 0);
+    }
+#undef FA_PDL
   } else {
     size_t lds = 2 * sizeof(float) * (size_t)pe * (q.kpad + 4);
     if (esplit > 1) lds = std::max(lds, sizeof(double) * 16 * (size_t)ntiles);
-#define FA_PD(KPAD) hipLaunchKernelGGL((k_pairdist<KPAD>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), lds, \
-      st, (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit, q.ce, q.rows, \
-      (double*)d_scratch)
+#define FA_PD(KPAD, R) hipLaunchKernelGGL((k_pairdist<KPAD, R>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), \
+      lds, st, (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit, q.ce,   \
+      q.rows, (double*)d_scratch)
+#define FA_PDR(KPAD) if (rt == 1) FA_PD(KPAD, 1); else if (rt == 2) FA_PD(KPAD, 2); else FA_PD(KPAD, 0)
     switch (q.kpad) {
-      case 64: FA_PD(64); break;
-      case 96: FA_PD(96); break;
-      default: FA_PD(128); break;
+      case 64: FA_PDR(64); break;
+      case 96: FA_PDR(96); break;
+      default: FA_PDR(128); break;
     }
+#undef FA_PDR
 #undef FA_PD
   }
   const dim3 blk(kBlock);

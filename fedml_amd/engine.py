@@ -818,12 +818,17 @@ class AggEngine:
 
     MAX_PAIR_K = 128  # kMaxPairK (fedml_amd/csrc/robust.hip): clients per fa_pairwise_sqdist launch
 
-    def pairwise_sqdist(self, segments: Sequence[Sequence[torch.Tensor]], stream=None) -> torch.Tensor:
+    def pairwise_sqdist(self, segments: Sequence[Sequence[torch.Tensor]], stream=None,
+                        diff_dtype: torch.dtype = torch.float32) -> torch.Tensor:
         """K x K float64 matrix of squared Euclidean distances between the clients' float32 vectors
         (segments[s][i] = client i's piece s), fa_pairwise_sqdist.  K > 128 (one launch holds at
         most 128 clients): clients in blocks of 64, one launch per pair of blocks (each launch the
         union of two blocks, its cross distances kept) -- every distance is still one device pass
-        over the two clients' vectors, the same per-pair arithmetic as the single launch."""
+        over the two clients' vectors, the same per-pair arithmetic as the single launch.
+        ``diff_dtype`` bfloat16 / float16: every difference rounded to that dtype before it is
+        squared (fa_pairwise_sqdist_rt; the reference's arithmetic for a bf16 / f16 model)."""
+        if diff_dtype not in _DIFF_DT:
+            raise ValueError(f"pairwise_sqdist: diff_dtype must be float32, bfloat16 or float16, not {diff_dtype}")
         k = len(segments[0]) if segments else 0
         if k < 2:
             raise ValueError("pairwise_sqdist: need at least two clients")
@@ -835,19 +840,19 @@ class AggEngine:
                     raise ValueError(f"segment {s} client {i}: float32 of {seg[0].numel()} elements expected")
                 _require_device(t, self.device, f"segment {s} client {i}")
         if k <= self.MAX_PAIR_K:
-            return self._pairwise_launch(segments, stream)
+            return self._pairwise_launch(segments, stream, diff_dtype)
         B = self.MAX_PAIR_K // 2
         blocks = [list(range(lo, min(k, lo + B))) for lo in range(0, k, B)]
         d = torch.zeros((k, k), dtype=torch.float64, device=self.device)
         for a in range(len(blocks)):
             for b in range(a + 1, len(blocks)):
                 ids = blocks[a] + blocks[b]
-                sub = self._pairwise_launch([[seg[i] for i in ids] for seg in segments], stream)
+                sub = self._pairwise_launch([[seg[i] for i in ids] for seg in segments], stream, diff_dtype)
                 idx = torch.tensor(ids, device=self.device)
                 d.index_put_((idx.view(-1, 1), idx.view(1, -1)), sub)  # diagonal blocks rewritten, same values
         return d
 
-    def _pairwise_launch(self, segments, stream=None) -> torch.Tensor:
+    def _pairwise_launch(self, segments, stream=None, diff_dtype=torch.float32) -> torch.Tensor:
         k = len(segments[0])
         in_ptrs = [t.data_ptr() for seg in segments for t in seg]
         nl = N.i64_array([seg[0].numel() for seg in segments])
@@ -857,10 +862,14 @@ class AggEngine:
             if scratch is None or scratch.numel() < need:
                 scratch = self._pd_scratch = torch.empty(max(need, 1), dtype=torch.uint8, device=self.device)
             d = torch.empty((k, k), dtype=torch.float64, device=self.device)
-            rc = self._lib.fa_pairwise_sqdist(self._ctx, len(segments), nl, k, N.ptr_array(in_ptrs), d.data_ptr(),
-                                              scratch.data_ptr(), scratch.numel(), self._stream(stream))
+            rc = self._lib.fa_pairwise_sqdist_rt(self._ctx, _DIFF_DT[diff_dtype], len(segments), nl, k,
+                                                 N.ptr_array(in_ptrs), d.data_ptr(), scratch.data_ptr(),
+                                                 scratch.numel(), self._stream(stream))
         N.check(rc, "fa_pairwise_sqdist")
         return d
+
+
+_DIFF_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}  # FA_DTYPE_F32 / BF16 / F16
 
 
 def get_engine(device: Optional[int] = None) -> AggEngine:

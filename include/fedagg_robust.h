@@ -7,6 +7,7 @@
  *                       torch.median(torch.cat(client vectors, -1), dim=-1).values
  *   fa_pairwise_sqdist  core/security/defense/krum_defense.py:52-66 (_compute_krum_score's
  *                       compute_euclidean_distance(v_i, v_j) ** 2 for every pair)
+ *   fa_pairwise_sqdist_rt  the same for bfloat16 / float16 models (differences in the model dtype)
  *
  * Contract (bit-exact; pinned by tests/golden/g16_*): for every element e, out[e] is the input
  * element (bit pattern) that ATen's median selects: the first NaN in client order if any client
@@ -46,6 +47,18 @@ int fa_coord_median(fa_ctx *ctx, int dtype, int32_t num_segments, const int64_t 
 int fa_pairwise_sqdist(fa_ctx *ctx, int32_t num_segments, const int64_t *seg_numel, int32_t k,
                        const void *const *d_in, void *d_dist, void *d_scratch, size_t scratch_bytes,
                        void *hip_stream);
+/*
+ * As fa_pairwise_sqdist, with every difference x_i[e] - x_j[e] rounded to `diff_dtype` before it is
+ * squared: FA_DTYPE_F32 (no rounding; = fa_pairwise_sqdist), FA_DTYPE_BF16 or FA_DTYPE_F16 (round
+ * to nearest even, overflow to inf).  Replaces the same loop for bfloat16 / float16 models, where
+ * the reference's vectorize_weight (core/security/common/utils.py:8-13) keeps the model's dtype and
+ * `(v1 - v2)` (utils.py:24-27) rounds each difference to it; the inputs stay float32 (the clients'
+ * values widened exactly).  The caller rounds sqrt(D) to the same dtype to reproduce the
+ * reference's `.norm()` result (the norm of a bf16/f16 tensor is returned in that dtype).
+ */
+int fa_pairwise_sqdist_rt(fa_ctx *ctx, int diff_dtype, int32_t num_segments, const int64_t *seg_numel, int32_t k,
+                          const void *const *d_in, void *d_dist, void *d_scratch, size_t scratch_bytes,
+                          void *hip_stream);
 size_t fa_pairwise_sqdist_scratch_bytes(int32_t num_segments, const int64_t *seg_numel, int32_t k);
 
 #ifdef __cplusplus

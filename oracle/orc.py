@@ -189,6 +189,9 @@ def coord_median(xs):
         L.orc_pairwise_sqdist.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p),
                                           ctypes.c_void_p]
         L.orc_pairwise_sqdist.restype = ctypes.c_int
+        L.orc_pairwise_sqdist_rt.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.POINTER(ctypes.c_void_p),
+                                             ctypes.c_int, ctypes.c_void_p]
+        L.orc_pairwise_sqdist_rt.restype = ctypes.c_int
         L._median_declared = True
     out = torch.empty_like(xs[0])
     rc = L.orc_coord_median(_DT[xs[0].dtype], xs[0].numel(), len(xs),
@@ -207,4 +210,20 @@ def pairwise_sqdist(xs):
     rc = lib().orc_pairwise_sqdist(xs[0].numel(), k, (ctypes.c_void_p * k)(*[x.data_ptr() for x in xs]), d.data_ptr())
     if rc != 0:
         raise RuntimeError(f"orc_pairwise_sqdist failed: {rc}")
+    return d
+
+
+def pairwise_sqdist_rt(xs, dtype):
+    """Squared distances of a bfloat16 / float16 model's vectors as the reference forms them
+    (differences rounded to ``dtype``, see orc_pairwise_sqdist_rt); xs: CPU vectors of any float
+    dtype holding values of ``dtype``."""
+    rt = {torch.bfloat16: 1, torch.float16: 2, torch.float32: 0}[dtype]
+    coord_median([torch.zeros(1)])
+    xs = [x.to(torch.float32).contiguous().reshape(-1) for x in xs]
+    k = len(xs)
+    d = torch.empty((k, k), dtype=torch.float64)
+    rc = lib().orc_pairwise_sqdist_rt(xs[0].numel(), k, (ctypes.c_void_p * k)(*[x.data_ptr() for x in xs]), rt,
+                                      d.data_ptr())
+    if rc != 0:
+        raise RuntimeError(f"orc_pairwise_sqdist_rt failed: {rc}")
     return d

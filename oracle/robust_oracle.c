@@ -66,6 +66,30 @@ int orc_coord_median(int dtype, int64_t n, int32_t k, const void *const *in, voi
 }
 
 /* d[i*k + j] = sum_e (x_i[e] - x_j[e])^2 in float64 (float32 inputs), every ordered pair */
+/* krum_defense.py:52-66 for bfloat16 / float16 models: vectorize_weight keeps the model dtype, so
+ * `(v_i - v_j)` rounds every difference to it (ATen's CPU sub: float arithmetic, one rounding to the
+ * storage type); the norm squares and sums those in float.  Here: the float32 difference rounded to
+ * bf16 (rt = 1) or f16 (rt = 2) by this oracle's own RNE conversions, squared and summed exactly in
+ * float64.  x: the clients' values widened to float32 (exact). */
+uint16_t orc_f32_to_bf16(float f);
+uint16_t orc_f32_to_f16(float f);
+int orc_pairwise_sqdist_rt(int64_t n, int32_t k, const float *const *x, int rt, double *d) {
+    if (k <= 0 || n < 0 || rt < 0 || rt > 2) return -1;
+    for (int32_t i = 0; i < k; ++i)
+        for (int32_t j = 0; j < k; ++j) {
+            double s = 0.0;
+            if (i != j)
+                for (int64_t e = 0; e < n; ++e) {
+                    float t = x[i][e] - x[j][e];
+                    if (rt == 1) t = orc_bf16_to_f32(orc_f32_to_bf16(t));
+                    else if (rt == 2) t = orc_f16_to_f32(orc_f32_to_f16(t));
+                    s += (double)t * (double)t;
+                }
+            d[(int64_t)i * k + j] = s;
+        }
+    return 0;
+}
+
 int orc_pairwise_sqdist(int64_t n, int32_t k, const float *const *x, double *d) {
     if (k <= 0 || n < 0) return -1;
     for (int32_t i = 0; i < k; ++i)

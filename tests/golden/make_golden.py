@@ -907,6 +907,38 @@ def cases_robust():
         json.dump({"K9_f4_m1": err}, fh)
 
 
+def cases_krum_half():
+    """Krum over bfloat16 / float16 models (krum_defense.py:27-66): vectorize_weight keeps the model
+    dtype, so `(v_i - v_j)` and `.norm()` run in it.  Records the reference's selection, scores and
+    every pair's `compute_euclidean_distance(v_i, v_j).item() ** 2` (utils.py:24-27); the f16
+    overflow case has a client far enough out that its distances' float16 norm overflows to inf."""
+    _, _, Krum = load_defenses()
+    import fedml.core.security.common.utils as su
+    flat = [("fc.weight", (10, 50), None), ("fc.bias", (10,), None)]
+    for dt, tag, K, f, m, scale in ((torch.bfloat16, "bf16", 10, 2, 1, 5.0), (torch.bfloat16, "bf16", 12, 2, 3, 5.0),
+                                    (torch.float16, "f16", 10, 2, 2, 5.0), (torch.float16, "f16ovf", 8, 1, 1, 6000.0)):
+        lay = [(k, sh, dt) for k, sh, _ in flat]
+        clients = _robust_clients(1990 + K + len(tag), K, lay, special=False)
+        g = torch.Generator().manual_seed(K + 7)
+        for b in range(f):  # byzantine clients: scaled noise, in the model dtype
+            for k2, v in clients[b * 3 % K].items():
+                clients[b * 3 % K][k2] = v + (scale * torch.randn(v.shape, generator=g)).to(v.dtype)
+        n = gen_counts(1990 + K, K)
+        raw = list(zip(n, clients))
+        d = Krum(Args(byzantine_client_num=f, krum_param_m=m))
+        sel = d.defend_before_aggregation(raw)
+        idx = [next(i for i, (_, c) in enumerate(raw) if c is sc) for _, sc in sel]
+        vec = [su.vectorize_weight(c) for c in clients]
+        assert vec[0].dtype == dt
+        scores = d._compute_krum_score(vec)
+        dists = [[su.compute_euclidean_distance(vec[i], vec[j]).item() ** 2 if i != j else 0.0 for j in range(K)]
+                 for i in range(K)]
+        write(f"g18_krum_{tag}_K{K}_f{f}_m{m}", clients, [clients[0]],
+              dict(kind="krum", n=n, byzantine_client_num=f, krum_param_m=m, selected=idx, scores=scores,
+                   dists=dists, vector_dtype=str(dt).replace("torch.", ""),
+                   ref="core/security/defense/krum_defense.py:27-66, common/utils.py:8-27"))
+
+
 def out2_equal(a, b):
     return all(np.array_equal(np.asarray(a[k]), np.asarray(b[k])) for k in a)
 

@@ -21,6 +21,7 @@ CASES = list_cases()
 ROB = {kind: [p for p in CASES if os.path.basename(p).startswith(kind)] for kind in ROBUST_PREFIXES}
 ids = lambda p: os.path.basename(p)[:-4]  # noqa: E731
 DEV = "cuda:0"
+WEIGHT = lambda k: "running_mean" not in k and "running_var" not in k and "num_batches_tracked" not in k  # noqa: E731
 
 
 @pytest.fixture(scope="module")
@@ -200,6 +201,50 @@ def test_krum_defense_golden(path, where):
     sel = d.defend_before_aggregation(raw)
     assert [next(i for i, (_, c) in enumerate(raw) if c is sc) for _, sc in sel] == meta["selected"]
     np.testing.assert_allclose(d._compute_krum_score(cl), meta["scores"], rtol=1e-5)
+
+
+@pytest.mark.parametrize("path", [p for p in ROB["g18_"] if "f16" in os.path.basename(p)], ids=ids)
+def test_pairwise_half_models_vs_reference(eng, path):
+    """bf16 / f16 models through fa_pairwise_sqdist_rt: within 1e-6 relative of the oracle's exact
+    sums of dtype-rounded differences, and after the mirror's norm rounding equal to every distance
+    the reference recorded (compute_euclidean_distance(v_i, v_j).item() ** 2, inf included)."""
+    from oracle import orc
+    from fedml_amd.core.security.defense.krum_defense import KrumDefense
+    meta, arrays = load_case(path)
+    cl = client_dicts(meta, arrays)
+    vdt = KrumDefense.vector_dtype(cl)
+    keys = [k for k in meta["keys"] if WEIGHT(k)]
+    segs = [[c[k].to(DEV).float().reshape(-1) for c in cl] for k in keys]
+    D = eng.pairwise_sqdist(segs, diff_dtype=vdt).cpu()
+    ref = orc.pairwise_sqdist_rt([torch.cat([c[k].float().reshape(-1) for k in keys]) for c in cl], vdt)
+    fin = torch.isfinite(ref)
+    assert torch.equal(torch.isfinite(D), fin)
+    off = fin & ~torch.eye(len(cl), dtype=torch.bool)
+    assert float(((D - ref).abs()[off] / ref[off]).max()) <= 1e-6
+    got = torch.sqrt(D).to(torch.float32).to(vdt).to(torch.float64).numpy() ** 2
+    np.testing.assert_array_equal(got, np.array(meta["dists"]))
+
+
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("K", [8, 40, 100])
+def test_pairwise_half_rounding_random(eng, dt, K):
+    """The rounding variant over both kernels (lane staging K <= 32, strided staging above) and a
+    ragged multi-segment layout, against the oracle restatement; float16 differences that overflow
+    give inf exactly where the oracle's do."""
+    from oracle import orc
+    g = torch.Generator().manual_seed(K)
+    sizes = [1000, 3, 4097]
+    xs = [[(torch.randn(n, generator=g) * (1 + i % 5) * (3e4 if dt == torch.float16 and i == 1 else 1)).to(dt)
+           for n in sizes] for i in range(K)]
+    segs = [[xs[i][s].to(DEV).float() for i in range(K)] for s in range(len(sizes))]
+    D = eng.pairwise_sqdist(segs, diff_dtype=dt).cpu()
+    ref = orc.pairwise_sqdist_rt([torch.cat(x) for x in xs], dt)
+    fin = torch.isfinite(ref)
+    assert torch.equal(torch.isfinite(D), fin)
+    off = fin & ~torch.eye(K, dtype=torch.bool)
+    assert float(((D - ref).abs()[off] / ref[off]).max()) <= 1e-6
+    if dt == torch.float16:
+        assert not bool(fin.all())
 
 
 def test_robust_errors(eng):
