@@ -210,6 +210,80 @@ k_median_off(const MSeg* __restrict__ segs, int nseg, const void* const* __restr
   else MedT<DT>::store(sg.out, e, fkey_inv(kr));
 }
 
+// Two lanes per column, K in (64, 128] (r02).  k_median_off at B = 128 holds 128 keys per lane:
+// 256 VGPRs with spills, 2 waves per SIMD (1 wave without spills was slower still: K = 128 1.49 ->
+// 1.99 ms), so HBM latency is exposed between the network's phases.  Here a column's B = 2N keys
+// (B = K rounded up to 8, as k_median_off) are split between two lanes of different waves: waves 0-1
+// of the workgroup hold clients 0..N-1 of 128 columns, waves 2-3 clients N..2N-1 of the same columns
+// (the half index is wave-uniform, so every load keeps the SGPR-base + 32-bit-offset form).  Each lane
+// sorts its N keys (SortNet<N>, median_nets.h: 1,086 min/max for N = 64, the same work as half of
+// B = 128's pruned selection network), the upper lanes hand their sorted keys to the lower lanes
+// through LDS, and the lower median -- rank N-1 of the 2N keys -- is max_j min(A[j], C[N-1-j]) (the N
+// pairwise minima of a sorted A and a reversed sorted C are the N smallest keys).  Padding as
+// k_median_off, all of it in the upper half, but the sentinels are the keys of -inf and +inf (a tie
+// with a real infinity selects the same bits), so a NaN shows as a sorted key outside [key(-inf),
+// key(+inf)] -- two compares per lane instead of one per key.  N keys + the merge fit 128 VGPRs
+// (4 waves per SIMD).  Same keys and rare-case rules as k_median_off: bit-exact.
+constexpr int k2lCols = kBlock / 2;  // columns per workgroup
+constexpr unsigned kNegInfKey = 0x007FFFFFu, kPosInfKey = 0xFF800000u;  // fkey(-inf), fkey(+inf)
+template <int DT, int N, bool EXACT>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(N <= 44 ? 5 : 4)))
+k_median_2l(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k) {
+  constexpr int B = 2 * N;
+  if constexpr (EXACT) k = B;
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  __shared__ u32x4 xs[N / 4][k2lCols];  // the upper lanes' N sorted keys, [quad][column]
+  __shared__ unsigned xn[k2lCols];      // the upper lanes' NaN flags
+  const int h = __builtin_amdgcn_readfirstlane((int)threadIdx.x / k2lCols);  // half: wave-uniform
+  const int c = (int)threadIdx.x % k2lCols;
+  const int64_t tile = blockIdx.x;
+  const MSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
+  const int64_t e = (tile - sg.tile_start) * k2lCols + c;
+  const bool live = e < sg.numel;
+  const int64_t ec = live ? e : sg.numel - 1;
+  const void* const* in = ptrs + sg.ptr_base;
+  const unsigned boff = (unsigned)ec * (unsigned)MedT<DT>::kBytes;
+  const int base = N * h;
+  const int lo_end = k + (B - 1) / 2 - ((k - 1) >> 1);  // slots [k, lo_end) low sentinels, [lo_end, B) high
+  unsigned key[N];
+#pragma unroll
+  for (int t = 0; t < N; ++t) key[t] = __float_as_uint(MedT<DT>::load_off(in[min(base + t, k - 1)], boff));
+#pragma unroll
+  for (int t = 0; t < N; ++t) {
+    const unsigned kk = key[t] ^ ((unsigned)((int)key[t] >> 31) | 0x80000000u);  // fkey
+    if constexpr (EXACT) {
+      key[t] = kk;
+    } else {
+      const unsigned real = 0u - (unsigned)(base + t < k);                 // uniform all-ones / zero
+      const unsigned sent = base + t < lo_end ? kNegInfKey : kPosInfKey;  // uniform
+      key[t] = (kk & real) | (sent & ~real);
+    }
+  }
+  SortNet<N>::run(key);
+  const bool nan = key[0] < kNegInfKey || key[N - 1] > kPosInfKey;  // a NaN key sorts outside the infinities
+  if (h == 1) {
+#pragma unroll
+    for (int q = 0; q < N / 4; ++q) xs[q][c] = u32x4{key[4 * q], key[4 * q + 1], key[4 * q + 2], key[4 * q + 3]};
+    xn[c] = nan;
+  }
+  __syncthreads();
+  if (h == 1) return;
+  unsigned kr = 0;
+#pragma unroll
+  for (int q = 0; q < N / 4; ++q) {  // partner keys 4q..4q+3 pair with own keys N-1-4q .. N-4-4q
+    const u32x4 b = xs[q][c];
+    kr = max(kr, min(key[N - 1 - 4 * q], b.x));
+    kr = max(kr, min(key[N - 2 - 4 * q], b.y));
+    kr = max(kr, min(key[N - 3 - 4 * q], b.z));
+    kr = max(kr, min(key[N - 4 - 4 * q], b.w));
+  }
+  if (!live) return;
+  const int r = (k - 1) >> 1;
+  const bool anynan = nan || xn[c] != 0;
+  if (anynan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, anynan, sg.out);
+  else MedT<DT>::store(sg.out, e, fkey_inv(kr));
+}
+
 // (B > 64: median_col's body written out -- called through median_col, B = 128 took 256 VGPRs,
 // 1 wave/SIMD, 1.6 -> 2.2 ms; B <= 64 the other way round)
 template <int DT, int B>
@@ -347,9 +421,35 @@ bool full_enabled() {
   return on != 0;
 }
 
+// Two lanes per column (k_median_2l) for K in (kMedian2lMin, 128]; FA_MEDIAN_2L=0 / 1 turns it off /
+// forces it for every K in (64, 128] (A/B measurement)
+constexpr int kMedian2lMin = 64;  // every K in (64, 128] (r02y: K = 65 and 96 within 2 % either way, the rest faster)
+bool use_2l(int dtype, int k, bool packed, bool off32) {
+  static const int mode = [] {
+    const char* e = getenv("FA_MEDIAN_2L");
+    return e ? atoi(e) : -1;
+  }();
+  if (dtype == FA_DTYPE_F64 || packed || !off32 || !full_enabled() || mode == 0 || k <= 64 || k > 128) return false;
+  return mode == 1 || k > kMedian2lMin;  // (A/B: tools/gpu_r02y.sh)
+}
+
 template <int DT>
-void launch_median(int k, bool packed, bool off32, dim3 grid, hipStream_t st, const MSeg* ds, int nseg,
-                   const void* const* dp) {
+void launch_median(int k, bool packed, bool off32, bool two_lane, dim3 grid, hipStream_t st, const MSeg* ds,
+                   int nseg, const void* const* dp) {
+  if constexpr (DT != FA_DTYPE_F64) {
+    if (two_lane) {
+      switch ((k + 7) / 8) {  // B = K rounded up to 8, N = B / 2 keys per lane
+#define FA_M2(Q)                                                                                                  \
+  case Q:                                                                                                       \
+    if (k == 8 * Q) hipLaunchKernelGGL((k_median_2l<DT, 4 * Q, true>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); \
+    else hipLaunchKernelGGL((k_median_2l<DT, 4 * Q, false>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);          \
+    return;
+        FA_M2(9) FA_M2(10) FA_M2(11) FA_M2(12) FA_M2(13) FA_M2(14) FA_M2(15) FA_M2(16)
+#undef FA_M2
+        default: break;
+      }
+    }
+  }
   if constexpr (DT == FA_DTYPE_F64) {
     hipLaunchKernelGGL((k_median_rank<DT>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);
   } else {
@@ -398,7 +498,12 @@ int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t*
     packed = d_out[s] && (uintptr_t)d_out[s] % 4 == 0;
     for (int i = 0; i < k && packed; ++i) packed = (uintptr_t)d_in[(int64_t)s * k + i] % 4 == 0;
   }
-  const int64_t tile_elems = packed ? 2 * kBlock : kBlock;  // coordinates per tile
+  // k_median_off addresses a client's element by a 32-bit byte offset: every segment must fit
+  const int64_t es = dtype == FA_DTYPE_F32 ? 4 : dtype == FA_DTYPE_F64 ? 8 : 2;
+  bool off32 = true;
+  for (int s = 0; s < num_segments; ++s) off32 = off32 && seg_numel[s] * es <= (int64_t)0xFFFFFFFFll;
+  const bool two_lane = use_2l(dtype, k, packed, off32);
+  const int64_t tile_elems = packed ? 2 * kBlock : two_lane ? k2lCols : kBlock;  // coordinates per tile
   int nseg = 0;
   int64_t tiles = 0;
   for (int s = 0; s < num_segments; ++s) {
@@ -439,15 +544,11 @@ int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t*
   const MSeg* ds = (const MSeg*)dv;
   const void* const* dp = (const void* const*)(dv + seg_bytes);
   const dim3 grid((unsigned)tiles);
-  // k_median_off addresses a client's element by a 32-bit byte offset: every segment must fit
-  const int64_t es = dtype == FA_DTYPE_F32 ? 4 : dtype == FA_DTYPE_F64 ? 8 : 2;
-  bool off32 = true;
-  for (int s = 0; s < num_segments; ++s) off32 = off32 && seg_numel[s] * es <= (int64_t)0xFFFFFFFFll;
   switch (dtype) {
-    case FA_DTYPE_F32: launch_median<FA_DTYPE_F32>(k, packed, off32, grid, st, ds, nseg, dp); break;
-    case FA_DTYPE_BF16: launch_median<FA_DTYPE_BF16>(k, packed, off32, grid, st, ds, nseg, dp); break;
-    case FA_DTYPE_F16: launch_median<FA_DTYPE_F16>(k, packed, off32, grid, st, ds, nseg, dp); break;
-    default: launch_median<FA_DTYPE_F64>(k, packed, off32, grid, st, ds, nseg, dp); break;
+    case FA_DTYPE_F32: launch_median<FA_DTYPE_F32>(k, packed, off32, two_lane, grid, st, ds, nseg, dp); break;
+    case FA_DTYPE_BF16: launch_median<FA_DTYPE_BF16>(k, packed, off32, two_lane, grid, st, ds, nseg, dp); break;
+    case FA_DTYPE_F16: launch_median<FA_DTYPE_F16>(k, packed, off32, two_lane, grid, st, ds, nseg, dp); break;
+    default: launch_median<FA_DTYPE_F64>(k, packed, off32, two_lane, grid, st, ds, nseg, dp); break;
   }
   FA_HIP(hipGetLastError());
   return release(slot, st);
@@ -532,6 +633,8 @@ PairSplit pair_split(int k) {
     q.pe = q.ce * q.esplit;
   }
   q.nblocks = 1024;  // workgroups (each writes all pair partials once)
+  static const char* ob = getenv("FA_PAIR_BLOCKS");  // measurement override (tools/gpu_r02v.sh)
+  if (ob && atoi(ob) >= 64 && atoi(ob) <= 16384) q.nblocks = atoi(ob);
   return q;
 }
 

@@ -132,6 +132,27 @@ def test_median_f32_ragged_and_unaligned(eng, k, off):
         assert torch.equal(o.cpu().view(torch.int32), exp.view(torch.int32))
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("k", [65, 72, 73, 88, 96, 97, 100, 113, 120, 121, 127, 128])
+def test_median_two_lanes_per_column(eng, dtype, k):
+    """K in (64, 128] (k_median_2l where the dispatch picks it: two lanes of different waves per
+    column, sorted halves merged
+    through LDS, +-inf-key sentinels) -- ragged segments around the 128-column tile, NaN (first NaN
+    wins, also when only the upper half holds it), +-0 ranks, ties, +-Inf; bit-exact to the oracle."""
+    from oracle import orc
+    g = torch.Generator().manual_seed(31 * k + (0 if dtype == torch.float32 else 1 if dtype == torch.bfloat16 else 2))
+    sizes = [1, 127, 128, 129, 3001]
+    cols = [_column_data(g, k, n, dtype, zeros=0.15) for n in sizes]
+    cols[4][k - 1][5] = float("nan")   # a NaN only in the upper half's clients
+    cols[4][k // 2 + 3][9] = float("-inf")  # a real -inf next to the low sentinels
+    cols[4][k - 2][9] = float("-inf")
+    outs = eng.coord_median([[x.to(DEV) for x in c] for c in cols])
+    for c, o in zip(cols, outs):
+        exp = orc.coord_median(c)
+        iv = torch.int32 if dtype == torch.float32 else torch.int16
+        assert torch.equal(o.cpu().view(iv), exp.view(iv))
+
+
 def test_median_all_zero_columns(eng):
     """Columns of only +-0 in every sign pattern: ATen returns the zero of rank (K-1)/2 by index."""
     from oracle import orc

@@ -10,6 +10,8 @@ SSA form and pruned backwards to what the output at rank P2/2 - 1 depends on (a 
 min or max half is dead emits only the other half).  The kernel pads K real keys to B with
 runtime low/high sentinels in the same way (robust.hip), so one network serves K in (B-8, B].
 
+Also SortNet<N> (N = 36, 40, ..., 64: a sort of N keys) for the two-lanes-per-column kernel k_median_2l.
+
 Run: python tools/gen_median_nets.py   (prints the min/max count per B)
 """
 from __future__ import annotations
@@ -99,6 +101,43 @@ def main(path):
         body.append(f"// B = {B}: {ops} min/max ops\n" + code)
     body.append("template <int B, typename K> __device__ __forceinline__ K select_mid(const K (&x)[B]) {\n"
                 "  return MidNet<B>::run(x);\n}")
+    # k_median_2l (robust.hip): a column's B keys split over two lanes, N = B/2 each; every lane sorts
+    # its N keys in place (all N outputs are used: the lower lane merges its own with the upper
+    # lane's).  Network: odd-even merge sort of 64 with the 64 - N extra inputs compile-time high
+    # sentinels folded away (a comparator with a constant input is a renaming).
+    lines = ["template <int N> struct SortNet;"]
+    counts2 = {}
+    for N in range(36, 65, 4):
+        pos = [("x", i) for i in range(N)] + [("H",)] * (64 - N)
+        ops = []
+        tmp = 0
+        for i, j in oddeven_merge_sort(64):
+            a, b = pos[i], pos[j]
+            if a[0] == "H" and b[0] == "H":
+                continue
+            if a[0] == "H" or b[0] == "H":  # the constant high goes to the max side
+                pos[i], pos[j] = (b, a) if a[0] == "H" else (a, b)
+                continue
+            ops.append((a, b, tmp))
+            pos[i], pos[j] = ("t", tmp, "min"), ("t", tmp, "max")
+            tmp += 1
+        assert all(pos[i][0] != "H" for i in range(N))
+        # emit in SSA over named temporaries; the outputs are copied back to x[0..N-1]
+        ref = lambda o: f"x[{o[1]}]" if o[0] == "x" else ("i" if o[2] == "min" else "a") + str(o[1])
+        L = [f"template <> struct SortNet<{N}> {{",
+             f"  template <typename K> __device__ __forceinline__ static void run(K (&x)[{N}]) {{"]
+        for a, b, t in ops:
+            L.append(f"    const K i{t} = kmin({ref(a)}, {ref(b)}), a{t} = kmax({ref(a)}, {ref(b)});")
+        moved = [i for i in range(N) if pos[i] != ("x", i)]
+        for i in moved:  # read every output before any x[] is overwritten
+            L.append(f"    const K o{i} = {ref(pos[i])};")
+        for i in moved:
+            L.append(f"    x[{i}] = o{i};")
+        L += ["  }", "};"]
+        lines.append("\n".join(L))
+        counts2[N] = 2 * len(ops)
+    body.append("// SortNet<N>::run(x): x[0..N-1] ascending (k_median_2l); min/max per N: " + str(counts2) +
+                "\n" + "\n\n".join(lines))
     hdr = (
         "// median_nets.h -- GENERATED by tools/gen_median_nets.py; do not edit.\n"
         "// MidNet<B>::run(keys): the key at rank (B-1)/2 of B keys, by a pruned Batcher odd-even merge\n"
