@@ -423,7 +423,8 @@ bool full_enabled() {
 
 // Two lanes per column (k_median_2l) for K in (kMedian2lMin, 128]; FA_MEDIAN_2L=0 / 1 turns it off /
 // forces it for every K in (64, 128] (A/B measurement)
-constexpr int kMedian2lMin = 64;  // every K in (64, 128] (r02y: K = 65 and 96 within 2 % either way, the rest faster)
+constexpr int kMedian2lMin = 64;  // every K in (64, 128] (r02y: K = 65 and 96 within 2 % either way, the rest faster;
+                                  // r02ab: at B = 40..64 the split measured 0-11 % slower, not used)
 bool use_2l(int dtype, int k, bool packed, bool off32) {
   static const int mode = [] {
     const char* e = getenv("FA_MEDIAN_2L");
