@@ -268,6 +268,14 @@ class ClientArena:
             self._pending.append(ev)
             return
         idx, pinned = self._stage_slot()
+        if not self.tiled:
+            self._pack_and_copy(i, state_dict, pinned)
+            with torch.cuda.stream(self._copy_stream):
+                ev = torch.cuda.Event()
+                ev.record(self._copy_stream)
+            self._staging[idx] = (pinned, ev)
+            self._pending.append(ev)
+            return
         views = self.layout.views(pinned, None)
         for k, v in views.items():
             v.copy_(state_dict[k])
@@ -286,6 +294,37 @@ class ClientArena:
             ev.record(self._copy_stream)
         self._staging[idx] = (pinned, ev)
         self._pending.append(ev)
+
+    PACK_CHUNK_BYTES = 8 << 20  # H2D issued per ~8 MB packed
+
+    def _pack_and_copy(self, i: int, state_dict, pinned) -> None:
+        """Pack the update into the pinned row and issue the H2D of every ~8 MB packed on the copy
+        stream at once, so the DMA of one piece runs while the next is packed (r02: the
+        pack-then-copy form left 0.6 ms of H2D after a 1.1 ms pack of a 47 MB update).  The pack is
+        torch's per-key copy_ (its OpenMP pool); the C++ thread-pool memcpy used for whole-round host
+        packing (_host.pack_range) measured slower here (K = 32 ResNet-18-GN last arrival: pack
+        1.30 ms with copy_ vs 1.8-2.4 ms with 4-16 threads, profiles/r02ah)."""
+        issued = {dt: 0 for dt in pinned}  # elements of each dtype group already handed to the DMA
+        packed = dict(issued)
+        pending = 0
+
+        def issue(final: bool):
+            with torch.cuda.stream(self._copy_stream):
+                for dt, buf in pinned.items():
+                    hi = buf.numel() if final else packed[dt]
+                    if hi > issued[dt]:
+                        self.bufs[dt][i][issued[dt]:hi].copy_(buf[issued[dt]:hi], non_blocking=True)
+                        issued[dt] = hi
+
+        for k in self.layout.keys:
+            dt, off, shape, n = self.layout.where[k]
+            pinned[dt][off:off + n].view(shape).copy_(state_dict[k])
+            packed[dt] = off + n
+            pending += n * pinned[dt].element_size()
+            if pending >= self.PACK_CHUNK_BYTES:
+                issue(False)
+                pending = 0
+        issue(True)
 
     def _wait_ingest(self):
         cur = torch.cuda.current_stream(self.device)

@@ -21,6 +21,7 @@ from typing import Dict, Optional
 
 import torch
 
+from ... import _host
 from ...arena import ArenaLayout, ClientArena
 
 
@@ -31,6 +32,7 @@ class ArrivalIngest:
         self.arena: Optional[ClientArena] = None
         self.parity = 0
         self._host: Dict[int, "OrderedDict[str, torch.Tensor]"] = {}
+        self._flat_host: Dict[int, list] = {}  # per round parity: pinned flat buffers, one per dtype group
 
     @staticmethod
     def wants(device) -> bool:
@@ -61,10 +63,16 @@ class ArrivalIngest:
         self.parity ^= 1
 
     def to_host(self, averaged) -> "OrderedDict[str, torch.Tensor]":
-        """The aggregated model in pinned host memory (one D2H per tensor on the current stream,
-        then a wait): the broadcast's send buffer.  Buffers alternate between two rounds."""
+        """The aggregated model in pinned host memory: the broadcast's send buffer.  The engine's
+        outputs are views of one device allocation per dtype group, so each group goes D2H as ONE
+        copy into a pinned flat buffer whose per-key views (built in C++, _host.carve) are returned
+        (r02: 122 per-key copies of a ResNet-18-GN model cost 1.47 ms, mostly per-copy overhead).
+        Other dicts: one D2H per tensor.  Buffers alternate between two rounds."""
         if not any(v.is_cuda for v in averaged.values()):
             return averaged
+        flat = self._to_host_flat(averaged)
+        if flat is not None:
+            return flat
         bufs = self._host.get(self.parity)
         if bufs is None or list(bufs.keys()) != list(averaged.keys()) or any(
                 bufs[k].shape != v.shape or bufs[k].dtype != v.dtype for k, v in averaged.items()):
@@ -74,6 +82,48 @@ class ArrivalIngest:
             bufs[k].copy_(v, non_blocking=True)
         torch.cuda.current_stream(next(iter(averaged.values())).device).synchronize()
         return bufs
+
+
+    def _to_host_flat(self, averaged):
+        groups = OrderedDict()  # device storage -> (dtype, storage, keys, element offsets, shapes)
+        for k, v in averaged.items():
+            if not v.is_cuda or not v.is_contiguous():
+                return None
+            st = v.untyped_storage()
+            g = groups.get(st.data_ptr())
+            if g is None:
+                g = groups[st.data_ptr()] = (v.dtype, st, [], [], [])
+            elif g[0] != v.dtype:
+                return None
+            g[2].append(k)
+            g[3].append(v.storage_offset())
+            g[4].append(tuple(v.shape))
+        if len(groups) > 8:  # not the engine's grouped outputs: per-tensor copies
+            return None
+        dev = next(iter(averaged.values())).device
+        cache = self._flat_host.setdefault(self.parity, [])
+        views = {}
+        for gi, (dt, st, keys, offs, shapes) in enumerate(groups.values()):
+            lo = min(offs)
+            n = max(o + _numel(s) for o, s in zip(offs, shapes)) - lo
+            if gi >= len(cache) or cache[gi].dtype != dt or cache[gi].numel() < n:
+                if gi >= len(cache):
+                    cache.append(None)
+                cache[gi] = torch.empty(max(n, 1), dtype=dt, pin_memory=True)
+            host = cache[gi][:n]
+            src = torch.empty(0, dtype=dt, device=dev).set_(st, lo, (n,))
+            host.copy_(src, non_blocking=True)
+            for k, hv in zip(keys, _host.carve(host, [o - lo for o in offs], list(shapes))):
+                views[k] = hv
+        torch.cuda.current_stream(dev).synchronize()
+        return OrderedDict((k, views[k]) for k in averaged.keys())
+
+
+def _numel(shape) -> int:
+    n = 1
+    for s in shape:
+        n *= s
+    return n
 
 
 def move_to_device(state_dict, device):

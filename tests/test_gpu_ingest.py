@@ -113,15 +113,20 @@ def _server(client_num):
     return FedMLAggregator(client_num=client_num, device="cuda:0", args=args, server_aggregator=S(None, args))
 
 
+@pytest.mark.parametrize("chunk", [None, 1024])
 @pytest.mark.parametrize("name", ["g3_fedavg_mixed_K5", "g2_fedavg_bf16_K7_P4099", "g1_fedavg_f32_K32_P4099",
                                   "g9_edge_values_K4"])
-def test_cross_silo_arrival_ingest_rounds(monkeypatch, name):
+def test_cross_silo_arrival_ingest_rounds(monkeypatch, name, chunk):
     """Updates adopted into arena rows as they arrive (out of order), three rounds (both row
     buffers, then the first again): the round's aggregation is ONE arena launch, bit-exact to the
     reference's output, the dicts now hold device tensors (as the reference's in-place move), and
-    the pinned host copy for the broadcast matches too."""
+    the pinned host copy for the broadcast matches too.  chunk = 1 KiB: the pinned pack hands
+    every ~1 KiB to the DMA (many pieces per dtype group, ragged against key boundaries)."""
     from golden_io import client_dicts, expected_dicts
     from refcases import assert_dict_bits
+    if chunk is not None:
+        from fedml_amd.arena import ClientArena
+        monkeypatch.setattr(ClientArena, "PACK_CHUNK_BYTES", chunk)
     meta, arr = _golden(name)
     exp = expected_dicts(meta, arr)[0]
     K = meta["num_clients"]
@@ -139,6 +144,34 @@ def test_cross_silo_arrival_ingest_rounds(monkeypatch, name):
         host = srv.get_global_model_params_host()
         assert all(v.is_pinned() for v in host.values())
         assert_dict_bits(host, exp, f"{name} host round {rnd}")
+
+
+def test_cross_silo_arrival_large_update_pipelined_pack():
+    """A 36 MB update (several 8 MB pack pieces per dtype group, float32 + int64 + bfloat16 keys)
+    through the cross-silo round: bit-exact to the oracle, and the pinned host result (one D2H per
+    dtype group, per-key views) equals the device result; two rounds."""
+    from oracle import orc
+    from refcases import bits_equal
+    srv = _server(3)
+    g = torch.Generator().manual_seed(5)
+
+    def upd():
+        return OrderedDict(a=torch.randn(4_000_001, generator=g), n=torch.randint(0, 9, (3,), generator=g),
+                           b=torch.randn(2_999_999, generator=g), h=torch.randn(1_000_003, generator=g).to(torch.bfloat16),
+                           c=torch.randn(7, generator=g))
+    for rnd in range(2):
+        ds = [upd() for _ in range(3)]
+        xs = {k: [d[k].clone() for d in ds] for k in ds[0]}
+        for i, d in enumerate(ds):
+            srv.add_local_trained_result(i, d, 10 * (i + 1))
+        assert srv.check_whether_all_receive()
+        avg, _, _ = srv.aggregate()
+        host = srv.get_global_model_params_host()
+        assert list(host.keys()) == list(xs.keys())
+        for k in xs:
+            exp = orc.weighted_sum(xs[k], MUL_W, [10 / 60, 20 / 60, 30 / 60])
+            assert bits_equal(avg[k].cpu(), exp), (rnd, k)
+            assert host[k].is_pinned() and bits_equal(host[k], exp), (rnd, k)
 
 
 def test_cross_silo_arrival_mixed_layouts_and_plain_dicts(monkeypatch):
