@@ -253,6 +253,8 @@ k_median_2l(const MSeg* __restrict__ segs, int nseg, const void* const* __restri
     const unsigned kk = key[t] ^ ((unsigned)((int)key[t] >> 31) | 0x80000000u);  // fkey
     if constexpr (EXACT) {
       key[t] = kk;
+    } else if (t < N - 8) {
+      key[t] = kk;  // K > B - 8: only the upper half's last 8 slots can hold sentinels
     } else {
       const unsigned real = 0u - (unsigned)(base + t < k);                 // uniform all-ones / zero
       const unsigned sent = base + t < lo_end ? kNegInfKey : kPosInfKey;  // uniform
