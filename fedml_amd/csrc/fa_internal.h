@@ -76,6 +76,7 @@ struct fa_ctx {
     void* dev = nullptr;
     size_t cap = 0;
     hipEvent_t ev = nullptr;
+    hipEvent_t staged = nullptr;  // the table copy on the side stream has landed (stage())
     bool pending = false;
   } slots[fa_detail::kSlots];
   int next = 0;

@@ -22,6 +22,8 @@
 //    so "acc = t_0" needs no select.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+
 #include <algorithm>
 #include <climits>
 #include <cstdarg>
@@ -1011,15 +1013,46 @@ bool stage_kernel_enabled() {
 }
 }  // namespace
 
-// A table of up to 256 KB goes by a copy kernel on the caller's stream: hipMemcpyAsync from pinned
-// memory ran as a separate copy whose completion the aggregation kernel then waited for (~30 us of
-// GPU time per call at 3,904 pointers, cfg2 through agg() on separate tensors).
+// A table of up to 256 KB goes by a copy kernel: hipMemcpyAsync from pinned memory ran as a separate
+// copy whose completion the aggregation kernel then waited for (~30 us of GPU time per call at 3,904
+// pointers, cfg2 through agg() on separate tensors).  The copy kernel runs on a per-device side
+// stream and the caller's stream waits for it (an event), so back-to-back calls copy call n+1's table
+// while call n's kernel is still running; the slot's device buffer is free (acquire_slot waited for
+// its previous reader).  FA_STAGE_SIDE=0: the copy on the caller's stream (A/B).
+namespace {
+bool stage_side_enabled() {
+  static const int on = [] {
+    const char* e = getenv("FA_STAGE_SIDE");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on != 0;
+}
+hipStream_t side_stream() {
+  static std::mutex m;
+  static hipStream_t ss[64] = {};
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(m);
+  if (!ss[d] && hipStreamCreateWithFlags(&ss[d], hipStreamNonBlocking) != hipSuccess) ss[d] = nullptr;
+  return ss[d];
+}
+}  // namespace
+
 int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st) {
   if (s->hmap && bytes <= (256u << 10) && stage_kernel_enabled()) {
     const int n16 = (int)((bytes + 15) / 16);  // slots are >= 16 KB and 16-byte multiples
     const int blocks = std::max(1, std::min(64, (n16 + kBlock - 1) / kBlock));
-    hipLaunchKernelGGL(k_stage_copy, dim3(blocks), dim3(kBlock), 0, st, (const u32x4*)s->hmap, (u32x4*)s->dev, n16);
+    hipStream_t cs = st;
+    if (stage_side_enabled()) {
+      hipStream_t ss = side_stream();
+      if (ss && (s->staged || hipEventCreateWithFlags(&s->staged, hipEventDisableTiming) == hipSuccess)) cs = ss;
+    }
+    hipLaunchKernelGGL(k_stage_copy, dim3(blocks), dim3(kBlock), 0, cs, (const u32x4*)s->hmap, (u32x4*)s->dev, n16);
     FA_HIP(hipGetLastError());
+    if (cs != st) {
+      FA_HIP(hipEventRecord(s->staged, cs));
+      FA_HIP(hipStreamWaitEvent(st, s->staged, 0));
+    }
     return FA_OK;
   }
   FA_HIP(hipMemcpyAsync(s->dev, s->host, bytes, hipMemcpyHostToDevice, st));
@@ -1080,6 +1113,7 @@ int fa_ctx_destroy(fa_ctx* c) {
   for (auto& s : c->slots) {
     if (s.pending && s.ev) (void)hipEventSynchronize(s.ev);
     if (s.ev) (void)hipEventDestroy(s.ev);
+    if (s.staged) (void)hipEventDestroy(s.staged);
     if (s.host) (void)hipHostFree(s.host);
     if (s.dev) (void)hipFree(s.dev);
   }
