@@ -225,15 +225,17 @@ k_median_off(const MSeg* __restrict__ segs, int nseg, const void* const* __restr
 // key(+inf)] -- two compares per lane instead of one per key.  N keys + the merge fit 128 VGPRs
 // (4 waves per SIMD).  Same keys and rare-case rules as k_median_off: bit-exact.
 constexpr int k2lCols = kBlock / 2;  // columns per workgroup
+#ifndef MEDIAN_2L_W
+#define MEDIAN_2L_W (N <= 40 ? 8 : N <= 48 ? 6 : 5)
+#endif
 constexpr unsigned kNegInfKey = 0x007FFFFFu, kPosInfKey = 0xFF800000u;  // fkey(-inf), fkey(+inf)
 template <int DT, int N, bool EXACT>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(N <= 44 ? 5 : 4)))
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MEDIAN_2L_W)))
 k_median_2l(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k) {
   constexpr int B = 2 * N;
   if constexpr (EXACT) k = B;
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   __shared__ u32x4 xs[N / 4][k2lCols];  // the upper lanes' N sorted keys, [quad][column]
-  __shared__ unsigned xn[k2lCols];      // the upper lanes' NaN flags
   const int h = __builtin_amdgcn_readfirstlane((int)threadIdx.x / k2lCols);  // half: wave-uniform
   const int c = (int)threadIdx.x % k2lCols;
   const int64_t tile = blockIdx.x;
@@ -266,11 +268,13 @@ k_median_2l(const MSeg* __restrict__ segs, int nseg, const void* const* __restri
   if (h == 1) {
 #pragma unroll
     for (int q = 0; q < N / 4; ++q) xs[q][c] = u32x4{key[4 * q], key[4 * q + 1], key[4 * q + 2], key[4 * q + 3]};
-    xn[c] = nan;
   }
   __syncthreads();
   if (h == 1) return;
   unsigned kr = 0;
+  // the upper half's NaN shows in its own sorted extremes (no flag array: N x 512 B of LDS per
+  // workgroup, so five 128-column workgroups share a CU at N = 64)
+  const bool cnan = xs[0][c].x < kNegInfKey || xs[N / 4 - 1][c].w > kPosInfKey;
 #pragma unroll
   for (int q = 0; q < N / 4; ++q) {  // partner keys 4q..4q+3 pair with own keys N-1-4q .. N-4-4q
     const u32x4 b = xs[q][c];
@@ -281,7 +285,7 @@ k_median_2l(const MSeg* __restrict__ segs, int nseg, const void* const* __restri
   }
   if (!live) return;
   const int r = (k - 1) >> 1;
-  const bool anynan = nan || xn[c] != 0;
+  const bool anynan = nan || cnan;
   if (anynan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, anynan, sg.out);
   else MedT<DT>::store(sg.out, e, fkey_inv(kr));
 }
