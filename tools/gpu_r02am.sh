@@ -1,5 +1,6 @@
 # k_median_2l occupancy (no NaN-flag array: N x 512 B LDS; waves/EU 8/6/5 by N) vs the committed kernel:
 # median GPU tests on the new library, then interleaved A/B by swapping the library file
+# (tools/ab/libfedagg_{base,new}.so were built from the parent commit and this one; not kept in the tree)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out/r02am
 cp tools/ab/libfedagg_new.so fedml_amd/libfedagg.so
