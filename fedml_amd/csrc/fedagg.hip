@@ -377,11 +377,21 @@ __device__ __forceinline__ void wsum_tile(const Seg* __restrict__ segs, int nseg
   }
 }
 
+// xcd = 1: workgroup -> tile mapping by XCD (the dispatcher deals workgroups to the 8 XCDs
+// round-robin; XCD x then walks a contiguous eighth of the tiles, so one XCD's L2 and address
+// translation caches see a few segments' allocations instead of all of them)
+__device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t tiles) {
+  constexpr int64_t kX = 8;
+  const int64_t x = bid % kX, j = bid / kX, q = tiles / kX, r = tiles % kX;
+  return x * q + min(x, r) + j;
+}
+
 template <int DT, int MODE, int U, int S, bool NT, bool PF>
 __global__ void __launch_bounds__(kBlock)
 k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
-       const void* const* __restrict__ ptrs, int k, double divisor, int64_t sstr) {
-  wsum_tile<DT, MODE, U, S, NT, PF>(segs, nseg, coef, ptrs, k, divisor, sstr, blockIdx.x);
+       const void* const* __restrict__ ptrs, int k, double divisor, int64_t sstr, int xcd) {
+  const int64_t t = xcd ? xcd_tile(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  wsum_tile<DT, MODE, U, S, NT, PF>(segs, nseg, coef, ptrs, k, divisor, sstr, t);
 }
 
 // Descriptor tables (segments | coefficients | pointers) small enough to travel as the kernel's
@@ -887,8 +897,17 @@ constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 template <int DT, int MODE, int U, int S, bool NT, bool PF>
 void launch_wsum(int64_t tiles, hipStream_t st, const Seg* segs, int nseg, const double* coef,
                  const void* const* ptrs, int k, double divisor, int64_t sstr) {
+  // multi-segment tables (separate tensors): XCD-contiguous tiles, FA_XCD_MAP=0 turns it off.  r02ao
+  // interleaved A/B: fragmented metric (26,112 tensors) 10.76-10.83 -> 10.64 ms, cfg2 on separate
+  // tensors 0.299-0.300 -> 0.292-0.299 ms.  One flat segment keeps the hardware's round-robin
+  // (tools/layout_probe.py: an XCD-contiguous split read 6.38-6.45 vs 6.62-6.72 TB/s there).
+  static const int xcd_env = [] {
+    const char* e = getenv("FA_XCD_MAP");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  const int xcd = xcd_env && nseg > 1 ? 1 : 0;
   hipLaunchKernelGGL((k_wsum<DT, MODE, U, S, NT, PF>), dim3((unsigned)tiles), dim3(kBlock), 0, st, segs,
-                     nseg, coef, ptrs, k, divisor, sstr);
+                     nseg, coef, ptrs, k, divisor, sstr, xcd);
 }
 
 // tables as the kernel argument: only the automatic shapes (variant 0: U = 8, S = 1; 5: U = 8, S = 2)
