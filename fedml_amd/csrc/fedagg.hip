@@ -898,9 +898,9 @@ template <int DT, int MODE, int U, int S, bool NT, bool PF>
 void launch_wsum(int64_t tiles, hipStream_t st, const Seg* segs, int nseg, const double* coef,
                  const void* const* ptrs, int k, double divisor, int64_t sstr) {
   // multi-segment tables (separate tensors): XCD-contiguous tiles, FA_XCD_MAP=0 turns it off.  r02ao
-  // interleaved A/B: fragmented metric (26,112 tensors) 10.76-10.83 -> 10.64 ms, cfg2 on separate
-  // tensors 0.299-0.300 -> 0.292-0.299 ms.  One flat segment keeps the hardware's round-robin
-  // (tools/layout_probe.py: an XCD-contiguous split read 6.38-6.45 vs 6.62-6.72 TB/s there).
+  // interleaved A/B: fragmented metric (26,112 tensors) 10.76-10.83 -> 10.64 ms.  One flat segment
+  // keeps the hardware's round-robin (tools/layout_probe.py: an XCD-contiguous split read 6.38-6.45
+  // vs 6.62-6.72 TB/s there).
   static const int xcd_env = [] {
     const char* e = getenv("FA_XCD_MAP");
     return e && e[0] == '0' ? 0 : 1;
