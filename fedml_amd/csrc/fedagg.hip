@@ -386,6 +386,14 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t tiles) {
   return x * q + min(x, r) + j;
 }
 
+bool xcd_map_enabled() {  // FA_XCD_MAP=0: round-robin workgroup -> tile order everywhere (A/B)
+  static const int on = [] {
+    const char* e = getenv("FA_XCD_MAP");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on != 0;
+}
+
 template <int DT, int MODE, int U, int S, bool NT, bool PF>
 __global__ void __launch_bounds__(kBlock)
 k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
@@ -421,8 +429,8 @@ template <int DT, int MODE, int U, int S, bool PF>
 __global__ void __launch_bounds__(kBlock)
 k_wsum_pair(const Seg* __restrict__ segs0, int nseg0, const void* const* __restrict__ ptrs0, int64_t sstr0,
             const Seg* __restrict__ segs1, int nseg1, const void* const* __restrict__ ptrs1, int64_t sstr1,
-            int64_t tiles1, const double* __restrict__ coef, int k, double divisor) {
-  const int64_t t = blockIdx.x;
+            int64_t tiles1, const double* __restrict__ coef, int k, double divisor, int xcd) {
+  const int64_t t = xcd ? xcd_tile(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;  // see k_wsum
   if (t < tiles1)
     wsum_tile<FA_DTYPE_I64, MODE, 8, 1, true, false>(segs1, nseg1, coef, ptrs1, k, divisor, sstr1, t);
   else
@@ -901,11 +909,7 @@ void launch_wsum(int64_t tiles, hipStream_t st, const Seg* segs, int nseg, const
   // interleaved A/B: fragmented metric (26,112 tensors) 10.76-10.83 -> 10.64 ms.  One flat segment
   // keeps the hardware's round-robin (tools/layout_probe.py: an XCD-contiguous split read 6.38-6.45
   // vs 6.62-6.72 TB/s there).
-  static const int xcd_env = [] {
-    const char* e = getenv("FA_XCD_MAP");
-    return e && e[0] == '0' ? 0 : 1;
-  }();
-  const int xcd = xcd_env && nseg > 1 ? 1 : 0;
+  const int xcd = xcd_map_enabled() && nseg > 1 ? 1 : 0;
   hipLaunchKernelGGL((k_wsum<DT, MODE, U, S, NT, PF>), dim3((unsigned)tiles), dim3(kBlock), 0, st, segs,
                      nseg, coef, ptrs, k, divisor, sstr, xcd);
 }
@@ -1413,7 +1417,7 @@ void launch_pair(int64_t tiles, hipStream_t st, const char* dev, const InlineDes
     hipLaunchKernelGGL((k_wsum_pair<DT, MODE, 8, S, false>), dim3((unsigned)tiles), dim3(kBlock), 0, st,
                        (const Seg*)dev, a.nseg0, (const void* const*)(dev + L.ptr0), a.sstr0,
                        (const Seg*)(dev + L.seg1), a.nseg1, (const void* const*)(dev + L.ptr1), a.sstr1, a.tiles1,
-                       (const double*)(dev + L.coef), a.k, a.divisor);
+                       (const double*)(dev + L.coef), a.k, a.divisor, xcd_map_enabled() && a.nseg0 > 1 ? 1 : 0);
 }
 
 template <int DT>
