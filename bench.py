@@ -9,13 +9,18 @@ B = K*P*4 (reads) + P*4 (write) = 64.5 GB.
 
   python bench.py [--gpus N --steps K --warmup W] [--config metric|resnet18|vit_bf16|hier|gossip]
 
-N > 1 (torch.distributed.run, one rank per GPU, RCCL over xGMI): the SAME total problem split by
+N > 1 (one rank per GPU, RCCL over xGMI): ``python bench.py --gpus N`` starts its N ranks itself
+(torch.distributed.run as a child process, before anything touches the GPU); under an outer
+torch.distributed.run (WORLD_SIZE set) it runs as one rank.  The SAME total problem is split by
 client group -- rank r holds clients [r*K/N, (r+1)*K/N) -- each rank forms its ordered local
-partial with the global weights (group step, HIP kernel), and the partials are SUM-reduced across
-the GPUs (global step): by default a reduce-scatter that leaves the global model partitioned over
-the GPUs (--collective reduce = the reference NCCL simulator's reduce to rank 0,
-simulation/nccl/base_framework/params.py:98-105), pipelined in chunks behind the local kernels
-(fedml_amd/distributed/group_reduce.py).  Total work is fixed, so scaling is "strong".
+partial with the global weights (group step, HIP kernel), and the partials are summed across the
+GPUs (global step): by default the "ordered" exchange, which delivers the WHOLE global model to
+rank 0 summed in rank order (bit-exact; the reference NCCL simulator's reduce to rank 0,
+simulation/nccl/base_framework/common.py:196-210), pipelined in chunks behind the local kernels
+(fedml_amd/distributed/group_reduce.py; --collective picks reduce / all_reduce / reduce_scatter /
+ordered_all).  Total work is fixed, so scaling is "strong"; roofline.frac at N > 1 is the whole
+step's aggregate GB/s over N x 8 TB/s.  Every collective has a process-group
+timeout (--pg-timeout) and every rank a stage watchdog (--stage-timeout), so a hang exits non-zero.
 
 Other configs (one JSON line each, same fields): resnet18 = cfg2 (ResNet-18-GN state_dict, 122
 tensors incl. 20 int64, K=32); vit_bf16 = cfg3 (ViT-B/16 layout, bf16, K=128); hier = cfg4 (8
@@ -65,6 +70,16 @@ def parse():
                         "ordered_all = the same on every rank; reduce = RCCL's reduce to rank 0 (the reference "
                         "NCCL simulator's call); reduce_scatter = the global model left SHARDED over the GPUs "
                         "(no rank holds all of it); all_reduce = RCCL all-reduce")
+    p.add_argument("--pg-timeout", type=float, default=180.0,
+                   help="N > 1: process-group timeout (s) of every collective (a hung RCCL op fails the rank)")
+    p.add_argument("--stage-timeout", type=float, default=300.0,
+                   help="a rank making no progress for this long in one stage exits 124, naming the stage")
+    p.add_argument("--launch-timeout", type=float, default=1500.0,
+                   help="--gpus N > 1 without an outer launcher: wall-clock limit (s) of the whole N-rank run")
+    p.add_argument("--exchange-impl", default="native", choices=["native", "torch"],
+                   help="N > 1 over RCCL: native = the whole step in one fa_group_reduce call of libfedagg "
+                        "(include/fedagg_comm.h, its own RCCL communicators); torch = the same algorithm issued "
+                        "per chunk through torch.distributed (group_reduce.py; always used over gloo)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     p.add_argument("--check-samples", type=int, default=65536)
@@ -87,12 +102,96 @@ def parse():
 
 
 # ----------------------------------------------------------------------------- distributed setup
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_cmd(n, argv, port, script=None):
+    """The torch.distributed.run command that starts ``n`` ranks of this script on one node
+    (rendezvous on 127.0.0.1), each with the caller's own arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port),
+            script or os.path.abspath(__file__)] + list(argv)
+
+
+def launch_ranks(n, argv, timeout_s, script=None):
+    """``python bench.py --gpus N`` without an outer launcher: start the N ranks as CHILD processes
+    (torch.distributed.run, one rank per GPU) -- nothing here has touched the GPU, and the parent
+    never execs -- relay their output (rank 0 prints the JSON line), and return the worst rc.  A
+    run that outlives ``timeout_s`` is killed as a process group and returns 124."""
+    import signal
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    env.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")  # a collective timeout tears the rank down
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")      # dmabuf IPC (the host driver's only mode)
+    p = subprocess.Popen(launch_cmd(n, argv, _free_port(), script), env=env, start_new_session=True)
+    try:
+        rc = p.wait(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        print(f"bench.py: the {n}-rank run exceeded {timeout_s:.0f} s; killing its process group",
+              file=sys.stderr, flush=True)
+        try:
+            os.killpg(p.pid, signal.SIGTERM)
+            p.wait(timeout=20)
+        except (subprocess.TimeoutExpired, ProcessLookupError):
+            try:
+                os.killpg(p.pid, signal.SIGKILL)
+            except ProcessLookupError:
+                pass
+            p.wait()
+        return 124
+    return rc if rc >= 0 else 128 - rc
+
+
+class Stage:
+    """Names what every rank is doing, and ends a rank that stays in one stage longer than
+    ``limit_s`` with a message naming the stage (and, inside the exchange, the chunk) and exit 124 --
+    so a hung collective fails the run promptly instead of spending the launcher's whole budget."""
+
+    def __init__(self, rank, limit_s):
+        import threading
+        self.rank, self.limit, self.name, self.t0 = rank, limit_s, "start", time.monotonic()
+        self._lock = threading.Lock()
+        if limit_s and limit_s > 0:
+            threading.Thread(target=self._watch, daemon=True).start()
+
+    def __call__(self, name):
+        with self._lock:
+            self.name, self.t0 = name, time.monotonic()
+
+    def done(self):
+        self.limit = float("inf")
+
+    def _watch(self):
+        while True:
+            time.sleep(1.0)
+            with self._lock:
+                name, dt = self.name, time.monotonic() - self.t0
+            if dt > self.limit:
+                try:
+                    from fedml_amd.distributed.group_reduce import last_issued
+                    where = last_issued()
+                except Exception:  # noqa: BLE001 -- diagnostics only
+                    where = None
+                print(f"bench.py rank {self.rank}: no progress for {dt:.0f} s in stage '{name}'"
+                      + (f" (last exchange op issued: {where})" if where else "") + "; exiting 124",
+                      file=sys.stderr, flush=True)
+                os._exit(124)
+
+
 def init_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world == 1 and args.gpus > 1:
-        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+        raise SystemExit("--gpus N > 1: WORLD_SIZE is 1 (launch through bench.py itself, or torch.distributed.run "
+                         "with --nproc-per-node N)")
+    if world > 1 and args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     # FEDML_AMD_BENCH_REHEARSAL=1: rehearse the N > 1 code path with every rank on device 0 over gloo
     # (RCCL refuses two ranks on one GPU); numbers from such a run are not measurements
     rehearsal = os.environ.get("FEDML_AMD_BENCH_REHEARSAL") == "1"
@@ -100,12 +199,16 @@ def init_dist(args):
         local = 0
     torch.cuda.set_device(local)
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        tmo = datetime.timedelta(seconds=args.pg_timeout)
         if rehearsal:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=tmo)
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
     return rank, world, local
 
 
@@ -236,6 +339,8 @@ class Timed:
     def __init__(self):
         self.pairs = []
         self.on = False
+        self.natives = []  # native GroupReducers: their local-step kernels are timed inside libfedagg
+        self.native_ms, self.native_launches = 0.0, 0
 
     def __enter__(self):
         if self.on:
@@ -249,12 +354,29 @@ class Timed:
             b.record(torch.cuda.current_stream())
             self.pairs.append((self.a, b))
 
+    def start(self):
+        for r in self.natives:  # drop the warmup steps' native local-step timings
+            r.local_time(reset=True)
+        self.on = True
+
+    def stop(self):
+        self.on = False
+        self.native_ms, self.native_launches = 0.0, 0
+        for r in self.natives:
+            ms, cnt = r.local_time(reset=True)
+            self.native_ms += ms
+            self.native_launches += cnt
+
     def avg_ms(self):
+        if self.native_launches:
+            return self.native_ms / self.native_launches
         d = [a.elapsed_time(b) for a, b in self.pairs]
         return float(np.mean(d)) if d else None
 
     def per_step_ms(self, steps):
         """Summed kernel time per step (several timed launches per step)."""
+        if self.native_launches:
+            return self.native_ms / steps
         d = [a.elapsed_time(b) for a, b in self.pairs]
         return float(np.sum(d)) / steps if d else None
 
@@ -266,10 +388,19 @@ def reducer(args, eng, timer, **kw):
     exchange is left out of that average: it is not the dominant kernel)."""
     from fedml_amd.distributed.group_reduce import GroupReducer
 
+    import torch.distributed as dist
+    if args.exchange_impl == "native" and dist.get_backend() == "nccl":
+        # the product path: one fa_group_reduce call per step (include/fedagg_comm.h), its local-step
+        # kernels HIP-event timed inside the library
+        red = GroupReducer(collective=args.collective, chunks=args.chunks, stream=masked_stream(eng, args),
+                           native=True, timing=True)
+        timer.natives.append(red)
+        return red
+
     def untimed_sum(xs_, mode, coef, div, o):
         return eng.weighted_sum(xs_, mode, coef, div, out=o)
     return GroupReducer(collective=args.collective, chunks=args.chunks, stream=masked_stream(eng, args),
-                        combine_sum=untimed_sum, **kw)
+                        combine_sum=untimed_sum, native=False, **kw)
 
 
 def count_bad(got, exp):
@@ -1402,10 +1533,74 @@ def pmc_traffic(workload):
         return None
 
 
+def roofline_block(wl, world, value, unit, achieved, kernel_ms, launch_bytes):
+    """The line's ``roofline`` object.  N = 1: the dominant kernel's algorithmic bytes per launch over
+    its HIP-event-timed average duration, against one GPU's 8 TB/s.  N > 1: the
+    WHOLE step -- local partials plus the cross-GPU exchange -- as aggregate GB/s (``value``) against
+    N x 8 TB/s; the per-rank local-kernel rate is kept beside it under ``local_kernel``.  ``traffic``
+    is the HBM bytes per launch of the committed rocprofv3 PMC run of this workload (not measured in
+    this run; ``traffic_source`` names the file), or null."""
+    traffic = pmc_traffic(wl["name"])
+    local = {"achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+             "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+             "kernel_avg_ms": round(kernel_ms, 4) if kernel_ms else None,
+             "algorithmic_bytes_per_launch": int(launch_bytes) if launch_bytes else None}
+    block = {"bound": "hbm"}
+    if world == 1:
+        block.update(local)
+    else:
+        peak = world * HBM_PEAK_GBS
+        block.update({"achieved": round(value, 1) if unit == "GB/s" else None, "peak": peak, "unit": "GB/s",
+                      "frac": round(value / peak, 4) if unit == "GB/s" else None,
+                      "definition": "whole step (local partials + exchange): aggregate GB/s / (N x 8 TB/s), "
+                                    "SURVEY.md 8(d)",
+                      "local_kernel": dict(local, definition="one rank's local-partial kernels: its algorithmic "
+                                                             "bytes / their summed HIP-event time / 8 TB/s")})
+    block["traffic"] = traffic
+    block["traffic_source"] = ("profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE/WRITE_SIZE of a separate "
+                               "profiling run of this workload, not measured in this run)" if traffic else None)
+    block["measured_read_ceiling"] = measured_ceiling()
+    return block
+
+
 # ----------------------------------------------------------------------------- main
+def cpu_probe(args):
+    """FEDML_AMD_BENCH_CPU_PROBE=1 (tests only, no GPU): each launched rank joins a gloo group,
+    sums its rank over the group and rank 0 prints one JSON line -- exercises the self-launch path
+    (launch_ranks) end to end on a CPU container."""
+    import datetime
+
+    import torch.distributed as dist
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.pg_timeout))
+    t = torch.tensor([float(rank)])
+    dist.all_reduce(t)
+    if os.environ.get("FEDML_AMD_BENCH_CPU_PROBE_FAIL_RANK") == str(rank):
+        raise SystemExit(3)
+    if os.environ.get("FEDML_AMD_BENCH_CPU_PROBE_HANG_RANK") == str(rank):
+        stage = Stage(rank, args.stage_timeout)
+        stage("probe hang")
+        time.sleep(3600)
+    if rank == 0:
+        print(json.dumps({"metric": "cpu probe", "n_gpus": world, "rank_sum": float(t.item())}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no outer launcher: start the N ranks as child processes before anything touches the GPU
+        if os.environ.get("FEDML_AMD_BENCH_REHEARSAL") != "1" and not os.environ.get("FEDML_AMD_BENCH_CPU_PROBE"):
+            have = torch.cuda.device_count()  # counts devices without initialising HIP on this image
+            if have < args.gpus:
+                raise SystemExit(f"--gpus {args.gpus}: only {have} HIP device(s) visible "
+                                 "(FEDML_AMD_BENCH_REHEARSAL=1 rehearses the N-rank path on one device over gloo)")
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout))
+    if os.environ.get("FEDML_AMD_BENCH_CPU_PROBE"):
+        return cpu_probe(args)
     rank, world, local = init_dist(args)
+    stage = Stage(rank, args.stage_timeout)
+    stage("setup")
     from fedml_amd.engine import get_engine
     eng = get_engine(local)
     if args.variant:
@@ -1415,12 +1610,15 @@ def main():
           "gossip": wl_gossip, "host": wl_host, "secagg": wl_secagg, "fedopt": wl_fedopt, "dropin_cpu": wl_dropin_cpu, "median": wl_median,
           "krum": wl_krum, "arrival": wl_arrival, "lr": wl_lr}[args.config](args, eng, rank, world, timer)
 
-    for _ in range(args.warmup):
+    for i in range(args.warmup):
+        stage(f"warmup step {i}")
         wl["step"]()
     torch.cuda.synchronize()
+    stage("barrier before the timed steps")
     barrier(world)
     torch.cuda.synchronize()
-    timer.on = True
+    timer.start()
+    stage("timed steps")
     t0 = time.perf_counter()
     lat = []
     for _ in range(args.steps):
@@ -1429,7 +1627,8 @@ def main():
     barrier(world)
     torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
-    timer.on = False
+    timer.stop()
+    stage("parity check")
     ms_per_step = elapsed / args.steps * 1e3
     if wl.get("latency"):  # the step returns its own latency (s); value = mean (or median) latency in ms
         value = float(np.median(lat) if wl.get("stat") == "median" else np.mean(lat)) * 1e3
@@ -1446,6 +1645,7 @@ def main():
     achieved = launch_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms else None
     parity = wl["parity"]()
     cpu = None
+    stage("cpu baseline")
     if rank == 0 and world == 1 and not args.no_cpu_baseline and wl.get("cpu_K"):
         cpu = wl["cpu"](args.cpu_seconds) if wl.get("cpu") else cpu_baseline(wl["cpu_K"], args.cpu_seconds)
         cpu.setdefault("cpu_model", cpu_model())
@@ -1471,17 +1671,12 @@ def main():
                        "parallelism": f"client-groups x{world}" +
                                       (f", {args.collective} over "
                                        f"{'gloo (one-GPU rehearsal)' if os.environ.get('FEDML_AMD_BENCH_REHEARSAL') else 'RCCL'}"
-                                       f" in {args.chunks} chunks"
+                                       + (" (native fa_group_reduce)" if timer.natives else " (torch.distributed)")
+                                       + f" in {args.chunks} chunks"
                                        + (f", local partials on {args.cu_mask} CUs" if args.cu_mask else "")
                                        if world > 1 else ""),
                        "kernel_variant": args.variant, "layout": args.layout},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                         "traffic": pmc_traffic(wl["name"]),
-                         "kernel_avg_ms": round(kernel_ms, 4) if kernel_ms else None,
-                         "measured_read_ceiling": measured_ceiling(),
-                         "algorithmic_bytes_per_launch": int(launch_bytes) if launch_bytes else None},
+            "roofline": roofline_block(wl, world, value, unit, achieved, kernel_ms, launch_bytes),
             "cpu_baseline": cpu,
             "parity": parity,
         }
@@ -1495,9 +1690,11 @@ def main():
             if wl.get("extra", {}).get("b2b_ms") is not None:  # all K updates arriving at once
                 line["latency_ms"]["all_arrive_at_once"] = wl["extra"]["b2b_ms"]
         print(json.dumps(line), flush=True)
+    stage("teardown")
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()
+    stage.done()
 
 
 if __name__ == "__main__":

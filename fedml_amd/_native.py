@@ -18,13 +18,13 @@ import torch  # noqa: F401  (load torch's HIP runtime before libfedagg.so)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfedagg.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 TILE_BYTES = 4096  # FA_TILE_BYTES
 
 F32, BF16, F16, F64, I64 = 0, 1, 2, 3, 4
 MUL_W, MUL_N_DIV_N, SUM = 0, 1, 2
 
-FA_OK, FA_ERR_INVALID, FA_ERR_DTYPE, FA_ERR_HIP, FA_ERR_NOMEM = 0, -1, -2, -3, -4
+FA_OK, FA_ERR_INVALID, FA_ERR_DTYPE, FA_ERR_HIP, FA_ERR_NOMEM, FA_ERR_COMM = 0, -1, -2, -3, -4, -5
 
 EXPORTED_SYMBOLS = (
     "fa_abi_version", "fa_ctx_create", "fa_ctx_destroy", "fa_weighted_sum",
@@ -36,7 +36,26 @@ EXPORTED_SYMBOLS = (
     "fa_finite_sum", "fa_finite_sum_tiled", "fa_finite_quantize", "fa_lcc_decode",
     # include/fedagg_robust.h
     "fa_coord_median", "fa_pairwise_sqdist", "fa_pairwise_sqdist_rt", "fa_pairwise_sqdist_scratch_bytes",
+    # include/fedagg_comm.h
+    "fa_comm_unique_id", "fa_comm_init", "fa_comm_wrap", "fa_comm_destroy", "fa_comm_size", "fa_local_out_dtype",
+    "fa_group_plan", "fa_group_reduce_scratch_bytes", "fa_group_reduce", "fa_comm_set_timing", "fa_comm_local_time",
+    "fa_comm_last_op",
 )
+
+# enum fa_exchange / fa_local_kind (include/fedagg_comm.h)
+XCHG_ORDERED, XCHG_ORDERED_ALL, XCHG_REDUCE, XCHG_ALL_REDUCE, XCHG_REDUCE_SCATTER = 0, 1, 2, 3, 4
+LOCAL_FLAT, LOCAL_TILED, LOCAL_GROUPED, LOCAL_GROUPED_TILED, LOCAL_PARTIAL = 0, 1, 2, 3, 4
+COMM_ID_BYTES = 128
+
+
+class LocalStep(ctypes.Structure):
+    """struct fa_local_step (include/fedagg_comm.h)."""
+    _fields_ = [("kind", ctypes.c_int32), ("dtype", ctypes.c_int32), ("mode", ctypes.c_int32), ("k", ctypes.c_int32),
+                ("d_in", ctypes.POINTER(ctypes.c_void_p)), ("tile_stride", ctypes.c_int64),
+                ("coef", ctypes.POINTER(ctypes.c_double)), ("divisor", ctypes.c_double),
+                ("num_groups", ctypes.c_int32), ("group_mode", ctypes.c_int32),
+                ("group_ptr", ctypes.POINTER(ctypes.c_int32)), ("group_coef", ctypes.POINTER(ctypes.c_double)),
+                ("group_divisor", ctypes.POINTER(ctypes.c_double)), ("d_partial", ctypes.c_void_p)]
 
 MOD_FIRST, MOD_EACH, MOD_END, REAL_F64 = 1, 2, 4, 8  # enum fa_finite_flags
 
@@ -145,6 +164,34 @@ def _declare(L):
                              _P_vp, _vp, _P_vp, _P_vp, _vp, _vp]
     L.fa_promote_add.restype = ctypes.c_int
     L.fa_promote_add.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _vp, _vp, _vp, _vp]
+    _P_ls = ctypes.POINTER(LocalStep)
+    L.fa_comm_unique_id.restype = ctypes.c_int
+    L.fa_comm_unique_id.argtypes = [_vp, ctypes.c_int64]
+    L.fa_comm_init.restype = ctypes.c_int
+    L.fa_comm_init.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, ctypes.POINTER(ctypes.c_void_p)]
+    L.fa_comm_wrap.restype = ctypes.c_int
+    L.fa_comm_wrap.argtypes = [ctypes.c_int, _vp, _vp, ctypes.POINTER(ctypes.c_void_p)]
+    L.fa_comm_destroy.restype = ctypes.c_int
+    L.fa_comm_destroy.argtypes = [_vp]
+    L.fa_comm_size.restype = ctypes.c_int
+    L.fa_comm_size.argtypes = [_vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]
+    L.fa_local_out_dtype.restype = ctypes.c_int
+    L.fa_local_out_dtype.argtypes = [ctypes.c_int, ctypes.c_int]
+    L.fa_group_plan.restype = ctypes.c_int
+    L.fa_group_plan.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                ctypes.c_int32, _P_i64, _P_i64, _P_i64, _P_i64]
+    L.fa_group_reduce_scratch_bytes.restype = ctypes.c_int
+    L.fa_group_reduce_scratch_bytes.argtypes = [_vp, ctypes.c_int, _P_ls, ctypes.c_int64, ctypes.c_int32,
+                                                ctypes.c_int32, ctypes.c_int32, _P_i64]
+    L.fa_group_reduce.restype = ctypes.c_int
+    L.fa_group_reduce.argtypes = [_vp, _vp, ctypes.c_int, _P_ls, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                  ctypes.c_int32, _vp, _vp, ctypes.c_int64, _vp]
+    L.fa_comm_set_timing.restype = ctypes.c_int
+    L.fa_comm_set_timing.argtypes = [_vp, ctypes.c_int]
+    L.fa_comm_local_time.restype = ctypes.c_int
+    L.fa_comm_local_time.argtypes = [_vp, ctypes.c_int, _P_d, _P_i64]
+    L.fa_comm_last_op.restype = ctypes.c_int
+    L.fa_comm_last_op.argtypes = [_vp, ctypes.c_char_p, ctypes.c_int64]
     L.fa_strerror.restype = ctypes.c_char_p
     L.fa_strerror.argtypes = [ctypes.c_int]
     L.fa_last_error.restype = ctypes.c_char_p

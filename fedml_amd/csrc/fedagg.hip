@@ -1102,6 +1102,7 @@ const char* fa_strerror(int code) {
     case FA_ERR_DTYPE: return "FA_ERR_DTYPE";
     case FA_ERR_HIP: return "FA_ERR_HIP";
     case FA_ERR_NOMEM: return "FA_ERR_NOMEM";
+    case FA_ERR_COMM: return "FA_ERR_COMM";
     default: return "FA_ERR_UNKNOWN";
   }
 }

@@ -52,7 +52,15 @@ from ..engine import MUL_N_DIV_N, MUL_W, SUM
 LocalSum = Callable[..., torch.Tensor]  # (xs, mode, coef, divisor, out) -> out
 
 COLLECTIVES = ("ordered", "ordered_all", "reduce", "all_reduce", "reduce_scatter")
+NATIVE_ALIGN = 256  # chunk / piece granularity (elements) of the native path on flat inputs
 _SECOND_GROUP: dict = {}  # process group -> a second communicator over the same ranks ("ordered")
+_LAST = [None]            # the last exchange operation this process issued (hang diagnostics)
+
+
+def last_issued():
+    """Name of the last exchange operation issued by this process ("chunk c/C <op>"), or None --
+    what a watchdog prints when a collective never completes."""
+    return _LAST[0]
 
 
 def _engine_local_sum(xs, mode, coef, divisor, out):
@@ -85,7 +93,8 @@ class GroupReducer:
 
     def __init__(self, group=None, collective: str = "ordered", dst: int = 0, chunks: int = 8,
                  local_sum: Optional[LocalSum] = None, local_grouped: Optional[Callable] = None,
-                 stream: Optional[torch.cuda.Stream] = None, combine_sum: Optional[LocalSum] = None):
+                 stream: Optional[torch.cuda.Stream] = None, combine_sum: Optional[LocalSum] = None,
+                 native: Optional[bool] = None, timing: bool = False):
         if collective not in COLLECTIVES:
             raise ValueError(f"unknown collective {collective!r}")
         self.group = group
@@ -107,7 +116,19 @@ class GroupReducer:
         # stream (AggEngine.cu_masked_stream) that leaves CUs free for RCCL's kernels
         self.stream = stream
         self._group2 = None
-        if collective in ("ordered", "ordered_all") and self.world > 1:
+        # native (the product path on GPUs): the whole step is ONE fa_group_reduce call of the C ABI
+        # (include/fedagg_comm.h) over libfedagg's own RCCL communicators; the torch.distributed form
+        # below is the same algorithm for CPU (gloo) tests and the one-GPU rehearsal, or with an
+        # injected local reduction
+        if native is None:
+            native = (local_sum is None and combine_sum is None and local_grouped is None and self.world > 1
+                      and dist.get_backend(group) == "nccl")
+        self.native = None
+        if native:
+            from .native_exchange import NativeExchange
+            self.native = NativeExchange(_native_comm(group), collective, dst, chunks)
+            self.native.comm.set_timing(timing)
+        elif collective in ("ordered", "ordered_all") and self.world > 1:
             self._group2 = _second_group(group)
         self._bufs: dict = {}
         self.owned = None  # "ordered": (lo, hi) pieces of the global model this rank summed, last call
@@ -117,6 +138,9 @@ class GroupReducer:
         """Global FedAvg of all ranks' clients; ``weights`` = this rank's GLOBAL w_i = n_i / N."""
         flat = [x.reshape(-1) for x in xs]
         w = list(weights)
+        if self.native is not None:
+            from .native_exchange import NativeExchange
+            return self._native_run(NativeExchange.flat(flat, MUL_W, w), flat[0].numel(), NATIVE_ALIGN, out)
         return self._run(flat, lambda part, a, b: self.local_sum([x[a:b] for x in flat], MUL_W, w, 1.0, part),
                          out, mode=MUL_W)
 
@@ -140,6 +164,10 @@ class GroupReducer:
         if len(flat) != gptr[-1]:
             raise ValueError("hierarchical_groups: client count does not match the groups")
         T = float(total)
+        if self.native is not None:
+            from .native_exchange import NativeExchange
+            return self._native_run(NativeExchange.grouped(flat, MUL_W, w, 1.0, gptr, MUL_N_DIV_N, gn, [T] * len(gn)),
+                                    flat[0].numel(), NATIVE_ALIGN, out)
 
         def local(part, a, b):
             sl = [x[a:b] for x in flat]
@@ -166,6 +194,9 @@ class GroupReducer:
         E = buf.shape[2]
         w = list(weights)
         rows = list(rows)
+        if self.native is not None:
+            from .native_exchange import NativeExchange
+            return self._native_run(NativeExchange.tiled(buf, rows, MUL_W, w), n, E, out)
 
         def local(part, a, b):
             if a % E:
@@ -182,10 +213,36 @@ class GroupReducer:
     def sum(self, xs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None):
         """Plain global sum (FedAvg_seq / FedDyn branches)."""
         flat = [x.reshape(-1) for x in xs]
+        if self.native is not None:
+            from .native_exchange import NativeExchange
+            return self._native_run(NativeExchange.flat(flat, SUM, None), flat[0].numel(), NATIVE_ALIGN, out)
         return self._run(flat, lambda part, a, b: self.local_sum([x[a:b] for x in flat], SUM, None, 1.0, part),
                          out, mode=SUM)
 
+    def local_time(self, reset: bool = True):
+        """Native path with ``timing=True``: (summed ms, launches) of the local-step kernels."""
+        if self.native is None:
+            raise RuntimeError("local_time: only the native exchange records local-step timing")
+        return self.native.comm.local_time(reset)
+
     # -------------------------------------------------------------- implementation
+    def _native_run(self, desc, n, align, out):
+        dev = torch.device("cuda", self.native.comm.device)
+        _LAST[0] = f"native fa_group_reduce ({self.collective}, {n} elements)"
+        if self.stream is None:
+            res = self.native.run(desc, n, align, out)
+        else:
+            caller = torch.cuda.current_stream(dev)
+            self.stream.wait_stream(caller)
+            if out is not None:
+                out.record_stream(self.stream)
+            res = self.native.run(desc, n, align, out, stream=self.stream)
+            caller.wait_stream(self.stream)
+            if res is not out:
+                res.record_stream(caller)
+        self.owned = self.native.owned(n, align) or None
+        return res
+
     def _run(self, flat, local, out, mode):
         return self._run_n(flat[0].numel(), flat[0].dtype, flat[0].device, local, out, mode)
 
@@ -224,6 +281,7 @@ class GroupReducer:
         for a, b in chunk_bounds(n, self.chunks, align):
             part = out[a:b]
             local(part, a, b)
+            _LAST[0] = f"{self.collective} of [{a}, {b}) of {n}"
             if self.collective == "reduce":
                 works.append(dist.reduce(part, dst=self.dst, op=dist.ReduceOp.SUM, group=self.group,
                                          async_op=True))
@@ -258,6 +316,7 @@ class GroupReducer:
             else:
                 for dstv, lo, hi in pieces:
                     local(dstv, lo, hi)
+            _LAST[0] = f"reduce_scatter of shard range [{a}, {b}) of {S}"
             works.append(dist.reduce_scatter_tensor(shard[a:b], stage[base: base + self.world * L],
                                                     op=dist.ReduceOp.SUM, group=self.group, async_op=True))
         for w in works:
@@ -295,6 +354,7 @@ class GroupReducer:
                 r0 = world * o0
                 self.combine_sum([recv[r0 + r * L: r0 + (r + 1) * L] for r in range(world)], SUM, None, 1.0,
                                  own[o0:o0 + L])
+            _LAST[0] = f"ordered chunk {c + 1}/{len(plan)}: delivery (second communicator)"
             if not to_all:  # deliver the summed pieces owner -> dst, consecutive in out[a:b]
                 osz = list(sizes) if me == dst else [0] * world
                 isz = [L if r == dst else 0 for r in range(world)]
@@ -318,6 +378,7 @@ class GroupReducer:
         for c, (a, b, sizes, starts) in enumerate(plan):
             local(send[a:b], a, b)
             L, o0 = sizes[me], offs[c]
+            _LAST[0] = f"ordered chunk {c + 1}/{len(plan)}: all_to_all to the owners"
             first.append(dist.all_to_all_single(recv[world * o0: world * (o0 + L)], send[a:b], [L] * world,
                                                 list(sizes), group=self.group, async_op=True))
             if c >= 1:  # software pipeline: chunk c-1's owner sum queues behind chunk c's partial
@@ -329,11 +390,22 @@ class GroupReducer:
         return out
 
 
+def _native_comm(group):
+    """This process's NativeComm over ``group`` (created collectively, once per group)."""
+    from .native_exchange import NativeComm
+    key = ("native", group if group is not None else dist.group.WORLD)
+    c = _SECOND_GROUP.get(key)
+    if c is None:
+        c = _SECOND_GROUP[key] = NativeComm(group)
+    return c
+
+
 def _second_group(group):
     """A second communicator over ``group``'s ranks (created collectively, once per group)."""
     key = group if group is not None else dist.group.WORLD  # a re-created default group is a new key
     g2 = _SECOND_GROUP.get(key)
     if g2 is None:
         ranks = dist.get_process_group_ranks(group) if group is not None else list(range(dist.get_world_size()))
-        g2 = _SECOND_GROUP[key] = dist.new_group(ranks)
+        # only the group's members enter (a reducer built over a subgroup must not need the others)
+        g2 = _SECOND_GROUP[key] = dist.new_group(ranks, use_local_synchronization=True)
     return g2

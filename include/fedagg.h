@@ -74,10 +74,11 @@ enum fa_status {
     FA_ERR_INVALID = -1,  /* null pointer, k <= 0, n < 0, bad CSR, ...   */
     FA_ERR_DTYPE = -2,    /* dtype/mode combination not supported          */
     FA_ERR_HIP = -3,      /* a HIP runtime call failed (see fa_last_error) */
-    FA_ERR_NOMEM = -4     /* staging allocation failed                     */
+    FA_ERR_NOMEM = -4,    /* staging allocation failed                     */
+    FA_ERR_COMM = -5      /* an RCCL call failed (fedagg_comm.h)           */
 };
 
-#define FA_ABI_VERSION 2
+#define FA_ABI_VERSION 3
 
 /* ABI version of the loaded library (== FA_ABI_VERSION of the header it was built with). */
 int fa_abi_version(void);

@@ -101,3 +101,87 @@ def test_cu_masked_stream_engine(pg):
         out = eng.weighted_sum(ys, 2)
     s.synchronize()
     assert _bits(out, orc.weighted_sum(xs, 2))
+
+
+# ----------------------------------------------------------------------------- native exchange (C ABI)
+@pytest.mark.parametrize("collective", ["ordered", "ordered_all", "reduce", "all_reduce", "reduce_scatter"])
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_native_group_reduce_flat_and_grouped(pg, collective, chunks):
+    """fa_group_reduce (include/fedagg_comm.h) over libfedagg's own RCCL communicator at world 1:
+    the chunked local step through the C ABI, the RCCL collectives (reduce / all_reduce /
+    reduce_scatter run through RCCL even at world 1) and the stream ordering, vs the oracle."""
+    from oracle import orc
+    from fedml_amd.distributed.group_reduce import GroupReducer
+    g = torch.Generator().manual_seed(11 + chunks)
+    K, P = 7, 250_003
+    xs = [torch.randn(P, generator=g) for _ in range(K)]
+    counts = [int(v) for v in torch.randint(50, 601, (K,), generator=g)]
+    N = sum(counts)
+    red = GroupReducer(collective=collective, chunks=chunks, native=True, timing=True)
+    assert red.native is not None
+    got = red.fedavg([x.cuda() for x in xs], [c / N for c in counts])
+    torch.cuda.synchronize()
+    exp = orc.weighted_sum(xs, 0, [c / N for c in counts])
+    assert _bits(got[:P], exp)
+    got = red.hierarchical([x.cuda() for x in xs], counts, 3 * N)
+    torch.cuda.synchronize()
+    G = orc.weighted_sum(xs, 0, [c / N for c in counts])
+    assert _bits(got[:P], orc.weighted_sum([G], 1, [N], float(3 * N)))
+    ms, launches = red.local_time()
+    assert launches >= 2 and ms > 0
+
+
+@pytest.mark.parametrize("collective", ["ordered", "reduce", "reduce_scatter"])
+def test_native_group_reduce_tiled_cu_masked(pg, collective):
+    """The bench's N > 1 step through the C ABI: tiled arena partials on a CU-masked stream."""
+    from oracle import orc
+    from fedml_amd.arena import ArenaLayout, ClientArena
+    from fedml_amd.distributed.group_reduce import GroupReducer
+    from fedml_amd.engine import get_engine
+    eng = get_engine(0)
+    g = torch.Generator().manual_seed(5)
+    K, P = 6, 1024 * 37 + 11
+    xs = [torch.randn(P, generator=g) for _ in range(K)]
+    counts = [int(v) for v in torch.randint(50, 601, (K,), generator=g)]
+    w = [c / sum(counts) for c in counts]
+    arena = ClientArena(ArenaLayout([("w", (P,), torch.float32)]), K, device="cuda:0", tiled=True)
+    for i, x in enumerate(xs):
+        arena.write(i, {"w": x.cuda()})
+    red = GroupReducer(collective=collective, chunks=3, stream=eng.cu_masked_stream(128), native=True)
+    got = red.fedavg_tiled(eng, arena.bufs[torch.float32], list(range(K)), w, P).clone()
+    torch.cuda.synchronize()
+    assert _bits(got[:P], orc.weighted_sum(xs, 0, w))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.int64])
+def test_native_group_reduce_dtypes(pg, dtype):
+    """bf16 partials (per-op bf16 rounding) and int64 SUM (two's-complement wrap) through RCCL."""
+    from oracle import orc
+    from fedml_amd.distributed.group_reduce import GroupReducer
+    g = torch.Generator().manual_seed(9)
+    K, P = 5, 70_001
+    if dtype == torch.int64:
+        xs = [torch.randint(-2**62, 2**62, (P,), generator=g, dtype=torch.int64) for _ in range(K)]
+    else:
+        xs = [torch.randn(P, generator=g).to(dtype) for _ in range(K)]
+    red = GroupReducer(collective="all_reduce", chunks=3, native=True)
+    if dtype == torch.int64:
+        got = red.sum([x.cuda() for x in xs])
+        exp = orc.weighted_sum(xs, 2)
+        torch.cuda.synchronize()
+        assert torch.equal(got.cpu(), exp)
+    else:
+        counts = [int(v) for v in torch.randint(50, 601, (K,), generator=g)]
+        w = [c / sum(counts) for c in counts]
+        got = red.fedavg([x.cuda() for x in xs], w)
+        torch.cuda.synchronize()
+        exp = orc.weighted_sum(xs, 0, w)
+        assert torch.equal(got.cpu().view(torch.int16), exp.view(torch.int16))
+
+
+def test_native_comm_last_op_and_plan(pg):
+    from fedml_amd.distributed.group_reduce import GroupReducer
+    red = GroupReducer(collective="reduce", chunks=2, native=True)
+    red.fedavg([torch.ones(5000, device="cuda")], [1.0])
+    torch.cuda.synchronize()
+    assert "ncclReduce" in red.native.comm.last_op()

@@ -12,7 +12,7 @@ import torch
 from conftest import ROOT, gpu_available
 from fedml_amd import _native as N
 
-HDRS = [os.path.join(ROOT, "include", h) for h in ("fedagg.h", "fedagg_finite.h", "fedagg_robust.h")]
+HDRS = [os.path.join(ROOT, "include", h) for h in ("fedagg.h", "fedagg_finite.h", "fedagg_robust.h", "fedagg_comm.h")]
 
 
 def declared_functions():
@@ -43,7 +43,7 @@ def test_library_is_a_gfx950_code_object():
 def test_strerror_names():
     L = N.lib()
     for code, name in [(0, b"FA_OK"), (-1, b"FA_ERR_INVALID"), (-2, b"FA_ERR_DTYPE"), (-3, b"FA_ERR_HIP"),
-                       (-4, b"FA_ERR_NOMEM"), (-99, b"FA_ERR_UNKNOWN")]:
+                       (-4, b"FA_ERR_NOMEM"), (-5, b"FA_ERR_COMM"), (-99, b"FA_ERR_UNKNOWN")]:
         assert L.fa_strerror(code) == name
 
 
@@ -92,3 +92,60 @@ def test_product_does_not_import_oracle():
                 src = open(os.path.join(dp, f)).read()
                 for bad in ("from oracle", "import oracle", "liborc", "torch_port"):
                     assert bad not in src, (f, bad)
+
+
+def test_library_links_rccl():
+    """The multi-GPU entry (include/fedagg_comm.h) calls RCCL directly: librccl is a dependency of the
+    library (resolved to the RCCL torch already loaded, same soname)."""
+    import subprocess
+    out = subprocess.run(["readelf", "-d", N.LIB_PATH], capture_output=True, text=True).stdout
+    assert "librccl.so" in out
+
+
+def test_comm_entries_reject_invalid_arguments_without_device():
+    L = N.lib()
+    assert L.fa_comm_unique_id(None, 128) == N.FA_ERR_INVALID
+    assert L.fa_comm_init(0, 2, 0, None, None) == N.FA_ERR_INVALID
+    h = ctypes.c_void_p()
+    assert L.fa_comm_init(0, 2, 5, (ctypes.c_uint8 * 128)(), ctypes.byref(h)) == N.FA_ERR_INVALID  # rank >= world
+    assert L.fa_comm_wrap(0, None, None, ctypes.byref(h)) == N.FA_ERR_INVALID
+    assert L.fa_comm_size(None, None, None) == N.FA_ERR_INVALID
+    assert L.fa_comm_destroy(None) == N.FA_OK
+    st = N.LocalStep(kind=N.LOCAL_FLAT, dtype=N.F32, mode=N.MUL_W, k=0)
+    assert L.fa_group_reduce(None, None, 0, ctypes.byref(st), 10, 2, 1, 0, None, None, 0, None) == N.FA_ERR_INVALID
+    need = ctypes.c_int64()
+    assert L.fa_group_reduce_scratch_bytes(None, 0, ctypes.byref(st), 10, 2, 1, 0, ctypes.byref(need)) == \
+        N.FA_ERR_INVALID
+    assert L.fa_comm_set_timing(None, 1) == N.FA_ERR_INVALID
+    assert L.fa_comm_local_time(None, 1, None, None) == N.FA_ERR_INVALID
+    assert L.fa_local_out_dtype(N.I64, N.MUL_W) == N.F32 and L.fa_local_out_dtype(N.I64, N.SUM) == N.I64
+    assert L.fa_local_out_dtype(N.BF16, N.MUL_W) == N.BF16
+    assert L.fa_group_plan(-1, 1, 1, 2, 0, 4, None, None, None, None) == N.FA_ERR_INVALID
+
+
+def test_local_step_struct_layout():
+    """ctypes' fa_local_step matches the C struct's field offsets (x86-64 SysV)."""
+    f = {name: getattr(N.LocalStep, name).offset for name, _ in N.LocalStep._fields_}
+    assert (f["d_in"], f["tile_stride"], f["coef"], f["divisor"], f["num_groups"], f["group_ptr"],
+            f["group_divisor"], f["d_partial"]) == (16, 24, 32, 40, 48, 56, 72, 80)
+    assert ctypes.sizeof(N.LocalStep) == 88
+
+
+@pytest.mark.parametrize("n,chunks,align,world,root", [
+    (125_000_000, 8, 1024, 8, 0), (125_000_000, 8, 1024, 2, 0), (1000, 3, 1, 4, 2), (7, 8, 1, 3, 0),
+    (0, 4, 256, 4, 0), (4099, 5, 256, 5, 4), (1 << 20, 1, 1024, 1, 0), (10, 64, 4, 8, 7)])
+def test_native_plan_matches_the_python_exchange(n, chunks, align, world, root):
+    """fa_group_plan (the C pipeline's chunks and owner pieces) is the plan of group_reduce.py's
+    torch.distributed form (the one the gloo tests run), so both deliver the same pieces."""
+    from fedml_amd.distributed.group_reduce import chunk_bounds, split_bounds
+    from fedml_amd.distributed.native_exchange import group_plan
+    plan = group_plan(n, chunks, align, world, root)
+    exp = chunk_bounds(n, chunks, align)
+    assert [(lo, hi) for lo, hi, _ in plan] == exp
+    owners = [r for r in range(world) if r != root]
+    for (a, b, pieces) in plan:
+        assert pieces[root] == (a, 0) or world == 1
+        if world == 1:
+            continue
+        for o, (lo, hi) in zip(owners, split_bounds(b - a, len(owners), align)):
+            assert pieces[o] == (a + lo, hi - lo)
