@@ -59,8 +59,15 @@ _LAST = [None]            # the last exchange operation this process issued (han
 
 def last_issued():
     """Name of the last exchange operation issued by this process ("chunk c/C <op>"), or None --
-    what a watchdog prints when a collective never completes."""
-    return _LAST[0]
+    what a watchdog prints when a collective never completes.  For the native exchange this is
+    the last RCCL operation libfedagg issued (fa_comm_last_op)."""
+    ops = [_LAST[0]] if _LAST[0] else []
+    for key, c in list(_SECOND_GROUP.items()):
+        if isinstance(key, tuple) and key[0] == "native":
+            op = c.last_op()
+            if op:
+                ops.append(f"libfedagg: {op}")
+    return "; ".join(ops) or None
 
 
 def _engine_local_sum(xs, mode, coef, divisor, out):
