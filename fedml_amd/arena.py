@@ -102,6 +102,11 @@ TILE_BYTES = 4096  # FA_TILE_BYTES (include/fedagg.h)
 _ADOPTED: Dict[int, Tuple["weakref.ref", int]] = {}
 
 
+# c10::ScalarType codes (match_rows compares them with the values' scalar_type())
+_SCALAR_TYPE = {torch.uint8: 0, torch.int8: 1, torch.int16: 2, torch.int32: 3, torch.int64: 4, torch.float16: 5,
+                torch.float32: 6, torch.float64: 7, torch.bool: 11, torch.bfloat16: 15}
+
+
 def tile_elems(dt: torch.dtype) -> int:
     return TILE_BYTES // torch.empty((), dtype=dt).element_size()
 
@@ -129,6 +134,7 @@ class ClientArena:
         self._next_stage = 0
         self._pending: List[torch.cuda.Event] = []
         self._rows_adopted: Dict[int, int] = {}  # row -> id of the state_dict adopted into it
+        self._handed: Dict[int, list] = {}        # row -> weakrefs of the row views adopt() handed out
 
     @classmethod
     def for_model(cls, template_state_dict, capacity: int, device=None, **kw) -> "ClientArena":
@@ -175,6 +181,7 @@ class ClientArena:
         tensors: packed into pinned staging and sent with one H2D per dtype group)."""
         if not 0 <= i < self.capacity:
             raise IndexError(f"arena row {i} out of range [0, {self.capacity})")
+        self._detach(i)
         for k in self.layout.keys:
             dt, _, shape, _ = self.layout.where[k]
             t = state_dict[k]  # KeyError on a missing key, like the reference's per-key access
@@ -206,21 +213,41 @@ class ClientArena:
             return
         self._write_host(i, state_dict)
 
+    def _detach(self, i: int) -> None:
+        """Row i is about to be overwritten: every row view handed out by an earlier adopt(i) that is
+        still alive (a caller kept the update dict, or one of its tensors) is moved to a private copy
+        first (``t.set_(t.clone())``, on the compute stream, which the overwrite is ordered after), so
+        it keeps its values -- in the reference each update owns its tensors."""
+        refs = self._handed.pop(i, None)
+        if not refs:
+            return
+        for r in refs:
+            t = r()
+            if t is not None:
+                t.set_(t.clone())
+
     def adopt(self, i: int, state_dict) -> None:
         """On-arrival ingest (the reference moves an arriving update to the server device in place,
         cross_silo/server/fedml_aggregator.py:57-66 -> ml_engine_adapter.py:234-254): copy the update
         into row i and rebind the dict's entries to the row's device views, in place.  The compute
         stream is ordered after the copy (a stream wait, no host block), so the rebound tensors
         are safe to use on it at once.  Later aggregations over adopted dicts are recognised by
-        ``resident_rows`` and run over the arena rows."""
+        ``resident_rows`` and run over the arena rows.
+
+        Ownership: the row is reused by a later adopt/write of row i (the round drivers alternate
+        rows by round); if the dict adopted now, or any of its tensors, is still referenced then,
+        those tensors are first moved to private copies (``_detach``), so a caller that keeps a
+        round's update never sees another round's values."""
         if self.tiled:
             raise TypeError("adopt: a tiled arena's rows are not tensor views (use a client-major arena)")
         if len(state_dict) != len(self.layout.keys) or any(k not in self.layout.where for k in state_dict):
             raise TypeError("adopt: the update's keys differ from the arena layout")
         self.write(i, state_dict)
         self._wait_ingest()
-        for k, v in self.slot(i).items():
+        views = self.slot(i)
+        for k, v in views.items():
             state_dict[k] = v
+        self._handed[i] = [weakref.ref(v) for v in views.values()]
         old = self._rows_adopted.get(i)  # the dict this row held before: no longer resident here
         if old is not None and _ADOPTED.get(old, (None, -1))[1] == i:
             _ADOPTED.pop(old, None)
@@ -228,16 +255,20 @@ class ClientArena:
         _ADOPTED[id(state_dict)] = (weakref.ref(self), i)
 
     def _ptr_table(self):
-        """Per key (layout order): device address of row 0's tensor and the row stride in bytes."""
+        """Per key (layout order): device address of row 0's tensor, the row stride in bytes, and
+        the view's (scalar type, ndim, sizes) record with its offsets (match_rows)."""
         t = getattr(self, "_ptr_tab", None)
         if t is None:
-            base, stride = [], []
+            base, stride, meta, moff = [], [], [], []
             for k in self.layout.keys:
-                dt, off, _, _ = self.layout.where[k]
+                dt, off, shape, _ = self.layout.where[k]
                 b = self.bufs[dt]
                 base.append(b.data_ptr() + off * b.element_size())
                 stride.append(b.stride(0) * b.element_size())
-            t = self._ptr_tab = (torch.tensor(base, dtype=torch.int64), torch.tensor(stride, dtype=torch.int64))
+                moff.append(len(meta))
+                meta += [_SCALAR_TYPE[dt], len(shape)] + [int(s) for s in shape]
+            t = self._ptr_tab = (torch.tensor(base, dtype=torch.int64), torch.tensor(stride, dtype=torch.int64),
+                                 torch.tensor(meta, dtype=torch.int64), torch.tensor(moff, dtype=torch.int64))
         return t
 
     def _stage_slot(self):
@@ -417,8 +448,8 @@ class ClientArena:
 def resident_rows(dicts, keys=None):
     """(arena, rows) when every dict of ``dicts`` was adopted by ONE client-major arena and still
     holds exactly that arena's row views, keys in the layout's order (checked in C++ by
-    fedml_amd._host.match_rows: the key order, each value's address, contiguity; dtype and shape
-    follow from the address being the arena's view, which adopt() created); else None."""
+    fedml_amd._host.match_rows: the key order, each value's address, contiguity, dtype and shape);
+    else None."""
     first = _ADOPTED.get(id(dicts[0]))
     if first is None:
         return None
@@ -431,7 +462,7 @@ def resident_rows(dicts, keys=None):
         if e is None or e[0]() is not arena:
             return None
         rows.append(e[1])
-    base, stride = arena._ptr_table()
-    if not _host.match_rows(list(dicts), arena.layout.keys, base, stride, rows):
+    base, stride, meta, moff = arena._ptr_table()
+    if not _host.match_rows(list(dicts), arena.layout.keys, base, stride, rows, meta, moff):
         return None
     return arena, rows

@@ -285,14 +285,23 @@ void pack_range(torch::Tensor src, torch::Tensor dst_off, torch::Tensor nbytes, 
 // base[t] + rows[i] * stride[t], contiguous?  The arena-resident fast path of a state_dict
 // aggregation (fedml_amd/arena.py resident_rows) needs only this, not gather()'s full validation
 // and tables: one pass, no allocation, early exit (~10 ns per tensor).
-bool match_rows(py::list dicts, py::list keys, torch::Tensor base, torch::Tensor stride, py::list rows) {
+//
+// meta: per key t, at meta[moff[t]]: the layout's scalar type, ndim, then the sizes -- a value that
+// sits at the right address but was re-viewed with another dtype or shape (x.view(torch.int32),
+// x.view(s2)) is not the arena's view, and the pointer-table path handles it.
+bool match_rows(py::list dicts, py::list keys, torch::Tensor base, torch::Tensor stride, py::list rows,
+                torch::Tensor meta, torch::Tensor moff) {
   const int64_t K = (int64_t)py::len(dicts);
   const int64_t T = (int64_t)py::len(keys);
   TORCH_CHECK(base.dtype() == torch::kInt64 && stride.dtype() == torch::kInt64 && base.numel() == T &&
               stride.numel() == T && base.is_contiguous() && stride.is_contiguous(), "match_rows: tables");
+  TORCH_CHECK(meta.dtype() == torch::kInt64 && moff.dtype() == torch::kInt64 && moff.numel() == T &&
+              meta.is_contiguous() && moff.is_contiguous(), "match_rows: meta tables");
   if ((int64_t)py::len(rows) != K) return false;
   const int64_t* B = base.data_ptr<int64_t>();
   const int64_t* S = stride.data_ptr<int64_t>();
+  const int64_t* M = meta.data_ptr<int64_t>();
+  const int64_t* MO = moff.data_ptr<int64_t>();
   for (int64_t i = 0; i < K; ++i) {
     PyObject* d = PyList_GET_ITEM(dicts.ptr(), i);
     if (!PyDict_Check(d) || PyDict_GET_SIZE(d) != T) return false;
@@ -311,6 +320,10 @@ bool match_rows(py::list dicts, py::list keys, torch::Tensor base, torch::Tensor
       if (!THPVariable_Check(v)) return false;
       const at::Tensor& x = THPVariable_Unpack(v);
       if ((int64_t)x.data_ptr() != B[t] + row * S[t] || !x.is_contiguous()) return false;
+      const int64_t* m = M + MO[t];
+      if ((int64_t)x.scalar_type() != m[0] || (int64_t)x.dim() != m[1]) return false;
+      for (int64_t a = 0; a < m[1]; ++a)
+        if (x.size(a) != m[2 + a]) return false;
     }
   }
   return true;

@@ -13,9 +13,15 @@ result's D2H remain after the last arrival.
 Rows are double-buffered by round parity, so round r+1's updates can be ingested while round r's
 result is still being read.  ``to_host`` copies the aggregated model into pinned buffers (also
 double-buffered) that a send path can pickle or post directly (fedml_server_manager.py:217-231).
+
+Ownership: a returned result (or an adopted update) stays valid for as long as the caller holds
+it.  Buffers are recycled two rounds later only when nothing outside still references the tensors
+handed out from them; otherwise the ingest takes fresh pinned buffers (to_host) or moves the held
+row views to private copies before the row is overwritten (ClientArena._detach).
 """
 from __future__ import annotations
 
+import weakref
 from collections import OrderedDict
 from typing import Dict, Optional
 
@@ -33,6 +39,7 @@ class ArrivalIngest:
         self.parity = 0
         self._host: Dict[int, "OrderedDict[str, torch.Tensor]"] = {}
         self._flat_host: Dict[int, list] = {}  # per round parity: pinned flat buffers, one per dtype group
+        self._handed: Dict[tuple, list] = {}    # (form, parity) -> weakrefs of the result tensors returned
 
     @staticmethod
     def wants(device) -> bool:
@@ -75,13 +82,16 @@ class ArrivalIngest:
             return flat
         bufs = self._host.get(self.parity)
         if bufs is None or list(bufs.keys()) != list(averaged.keys()) or any(
-                bufs[k].shape != v.shape or bufs[k].dtype != v.dtype for k, v in averaged.items()):
+                bufs[k].shape != v.shape or bufs[k].dtype != v.dtype for k, v in averaged.items()) or \
+                _held(self._handed.get(("dict", self.parity))):
             bufs = self._host[self.parity] = OrderedDict(
                 (k, torch.empty(v.shape, dtype=v.dtype, pin_memory=True)) for k, v in averaged.items())
         for k, v in averaged.items():
             bufs[k].copy_(v, non_blocking=True)
         torch.cuda.current_stream(next(iter(averaged.values())).device).synchronize()
-        return bufs
+        out = OrderedDict((k, t.view(t.shape)) for k, t in bufs.items())  # caller-side tensor objects
+        self._handed[("dict", self.parity)] = [weakref.ref(t) for t in out.values()]
+        return out
 
 
     def _to_host_flat(self, averaged):
@@ -102,6 +112,10 @@ class ArrivalIngest:
             return None
         dev = next(iter(averaged.values())).device
         cache = self._flat_host.setdefault(self.parity, [])
+        if _held(self._handed.get(("flat", self.parity))):
+            # the caller still holds (part of) the result these buffers carried two rounds ago: leave
+            # them to it and take fresh ones (the reference returns a dict that stays valid)
+            cache = self._flat_host[self.parity] = []
         views = {}
         for gi, (dt, st, keys, offs, shapes) in enumerate(groups.values()):
             lo = min(offs)
@@ -116,7 +130,13 @@ class ArrivalIngest:
             for k, hv in zip(keys, _host.carve(host, [o - lo for o in offs], list(shapes))):
                 views[k] = hv
         torch.cuda.current_stream(dev).synchronize()
+        self._handed[("flat", self.parity)] = [weakref.ref(v) for v in views.values()]
         return OrderedDict((k, views[k]) for k in averaged.keys())
+
+
+def _held(refs) -> bool:
+    """Is any tensor of an earlier result still referenced outside the ingest?"""
+    return bool(refs) and any(r() is not None for r in refs)
 
 
 def _numel(shape) -> int:

@@ -70,7 +70,8 @@ def aggregate(dicts: Sequence[Dict[str, torch.Tensor]], mode: int, coef: Optiona
             return _aggregate_device(keys, ptrs, numel, codes, shapes, dev, len(dicts), mode, coef, divisor, engine)
         if dev == "cpu" and os.environ.get("FEDML_AMD_HOST_PATH", "packed") == "packed":
             nbytes = sum(n * _ELEM[c] for n, c in zip(numel.tolist(), codes.tolist())) * len(dicts)
-            if nbytes <= _SMALL_HOST_BYTES:
+            # the zero-copy kernel takes at most _HOST_MAX_TABLE keys and clients (fa_weighted_sum_host)
+            if nbytes <= _SMALL_HOST_BYTES and len(keys) <= _HOST_MAX_TABLE and len(dicts) <= _HOST_MAX_TABLE:
                 return _aggregate_host_small(keys, ptrs, numel, codes, shapes, len(dicts), mode, coef, divisor,
                                              engine)
             return _aggregate_host(keys, ptrs, numel, codes, shapes, len(dicts), mode, coef, divisor, engine)
@@ -94,6 +95,7 @@ def _aggregate_device(keys, ptrs, numel, codes, shapes, dev, k, mode, coef, divi
 
 _ELEM = {0: 4, 1: 2, 2: 2, 3: 8, 4: 8}  # bytes per element of each dtype code
 _SMALL_HOST_BYTES = 4 << 20             # CPU rounds up to this size: zero-copy kernel (fa_weighted_sum_host)
+_HOST_MAX_TABLE = 4096                  # fa_weighted_sum_host's limit on num_segments and on k
 
 
 def _aggregate_host_small(keys, ptrs, numel, codes, shapes, k, mode, coef, divisor, engine):

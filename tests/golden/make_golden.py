@@ -939,6 +939,17 @@ def cases_krum_half():
                    ref="core/security/defense/krum_defense.py:27-66, common/utils.py:8-27"))
 
 
+def cases_sp_sampling():
+    """The SP round driver's client sampling (simulation/sp/fedavg/fedavg_api.py:127-135), run from the
+    reference itself: the client indexes per round for several (in_total, per_round) settings."""
+    fn = extract_method("simulation/sp/fedavg/fedavg_api.py", "FedAvgAPI", "_client_sampling")
+    cases = {}
+    for total, per in ((10, 10), (10, 4), (7, 3), (100, 10), (1000, 64), (5, 9)):
+        cases[f"{total}_{per}"] = [[int(v) for v in fn(None, r, total, per)] for r in range(6)]
+    with open(os.path.join(HERE, "g20_sp_sampling.json"), "w") as fh:
+        json.dump({"ref": "simulation/sp/fedavg/fedavg_api.py:127-135", "rounds": 6, "cases": cases}, fh)
+
+
 def out2_equal(a, b):
     return all(np.array_equal(np.asarray(a[k]), np.asarray(b[k])) for k in a)
 

@@ -123,3 +123,52 @@ def test_fedavg_api_train_loop():
     exp = run_rounds(_ref_aggregate, "cuda:0", n_clients=3)
     assert_dict_bits(OrderedDict((k, v.cpu()) for k, v in got.items()),
                      OrderedDict((k, v.cpu()) for k, v in exp.items()), "FedAvgAPI.train")
+
+
+def run_rounds_sampled(aggregate, device, total, per_round, rounds=3, epochs=1, keep=None):
+    """The reference's SP loop with its client sampling (fedavg_api.py:80-84, 127-135: np.random.seed
+    (round_idx) + np.random.choice without replacement) and its aggregation on CPU copies."""
+    import numpy as np
+    torch.manual_seed(0)
+    args = types.SimpleNamespace(learning_rate=0.05, epochs=epochs, comm_round=rounds)
+    global_model = LogisticRegression().to(device)
+    trainers = [make_trainer_cls()(LogisticRegression().to(device), args) for _ in range(total)]
+    data, nums = client_data(total)
+    w_global = OrderedDict((k, v.clone()) for k, v in global_model.state_dict().items())
+    for r in range(rounds):
+        if total == per_round:
+            idx = list(range(total))
+        else:
+            np.random.seed(r)
+            idx = np.random.choice(range(total), min(per_round, total), replace=False)
+        w_locals = []
+        for i in idx:
+            t = trainers[int(i)]
+            t.set_model_params(copy.deepcopy(w_global))
+            t.train(data[int(i)], device, args)
+            w_locals.append((nums[int(i)], t.get_model_params()))
+        w_global = aggregate(w_locals)
+        if keep is not None:
+            keep.append(OrderedDict((k, v.detach().cpu().clone()) for k, v in w_global.items()))
+    return w_global
+
+
+@pytest.mark.parametrize("where", ["cuda:0", "cpu"])
+def test_fedavg_api_train_samples_like_the_reference(where):
+    """FedAvgAPI.train with client_num_per_round < client_num_in_total and no injected sampler: the
+    reference's _client_sampling picks the clients, and the global model after 3 rounds is
+    bit-identical to the reference loop's; on a CPU model the result stays on the CPU."""
+    from fedml_amd.simulation.sp.fedavg_api import FedAvgAPI
+    torch.manual_seed(0)
+    total, per_round = 7, 3
+    args = types.SimpleNamespace(learning_rate=0.05, epochs=1, comm_round=3, client_num_in_total=total,
+                                 client_num_per_round=per_round)
+    model = LogisticRegression().to(where)
+    trainers = [make_trainer_cls()(LogisticRegression().to(where), args) for _ in range(total)]
+    data, nums = client_data(total)
+    api = FedAvgAPI(args, where, model, trainers, data, nums)
+    got = api.train()
+    exp = run_rounds_sampled(_ref_aggregate, where, total, per_round)
+    assert all(v.device.type == torch.device(where).type for v in got.values())
+    assert_dict_bits(OrderedDict((k, v.cpu()) for k, v in got.items()),
+                     OrderedDict((k, v.cpu()) for k, v in exp.items()), "FedAvgAPI.train sampled")

@@ -216,3 +216,81 @@ def test_mpi_aggregator_arrival_ingest(monkeypatch):
             assert spy.n == rnd + 1
             assert all(not v.is_cuda for v in avg.values())
             assert_dict_bits(avg, expected_dicts(meta, arr)[0], f"{name} round {rnd}")
+
+
+def test_mpi_results_stay_valid_across_rounds():
+    """A caller that keeps round r's global model (the MPI aggregator returns pinned host tensors
+    the ingest double-buffers) finds it unchanged after rounds r+1 and r+2, while those rounds'
+    results are right too (reference FedAVGAggregator.py:99-116 returns a dict that stays valid)."""
+    from oracle import orc
+    from fedml_amd.simulation.mpi.fedavg_aggregator import FedAVGAggregator
+    K = 4
+    agg = FedAVGAggregator(K, device="cuda:0")
+    g = torch.Generator().manual_seed(21)
+    kept, exps = [], []
+    for rnd in range(4):
+        cl = [OrderedDict(w=torch.randn(5000, generator=g), b=torch.randn(7, generator=g)) for _ in range(K)]
+        xs = {k: [d[k].clone() for d in cl] for k in cl[0]}
+        n = [10 + 5 * i + rnd for i in range(K)]
+        for i in range(K):
+            agg.add_local_trained_result(i, cl[i], n[i])
+        assert agg.check_whether_all_receive()
+        avg = agg.aggregate()
+        exp = {k: orc.weighted_sum(xs[k], 1, n, float(sum(n))) for k in xs}
+        kept.append(avg)
+        exps.append(exp)
+        for r, (a, e) in enumerate(zip(kept, exps)):
+            for k in e:
+                assert _bits(a[k], e[k]), f"round {r}'s kept result changed at round {rnd} ({k})"
+
+
+def test_cross_silo_host_result_and_kept_updates_stay_valid():
+    """The cross-silo server: a caller keeps round r's pinned host result AND round r's adopted
+    update dicts; rounds r+1 / r+2 reuse the same rows and pinned buffers, yet the kept objects
+    keep round r's values (the held row views are moved to private copies, the held pinned buffers
+    are not recycled), and every round stays bit-exact."""
+    from oracle import orc
+    srv = _server(3)
+    g = torch.Generator().manual_seed(33)
+    kept_host, kept_upd = [], []
+    for rnd in range(3):
+        ds = [OrderedDict(a=torch.randn(3001, generator=g), n=torch.randint(0, 9, (2,), generator=g)) for _ in range(3)]
+        xs = {k: [d[k].clone() for d in ds] for k in ds[0]}
+        for i, d in enumerate(ds):
+            srv.add_local_trained_result(i, d, 10 * (i + 1))
+        assert srv.check_whether_all_receive()
+        avg, _, _ = srv.aggregate()
+        host = srv.get_global_model_params_host()
+        exp = {k: orc.weighted_sum(xs[k], MUL_W, [10 / 60, 20 / 60, 30 / 60]) for k in xs}
+        for k in exp:
+            assert _bits(avg[k].cpu(), exp[k]) and _bits(host[k], exp[k]), (rnd, k)
+        kept_host.append((host, exp))
+        kept_upd.append((ds, xs))
+    torch.cuda.synchronize()
+    for r, (h, e) in enumerate(kept_host):
+        for k in e:
+            assert _bits(h[k], e[k]), f"round {r}'s kept host result changed ({k})"
+    for r, (ds, xs) in enumerate(kept_upd):
+        for i, d in enumerate(ds):
+            for k in xs:
+                assert torch.equal(d[k].cpu(), xs[k][i]), f"round {r}'s kept update {i} changed ({k})"
+
+
+def test_arena_adopt_detaches_held_views():
+    """ClientArena.adopt into a row whose previous dict is still held: the held tensors keep their
+    values (private copies), a dropped dict costs nothing, and the arena fast path still applies
+    to the new dicts."""
+    from fedml_amd.arena import ClientArena, resident_rows
+    g = torch.Generator().manual_seed(4)
+    mk = lambda: OrderedDict(w=torch.randn(1000, generator=g).cuda(), b=torch.randn(3, generator=g).cuda())  # noqa: E731
+    d0 = mk()
+    arena = ClientArena.for_model(d0, 2, device="cuda:0")
+    arena.adopt(0, d0)
+    keep = d0["w"].clone()
+    t_held = d0["w"]
+    d1 = mk()
+    arena.adopt(0, d1)  # overwrites row 0: d0's tensors must be detached first
+    torch.cuda.synchronize()
+    assert torch.equal(t_held, keep) and torch.equal(d0["w"], keep)
+    assert d0["w"].data_ptr() != d1["w"].data_ptr()
+    assert resident_rows([d1]) is not None and resident_rows([d0]) is None

@@ -149,3 +149,21 @@ def test_native_plan_matches_the_python_exchange(n, chunks, align, world, root):
             continue
         for o, (lo, hi) in zip(owners, split_bounds(b - a, len(owners), align)):
             assert pieces[o] == (a + lo, hi - lo)
+
+
+def test_match_rows_checks_dtype_and_shape():
+    """The arena fast path's C++ check (fedml_amd._host.match_rows) accepts only the layout's own
+    views: a same-address re-view with another dtype or shape is rejected."""
+    from fedml_amd import _host
+    buf = torch.zeros(2, 16)
+    base = torch.tensor([buf.data_ptr(), buf.data_ptr() + 12 * 4], dtype=torch.int64)
+    stride = torch.tensor([16 * 4, 16 * 4], dtype=torch.int64)
+    meta = torch.tensor([6, 2, 3, 4, 6, 1, 4], dtype=torch.int64)  # float32 (3, 4); float32 (4,)
+    moff = torch.tensor([0, 4], dtype=torch.int64)
+    ok = {"w": buf[1, :12].view(3, 4), "b": buf[1, 12:16]}
+    assert _host.match_rows([ok], ["w", "b"], base, stride, [1], meta, moff)
+    assert not _host.match_rows([{"w": buf[1, :12].view(4, 3), "b": buf[1, 12:16]}], ["w", "b"], base, stride, [1],
+                                meta, moff)
+    assert not _host.match_rows([{"w": buf[1, :12].view(3, 4).view(torch.int32), "b": buf[1, 12:16]}], ["w", "b"],
+                                base, stride, [1], meta, moff)
+    assert not _host.match_rows([ok], ["w", "b"], base, stride, [0], meta, moff)
