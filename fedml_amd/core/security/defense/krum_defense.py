@@ -10,7 +10,8 @@ squaring -- float32, or the model's dtype for bfloat16 / float16 models, whose d
 reference also rounds to that dtype (``vectorize_weight`` keeps it; the device pass does the same,
 ``fa_pairwise_sqdist_rt``) -- so near-equal scores order the same way; the selection is checked
 against the reference (tests/golden/g18_*, including bf16 / f16 models).  float64 models are
-measured in float32 (differences within 1e-6 relative of the reference's float64 norms).
+measured in float64 throughout, as the reference measures them (fa_pairwise_sqdist_rt with
+FA_DTYPE_F64; g18_krum_f64_* includes a near-tie that float32 distances would order differently).
 """
 from __future__ import annotations
 
@@ -61,7 +62,8 @@ class KrumDefense(object):
         rounded to that dtype as the reference's ``v_i - v_j`` does."""
         keys = [k for k in grads[0].keys() if is_weight_param(k)]
         vdt = self.vector_dtype(grads)
-        diff_dt = vdt if vdt in (torch.bfloat16, torch.float16) else torch.float32
+        diff_dt = vdt if vdt in (torch.bfloat16, torch.float16, torch.float64) else torch.float32
+        in_dt = torch.float64 if diff_dt == torch.float64 else torch.float32
         dev = next((g[k].device for g in grads for k in keys if g[k].is_cuda), None)
         eng = get_engine(dev.index if dev is not None else None)
         segs = []
@@ -71,7 +73,7 @@ class KrumDefense(object):
                 t = g[k]
                 if t.device != eng.device:
                     t = t.to(eng.device)
-                col.append(t.to(torch.float32).contiguous().reshape(-1))
+                col.append(t.to(in_dt).contiguous().reshape(-1))
             segs.append(col)
         return eng.pairwise_sqdist(segs, diff_dtype=diff_dt).cpu().numpy()
 
@@ -79,11 +81,13 @@ class KrumDefense(object):
         D = self.pairwise_sq_distances(grads)
         num_client = len(grads)
         # the reference's compute_euclidean_distance(...).item() ** 2: the norm in the vector's dtype
-        # (computed in float, rounded to float32 / bf16 / f16; float64 models: float32 here), squared
+        # (rounded to float32 / bf16 / f16; a float64 vector's norm stays float64), squared
         vdt = self.vector_dtype(grads)
-        norms = torch.from_numpy(np.sqrt(D)).to(torch.float32)
-        if vdt in (torch.bfloat16, torch.float16):
-            norms = norms.to(vdt)
+        norms = torch.from_numpy(np.sqrt(D))
+        if vdt != torch.float64:
+            norms = norms.to(torch.float32)
+            if vdt in (torch.bfloat16, torch.float16):
+                norms = norms.to(vdt)
         norms = norms.to(torch.float64).numpy()
         krum_scores = []
         for i in range(num_client):

@@ -596,37 +596,38 @@ constexpr int kNPL = 8;       // k_pairdist_lane: coordinates of one client stag
 // loads; larger K -- k_pairdist, `rows` lanes per client reading consecutive floats, 16 elements per
 // thread (r02: K = 64 / 100 / 128: 2.59 / 3.99 / 6.58 -> 2.0 / 3.7 / 6.38 ms; at K <= 32 the
 // per-element form's extra instructions cost more than its coalescing gains).
-struct PairSplit { int kp, kpad, nb, ntiles, esplit, nthreads, rows, ce, pe, nblocks; bool lane; };
+struct PairSplit { int kp, kpad, nb, ntiles, esplit, nthreads, rows, ce, pe, nblocks, dgroups; bool lane; };
+// Tiles: 4x4 pair tiles of the STRICT upper triangle of 4-client blocks (bi < bj), one per thread and
+// coordinate slice; the pairs inside a block (6 per block) are spread over all threads as a second,
+// small phase per chunk (see k_pairdist), so no thread computes the 10 wasted slots of a diagonal tile
+// and the workgroup is a whole number of waves (r03: K = 128 took 528 threads = 9 waves with diagonal
+// tiles -> one workgroup per CU at 96 VGPRs; 496 tiles -> 512 threads, two workgroups per CU).
 PairSplit pair_split(int k) {
   PairSplit q;
   q.kp = (k + 3) & ~3;
   q.kpad = q.kp <= 64 ? 64 : q.kp <= 96 ? 96 : 128;  // k_pairdist (kp > 32)
   q.nb = q.kp / 4;
-  q.ntiles = q.nb * (q.nb + 1) / 2;
-  if (q.ntiles <= 128) {
-    q.esplit = std::min(kPE, kBlock / q.ntiles);
+  q.ntiles = q.nb * (q.nb - 1) / 2;
+  auto waves = [](int th) { return (th + 63) / 64 * 64; };
+  if (q.ntiles == 0) {
+    q.esplit = 1;
+  } else if (q.kp <= 32) {  // k_pairdist_lane: about 256 threads (r03e sweep, K = 32: 9 x 28 tiles best)
+    q.esplit = std::max(1, std::min(kPE, kBlock / q.ntiles));
   } else {
-    // chunks of >= 64 coordinates (pe grows with the staging threads per client, nthreads / kp),
-    // then the fewest threads that keep >= 90% of the last wave's lanes; no such split (K > 112):
-    // the largest chunk
-    int best = -1, best_pe = -1;
-    for (int e = 1; e * q.ntiles <= kMaxPairThreads; ++e) {
-      const int th = e * q.ntiles, pe = (th / q.kp) * kNP;
-      const bool full = (double)th / (64.0 * ((th + 63) / 64)) >= 0.9;
-      if (pe >= 64 && full) { best = e; break; }
-      if (pe > best_pe) { best_pe = pe; q.esplit = e; }
-    }
-    if (best > 0) q.esplit = best;
+    // k_pairdist: the most slices whose waves stay >= 90% full, up to 512 threads while the tiles are
+    // few (<= 128) and 1024 otherwise -- r03e sweep: K = 64 / 100 / 128 fastest at 4 / 3 / 2 slices
+    // (512 / 960 / 1024 threads: 1.56 / 3.69 / 5.18 ms vs 2.63 / 6.19 / 5.44 ms at one or two)
+    const int cap = q.ntiles <= 128 ? 512 : kMaxPairThreads;
+    q.esplit = 1;
+    for (int e = 1; waves(e * q.ntiles) <= cap; ++e)
+      if ((double)(e * q.ntiles) / waves(e * q.ntiles) >= 0.9) q.esplit = e;
   }
   // measurement override (tools/krum_split.sh sweeps): FA_PAIR_SPLIT="esplit"
   static const char* ov = getenv("FA_PAIR_SPLIT");
   const int oe = ov ? atoi(ov) : 0;
-  if (oe >= 1 && oe * q.ntiles <= kMaxPairThreads && (oe == 1 || 16 * 8 * q.ntiles <= 65536)) q.esplit = oe;
-  q.nthreads = q.ntiles * q.esplit;
-  if (q.nthreads < q.kp) {  // every client needs a staging thread (small K: more slices)
-    q.esplit = (q.kp + q.ntiles - 1) / q.ntiles;
-    q.nthreads = q.ntiles * q.esplit;
-  }
+  if (oe >= 1 && q.ntiles > 0 && waves(oe * q.ntiles) <= kMaxPairThreads) q.esplit = oe;
+  q.nthreads = std::max(64, waves(q.ntiles * q.esplit));
+  if (q.nthreads < q.kp) q.nthreads = waves(q.kp);  // every client needs a staging thread
   q.rows = q.nthreads / q.kp;
   q.lane = q.kp <= 32;
   if (q.lane) {  // k_pairdist_lane: slices of pe / esplit coordinates, not necessarily equal
@@ -635,14 +636,27 @@ PairSplit pair_split(int k) {
   } else {
     // a slice is one float32 run at most, and every element of a chunk has a staging thread
     q.ce = std::max(1, std::min(kPE, q.rows * kNPS / q.esplit));
-    // two LDS buffers of pe rows: at most 80 KB, so two workgroups share a CU
-    while (q.ce > 1 && 2 * sizeof(float) * (size_t)q.ce * q.esplit * (q.kpad + 4) > 80 * 1024) --q.ce;
+    // two LDS buffers of pe rows: at most 80 KB, so two workgroups share a CU -- or, for a workgroup of
+    // more than 512 threads (alone on its CU at <= 128 VGPRs), up to FA_PAIR_LDS_KB (default 80)
+    static const char* lk = getenv("FA_PAIR_LDS_KB");
+    const size_t cap_kb = q.nthreads > 512 && lk && atoi(lk) >= 16 && atoi(lk) <= 150 ? atoi(lk) : 80;
+    while (q.ce > 1 && 2 * sizeof(float) * (size_t)q.ce * q.esplit * (q.kpad + 4) > cap_kb * 1024) --q.ce;
     q.pe = q.ce * q.esplit;
   }
+  q.dgroups = q.nthreads / q.nb;  // threads per block in the within-block phase
   q.nblocks = 1024;  // workgroups (each writes all pair partials once)
   static const char* ob = getenv("FA_PAIR_BLOCKS");  // measurement override (tools/gpu_r02v.sh)
   if (ob && atoi(ob) >= 64 && atoi(ob) <= 16384) q.nblocks = atoi(ob);
   return q;
+}
+
+// LDS bytes a pair kernel launch needs: the two staging buffers, and in the epilogue the slice
+// reduction of the tiles (esplit > 1) and the within-block reduction (6 doubles per thread).
+size_t pair_lds_bytes(const PairSplit& q) {
+  const int stride = q.lane ? q.kp + 4 : q.kpad + 4;
+  size_t lds = 2 * sizeof(float) * (size_t)q.pe * stride;
+  if (q.esplit > 1) lds = std::max(lds, sizeof(double) * 16 * (size_t)q.ntiles);
+  return std::max(lds, sizeof(double) * 6 * (size_t)q.nthreads);
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -670,22 +684,130 @@ __device__ __forceinline__ f32x2 round_diff(f32x2 d) {
   else return d;
 }
 
+
+// tile -> (bi, bj), bi < bj: row-major over the strict upper triangle of nb blocks
+__device__ __forceinline__ void tile_blocks(int tile, int nb, int& bi, int& bj) {
+  int r = 0, rem = tile;
+  while (rem >= nb - 1 - r) { rem -= nb - 1 - r; ++r; }
+  bi = r;
+  bj = r + 1 + rem;
+}
+
+__device__ __forceinline__ int64_t pair_index(int i, int j, int k) {  // i < j
+  return (int64_t)i * k - (int64_t)i * (i + 1) / 2 + (j - i - 1);
+}
+
+// The within-block phase: thread t sums the 6 pairs (4b + i, 4b + j), i < j < 4, of block b = t % nb
+// over the chunk's coordinates e = t / nb, t / nb + dg, ... (dg = threads per block) -- one 16-byte
+// LDS read and 3 packed differences per coordinate; float32 runs, float64 across runs, as the tiles.
+template <int RT>
+struct Within {
+  f32x2 acc[3];
+  double accd[6];
+  int run;
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) acc[u] = f32x2{0.0f, 0.0f};
+#pragma unroll
+    for (int u = 0; u < 6; ++u) accd[u] = 0.0;
+    run = 0;
+  }
+  __device__ __forceinline__ void flush() {
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+      accd[2 * u] += (double)acc[u].x;
+      accd[2 * u + 1] += (double)acc[u].y;
+      acc[u] = f32x2{0.0f, 0.0f};
+    }
+    run = 0;
+  }
+  __device__ __forceinline__ void add(const float* lb, int stride, int pe, int e0, int dg, int b) {
+    for (int e = e0; e < pe; e += dg) {
+      const float4 v = *(const float4*)&lb[e * stride + 4 * b];
+      const f32x2 x = round_diff<RT>(f32x2{v.x, v.x} - f32x2{v.y, v.z});  // (0,1) (0,2)
+      const f32x2 y = round_diff<RT>(f32x2{v.x, v.y} - f32x2{v.w, v.z});  // (0,3) (1,2)
+      const f32x2 z = round_diff<RT>(f32x2{v.y, v.z} - f32x2{v.w, v.w});  // (1,3) (2,3)
+      acc[0] = __builtin_elementwise_fma(x, x, acc[0]);
+      acc[1] = __builtin_elementwise_fma(y, y, acc[1]);
+      acc[2] = __builtin_elementwise_fma(z, z, acc[2]);
+    }
+  }
+  // after each chunk: dmax = most coordinates one chunk adds (uniform)
+  __device__ __forceinline__ void step(int dmax) {
+    run += dmax;
+    if (run + dmax > kPE) flush();
+  }
+};
+
+// Epilogue of both pair kernels: the block's partials of every pair (i < j < k) into `out` -- the
+// tiles (their esplit slices added in slice order through LDS), then the within-block pairs (the dg
+// threads of a block added in thread order through LDS).  Every thread of the block calls it.
+__device__ __forceinline__ void pair_epilogue(float* lds, const double (&accd)[16], bool pact, int es, int tile,
+                                              int bi, int bj, int ntiles, int esplit, int nb, int k,
+                                              const double (&waccd)[6], bool dact, int dg, double* out) {
+  const int t = threadIdx.x;
+  double* red = (double*)lds;
+  if (esplit == 1) {
+    if (pact) {
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int i = 4 * bi + u / 4, j = 4 * bj + u % 4;
+        if (j < k) out[pair_index(i, j, k)] = accd[u];
+      }
+    }
+  } else {
+    __syncthreads();
+    for (int s = 0; s < esplit; ++s) {
+      if (pact && es == s) {
+#pragma unroll
+        for (int u = 0; u < 16; ++u) red[tile * 16 + u] = (s == 0 ? 0.0 : red[tile * 16 + u]) + accd[u];
+      }
+      __syncthreads();
+    }
+    for (int idx = t; idx < ntiles * 16; idx += (int)blockDim.x) {
+      const int u = idx % 16;
+      int r, c;
+      tile_blocks(idx / 16, nb, r, c);
+      const int i = 4 * r + u / 4, j = 4 * c + u % 4;
+      if (j < k) out[pair_index(i, j, k)] = red[idx];
+    }
+  }
+  __syncthreads();  // LDS reused for the within-block sums
+  if (dact) {
+#pragma unroll
+    for (int p = 0; p < 6; ++p) red[t * 6 + p] = waccd[p];
+  }
+  __syncthreads();
+  for (int idx = t; idx < nb * 6; idx += (int)blockDim.x) {
+    const int b = idx / 6, p = idx % 6;
+    double sum = 0.0;
+    for (int g = 0; g < dg; ++g) sum += red[(g * nb + b) * 6 + p];
+    const int i = 4 * b + (p < 3 ? 0 : p < 5 ? 1 : 2), j = 4 * b + (p < 3 ? p + 1 : p < 5 ? p - 1 : 3);
+    if (j < k) out[pair_index(i, j, k)] = sum;
+  }
+}
+
 // K <= 32 (kp <= 32): the r01 form -- a lane per client stages 8 consecutive coordinates (two 16-byte
 // loads), slices of pe / esplit coordinates (pe = rows * 8); measured faster there than the
 // strided form below (K = 16 / 32: 0.20 / 0.59 vs 0.27 / 0.65 ms)
 template <bool VEC, int RT>
-__global__ void __launch_bounds__(kMaxPairThreads) __attribute__((amdgpu_waves_per_eu(5)))
+__global__ void __launch_bounds__(kMaxPairThreads) __attribute__((amdgpu_waves_per_eu(4)))
 k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int kp,
            int64_t nchunks, int ntiles, int esplit, int pe, double* __restrict__ partial) {
   extern __shared__ float lds[];              // [2][pe][kp + 4]
   const int stride = kp + 4;
   const int nb = kp / 4;
-  const int t = threadIdx.x;                     // blockDim.x == ntiles * esplit
-  const int es = t / ntiles;                     // coordinate slice
-  const int tile = t % ntiles;
-  int bi = 0, rem = tile;  // tile -> (bi, bj), bi <= bj, row-major upper triangle
-  while (rem >= nb - bi) { rem -= nb - bi; ++bi; }
-  const int bj = bi + rem;
+  const int t = threadIdx.x;                     // blockDim.x >= ntiles * esplit, whole waves
+  const bool pact = t < ntiles * esplit;         // the rest only stage and take part in the within phase
+  const int es = pact ? t / ntiles : 0;          // coordinate slice
+  const int tile = pact ? t % ntiles : 0;
+  int bi = 0, bj = 1;
+  if (pact) tile_blocks(tile, nb, bi, bj);
+  const int dg = (int)blockDim.x / nb;           // within-block phase: threads per block
+  const bool dact = t < dg * nb;
+  const int db = t % nb, de0 = t / nb;
+  Within<RT> wb;
+  wb.init();
   double accd[16];
   f32x2 acc[8];
   int run = 0;  // coordinates summed in acc since the last flush
@@ -772,7 +894,7 @@ k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __re
     // packed fp32 (v_pk_add_f32 / v_pk_fma_f32): pair (x, y), (x, y+1) per instruction -- the same
     // per-element IEEE sub and fused multiply-add as the scalar form, half the VALU issue slots
 #pragma unroll 2  // two coordinates' LDS reads in flight (K = 128: 7.0 -> 6.5 ms; 4 was slower)
-    for (int e = e_lo; e < e_hi; ++e) {
+    for (int e = e_lo; e < (pact ? e_hi : e_lo); ++e) {
       const float4 a = *(const float4*)&lb[e * stride + 4 * bi];
       const float4 b = *(const float4*)&lb[e * stride + 4 * bj];
       const float av[4] = {a.x, a.y, a.z, a.w};
@@ -787,6 +909,8 @@ k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __re
     }
     run += e_hi - e_lo;
     if (run + (e_hi - e_lo) > kPE) flush();  // float runs of <= kPE coordinates, then float64
+    if (dact) wb.add(lb, stride, pe, de0, dg, db);
+    wb.step((pe + dg - 1) / dg);
     if (ch + 1 < c1) {
       put(cur ^ 1);  // buffer cur ^ 1 was last read before the previous barrier
       if (ch + 2 < c1) load(ch + 2);
@@ -794,41 +918,15 @@ k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __re
     __syncthreads();
   }
   flush();
-  // write the block's upper-triangle partials: pair (i, j), i < j -> index i*k - i*(i+1)/2 + (j-i-1);
-  // with esplit > 1 the slices of a tile are first added in slice order through LDS (reused as
-  // [ntiles * 16] doubles, sized by the host)
-  const int64_t npairs = (int64_t)k * (k - 1) / 2;
-  double* out = partial + (int64_t)blockIdx.x * npairs;
-  if (esplit == 1) {
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int i = 4 * bi + u / 4, j = 4 * bj + u % 4;
-      if (i < j && j < k) out[(int64_t)i * k - (int64_t)i * (i + 1) / 2 + (j - i - 1)] = accd[u];
-    }
-    return;
-  }
-  __syncthreads();
-  double* red = (double*)lds;
-  for (int s = 0; s < esplit; ++s) {
-    if (es == s) {
-#pragma unroll
-      for (int u = 0; u < 16; ++u) red[tile * 16 + u] = (s == 0 ? 0.0 : red[tile * 16 + u]) + accd[u];
-    }
-    __syncthreads();
-  }
-  for (int idx = t; idx < ntiles * 16; idx += (int)blockDim.x) {
-    const int tl = idx / 16, u = idx % 16;
-    int r = 0, rm = tl;
-    while (rm >= nb - r) { rm -= nb - r; ++r; }
-    const int i = 4 * r + u / 4, j = 4 * (r + rm) + u % 4;
-    if (i < j && j < k) out[(int64_t)i * k - (int64_t)i * (i + 1) / 2 + (j - i - 1)] = red[idx];
-  }
+  wb.flush();
+  pair_epilogue(lds, accd, pact, es, tile, bi, bj, ntiles, esplit, nb, k, wb.accd, dact, dg,
+                partial + (int64_t)blockIdx.x * ((int64_t)k * (k - 1) / 2));
 }
 
-// waves_per_eu(5): <= 102 VGPRs, so two 10-wave groups share a CU (with 1024-thread bounds alone the
-// compiler took 100 -> 4 waves/SIMD -> one group per CU, idle across every barrier)
+// waves_per_eu(4): <= 128 VGPRs, the budget at which a CU holds 16 waves (MI355X_MICROARCH.md: waves
+// per CU halve at 64 / 128 VGPRs) -- two 8-wave workgroups of 512 threads (K = 128)
 template <int KPAD, int RT>
-__global__ void __launch_bounds__(kMaxPairThreads) __attribute__((amdgpu_waves_per_eu(5)))
+__global__ void __launch_bounds__(kMaxPairThreads) __attribute__((amdgpu_waves_per_eu(4)))
 k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int kp,
            int64_t nchunks, int ntiles, int esplit, int ce, int rows, double* __restrict__ partial) {
   constexpr int S = KPAD + 4;                    // LDS row stride (floats), 16-byte rows
@@ -836,12 +934,17 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
   extern __shared__ float lds[];                 // [2][pe][S]
   const int pe = ce * esplit;
   const int nb = kp / 4;
-  const int t = threadIdx.x;                     // blockDim.x == ntiles * esplit
-  const int es = t / ntiles;                     // coordinate slice
-  const int tile = t % ntiles;
-  int bi = 0, rem = tile;  // tile -> (bi, bj), bi <= bj, row-major upper triangle
-  while (rem >= nb - bi) { rem -= nb - bi; ++bi; }
-  const int bj = bi + rem;
+  const int t = threadIdx.x;                     // blockDim.x >= ntiles * esplit, whole waves
+  const bool pact = t < ntiles * esplit;         // the rest only stage and take part in the within phase
+  const int es = pact ? t / ntiles : 0;          // coordinate slice
+  const int tile = pact ? t % ntiles : 0;
+  int bi = 0, bj = 1;
+  if (pact) tile_blocks(tile, nb, bi, bj);
+  const int dg = (int)blockDim.x / nb;           // within-block phase: threads per block
+  const bool dact = t < dg * nb;
+  const int db = t % nb, de0 = t / nb;
+  Within<RT> wb;
+  wb.init();
   double accd[16];
   f32x2 acc[8];
   int run = 0;  // coordinates summed in acc since the last flush (uniform)
@@ -923,7 +1026,7 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
     // packed fp32 (v_pk_add_f32 / v_pk_fma_f32): pair (x, y), (x, y+1) per instruction -- the same
     // per-element IEEE sub and fused multiply-add as the scalar form, half the VALU issue slots
 #pragma unroll 2  // two coordinates' LDS reads in flight (K = 128: 7.0 -> 6.5 ms; 4 was slower)
-    for (int i = 0; i < ce; ++i) {
+    for (int i = 0; i < (pact ? ce : 0); ++i) {
       const float4 a = *(const float4*)(pa + i * S);
       const float4 b = *(const float4*)(pb + i * S);
       const float av[4] = {a.x, a.y, a.z, a.w};
@@ -938,6 +1041,8 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
     }
     run += ce;
     if (run + ce > kPE) flush();  // float runs of <= kPE coordinates, then float64
+    if (dact) wb.add(lds + cur * bufsz, S, pe, de0, dg, db);
+    wb.step((pe + dg - 1) / dg);
     if (ch + 1 < c1) {
       put(cur ^ 1);  // buffer cur ^ 1 was last read before the previous barrier
       if (ch + 2 < c1) load(ch + 2);
@@ -945,35 +1050,65 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
     __syncthreads();
   }
   flush();
-  // write the block's upper-triangle partials: pair (i, j), i < j -> index i*k - i*(i+1)/2 + (j-i-1);
-  // with esplit > 1 the slices of a tile are first added in slice order through LDS (reused as
-  // [ntiles * 16] doubles, sized by the host)
-  const int64_t npairs = (int64_t)k * (k - 1) / 2;
-  double* out = partial + (int64_t)blockIdx.x * npairs;
-  if (esplit == 1) {
+  wb.flush();
+  pair_epilogue(lds, accd, pact, es, tile, bi, bj, ntiles, esplit, nb, k, wb.accd, dact, dg,
+                partial + (int64_t)blockIdx.x * ((int64_t)k * (k - 1) / 2));
+}
+
+// float64 models (krum_defense.py:50-66 over vectorize_weight's float64 vector, common/utils.py:8-30):
+// every difference and square in float64, as the reference computes them (no float32 step).  A rare
+// path, written for clarity: a workgroup stages kC64 coordinates of all k clients in LDS ([e][client]
+// doubles), each thread owns pairs p = t, t + 256, ... (<= 32 of them, k <= 128) and adds their
+// squared differences over the chunk with float64 FMAs; per-block partials go through
+// k_pairdist_reduce like the float32 kernels'.
+constexpr int kC64 = 32;
+__global__ void __launch_bounds__(kBlock)
+k_pairdist_f64(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k,
+               int64_t nchunks, double* __restrict__ partial) {
+  extern __shared__ double ldsd[];  // [kC64][k]
+  const int t = threadIdx.x;
+  const int npairs = k * (k - 1) / 2;
+  constexpr int kPPT = (kMaxPairK * (kMaxPairK - 1) / 2 + kBlock - 1) / kBlock;  // 32
+  double acc[kPPT];
+  int pij[kPPT];  // i | j << 8 of pair t + q * kBlock
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int i = 4 * bi + u / 4, j = 4 * bj + u % 4;
-      if (i < j && j < k) out[(int64_t)i * k - (int64_t)i * (i + 1) / 2 + (j - i - 1)] = accd[u];
-    }
-    return;
+  for (int q = 0; q < kPPT; ++q) {
+    acc[q] = 0.0;
+    const int p = t + q * kBlock;
+    int i = 0, rem = p;
+    if (p < npairs)
+      while (rem >= k - 1 - i) { rem -= k - 1 - i; ++i; }
+    pij[q] = p < npairs ? (i | ((i + 1 + rem) << 8)) : 0;
   }
-  __syncthreads();
-  double* red = (double*)lds;
-  for (int s = 0; s < esplit; ++s) {
-    if (es == s) {
-#pragma unroll
-      for (int u = 0; u < 16; ++u) red[tile * 16 + u] = (s == 0 ? 0.0 : red[tile * 16 + u]) + accd[u];
+  const int64_t c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
+  for (int64_t ch = c0; ch < c1; ++ch) {
+    const int si = nseg > 1 ? find_seg(segs, nseg, ch) : 0;
+    const PSeg sg = segs[si];
+    const int64_t b0 = (ch - sg.tile_start) * kC64;
+    __syncthreads();  // the previous chunk's reads are done
+    for (int idx = t; idx < kC64 * k; idx += kBlock) {  // consecutive threads: consecutive coordinates
+      const int i = idx / kC64, e = idx % kC64;
+      const double* src = (const double*)ptrs[sg.ptr_base + i];
+      ldsd[e * k + i] = b0 + e < sg.numel ? src[b0 + e] : 0.0;
     }
     __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kPPT; ++q) {
+      if (t + q * kBlock < npairs) {
+        const int i = pij[q] & 0xff, j = pij[q] >> 8;
+        double s = acc[q];
+        for (int e = 0; e < kC64; ++e) {
+          const double d = ldsd[e * k + i] - ldsd[e * k + j];
+          s = __builtin_fma(d, d, s);
+        }
+        acc[q] = s;
+      }
+    }
   }
-  for (int idx = t; idx < ntiles * 16; idx += (int)blockDim.x) {
-    const int tl = idx / 16, u = idx % 16;
-    int r = 0, rm = tl;
-    while (rm >= nb - r) { rm -= nb - r; ++r; }
-    const int i = 4 * r + u / 4, j = 4 * (r + rm) + u % 4;
-    if (i < j && j < k) out[(int64_t)i * k - (int64_t)i * (i + 1) / 2 + (j - i - 1)] = red[idx];
-  }
+  double* out = partial + (int64_t)blockIdx.x * npairs;
+#pragma unroll
+  for (int q = 0; q < kPPT; ++q)
+    if (t + q * kBlock < npairs) out[t + q * kBlock] = acc[q];
 }
 
 __global__ void __launch_bounds__(kBlock)
@@ -1021,8 +1156,11 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
                           const void* const* d_in, void* d_dist, void* d_scratch, size_t scratch_bytes,
                           void* hip_stream) {
   if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
-  if (diff_dtype != FA_DTYPE_F32 && diff_dtype != FA_DTYPE_BF16 && diff_dtype != FA_DTYPE_F16)
-    return fail(FA_ERR_INVALID, "fa_pairwise_sqdist_rt: diff_dtype must be F32, BF16 or F16 (got %d)", diff_dtype);
+  if (diff_dtype != FA_DTYPE_F32 && diff_dtype != FA_DTYPE_BF16 && diff_dtype != FA_DTYPE_F16 &&
+      diff_dtype != FA_DTYPE_F64)
+    return fail(FA_ERR_INVALID, "fa_pairwise_sqdist_rt: diff_dtype must be F32, BF16, F16 or F64 (got %d)",
+                diff_dtype);
+  const bool f64 = diff_dtype == FA_DTYPE_F64;
   const int rt = diff_dtype == FA_DTYPE_BF16 ? 1 : diff_dtype == FA_DTYPE_F16 ? 2 : 0;
   if (k < 2 || k > kMaxPairK || num_segments <= 0 || !seg_numel || !d_in || !d_dist)
     return fail(FA_ERR_INVALID, "fa_pairwise_sqdist: invalid arguments (2 <= k <= %d)", kMaxPairK);
@@ -1030,7 +1168,7 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
   const int kp = q.kp, ntiles = q.ntiles, esplit = q.esplit, pe = q.pe;
   if (q.nthreads > kMaxPairThreads) return fail(FA_ERR_INVALID, "fa_pairwise_sqdist: k too large");
   int nseg = 0;
-  int64_t nchunks = 0;
+  int64_t nchunks = 0, nchunks64 = 0;
   for (int s = 0; s < num_segments; ++s) {
     if (seg_numel[s] < 0) return fail(FA_ERR_INVALID, "segment %d has negative numel", s);
     if (seg_numel[s] == 0) continue;
@@ -1038,8 +1176,11 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
       if (!d_in[(int64_t)s * k + i]) return fail(FA_ERR_INVALID, "segment %d client %d: input NULL", s, i);
     ++nseg;
     nchunks += (seg_numel[s] + pe - 1) / pe;
+    nchunks64 += (seg_numel[s] + kC64 - 1) / kC64;
   }
   const int64_t npairs = (int64_t)k * (k - 1) / 2;
+  // workgroups: the same count for every diff dtype (fa_pairwise_sqdist_scratch_bytes sizes the
+  // partials by it), float64 chunks spread over them
   const int nblocks = (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, q.nblocks));
   if (scratch_bytes < sizeof(double) * (size_t)npairs * nblocks || !d_scratch)
     return fail(FA_ERR_INVALID, "fa_pairwise_sqdist: scratch must hold %zu bytes",
@@ -1061,20 +1202,23 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
   const void** hp = (const void**)(h + seg_bytes);
   int j = 0;
   int64_t c0 = 0;
+  const int64_t cpe = f64 ? kC64 : pe;  // coordinates per chunk
   for (int s = 0; s < num_segments; ++s) {
     const int64_t n = seg_numel[s];
     if (n == 0) continue;
     for (int i = 0; i < k; ++i) hp[(int64_t)j * k + i] = d_in[(int64_t)s * k + i];
     hs[j] = PSeg{n, c0, j * k, 0, 0};
-    c0 += (n + pe - 1) / pe;
+    c0 += (n + cpe - 1) / cpe;
     ++j;
   }
   rc = stage(slot, seg_bytes + ptr_bytes, st);
   if (rc) return rc;
   const char* dv = (const char*)slot->dev;
-  if (q.lane) {
-    size_t lds = 2 * sizeof(float) * (size_t)pe * (kp + 4);
-    if (esplit > 1) lds = std::max(lds, sizeof(double) * 16 * (size_t)ntiles);
+  if (f64) {
+    hipLaunchKernelGGL(k_pairdist_f64, dim3((unsigned)nblocks), dim3(kBlock), sizeof(double) * kC64 * k, st,
+                       (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, nchunks64, (double*)d_scratch);
+  } else if (q.lane) {
+    const size_t lds = pair_lds_bytes(q);
     bool vec = true;  // 16-byte loads: every client segment 16-byte aligned (chunk starts are multiples of 8)
     for (int i = 0; i < j * k; ++i) vec = vec && ((uintptr_t)hp[i] % 16 == 0);
 #define FA_PDL(V, R) hipLaunchKernelGGL((k_pairdist_lane<V, R>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), \
@@ -1087,8 +1231,7 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
     }
 #undef FA_PDL
   } else {
-    size_t lds = 2 * sizeof(float) * (size_t)pe * (q.kpad + 4);
-    if (esplit > 1) lds = std::max(lds, sizeof(double) * 16 * (size_t)ntiles);
+    const size_t lds = pair_lds_bytes(q);
 #define FA_PD(KPAD, R) hipLaunchKernelGGL((k_pairdist<KPAD, R>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), \
       lds, st, (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit, q.ce,   \
       q.rows, (double*)d_scratch)

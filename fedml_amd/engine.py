@@ -826,9 +826,12 @@ class AggEngine:
         union of two blocks, its cross distances kept) -- every distance is still one device pass
         over the two clients' vectors, the same per-pair arithmetic as the single launch.
         ``diff_dtype`` bfloat16 / float16: every difference rounded to that dtype before it is
-        squared (fa_pairwise_sqdist_rt; the reference's arithmetic for a bf16 / f16 model)."""
+        squared (fa_pairwise_sqdist_rt; the reference's arithmetic for a bf16 / f16 model);
+        float64: the inputs are float64 vectors, measured in float64 throughout (a float64 model)."""
         if diff_dtype not in _DIFF_DT:
-            raise ValueError(f"pairwise_sqdist: diff_dtype must be float32, bfloat16 or float16, not {diff_dtype}")
+            raise ValueError("pairwise_sqdist: diff_dtype must be float32, bfloat16, float16 or float64, "
+                             f"not {diff_dtype}")
+        in_dt = torch.float64 if diff_dtype == torch.float64 else torch.float32
         k = len(segments[0]) if segments else 0
         if k < 2:
             raise ValueError("pairwise_sqdist: need at least two clients")
@@ -836,8 +839,8 @@ class AggEngine:
             if len(seg) != k:
                 raise ValueError(f"segment {s}: {len(seg)} clients, expected {k}")
             for i, t in enumerate(seg):
-                if t.dtype != torch.float32 or t.numel() != seg[0].numel():
-                    raise ValueError(f"segment {s} client {i}: float32 of {seg[0].numel()} elements expected")
+                if t.dtype != in_dt or t.numel() != seg[0].numel():
+                    raise ValueError(f"segment {s} client {i}: {in_dt} of {seg[0].numel()} elements expected")
                 _require_device(t, self.device, f"segment {s} client {i}")
         if k <= self.MAX_PAIR_K:
             return self._pairwise_launch(segments, stream, diff_dtype)
@@ -869,7 +872,7 @@ class AggEngine:
         return d
 
 
-_DIFF_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}  # FA_DTYPE_F32 / BF16 / F16
+_DIFF_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3}  # FA_DTYPE_*
 
 
 def get_engine(device: Optional[int] = None) -> AggEngine:

@@ -55,6 +55,9 @@ int fa_pairwise_sqdist(fa_ctx *ctx, int32_t num_segments, const int64_t *seg_num
  * `(v1 - v2)` (utils.py:24-27) rounds each difference to it; the inputs stay float32 (the clients'
  * values widened exactly).  The caller rounds sqrt(D) to the same dtype to reproduce the
  * reference's `.norm()` result (the norm of a bf16/f16 tensor is returned in that dtype).
+ * FA_DTYPE_F64: float64 models -- the inputs are FLOAT64 vectors and every difference, square and
+ * sum is computed in float64 (the reference's vectorize_weight keeps float64 and `(v1 - v2).norm()`
+ * runs in it; krum_defense.py:50-66).
  */
 int fa_pairwise_sqdist_rt(fa_ctx *ctx, int diff_dtype, int32_t num_segments, const int64_t *seg_numel, int32_t k,
                           const void *const *d_in, void *d_dist, void *d_scratch, size_t scratch_bytes,

@@ -950,6 +950,54 @@ def cases_sp_sampling():
         json.dump({"ref": "simulation/sp/fedavg/fedavg_api.py:127-135", "rounds": 6, "cases": cases}, fh)
 
 
+def cases_krum_f64():
+    """Krum over float64 models (krum_defense.py:27-66): vectorize_weight keeps float64, so every
+    `(v_i - v_j).norm()` runs in float64.  `near_tie`: the honest clients are one base vector plus
+    offsets of ~1e-10, below float32's resolution of the values -- in float32 every honest distance
+    would round to 0 and the selection would fall to the lowest index, while the reference's float64
+    distances (and its float32 scores, which still resolve ~1e-20) pick another client."""
+    _, _, Krum = load_defenses()
+    import fedml.core.security.common.utils as su
+    lay = [("fc.weight", (10, 50), torch.float64), ("fc.bias", (10,), torch.float64),
+           ("bn.running_mean", (10,), torch.float64)]
+    for tag, K, f, m in (("spread", 10, 2, 1), ("spread", 12, 2, 3), ("near_tie", 10, 2, 1), ("near_tie", 11, 2, 2)):
+        g = torch.Generator().manual_seed(2024 + K + len(tag))
+        if tag == "spread":
+            clients = _robust_clients(3030 + K, K, lay, special=False)
+            for b in range(f):
+                for k2, v in clients[b * 3 % K].items():
+                    clients[b * 3 % K][k2] = v + 5.0 * torch.randn(v.shape, generator=g, dtype=torch.float64)
+        else:
+            base = _robust_clients(3030 + K, 1, lay, special=False)[0]
+            clients = []
+            for i in range(K):
+                scale = 1e-10 * (1.0 + 0.37 * ((i + 5) % K))  # the tightest client is not client 0
+                clients.append(OrderedDict((k2, v + scale * torch.randn(v.shape, generator=g, dtype=torch.float64))
+                                           for k2, v in base.items()))
+            for b in range(f):
+                for k2, v in clients[(b * 3 + 1) % K].items():
+                    clients[(b * 3 + 1) % K][k2] = v + 5.0 * torch.randn(v.shape, generator=g, dtype=torch.float64)
+        n = gen_counts(3030 + K, K)
+        raw = list(zip(n, clients))
+        d = Krum(Args(byzantine_client_num=f, krum_param_m=m))
+        sel = d.defend_before_aggregation(raw)
+        idx = [next(i for i, (_, c) in enumerate(raw) if c is sc) for _, sc in sel]
+        vec = [su.vectorize_weight(c) for c in clients]
+        assert vec[0].dtype == torch.float64
+        scores = d._compute_krum_score(vec)
+        dists = [[su.compute_euclidean_distance(vec[i], vec[j]).item() ** 2 if i != j else 0.0 for j in range(K)]
+                 for i in range(K)]
+        if tag == "near_tie":  # the float32 measurement would not reproduce this selection
+            v32 = [v.float() for v in vec]
+            s32 = d._compute_krum_score(v32)
+            idx32 = torch.argsort(torch.Tensor(s32)).tolist()[:m]
+            assert idx32 != idx, (idx32, idx)
+        write(f"g18_krum_f64_{tag}_K{K}_f{f}_m{m}", clients, [clients[0]],
+              dict(kind="krum", n=n, byzantine_client_num=f, krum_param_m=m, selected=idx, scores=scores,
+                   dists=dists, vector_dtype="float64",
+                   ref="core/security/defense/krum_defense.py:27-66, common/utils.py:8-27"))
+
+
 def out2_equal(a, b):
     return all(np.array_equal(np.asarray(a[k]), np.asarray(b[k])) for k in a)
 

@@ -78,9 +78,13 @@ def test_krum_selection_with_oracle_distances(path, monkeypatch):
     cl = client_dicts(meta, arrays)
     keys = [k for k in meta["keys"] if WEIGHT(k)]
     vdt = KrumDefense.vector_dtype(cl)
-    vecs = [torch.cat([c[k].float().reshape(-1) for k in keys]) for c in cl]
-    D = (orc.pairwise_sqdist_rt(vecs, vdt) if vdt in (torch.bfloat16, torch.float16)
-         else orc.pairwise_sqdist(vecs)).numpy()
+    if vdt == torch.float64:  # float64 models: float64 differences and sums (numpy), as the reference
+        X = np.stack([torch.cat([c[k].reshape(-1) for k in keys]).numpy() for c in cl])
+        D = ((X[:, None, :] - X[None, :, :]) ** 2).sum(-1)
+    else:
+        vecs = [torch.cat([c[k].float().reshape(-1) for k in keys]) for c in cl]
+        D = (orc.pairwise_sqdist_rt(vecs, vdt) if vdt in (torch.bfloat16, torch.float16)
+             else orc.pairwise_sqdist(vecs)).numpy()
     d = KrumDefense(types.SimpleNamespace(byzantine_client_num=meta["byzantine_client_num"],
                                           krum_param_m=meta["krum_param_m"]))
     monkeypatch.setattr(d, "pairwise_sq_distances", lambda grads: D)
@@ -122,3 +126,14 @@ def test_pairwise_oracle_matches_numpy():
     X = torch.stack(xs).double().numpy()
     ref = ((X[:, None, :] - X[None, :, :]) ** 2).sum(-1)
     np.testing.assert_allclose(D, ref, rtol=1e-12)
+
+
+def test_krum_f64_fixtures_present_and_float64():
+    """g18_krum_f64_*: float64 models, including near-ties a float32 measurement would order
+    differently (make_golden.py cases_krum_f64 asserts that when it writes them)."""
+    from fedml_amd.core.security.defense.krum_defense import KrumDefense
+    paths = [p for p in ROB["g18_"] if "f64" in os.path.basename(p)]
+    assert len(paths) >= 4 and any("near_tie" in p for p in paths)
+    for p in paths:
+        meta, arrays = load_case(p)
+        assert KrumDefense.vector_dtype(client_dicts(meta, arrays)) == torch.float64
