@@ -33,7 +33,8 @@ EXPORTED_SYMBOLS = (
     "fa_ctx_set_mix_band", "fa_stream_create_cu_masked", "fa_stream_destroy", "fa_strerror", "fa_last_error",
     "fa_promote_add", "fa_weighted_sum_host", "fa_pushsum",
     # include/fedagg_finite.h
-    "fa_finite_sum", "fa_finite_sum_tiled", "fa_finite_quantize", "fa_lcc_decode",
+    "fa_finite_sum", "fa_finite_sum_tiled", "fa_finite_quantize", "fa_lcc_decode", "fa_mt_randint_sum",
+    "fa_mt_randint_sum_scratch_bytes",
     # include/fedagg_robust.h
     "fa_coord_median", "fa_pairwise_sqdist", "fa_pairwise_sqdist_rt", "fa_pairwise_sqdist_scratch_bytes",
     # include/fedagg_comm.h
@@ -147,6 +148,11 @@ def _declare(L):
     L.fa_lcc_decode.restype = ctypes.c_int
     L.fa_lcc_decode.argtypes = [_vp, ctypes.c_int32, ctypes.c_int32, ctypes.c_int64, _P_i64, _vp, ctypes.c_int64,
                                 ctypes.c_int64, _vp, _vp]
+    L.fa_mt_randint_sum.restype = ctypes.c_int
+    L.fa_mt_randint_sum.argtypes = [_vp, ctypes.c_int32, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_int8),
+                                    ctypes.c_int64, ctypes.c_int64, _vp, _vp, ctypes.c_size_t, _vp]
+    L.fa_mt_randint_sum_scratch_bytes.restype = ctypes.c_size_t
+    L.fa_mt_randint_sum_scratch_bytes.argtypes = [ctypes.c_int64]
     L.fa_coord_median.restype = ctypes.c_int
     L.fa_coord_median.argtypes = [_vp, ctypes.c_int, ctypes.c_int32, _P_i64, ctypes.c_int32, _P_vp, _P_vp, _vp]
     L.fa_pairwise_sqdist.restype = ctypes.c_int

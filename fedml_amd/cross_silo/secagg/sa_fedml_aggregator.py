@@ -9,10 +9,11 @@ multiplies by 1/len(active).  Note that the reference server clears every flag i
 the first client's model survives; this mirror reproduces whatever the flags say
 (tests/golden/g15_*).
 
-The aggregate mask itself comes from ``aggregate_mask_reconstruction`` -- BGW decoding of the
-secret shares plus re-expansion of every client's numpy MT19937 mask stream (:92-136).  That PRG
-expansion is host-side control logic outside this path (scope): subclasses or callers
-provide it (e.g. a precomputed mask), and the base method raises.
+The aggregate mask comes from ``aggregate_mask_reconstruction`` (:92-136): BGW decoding of the
+secret shares on the host (a few scalars per client), then every surviving client's numpy MT19937
+mask stream -- and, for a dropped client, its pairwise streams -- re-expanded ON THE DEVICE and
+summed mod p by ``fa_mt_randint_sum`` (bit-exact to numpy's legacy seeding and masked randint;
+tests/golden/g21_*).  ``aggregate_model_reconstruction`` keeps that mask on the device.
 """
 from __future__ import annotations
 
@@ -23,6 +24,7 @@ import numpy as np
 import torch
 
 from ...core.mpc import lightsecagg as fin
+from ...core.mpc import secagg as sa
 from ...engine import get_engine
 
 
@@ -78,14 +80,27 @@ class SecAggAggregator(object):
             self.flag_client_model_uploaded_dict[idx] = False
         return True
 
+    def _aggregate_mask_device(self, active_clients, SS_rx, public_key_list):  # noqa: N803
+        """The aggregate mask as an int64 device tensor (see aggregate_mask_reconstruction)."""
+        N = self.targeted_number_active_clients
+        flags = [self.flag_client_model_uploaded_dict[i] for i in range(N)]
+        seeds, signs = sa.mask_streams(N, flags, active_clients, SS_rx, public_key_list, self.privacy_guarantee,
+                                       self.prime_number)
+        return self._engine.mt_randint_sum(seeds, signs, self.prime_number, self.total_dimension)
+
     def aggregate_mask_reconstruction(self, active_clients, SS_rx, public_key_list):  # noqa: N803
-        raise NotImplementedError(
-            "SecAgg's PRG mask re-expansion (numpy MT19937 streams, sa_fedml_aggregator.py:92-136) is outside "
-            "the accelerated path: override aggregate_mask_reconstruction or pass the aggregate mask")
+        """Reference :92-136: for every client i < targeted_number_active_clients, BGW-decode its
+        secret from the first T + 1 active clients' shares; a client whose model arrived adds
+        randint(0, p, d) seeded by it, a dropped one adds its pairwise masks (sign by index order);
+        everything mod p.  Returned as numpy int64 like the reference's."""
+        return self._aggregate_mask_device(active_clients, SS_rx, public_key_list).cpu().numpy()
 
     def aggregate_model_reconstruction(self, active_clients_first_round, active_clients_second_round, SS_rx,
                                        public_key_list):  # noqa: N803
-        aggregate_mask = self.aggregate_mask_reconstruction(active_clients_second_round, SS_rx, public_key_list)
+        if type(self).aggregate_mask_reconstruction is SecAggAggregator.aggregate_mask_reconstruction:
+            aggregate_mask = self._aggregate_mask_device(active_clients_second_round, SS_rx, public_key_list)
+        else:  # a subclass's own mask (kept as the override point it was)
+            aggregate_mask = self.aggregate_mask_reconstruction(active_clients_second_round, SS_rx, public_key_list)
         eng = self._engine
         mask = fin._dev(aggregate_mask, eng, torch.int64).reshape(-1)
         p = self.prime_number

@@ -400,6 +400,127 @@ ModP make_modp(int64_t p) {
   return m;
 }
 
+
+// ============================================================================================
+// SecAgg mask re-expansion: numpy legacy RandomState(seed).randint(0, p, size=n) per stream, on the
+// device.  One wave per stream: the 624-word MT19937 state lives in LDS; each twist regenerates it
+// in three dependency-free phases (words [0, 227) read only old words; [227, 454) read the new
+// [0, 227); [454, 624) the new [227, 397) and word 0), every lane reading its inputs before any
+// lane writes; then each word is tempered, masked and accepted or rejected, and the accepted
+// draws are placed in stream order by a ballot prefix count.  The signed values go into a uint64
+// accumulator with no-return atomics (streams are batched so that a batch's sum of values in
+// [0, p) cannot wrap); a fold kernel reduces each batch mod p into d_out.
+constexpr int kMtN = 624, kMtM = 397;
+constexpr uint32_t kMtA = 0x9908b0dfu, kMtUp = 0x80000000u, kMtLo = 0x7fffffffu;
+
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+
+__device__ __forceinline__ uint32_t mt_mix(uint32_t cur, uint32_t next, uint32_t far) {
+  const uint32_t y = (cur & kMtUp) | (next & kMtLo);
+  return far ^ (y >> 1) ^ ((y & 1u) ? kMtA : 0u);
+}
+
+// numpy mt19937_gen over the state in LDS (one wave, lane = 0..63)
+__device__ __forceinline__ void mt_twist(uint32_t* mt, int lane) {
+  uint32_t nv[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {  // [0, 227): mt[i + 397] is old
+    const int i = r * 64 + lane;
+    if (i < kMtN - kMtM) nv[r] = mt_mix(mt[i], mt[i + 1], mt[i + kMtM]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = r * 64 + lane;
+    if (i < kMtN - kMtM) mt[i] = nv[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {  // [227, 454): mt[i - 227] is new
+    const int i = kMtN - kMtM + r * 64 + lane;
+    if (i < 2 * (kMtN - kMtM)) nv[r] = mt_mix(mt[i], mt[i + 1], mt[i + kMtM - kMtN]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int i = kMtN - kMtM + r * 64 + lane;
+    if (i < 2 * (kMtN - kMtM)) mt[i] = nv[r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {  // [454, 624): mt[i - 227] and (i = 623) mt[0] are new
+    const int i = 2 * (kMtN - kMtM) + r * 64 + lane;
+    if (i < kMtN) nv[r] = mt_mix(mt[i], i + 1 < kMtN ? mt[i + 1] : mt[0], mt[i + kMtM - kMtN]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    const int i = 2 * (kMtN - kMtM) + r * 64 + lane;
+    if (i < kMtN) mt[i] = nv[r];
+  }
+  __syncthreads();
+}
+
+template <bool WIDE>
+__global__ void __launch_bounds__(64)
+k_mt_randint(const uint32_t* __restrict__ seeds, const int8_t* __restrict__ signs, uint64_t rng, uint64_t mask,
+             uint64_t p, int64_t n, unsigned long long* __restrict__ acc) {
+  __shared__ uint32_t mt[kMtN];
+  const int lane = threadIdx.x;
+  const int s = blockIdx.x;
+  const bool neg = signs[s] < 0;
+  if (lane == 0) {  // numpy mt19937_seed (init_genrand): a serial recurrence, 624 steps
+    uint32_t x = seeds[s];
+    for (int i = 0; i < kMtN; ++i) {
+      mt[i] = x;
+      x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)(i + 1);
+    }
+  }
+  __syncthreads();
+  int64_t count = 0;  // draws accepted so far (wave-uniform)
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  constexpr int kVals = WIDE ? kMtN / 2 : kMtN;  // candidate values per twist (64-bit: word pairs)
+  while (count < n) {
+    mt_twist(mt, lane);
+#pragma unroll 1
+    for (int r = 0; r * 64 < kVals && count < n; ++r) {
+      const int w = r * 64 + lane;
+      bool ok = false;
+      uint64_t v = 0;
+      if (w < kVals) {
+        if constexpr (WIDE) {
+          v = ((uint64_t)mt_temper(mt[2 * w]) << 32 | mt_temper(mt[2 * w + 1])) & mask;
+        } else {
+          v = mt_temper(mt[w]) & (uint32_t)mask;
+        }
+        ok = v <= rng;
+      }
+      const uint64_t bal = __ballot(ok);
+      const int64_t pos = count + __popcll(bal & below);
+      if (ok && pos < n && v != 0) atomicAdd(acc + pos, (unsigned long long)(neg ? p - v : v));
+      count += __popcll(bal);
+    }
+  }
+}
+
+// total[e] = (first ? 0 : total[e]) + acc[e] mod p, reduced to [0, p); acc cleared for the next batch
+__global__ void __launch_bounds__(kBlock)
+k_mt_fold(unsigned long long* __restrict__ acc, int64_t* __restrict__ total, int64_t n, uint64_t p, int first) {
+  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (int64_t)gridDim.x * kBlock) {
+    const uint64_t a = acc[e] % p;
+    uint64_t t = first ? a : (uint64_t)total[e] + a;
+    if (t >= p) t -= p;
+    total[e] = (int64_t)t;
+    acc[e] = 0;
+  }
+}
+
 }  // namespace
 
 // ============================================================================================ ABI
@@ -628,6 +749,62 @@ int fa_lcc_decode(fa_ctx* ctx, int32_t rows, int32_t k, int64_t m, const int64_t
   } else {
     hipLaunchKernelGGL(k_lcc_decode, dim3((unsigned)blocks), dim3(kBlock), 0, st, (const long long*)dv,
                        rows_needed, k, m, (const long long*)d_f, n_out, (long long*)d_out, mp, (const int*)nullptr);
+  }
+  FA_HIP(hipGetLastError());
+  return release(slot, st);
+}
+
+
+size_t fa_mt_randint_sum_scratch_bytes(int64_t n) { return n > 0 ? sizeof(uint64_t) * (size_t)n : 0; }
+
+int fa_mt_randint_sum(fa_ctx* ctx, int32_t num_streams, const uint32_t* seeds, const int8_t* signs, int64_t prime,
+                      int64_t n, void* d_out, void* d_scratch, size_t scratch_bytes, void* hip_stream) {
+  if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (num_streams < 0 || n < 0 || prime <= 0 || (num_streams > 0 && (!seeds || !signs)) || (n > 0 && !d_out))
+    return fail(FA_ERR_INVALID, "fa_mt_randint_sum: invalid arguments");
+  if (n > 0 && (!d_scratch || scratch_bytes < fa_mt_randint_sum_scratch_bytes(n)))
+    return fail(FA_ERR_INVALID, "fa_mt_randint_sum: scratch must hold %zu bytes", fa_mt_randint_sum_scratch_bytes(n));
+  for (int s = 0; s < num_streams; ++s)
+    if (signs[s] != 1 && signs[s] != -1)
+      return fail(FA_ERR_INVALID, "fa_mt_randint_sum: sign %d of stream %d", signs[s], s);
+  DeviceGuard g(ctx->device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
+  hipStream_t st = (hipStream_t)hip_stream;
+  if (n == 0) return FA_OK;
+  const uint64_t p = (uint64_t)prime, rng = p - 1;
+  uint64_t mask = rng;
+  for (int sh = 1; sh < 64; sh <<= 1) mask |= mask >> sh;
+  const bool wide = rng > 0xFFFFFFFFull;
+  FA_HIP(hipMemsetAsync(d_out, 0, sizeof(int64_t) * (size_t)n, st));
+  if (num_streams == 0 || rng == 0) return FA_OK;  // randint(0, 1) draws nothing and is all zeros
+  FA_HIP(hipMemsetAsync(d_scratch, 0, sizeof(uint64_t) * (size_t)n, st));
+  // streams per batch: a batch's sum of values in [0, p) must not wrap 64 bits
+  const uint64_t per = std::min<uint64_t>((uint64_t)num_streams, UINT64_MAX / rng);
+  const size_t seed_b = align16(sizeof(uint32_t) * num_streams);
+  const size_t tab = seed_b + align16((size_t)num_streams);
+  fa_ctx::Slot* slot = nullptr;
+  int rc = acquire_slot(ctx, tab, &slot);
+  if (rc) return rc;
+  char* h = (char*)slot->host;
+  memcpy(h, seeds, sizeof(uint32_t) * num_streams);
+  memcpy(h + seed_b, signs, (size_t)num_streams);
+  rc = stage(slot, tab, st);
+  if (rc) return rc;
+  const uint32_t* dseeds = (const uint32_t*)slot->dev;
+  const int8_t* dsigns = (const int8_t*)((const char*)slot->dev + seed_b);
+  const unsigned fold_blocks = (unsigned)std::min<int64_t>((n + kBlock - 1) / kBlock, 4096);
+  int first = 1;
+  for (uint64_t s0 = 0; s0 < (uint64_t)num_streams; s0 += per) {
+    const unsigned b = (unsigned)std::min<uint64_t>(per, (uint64_t)num_streams - s0);
+    if (wide)
+      hipLaunchKernelGGL(k_mt_randint<true>, dim3(b), dim3(64), 0, st, dseeds + s0, dsigns + s0, rng, mask, p, n,
+                         (unsigned long long*)d_scratch);
+    else
+      hipLaunchKernelGGL(k_mt_randint<false>, dim3(b), dim3(64), 0, st, dseeds + s0, dsigns + s0, rng, mask, p, n,
+                         (unsigned long long*)d_scratch);
+    hipLaunchKernelGGL(k_mt_fold, dim3(fold_blocks), dim3(kBlock), 0, st, (unsigned long long*)d_scratch,
+                       (int64_t*)d_out, n, p, first);
+    first = 0;
   }
   FA_HIP(hipGetLastError());
   return release(slot, st);

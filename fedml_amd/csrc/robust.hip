@@ -596,7 +596,15 @@ constexpr int kNPL = 8;       // k_pairdist_lane: coordinates of one client stag
 // loads; larger K -- k_pairdist, `rows` lanes per client reading consecutive floats, 16 elements per
 // thread (r02: K = 64 / 100 / 128: 2.59 / 3.99 / 6.58 -> 2.0 / 3.7 / 6.38 ms; at K <= 32 the
 // per-element form's extra instructions cost more than its coalescing gains).
-struct PairSplit { int kp, kpad, nb, ntiles, esplit, nthreads, rows, ce, pe, nblocks, dgroups; bool lane; };
+struct PairSplit { int kp, kpad, nb, ntiles, esplit, nthreads, rows, ce, pe, nblocks, dgroups, npl; bool lane; };
+// k_pairdist_lane: coordinates staged per lane and chunk, kNPL or 16 (FA_PAIR_NPL=16, A/B)
+int pair_npl() {
+  static const int v = [] {
+    const char* e = getenv("FA_PAIR_NPL");
+    return e && atoi(e) == 16 ? 16 : kNPL;
+  }();
+  return v;
+}
 // Tiles: 4x4 pair tiles of the STRICT upper triangle of 4-client blocks (bi < bj), one per thread and
 // coordinate slice; the pairs inside a block (6 per block) are spread over all threads as a second,
 // small phase per chunk (see k_pairdist), so no thread computes the 10 wasted slots of a diagonal tile
@@ -630,16 +638,19 @@ PairSplit pair_split(int k) {
   if (q.nthreads < q.kp) q.nthreads = waves(q.kp);  // every client needs a staging thread
   q.rows = q.nthreads / q.kp;
   q.lane = q.kp <= 32;
+  q.npl = kNPL;
   if (q.lane) {  // k_pairdist_lane: slices of pe / esplit coordinates, not necessarily equal
-    q.pe = q.rows * kNPL;
+    q.npl = pair_npl();
+    q.pe = q.rows * q.npl;
     q.ce = 0;
   } else {
     // a slice is one float32 run at most, and every element of a chunk has a staging thread
     q.ce = std::max(1, std::min(kPE, q.rows * kNPS / q.esplit));
     // two LDS buffers of pe rows: at most 80 KB, so two workgroups share a CU -- or, for a workgroup of
-    // more than 512 threads (alone on its CU at <= 128 VGPRs), up to FA_PAIR_LDS_KB (default 80)
+    // more than 512 threads (alone on its CU at <= 128 VGPRs), up to 150 KB (FA_PAIR_LDS_KB; r03f:
+    // K = 100 / 128 3.67 / 5.10 -> 3.40 / 4.89 ms with 150 vs 80)
     static const char* lk = getenv("FA_PAIR_LDS_KB");
-    const size_t cap_kb = q.nthreads > 512 && lk && atoi(lk) >= 16 && atoi(lk) <= 150 ? atoi(lk) : 80;
+    const size_t cap_kb = q.nthreads <= 512 ? 80 : lk && atoi(lk) >= 16 && atoi(lk) <= 150 ? atoi(lk) : 150;
     while (q.ce > 1 && 2 * sizeof(float) * (size_t)q.ce * q.esplit * (q.kpad + 4) > cap_kb * 1024) --q.ce;
     q.pe = q.ce * q.esplit;
   }
@@ -695,6 +706,22 @@ __device__ __forceinline__ void tile_blocks(int tile, int nb, int& bi, int& bj) 
 
 __device__ __forceinline__ int64_t pair_index(int i, int j, int k) {  // i < j
   return (int64_t)i * k - (int64_t)i * (i + 1) / 2 + (j - i - 1);
+}
+
+// One coordinate of a 4x4 pair tile: clients 4bi..4bi+3 (a) against 4bj..4bj+3 (b), packed fp32
+// (v_pk_add_f32 / v_pk_fma_f32): pair (x, y), (x, y+1) per instruction -- the same per-element IEEE
+// sub and fused multiply-add as the scalar form, half the VALU issue slots.
+template <int RT>
+__device__ __forceinline__ void pair_tile(const float4 a, const float4 b, f32x2 (&acc)[8]) {
+  const float av[4] = {a.x, a.y, a.z, a.w};
+  const f32x2 b01 = {b.x, b.y}, b23 = {b.z, b.w};
+#pragma unroll
+  for (int x = 0; x < 4; ++x) {
+    const f32x2 ax = {av[x], av[x]};
+    const f32x2 d0 = round_diff<RT>(ax - b01), d1 = round_diff<RT>(ax - b23);
+    acc[2 * x] = __builtin_elementwise_fma(d0, d0, acc[2 * x]);
+    acc[2 * x + 1] = __builtin_elementwise_fma(d1, d1, acc[2 * x + 1]);
+  }
 }
 
 // The within-block phase: thread t sums the 6 pairs (4b + i, 4b + j), i < j < 4, of block b = t % nb
@@ -790,7 +817,7 @@ __device__ __forceinline__ void pair_epilogue(float* lds, const double (&accd)[1
 // K <= 32 (kp <= 32): the r01 form -- a lane per client stages 8 consecutive coordinates (two 16-byte
 // loads), slices of pe / esplit coordinates (pe = rows * 8); measured faster there than the
 // strided form below (K = 16 / 32: 0.20 / 0.59 vs 0.27 / 0.65 ms)
-template <bool VEC, int RT>
+template <bool VEC, int RT, bool PF, int NPL>
 __global__ void __launch_bounds__(kMaxPairThreads) __attribute__((amdgpu_waves_per_eu(4)))
 k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int kp,
            int64_t nchunks, int ntiles, int esplit, int pe, double* __restrict__ partial) {
@@ -825,14 +852,14 @@ k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __re
     run = 0;
   };
   const int e_lo = (int)((int64_t)es * pe / esplit), e_hi = (int)((int64_t)(es + 1) * pe / esplit);
-  // staging role: client sc, kNPL consecutive coordinates from se of every chunk (pe = (nthreads / kp)
-  // * kNPL, so the row (t / kp) < nthreads / kp of a staging thread is exactly se < pe).  Registers
+  // staging role: client sc, NPL consecutive coordinates from se of every chunk (pe = (nthreads / kp)
+  // * NPL, so the row (t / kp) < nthreads / kp of a staging thread is exactly se < pe).  Registers
   // hold the next chunk while the current one is computed (see the pipeline below); they go to LDS
   // transposed, [e][client].
-  const int sc = t % kp, se = (t / kp) * kNPL;
+  const int sc = t % kp, se = (t / kp) * NPL;
   const bool sact = se < pe && sc < k;
   const bool swr = se < pe;            // clients k..kp-1 are staged as zeros
-  float v[kNPL];
+  float v[NPL];
   int cseg = -1;
   const float* src = nullptr;
   int64_t snum = 0;
@@ -847,13 +874,13 @@ k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __re
     const int64_t b0 = (ch - sg.tile_start) * pe + se;
     if (!sact) {
 #pragma unroll
-      for (int u = 0; u < kNPL; ++u) v[u] = 0.0f;
-    } else if (b0 + kNPL <= snum) {  // whole run: one base address, immediate offsets
+      for (int u = 0; u < NPL; ++u) v[u] = 0.0f;
+    } else if (b0 + NPL <= snum) {  // whole run: one base address, immediate offsets
       const __attribute__((address_space(1))) float* g = (const __attribute__((address_space(1))) float*)(src + b0);
       if constexpr (VEC) {
         typedef float f32x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
-        for (int u = 0; u < kNPL / 4; ++u) {
+        for (int u = 0; u < NPL / 4; ++u) {
           const f32x4 q = ((const __attribute__((address_space(1))) f32x4*)g)[u];
           v[4 * u] = q.x;
           v[4 * u + 1] = q.y;
@@ -862,11 +889,11 @@ k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __re
         }
       } else {
 #pragma unroll
-        for (int u = 0; u < kNPL; ++u) v[u] = g[u];
+        for (int u = 0; u < NPL; ++u) v[u] = g[u];
       }
     } else {  // the segment's last run: coordinates past the end add 0 to every sum
 #pragma unroll
-      for (int u = 0; u < kNPL; ++u) v[u] = b0 + u < snum ? gld<float>(src, b0 + u) : 0.0f;
+      for (int u = 0; u < NPL; ++u) v[u] = b0 + u < snum ? gld<float>(src, b0 + u) : 0.0f;
     }
   };
   // two LDS buffers: chunk i is computed from buffer i & 1 while chunk i + 1 is written to the other
@@ -875,7 +902,7 @@ k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __re
   auto put = [&](int buf) {
     if (swr) {
 #pragma unroll
-      for (int u = 0; u < kNPL; ++u) lds[buf * bufsz + (se + u) * stride + sc] = v[u];
+      for (int u = 0; u < NPL; ++u) lds[buf * bufsz + (se + u) * stride + sc] = v[u];
     }
   };
   // each workgroup takes a contiguous run of chunks: a 128-byte line split between two chunks is then
@@ -893,18 +920,26 @@ k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __re
     const float* lb = lds + cur * bufsz;
     // packed fp32 (v_pk_add_f32 / v_pk_fma_f32): pair (x, y), (x, y+1) per instruction -- the same
     // per-element IEEE sub and fused multiply-add as the scalar form, half the VALU issue slots
-#pragma unroll 2  // two coordinates' LDS reads in flight (K = 128: 7.0 -> 6.5 ms; 4 was slower)
-    for (int e = e_lo; e < (pact ? e_hi : e_lo); ++e) {
-      const float4 a = *(const float4*)&lb[e * stride + 4 * bi];
-      const float4 b = *(const float4*)&lb[e * stride + 4 * bj];
-      const float av[4] = {a.x, a.y, a.z, a.w};
-      const f32x2 b01 = {b.x, b.y}, b23 = {b.z, b.w};
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const f32x2 ax = {av[x], av[x]};
-        const f32x2 d0 = round_diff<RT>(ax - b01), d1 = round_diff<RT>(ax - b23);
-        acc[2 * x] = __builtin_elementwise_fma(d0, d0, acc[2 * x]);
-        acc[2 * x + 1] = __builtin_elementwise_fma(d1, d1, acc[2 * x + 1]);
+    if (pact && e_hi > e_lo) {
+      // PF: the next coordinate's two 16-byte reads are issued before this one's arithmetic, so the
+      // LDS latency hides behind it (r03c PMC: 39% of wave cycles waiting, lgkmcnt(0) after each read)
+      const float* pa = lb + 4 * bi;
+      const float* pb = lb + 4 * bj;
+      float4 a = *(const float4*)&pa[e_lo * stride];
+      float4 b = *(const float4*)&pb[e_lo * stride];
+#pragma unroll 2
+      for (int e = e_lo; e < e_hi; ++e) {
+        float4 an = a, bn = b;
+        if constexpr (PF) {
+          const int e1 = e + 1 < e_hi ? e + 1 : e;
+          an = *(const float4*)&pa[e1 * stride];
+          bn = *(const float4*)&pb[e1 * stride];
+        } else {
+          a = *(const float4*)&pa[e * stride];
+          b = *(const float4*)&pb[e * stride];
+        }
+        pair_tile<RT>(a, b, acc);
+        if constexpr (PF) { a = an; b = bn; }
       }
     }
     run += e_hi - e_lo;
@@ -925,7 +960,7 @@ k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __re
 
 // waves_per_eu(4): <= 128 VGPRs, the budget at which a CU holds 16 waves (MI355X_MICROARCH.md: waves
 // per CU halve at 64 / 128 VGPRs) -- two 8-wave workgroups of 512 threads (K = 128)
-template <int KPAD, int RT>
+template <int KPAD, int RT, bool PF>
 __global__ void __launch_bounds__(kMaxPairThreads) __attribute__((amdgpu_waves_per_eu(4)))
 k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int kp,
            int64_t nchunks, int ntiles, int esplit, int ce, int rows, double* __restrict__ partial) {
@@ -1025,18 +1060,22 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
     const float* pb = lds + cur * bufsz + off_b;
     // packed fp32 (v_pk_add_f32 / v_pk_fma_f32): pair (x, y), (x, y+1) per instruction -- the same
     // per-element IEEE sub and fused multiply-add as the scalar form, half the VALU issue slots
-#pragma unroll 2  // two coordinates' LDS reads in flight (K = 128: 7.0 -> 6.5 ms; 4 was slower)
-    for (int i = 0; i < (pact ? ce : 0); ++i) {
-      const float4 a = *(const float4*)(pa + i * S);
-      const float4 b = *(const float4*)(pb + i * S);
-      const float av[4] = {a.x, a.y, a.z, a.w};
-      const f32x2 b01 = {b.x, b.y}, b23 = {b.z, b.w};
-#pragma unroll
-      for (int x = 0; x < 4; ++x) {
-        const f32x2 ax = {av[x], av[x]};
-        const f32x2 d0 = round_diff<RT>(ax - b01), d1 = round_diff<RT>(ax - b23);
-        acc[2 * x] = __builtin_elementwise_fma(d0, d0, acc[2 * x]);
-        acc[2 * x + 1] = __builtin_elementwise_fma(d1, d1, acc[2 * x + 1]);
+    if (pact) {
+      float4 a = *(const float4*)pa;
+      float4 b = *(const float4*)pb;
+#pragma unroll 2
+      for (int i = 0; i < ce; ++i) {
+        float4 an = a, bn = b;
+        if constexpr (PF) {  // next coordinate's reads in flight during this one's arithmetic
+          const int i1 = i + 1 < ce ? i + 1 : i;
+          an = *(const float4*)(pa + i1 * S);
+          bn = *(const float4*)(pb + i1 * S);
+        } else {
+          a = *(const float4*)(pa + i * S);
+          b = *(const float4*)(pb + i * S);
+        }
+        pair_tile<RT>(a, b, acc);
+        if constexpr (PF) { a = an; b = bn; }
       }
     }
     run += ce;
@@ -1214,6 +1253,10 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
   rc = stage(slot, seg_bytes + ptr_bytes, st);
   if (rc) return rc;
   const char* dv = (const char*)slot->dev;
+  static const int pf = [] {  // FA_PAIR_PF=0: no register prefetch of the next coordinate (A/B)
+    const char* e = getenv("FA_PAIR_PF");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
   if (f64) {
     hipLaunchKernelGGL(k_pairdist_f64, dim3((unsigned)nblocks), dim3(kBlock), sizeof(double) * kC64 * k, st,
                        (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, nchunks64, (double*)d_scratch);
@@ -1221,7 +1264,9 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
     const size_t lds = pair_lds_bytes(q);
     bool vec = true;  // 16-byte loads: every client segment 16-byte aligned (chunk starts are multiples of 8)
     for (int i = 0; i < j * k; ++i) vec = vec && ((uintptr_t)hp[i] % 16 == 0);
-#define FA_PDL(V, R) hipLaunchKernelGGL((k_pairdist_lane<V, R>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), \
+#define FA_PDL(V, R) if (pf) FA_PDL1(V, R, true); else FA_PDL1(V, R, false)
+#define FA_PDL1(V, R, P) if (q.npl == 16) FA_PDL2(V, R, P, 16); else FA_PDL2(V, R, P, kNPL)
+#define FA_PDL2(V, R, P, NP) hipLaunchKernelGGL((k_pairdist_lane<V, R, P, NP>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), \
       lds, st, (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit, pe,      \
       (double*)d_scratch)
     if (vec) {
@@ -1230,9 +1275,12 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
       if (rt == 1) FA_PDL(false, 1); else if (rt == 2) FA_PDL(false, 2); else FA_PDL(false, 0);
     }
 #undef FA_PDL
+#undef FA_PDL1
+#undef FA_PDL2
   } else {
     const size_t lds = pair_lds_bytes(q);
-#define FA_PD(KPAD, R) hipLaunchKernelGGL((k_pairdist<KPAD, R>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), \
+#define FA_PD(KPAD, R) if (pf) FA_PD2(KPAD, R, true); else FA_PD2(KPAD, R, false)
+#define FA_PD2(KPAD, R, P) hipLaunchKernelGGL((k_pairdist<KPAD, R, P>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), \
       lds, st, (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit, q.ce,   \
       q.rows, (double*)d_scratch)
 #define FA_PDR(KPAD) if (rt == 1) FA_PD(KPAD, 1); else if (rt == 2) FA_PD(KPAD, 2); else FA_PD(KPAD, 0)
@@ -1243,6 +1291,7 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
     }
 #undef FA_PDR
 #undef FA_PD
+#undef FA_PD2
   }
   const dim3 blk(kBlock);
   hipLaunchKernelGGL(k_pairdist_reduce, dim3((unsigned)((npairs + 7) / 8)), blk, 0,

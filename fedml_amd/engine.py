@@ -782,6 +782,35 @@ class AggEngine:
         return out
 
     # ------------------------------------------------------------------ robust aggregation
+    def mt_randint_sum(self, seeds: Sequence[int], signs: Sequence[int], prime: int, n: int,
+                       out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """sum_s sign_s * np.random.RandomState(seed_s).randint(0, prime, size=n), mod prime, as an
+        int64 device tensor (fa_mt_randint_sum: numpy's legacy MT19937 streams expanded on the
+        device, bit-exact) -- SecAgg's mask re-expansion (sa_fedml_aggregator.py:92-136)."""
+        if len(seeds) != len(signs):
+            raise ValueError("mt_randint_sum: one sign per seed")
+        for v in seeds:
+            if not 0 <= int(v) <= 0xFFFFFFFF:
+                raise ValueError("Seed must be between 0 and 2**32 - 1")
+        n = int(n)
+        if out is None:
+            out = torch.empty(max(n, 0), dtype=torch.int64, device=self.device)
+        _require_device(out, self.device, "out")
+        if out.dtype != torch.int64 or out.numel() < n:
+            raise ValueError(f"mt_randint_sum: out must be int64 with >= {n} elements")
+        S = len(seeds)
+        sd = (N.ctypes.c_uint32 * max(S, 1))(*[int(v) for v in seeds])
+        sg = (N.ctypes.c_int8 * max(S, 1))(*[int(v) for v in signs])
+        with self.lock:
+            need = self._lib.fa_mt_randint_sum_scratch_bytes(n)
+            scratch = getattr(self, "_mt_scratch", None)
+            if need and (scratch is None or scratch.numel() < need):
+                scratch = self._mt_scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
+            rc = self._lib.fa_mt_randint_sum(self._ctx, S, sd, sg, int(prime), n, out.data_ptr(),
+                                             scratch.data_ptr() if need else None, need, self._stream(stream))
+        N.check(rc, "fa_mt_randint_sum")
+        return out
+
     def coord_median(self, segments: Sequence[Sequence[torch.Tensor]],
                      outs: Optional[Sequence[torch.Tensor]] = None, stream=None) -> List[torch.Tensor]:
         """Coordinate-wise median over clients (fa_coord_median): segments[s][i] = client i's

@@ -89,6 +89,24 @@ int fa_finite_quantize(fa_ctx *ctx, int dtype, int32_t num_segments, const int64
 int fa_lcc_decode(fa_ctx *ctx, int32_t rows, int32_t k, int64_t m, const int64_t *coef,
                   const void *d_f, int64_t prime, int64_t n_out, void *d_out, void *hip_stream);
 
+/*
+ * SecAgg's mask re-expansion (cross_silo/secagg/sa_fedml_aggregator.py:92-136): numpy's legacy
+ *   np.random.seed(seed_s); R_s = np.random.randint(0, prime, size=n)
+ * for every stream s (MT19937 seeded by init_genrand; each draw 32-bit masked rejection when
+ * prime - 1 <= 0xFFFFFFFF, else 64-bit draws hi << 32 | lo with masked rejection -- numpy's
+ * random_bounded_uint64_fill with use_masked), summed with signs and reduced:
+ *   d_out[e] = mod(sum_s sign_s * R_s[e])    (in [0, prime), int64)
+ * which is what the reference's loop of masks, `np.mod(mask + temp, p)` and `aggregated_mask +=`
+ * leaves (modular sums; every intermediate stays below 2 p).  seeds / signs are HOST arrays of
+ * num_streams entries (seed in [0, 2^32), sign +1 or -1).  d_scratch: at least
+ * fa_mt_randint_sum_scratch_bytes(n) bytes of device memory.  One workgroup of one wave expands
+ * each stream (MT19937 is sequential per stream); the streams run in parallel.
+ */
+int fa_mt_randint_sum(fa_ctx *ctx, int32_t num_streams, const uint32_t *seeds, const int8_t *signs,
+                      int64_t prime, int64_t n, void *d_out, void *d_scratch, size_t scratch_bytes,
+                      void *hip_stream);
+size_t fa_mt_randint_sum_scratch_bytes(int64_t n);
+
 #ifdef __cplusplus
 }
 #endif

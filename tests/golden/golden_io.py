@@ -90,9 +90,13 @@ def expected_dicts(meta: dict, arrays: dict):
     return out
 
 
+RAW_PREFIXES = ("g21_",)  # plain-array fixtures (np.load, their own meta), not load_case's format
+
+
 def list_cases():
     return sorted(
-        os.path.join(GOLDEN_DIR, f) for f in os.listdir(GOLDEN_DIR) if f.endswith(".npz")
+        os.path.join(GOLDEN_DIR, f) for f in os.listdir(GOLDEN_DIR)
+        if f.endswith(".npz") and not f.startswith(RAW_PREFIXES)
     )
 
 

@@ -786,6 +786,33 @@ def cases_secagg():
         WRITTEN.append((name, os.path.getsize(os.path.join(HERE, name + ".npz"))))
 
 
+def cases_sa_mask():
+    """SecAgg's mask re-expansion (cross_silo/secagg/sa_fedml_aggregator.py:92-136), run from the
+    reference itself: BGW decoding of the shares, then numpy's legacy MT19937 streams
+    (np.random.seed + randint) per surviving client (flag set) or per pair of a dropped client --
+    all / none / some flagged, a rejection-heavy prime (40961: 37.5% of draws rejected), d > 624."""
+    _, sa = load_mpc()
+    amr = extract_method("cross_silo/secagg/sa_fedml_aggregator.py", "SecAggAggregator",
+                         "aggregate_mask_reconstruction", {"BGW_decoding": sa.BGW_decoding})
+    rng = np.random.RandomState(4242)
+    for N, p, d, flags in ((4, 2 ** 15 - 19, 3001, "all"), (5, 40961, 2500, "none"), (6, 2 ** 31 - 1, 1500, "some"),
+                           (3, 40961, 700, "some")):
+        T = int(np.floor(N / 2))
+        SS_rx = rng.randint(0, p, size=(N, N)).astype(np.int64)
+        public_key_list = rng.randint(0, p, size=(2, N)).astype(np.int64)
+        active = [int(v) for v in rng.permutation(N)]
+        fl = {i: {"all": True, "none": False, "some": i % 2 == 0}[flags] for i in range(N)}
+        self_ = types.SimpleNamespace(total_dimension=d, privacy_guarantee=T, prime_number=p,
+                                      targeted_number_active_clients=N, flag_client_model_uploaded_dict=dict(fl))
+        mask = amr(self_, active, SS_rx, public_key_list)
+        name = f"g21_sa_mask_{flags}_N{N}_p{p}"
+        np.savez(os.path.join(HERE, name + ".npz"), SS_rx=SS_rx, public_key_list=public_key_list,
+                 active=np.array(active, dtype=np.int64), flags=np.array([fl[i] for i in range(N)]),
+                 mask=np.asarray(mask, dtype=np.int64), meta=np.array(json.dumps(dict(
+                     kind="sa_mask", N=N, T=T, p=p, d=d, ref="cross_silo/secagg/sa_fedml_aggregator.py:92-136"))))
+        WRITTEN.append((name, os.path.getsize(os.path.join(HERE, name + ".npz"))))
+
+
 def load_defenses():
     for name, sub in [("fedml", ""), ("fedml.core", "/core"), ("fedml.core.security", "/core/security"),
                       ("fedml.core.security.common", "/core/security/common"),

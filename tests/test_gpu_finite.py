@@ -162,8 +162,63 @@ def test_secagg_aggregator_golden(path):
     agg.flag_client_model_uploaded_dict = {i: bool(f) for i, f in enumerate(meta["flags"])}
     out = agg.aggregate_model_reconstruction(list(range(N)), list(range(N)), None, None)
     assert_dict_bits(OrderedDict((k, v.cpu()) for k, v in out.items()), exp, "secagg")
-    with pytest.raises(NotImplementedError):
-        SecAggAggregator(None, None, 0, {}, {}, {}, N, DEV, args, tr).aggregate_mask_reconstruction([], None, None)
+
+
+MASKS = sorted(os.path.join(os.path.dirname(__file__), "golden", p)
+               for p in os.listdir(os.path.join(os.path.dirname(__file__), "golden")) if p.startswith("g21_"))
+
+
+def _mask_case(path):
+    import json
+    z = np.load(path)
+    return json.loads(str(z["meta"])), z
+
+
+@pytest.mark.parametrize("path", MASKS, ids=ids)
+def test_secagg_mask_reconstruction_golden(path):
+    """SecAggAggregator.aggregate_mask_reconstruction with no override: BGW decoding on the host and
+    the numpy MT19937 streams expanded on the device (fa_mt_randint_sum) reproduce the reference's
+    aggregate mask bit for bit (g21: all / none / some clients' models arrived; 37.5% rejection)."""
+    from fedml_amd.cross_silo.secagg import SecAggAggregator
+    meta, z = _mask_case(path)
+    N = meta["N"]
+    args = types.SimpleNamespace(prime_number=meta["p"], precision_parameter=8, worker_num=N)
+    agg = SecAggAggregator(None, None, 0, {}, {}, {}, N, DEV, args, None)
+    agg.total_dimension = meta["d"]
+    agg.flag_client_model_uploaded_dict = {i: bool(f) for i, f in enumerate(z["flags"])}
+    got = agg.aggregate_mask_reconstruction([int(v) for v in z["active"]], z["SS_rx"], z["public_key_list"])
+    assert isinstance(got, np.ndarray) and got.dtype == np.int64
+    assert np.array_equal(got, z["mask"])
+
+
+@pytest.mark.parametrize("p", [32749, 40961, 2 ** 31 - 1, 2 ** 32, 2 ** 32 + 15, 2 ** 61 - 1])
+def test_mt_randint_sum_vs_numpy(eng, p):
+    """fa_mt_randint_sum against numpy's own legacy streams at a larger size (n = 200,003, 320 twist
+    blocks per stream): mixed signs, repeated seeds, seed 0 and 2^32 - 1; the 64-bit draw path
+    (p > 2^32) and the stream batching that keeps 64-bit sums from wrapping (p = 2^61 - 1: 7 streams
+    per batch, 11 streams here)."""
+    n = 200_003
+    seeds = [0, 1, 2 ** 32 - 1, 987654321, 5, 5, 31337, 2 ** 31, 77, 1234567, 4242]
+    signs = [1, -1, 1, -1, 1, 1, -1, 1, -1, 1, -1]
+    got = eng.mt_randint_sum(seeds, signs, p, n).cpu().numpy()
+    acc = np.zeros(n, dtype=object)
+    for s, g in zip(seeds, signs):
+        np.random.seed(s)
+        acc = acc + g * np.random.randint(0, p, size=n).astype(object)
+    exp = np.array([int(a) % p for a in acc], dtype=np.int64)
+    assert np.array_equal(got, exp)
+
+
+def test_mt_randint_sum_edges(eng):
+    from oracle import mt_port
+    assert torch.equal(eng.mt_randint_sum([3], [1], 1, 10).cpu(), torch.zeros(10, dtype=torch.int64))  # p = 1
+    assert eng.mt_randint_sum([], [], 7, 5).cpu().tolist() == [0] * 5
+    assert eng.mt_randint_sum([9], [1], 7, 0).numel() == 0
+    for n in (1, 623, 624, 625, 1249):  # around twist-block boundaries
+        got = eng.mt_randint_sum([11, 12], [1, -1], 40961, n).cpu().numpy()
+        assert np.array_equal(got, mt_port.randint_sum([11, 12], [1, -1], 40961, n))
+    with pytest.raises(ValueError):
+        eng.mt_randint_sum([2 ** 32], [1], 7, 3)
 
 
 # ----------------------------------------------------------------------------- vs the C oracle

@@ -141,3 +141,46 @@ def test_numpy_port_matches_golden(path):
     got = secagg_port.lsa_reconstruct(models, arrays["aggregate_mask"], meta["dims"], meta["p"], meta["q_bits"])
     for k in meta["keys"]:
         assert bits_equal(got[k].reshape(-1), exp[k].reshape(-1)), k
+
+
+@pytest.mark.parametrize("p", [2, 7, 32749, 40961, 2**31 - 1, 2**32, 2**32 + 15, 2**61 - 1])
+def test_mt_port_matches_numpy_legacy_randint(p):
+    """oracle/mt_port.py (the restatement of numpy's legacy seeding, MT19937 and masked bounded
+    draws) reproduces np.random.seed(s); np.random.randint(0, p, size=n) exactly, including the
+    32-bit (p - 1 <= 2^32 - 1) and 64-bit draw paths and heavy rejection (p = 40961: 37.5%)."""
+    from oracle import mt_port
+    for seed in (0, 1, 12345, 2**32 - 1):
+        for n in (1, 623, 624, 625, 2000):
+            np.random.seed(seed)
+            exp = np.random.randint(0, p, size=n).astype(int)
+            got = mt_port.randint(seed, p, n)
+            assert np.array_equal(got, exp), (p, seed, n)
+
+
+def test_mt_port_seed_bounds_like_numpy():
+    from oracle import mt_port
+    for bad in (-1, 2**32):
+        with pytest.raises(ValueError) as e1:
+            np.random.seed(bad)
+        with pytest.raises(ValueError) as e2:
+            mt_port.seed_state(bad)
+        assert str(e1.value) == str(e2.value)
+
+
+MASK_CASES = sorted(p for p in os.listdir(os.path.join(os.path.dirname(__file__), "golden")) if p.startswith("g21_"))
+
+
+@pytest.mark.parametrize("name", MASK_CASES)
+def test_sa_mask_streams_and_oracle_match_reference(name):
+    """The host half of SecAgg's mask re-expansion (BGW decoding -> (seed, sign) streams,
+    fedml_amd/core/mpc/secagg.py) with the oracle's expansion of those streams reproduces the
+    reference's aggregate_mask_reconstruction (g21, generated from the reference)."""
+    import json
+    from oracle import mt_port
+    from fedml_amd.core.mpc.secagg import mask_streams
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", name))
+    meta = json.loads(str(z["meta"]))
+    seeds, signs = mask_streams(meta["N"], list(z["flags"]), [int(v) for v in z["active"]], z["SS_rx"],
+                                z["public_key_list"], meta["T"], meta["p"])
+    got = mt_port.randint_sum(seeds, signs, meta["p"], meta["d"])
+    assert np.array_equal(got, z["mask"])
