@@ -55,7 +55,7 @@ def parse():
     p.add_argument("--config", default="metric",
                    choices=["metric", "fragmented", "resnet18", "vit_bf16", "hier", "gossip", "host", "secagg", "fedopt",
                             "dropin_cpu", "median",
-                            "krum", "arrival", "lr"])
+                            "krum", "arrival", "lr", "samask"])
     p.add_argument("--clients", type=int, default=None)
     p.add_argument("--params", type=int, default=None)
     p.add_argument("--variant", type=int, default=0, help="kernel variant (fa_ctx_set_variant)")
@@ -1318,6 +1318,72 @@ def wl_secagg(args, eng, rank, world, timer):
                               "counts the LCC mask decoding (U x m int64 in, P int64 out)")
 
 
+def wl_samask(args, eng, rank, world, timer):
+    """§8(f) #4, r03: SecAgg's server mask re-expansion (cross_silo/secagg/sa_fedml_aggregator.py:92-136)
+    for N = K clients of ResNet-18 size: every surviving client's numpy MT19937 stream
+    (np.random.seed(b_u); randint(0, p, d)) and, for each dropped client, its N - 1 pairwise streams,
+    summed mod p -- fa_mt_randint_sum, one wave per stream.  BGW decoding (a few scalars per client) is
+    host work outside the step.  ``--variant`` = dropped clients (default 0).  value = latency (ms)."""
+    if world > 1:
+        raise SystemExit("samask config: single GPU")
+    K = args.clients or 32
+    P = args.params or RESNET18_P
+    p = 2 ** 31 - 1
+    dropped = max(0, min(K, args.variant))
+    rng = np.random.RandomState(5)
+    seeds, signs = [], []
+    for i in range(K):
+        if i >= dropped:  # model arrived: its own mask stream
+            seeds.append(int(rng.randint(0, 2 ** 31 - 1)))
+            signs.append(1)
+        else:  # dropped: its pairwise streams, sign by index order
+            for j in range(K):
+                if j != i:
+                    seeds.append(int(rng.randint(0, 2 ** 31 - 1)))
+                    signs.append(-1 if j < i else 1)
+    out = torch.empty(P, dtype=torch.int64, device="cuda")
+    state = {}
+
+    def step():
+        t0 = time.perf_counter()
+        with timer:
+            eng.mt_randint_sum(seeds, signs, p, P, out=out)
+        torch.cuda.current_stream().synchronize()
+        state["out"] = out
+        return time.perf_counter() - t0
+
+    def parity():
+        n = min(P, 100_000)  # a prefix: the first n draws of a stream do not depend on its length
+        acc = np.zeros(n, dtype=object)
+        for s_, g_ in zip(seeds, signs):
+            np.random.seed(s_)
+            acc = acc + g_ * np.random.randint(0, p, size=n).astype(object)
+        exp = np.array([int(a) % p for a in acc], dtype=np.int64)
+        ok = np.array_equal(out[:n].cpu().numpy(), exp)
+        return (f"{'bit-exact' if ok else 'MISMATCH'} vs numpy's own legacy streams (np.random.seed + randint, "
+                f"the reference's calls) summed mod p, on the first {n} elements of all {len(seeds)} streams")
+
+    def cpu(budget_s):
+        """The reference's loop body for surviving clients (seed, randint, +=, mod) on a sample of
+        streams, scaled to all streams (each stream is sequential, numpy runs one at a time)."""
+        ns = max(1, min(len(seeds), 4))
+        t0 = time.perf_counter()
+        agg = 0
+        for s_ in seeds[:ns]:
+            np.random.seed(s_)
+            agg = np.mod(agg + np.random.randint(0, p, size=P).astype(int), p)
+        dt = (time.perf_counter() - t0) / ns
+        return {"value": round(dt * len(seeds) * 1e3, 2), "unit": "ms", "cores": 1, "kind": "reference",
+                "sample": f"{ns} of {len(seeds)} streams of np.random.seed + np.random.randint(0, p, size={P}) + "
+                          "np.mod accumulate (numpy, the reference's own calls, sa_fedml_aggregator.py:104-107), "
+                          "timed and scaled to all streams"}
+
+    return dict(name=f"secagg_mask_expand_N{K}_dropped{dropped}_P{P}_int64", dtype="u32 (MT19937) -> int64", step=step,
+                parity=parity, cpu=cpu, latency=True, stat="median", clients=K, params=P, cpu_K=K, bytes_total=None,
+                launch_bytes=None, metric_name=f"SecAgg mask re-expansion latency, {len(seeds)} streams x {P} draws",
+                data=f"{len(seeds)} MT19937 streams (seeds from RandomState(5)), p = 2^31 - 1")
+
+
 def _robust_inputs(K, P):
     Ppad = -(-P // 64) * 64  # ClientArena row alignment
     g = torch.Generator(device="cuda").manual_seed(21)
@@ -1608,7 +1674,8 @@ def main():
     timer = Timed()
     wl = {"metric": wl_metric, "fragmented": wl_fragmented, "resnet18": wl_layout, "vit_bf16": wl_layout, "hier": wl_hier,
           "gossip": wl_gossip, "host": wl_host, "secagg": wl_secagg, "fedopt": wl_fedopt, "dropin_cpu": wl_dropin_cpu, "median": wl_median,
-          "krum": wl_krum, "arrival": wl_arrival, "lr": wl_lr}[args.config](args, eng, rank, world, timer)
+          "krum": wl_krum, "arrival": wl_arrival, "lr": wl_lr, "samask": wl_samask}[args.config](args, eng, rank, world,
+                                                                                               timer)
 
     for i in range(args.warmup):
         stage(f"warmup step {i}")
