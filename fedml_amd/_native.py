@@ -39,7 +39,7 @@ EXPORTED_SYMBOLS = (
     "fa_coord_median", "fa_pairwise_sqdist", "fa_pairwise_sqdist_rt", "fa_pairwise_sqdist_scratch_bytes",
     # include/fedagg_comm.h
     "fa_comm_unique_id", "fa_comm_init", "fa_comm_wrap", "fa_comm_destroy", "fa_comm_size", "fa_local_out_dtype",
-    "fa_group_plan", "fa_group_reduce_scratch_bytes", "fa_group_reduce", "fa_comm_set_timing", "fa_comm_local_time",
+    "fa_group_plan", "fa_group_ops", "fa_group_reduce_scratch_bytes", "fa_group_reduce", "fa_comm_set_timing", "fa_comm_local_time",
     "fa_comm_last_op",
 )
 
@@ -186,6 +186,10 @@ def _declare(L):
     L.fa_group_plan.restype = ctypes.c_int
     L.fa_group_plan.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                 ctypes.c_int32, _P_i64, _P_i64, _P_i64, _P_i64]
+    L.fa_group_ops.restype = ctypes.c_int
+    L.fa_group_ops.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                               ctypes.c_int32, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P_i32,
+                               _P_i32, _P_i32, _P_i64, _P_i64]
     L.fa_group_reduce_scratch_bytes.restype = ctypes.c_int
     L.fa_group_reduce_scratch_bytes.argtypes = [_vp, ctypes.c_int, _P_ls, ctypes.c_int64, ctypes.c_int32,
                                                 ctypes.c_int32, ctypes.c_int32, _P_i64]

@@ -145,6 +145,36 @@ void make_plan(int64_t n, int32_t chunks, int32_t align, int world, int root, in
   }
 }
 
+// One point-to-point operation of the ordered exchange, as the executor issues it.
+struct P2p {
+  int peer;
+  bool send;
+  int buf;         // FA_XBUF_*: the send buffer (partials), the recv buffer, or d_out
+  int64_t offset;  // elements into that buffer
+  int64_t count;   // elements
+};
+
+// The ops of rank `me` in chunk ch: phase 0 = partials to the owners (communicator 1), phase 1 = the
+// summed pieces to the root / to every rank (communicator 2).  A pure function of the plan: every
+// rank derives its sends and its peers' matching receives from the same plan (fa_group_ops exports it
+// for the CPU test that pairs them up and replays the data movement).
+void xchg_ops(const Plan& p, int world, int me, int root, bool to_all, int phase, int64_t ch, std::vector<P2p>& ops) {
+  ops.clear();
+  const int64_t L_me = p.psize[ch * world + me], s_me = p.pstart[ch * world + me];
+  const int64_t r0 = world * p.roff[ch];
+  for (int r = 0; r < world; ++r) {
+    if (r == me) continue;
+    const int64_t Lr = p.psize[ch * world + r], sr = p.pstart[ch * world + r];
+    if (phase == 0) {
+      if (Lr) ops.push_back(P2p{r, true, FA_XBUF_SEND, sr, Lr});
+      if (L_me) ops.push_back(P2p{r, false, FA_XBUF_RECV, r0 + r * L_me, L_me});
+    } else {
+      if ((to_all || me == root) && Lr) ops.push_back(P2p{r, false, FA_XBUF_OUT, sr, Lr});
+      if (L_me && (to_all || r == root)) ops.push_back(P2p{r, true, FA_XBUF_OUT, s_me, L_me});
+    }
+  }
+}
+
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 struct Scratch {
@@ -256,35 +286,38 @@ int ordered(fa_ctx* ctx, fa_comm* c, bool to_all, const fa_local_step* L, int64_
   if (!rc) rc = order(c, st, c->sb);
   if (rc) return rc;
 
+  std::vector<P2p> ops;
+  char* bufs[3] = {(char*)send, recv, out};
+  auto issue = [&](const std::vector<P2p>& list, ncclComm_t comm, hipStream_t s, const char* what) -> int {
+    ncclResult_t res = ncclGroupStart();
+    for (size_t q = 0; q < list.size() && res == ncclSuccess; ++q) {
+      const P2p& o = list[q];
+      char* ptr = bufs[o.buf] + o.offset * osz;
+      res = o.send ? ncclSend(ptr, (size_t)o.count, nt, o.peer, comm, s) : ncclRecv(ptr, (size_t)o.count, nt, o.peer, comm, s);
+    }
+    const ncclResult_t end = ncclGroupEnd();  // closes the group whatever happened inside it
+    if (res != ncclSuccess) return fail(FA_ERR_COMM, "%s send/recv: %s", what, ncclGetErrorString(res));
+    if (end != ncclSuccess) return fail(FA_ERR_COMM, "%s ncclGroupEnd: %s", what, ncclGetErrorString(end));
+    return FA_OK;
+  };
+
   auto finish = [&](int64_t ch) -> int {  // owners' sum of chunk ch, then its delivery
     const int64_t L_me = p.psize[ch * world + me], s_me = p.pstart[ch * world + me];
     const int64_t r0 = world * p.roff[ch];
-    FA_HIP(hipStreamWaitEvent(st, after_a2a[ch], 0));
-    if (L_me) {
+    if (L_me) {  // a rank with no piece (the root) neither waits for its sends nor orders its receives
+      FA_HIP(hipStreamWaitEvent(st, after_a2a[ch], 0));  // behind the S(um)'s own stream, not the host
       for (int r = 0; r < world; ++r)
         sum_in[r] = r == me ? (const void*)(send + s_me * osz) : (const void*)(recv + (r0 + r * L_me) * osz);
       int rc2 = fa_weighted_sum(ctx, fa_local_out_dtype(L->dtype, L->mode), FA_MODE_SUM, L_me, world, sum_in.data(),
                                 nullptr, 1.0, out + s_me * osz, st);
       if (rc2) return rc2;
+      rc2 = order(c, st, c->sb);
+      if (rc2) return rc2;
     }
-    int rc2 = order(c, st, c->sb);
-    if (rc2) return rc2;
     set_op(c, "chunk %lld/%lld: delivery of the summed pieces %s", (long long)(ch + 1), (long long)p.C,
            to_all ? "to every rank" : "to the root");
-    FA_NCCL(ncclGroupStart());
-    ncclResult_t res = ncclSuccess;
-    for (int r = 0; r < world && res == ncclSuccess; ++r) {
-      if (r == me) continue;
-      const int64_t Lr = p.psize[ch * world + r], sr = p.pstart[ch * world + r];
-      const bool i_recv = to_all || me == root;
-      const bool i_send = L_me && (to_all || r == root);
-      if (i_recv && Lr) res = ncclRecv(out + sr * osz, (size_t)Lr, nt, r, c->c2, c->sb);
-      if (res == ncclSuccess && i_send) res = ncclSend(out + s_me * osz, (size_t)L_me, nt, r, c->c2, c->sb);
-    }
-    ncclResult_t end = ncclGroupEnd();
-    if (res != ncclSuccess) return fail(FA_ERR_COMM, "delivery send/recv: %s", ncclGetErrorString(res));
-    if (end != ncclSuccess) return fail(FA_ERR_COMM, "delivery ncclGroupEnd: %s", ncclGetErrorString(end));
-    return FA_OK;
+    xchg_ops(p, world, me, root, to_all, 1, ch, ops);
+    return issue(ops, c->c2, c->sb, "delivery");
   };
 
   for (int64_t ch = 0; ch < p.C; ++ch) {
@@ -298,17 +331,9 @@ int ordered(fa_ctx* ctx, fa_comm* c, bool to_all, const fa_local_step* L, int64_
     const int64_t L_me = p.psize[ch * world + me], r0 = world * p.roff[ch];
     set_op(c, "chunk %lld/%lld: partials to the owners (point-to-point over every link)", (long long)(ch + 1),
            (long long)p.C);
-    FA_NCCL(ncclGroupStart());
-    ncclResult_t res = ncclSuccess;
-    for (int r = 0; r < world && res == ncclSuccess; ++r) {
-      if (r == me) continue;
-      const int64_t Lr = p.psize[ch * world + r], sr = p.pstart[ch * world + r];
-      if (Lr) res = ncclSend(send + sr * osz, (size_t)Lr, nt, r, c->c1, c->sa);
-      if (res == ncclSuccess && L_me) res = ncclRecv(recv + (r0 + r * L_me) * osz, (size_t)L_me, nt, r, c->c1, c->sa);
-    }
-    ncclResult_t end = ncclGroupEnd();
-    if (res != ncclSuccess) return fail(FA_ERR_COMM, "owner send/recv: %s", ncclGetErrorString(res));
-    if (end != ncclSuccess) return fail(FA_ERR_COMM, "owner ncclGroupEnd: %s", ncclGetErrorString(end));
+    xchg_ops(p, world, me, root, to_all, 0, ch, ops);
+    rc = issue(ops, c->c1, c->sa, "owner");
+    if (rc) return rc;
     rc = event(c, &after_a2a[ch]);
     if (rc) return rc;
     FA_HIP(hipEventRecord(after_a2a[ch], c->sa));
@@ -511,6 +536,28 @@ int fa_group_plan(int64_t n, int32_t chunks, int32_t align, int32_t world, int32
     }
   }
   return (int)p.C;
+}
+
+int fa_group_ops(int64_t n, int32_t chunks, int32_t align, int32_t world, int32_t rank, int32_t root, int deliver_all,
+                 int32_t phase, int32_t chunk, int32_t max_ops, int32_t* peer, int32_t* is_send, int32_t* buf,
+                 int64_t* offset, int64_t* count) {
+  if (n < 0 || chunks < 1 || align < 1 || world < 1 || rank < 0 || rank >= world || root < 0 || root >= world ||
+      (phase != 0 && phase != 1) || chunk < 0)
+    return fail(FA_ERR_INVALID, "fa_group_ops: invalid arguments");
+  Plan p;
+  make_plan(n, chunks, align, world, root, rank, &p);
+  if (chunk >= p.C) return fail(FA_ERR_INVALID, "fa_group_ops: chunk %d of %lld", chunk, (long long)p.C);
+  std::vector<P2p> ops;
+  if (world > 1) xchg_ops(p, world, rank, root, deliver_all != 0, phase, chunk, ops);
+  if ((int64_t)ops.size() > max_ops) return fail(FA_ERR_INVALID, "fa_group_ops: %zu ops > max_ops", ops.size());
+  for (size_t q = 0; q < ops.size(); ++q) {
+    if (peer) peer[q] = ops[q].peer;
+    if (is_send) is_send[q] = ops[q].send;
+    if (buf) buf[q] = ops[q].buf;
+    if (offset) offset[q] = ops[q].offset;
+    if (count) count[q] = ops[q].count;
+  }
+  return (int)ops.size();
 }
 
 int fa_group_reduce_scratch_bytes(const fa_comm* c, int exchange, const fa_local_step* L, int64_t n,

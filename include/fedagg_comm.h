@@ -121,6 +121,22 @@ int fa_local_out_dtype(int dtype, int mode);
 int fa_group_plan(int64_t n, int32_t chunks, int32_t align, int32_t world, int32_t root, int32_t max_chunks,
                   int64_t *chunk_lo, int64_t *chunk_hi, int64_t *piece_start, int64_t *piece_size);
 
+/* Buffers of the ordered exchange's point-to-point operations (fa_group_ops). */
+enum fa_xchg_buf { FA_XBUF_SEND = 0, FA_XBUF_RECV = 1, FA_XBUF_OUT = 2 };
+
+/*
+ * The point-to-point operations rank `rank` issues for chunk `chunk` of the ordered exchanges
+ * (phase 0: every rank's partial pieces to the owners, on the first communicator; phase 1: the
+ * owners' summed pieces to the root, or to every rank with deliver_all), exactly as
+ * fa_group_reduce issues them: op q goes to/from peer[q] (is_send[q]), count[q] elements at
+ * offset[q] of buffer buf[q] (FA_XBUF_SEND: this rank's partial, FA_XBUF_RECV: the receive area,
+ * rank-major per piece, FA_XBUF_OUT: d_out).  A pure function (no device): a binding or a test
+ * can check that every rank's sends meet their peers' receives.  Returns the op count or < 0.
+ */
+int fa_group_ops(int64_t n, int32_t chunks, int32_t align, int32_t world, int32_t rank, int32_t root, int deliver_all,
+                 int32_t phase, int32_t chunk, int32_t max_ops, int32_t *peer, int32_t *is_send, int32_t *buf,
+                 int64_t *offset, int64_t *count);
+
 /* Bytes of device scratch fa_group_reduce needs for these arguments (on this rank). */
 int fa_group_reduce_scratch_bytes(const fa_comm *comm, int exchange, const fa_local_step *local, int64_t n,
                                   int32_t chunks, int32_t align, int32_t root, int64_t *bytes);

@@ -1,6 +1,8 @@
 # r03i: finite (SecAgg mask) tests, SecAgg mask bench, then the Krum A/B (r03g)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r03i; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_distributed.py -x -q --timeout 120 --timeout-method thread > $O/dist.log 2>&1 || { tail -40 $O/dist.log; exit 1; }
+tail -1 $O/dist.log
 timeout -k 10 300 python -u -m pytest tests/test_gpu_finite.py -x -q --timeout 120 --timeout-method thread > $O/finite.log 2>&1 || { tail -40 $O/finite.log; exit 1; }
 tail -1 $O/finite.log
 for D in 0 4; do
