@@ -1707,9 +1707,9 @@ def main():
     launch_bytes = wl["launch_bytes"]
     if wl.get("step_bytes"):  # several launches per step: this rank's bytes over the summed kernel time
         kernel_ms, launch_bytes = timer.per_step_ms(args.steps), wl["step_bytes"]
-    elif launch_bytes is None and kernel_ms:  # layout configs: the whole aggregate() call per step
+    elif launch_bytes is None and kernel_ms and wl.get("bytes_total"):  # layout configs: the whole call per step
         launch_bytes = wl["bytes_total"] / world
-    achieved = launch_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms else None
+    achieved = launch_bytes / (kernel_ms * 1e-3) / 1e9 if kernel_ms and launch_bytes else None
     parity = wl["parity"]()
     cpu = None
     stage("cpu baseline")

@@ -426,43 +426,27 @@ __device__ __forceinline__ uint32_t mt_mix(uint32_t cur, uint32_t next, uint32_t
   return far ^ (y >> 1) ^ ((y & 1u) ? kMtA : 0u);
 }
 
-// numpy mt19937_gen over the state in LDS (one wave, lane = 0..63)
-__device__ __forceinline__ void mt_twist(uint32_t* mt, int lane) {
-  uint32_t nv[4];
+// numpy mt19937_gen, out of place: B = the generation after A (one wave, lane = 0..63).  Written to
+// another buffer, the recurrence needs no read-before-write split: [0, 227) reads A only, [227, 454)
+// reads A and B[0, 227), [454, 624) reads A and B[227, 397) and B[0] -- one barrier per range.
+__device__ __forceinline__ void mt_next_block(const uint32_t* A, uint32_t* B, int lane) {
+  constexpr int a = kMtN - kMtM;  // 227
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {  // [0, 227): mt[i + 397] is old
+  for (int r = 0; r < 4; ++r) {
     const int i = r * 64 + lane;
-    if (i < kMtN - kMtM) nv[r] = mt_mix(mt[i], mt[i + 1], mt[i + kMtM]);
+    if (i < a) B[i] = mt_mix(A[i], A[i + 1], A[i + kMtM]);
   }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int i = r * 64 + lane;
-    if (i < kMtN - kMtM) mt[i] = nv[r];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {  // [227, 454): mt[i - 227] is new
-    const int i = kMtN - kMtM + r * 64 + lane;
-    if (i < 2 * (kMtN - kMtM)) nv[r] = mt_mix(mt[i], mt[i + 1], mt[i + kMtM - kMtN]);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int i = kMtN - kMtM + r * 64 + lane;
-    if (i < 2 * (kMtN - kMtM)) mt[i] = nv[r];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < 3; ++r) {  // [454, 624): mt[i - 227] and (i = 623) mt[0] are new
-    const int i = 2 * (kMtN - kMtM) + r * 64 + lane;
-    if (i < kMtN) nv[r] = mt_mix(mt[i], i + 1 < kMtN ? mt[i + 1] : mt[0], mt[i + kMtM - kMtN]);
+    const int i = a + r * 64 + lane;
+    if (i < 2 * a) B[i] = mt_mix(A[i], A[i + 1], B[i - a]);
   }
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < 3; ++r) {
-    const int i = 2 * (kMtN - kMtM) + r * 64 + lane;
-    if (i < kMtN) mt[i] = nv[r];
+    const int i = 2 * a + r * 64 + lane;
+    if (i < kMtN) B[i] = mt_mix(A[i], i + 1 < kMtN ? A[i + 1] : B[0], B[i - a]);
   }
   __syncthreads();
 }
@@ -471,39 +455,45 @@ template <bool WIDE>
 __global__ void __launch_bounds__(64)
 k_mt_randint(const uint32_t* __restrict__ seeds, const int8_t* __restrict__ signs, uint64_t rng, uint64_t mask,
              uint64_t p, int64_t n, unsigned long long* __restrict__ acc) {
-  __shared__ uint32_t mt[kMtN];
+  __shared__ uint32_t mt[2][kMtN];  // the last two generations of the state
   const int lane = threadIdx.x;
   const int s = blockIdx.x;
   const bool neg = signs[s] < 0;
   if (lane == 0) {  // numpy mt19937_seed (init_genrand): a serial recurrence, 624 steps
     uint32_t x = seeds[s];
     for (int i = 0; i < kMtN; ++i) {
-      mt[i] = x;
+      mt[0][i] = x;
       x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)(i + 1);
     }
   }
   __syncthreads();
   int64_t count = 0;  // draws accepted so far (wave-uniform)
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  constexpr int kVals = WIDE ? kMtN / 2 : kMtN;  // candidate values per twist (64-bit: word pairs)
+  constexpr int kVals = WIDE ? kMtN / 2 : kMtN;  // candidate values per generation (64-bit: word pairs)
+  constexpr int kRounds = (kVals + 63) / 64;
+  int cur = 0;
   while (count < n) {
-    mt_twist(mt, lane);
-#pragma unroll 1
-    for (int r = 0; r * 64 < kVals && count < n; ++r) {
+    mt_next_block(mt[cur], mt[cur ^ 1], lane);
+    cur ^= 1;
+    const uint32_t* w32 = mt[cur];
+    uint64_t v[kRounds];
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {  // every read of the block in flight at once
       const int w = r * 64 + lane;
-      bool ok = false;
-      uint64_t v = 0;
       if (w < kVals) {
-        if constexpr (WIDE) {
-          v = ((uint64_t)mt_temper(mt[2 * w]) << 32 | mt_temper(mt[2 * w + 1])) & mask;
-        } else {
-          v = mt_temper(mt[w]) & (uint32_t)mask;
-        }
-        ok = v <= rng;
+        if constexpr (WIDE) v[r] = (uint64_t)mt_temper(w32[2 * w]) << 32 | mt_temper(w32[2 * w + 1]);
+        else v[r] = mt_temper(w32[w]);
+        v[r] &= mask;
+      } else {
+        v[r] = ~0ull;  // past the block: never accepted (> rng)
       }
+    }
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+      const bool ok = v[r] <= rng;
       const uint64_t bal = __ballot(ok);
       const int64_t pos = count + __popcll(bal & below);
-      if (ok && pos < n && v != 0) atomicAdd(acc + pos, (unsigned long long)(neg ? p - v : v));
+      if (ok && pos < n && v[r] != 0) atomicAdd(acc + pos, (unsigned long long)(neg ? p - v[r] : v[r]));
       count += __popcll(bal);
     }
   }

@@ -597,11 +597,12 @@ constexpr int kNPL = 8;       // k_pairdist_lane: coordinates of one client stag
 // thread (r02: K = 64 / 100 / 128: 2.59 / 3.99 / 6.58 -> 2.0 / 3.7 / 6.38 ms; at K <= 32 the
 // per-element form's extra instructions cost more than its coalescing gains).
 struct PairSplit { int kp, kpad, nb, ntiles, esplit, nthreads, rows, ce, pe, nblocks, dgroups, npl; bool lane; };
-// k_pairdist_lane: coordinates staged per lane and chunk, kNPL or 16 (FA_PAIR_NPL=16, A/B)
+// k_pairdist_lane: coordinates staged per lane and chunk, 16 (r03g interleaved A/B, 2 x 2 runs: K = 16 /
+// 32 0.214-0.217 / 0.580-0.597 ms at 8 -> 0.195-0.196 / 0.533-0.561 at 16); FA_PAIR_NPL=8 restores kNPL
 int pair_npl() {
   static const int v = [] {
     const char* e = getenv("FA_PAIR_NPL");
-    return e && atoi(e) == 16 ? 16 : kNPL;
+    return e && atoi(e) == kNPL ? kNPL : 16;
   }();
   return v;
 }
@@ -1253,9 +1254,13 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
   rc = stage(slot, seg_bytes + ptr_bytes, st);
   if (rc) return rc;
   const char* dv = (const char*)slot->dev;
-  static const int pf = [] {  // FA_PAIR_PF=0: no register prefetch of the next coordinate (A/B)
+  // FA_PAIR_PF=1: the next coordinate's LDS reads issued before this one's arithmetic.  Off by default:
+  // r03g interleaved A/B, 2 x 2 runs, slower at every K (K = 32 / 64 / 128: 0.580-0.597 / 1.591-1.592 /
+  // 4.97-5.00 ms without vs 0.598-0.616 / 1.627-1.634 / 5.12-5.14 with) -- at 16 waves per CU the LDS
+  // latency is hidden by the other waves, and the extra 8 VGPRs of operands cost more
+  static const int pf = [] {
     const char* e = getenv("FA_PAIR_PF");
-    return e && e[0] == '0' ? 0 : 1;
+    return e && e[0] == '1' ? 1 : 0;
   }();
   if (f64) {
     hipLaunchKernelGGL(k_pairdist_f64, dim3((unsigned)nblocks), dim3(kBlock), sizeof(double) * kC64 * k, st,
