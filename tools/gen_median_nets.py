@@ -101,17 +101,18 @@ def main(path):
         body.append(f"// B = {B}: {ops} min/max ops\n" + code)
     body.append("template <int B, typename K> __device__ __forceinline__ K select_mid(const K (&x)[B]) {\n"
                 "  return MidNet<B>::run(x);\n}")
-    # k_median_2l (robust.hip): a column's B keys split over two lanes, N = B/2 each; every lane sorts
-    # its N keys in place (all N outputs are used: the lower lane merges its own with the upper
-    # lane's).  Network: odd-even merge sort of 64 with the 64 - N extra inputs compile-time high
-    # sentinels folded away (a comparator with a constant input is a renaming).
+    # k_median_2l / k_median_4l (robust.hip): a column's B keys split over two (four) lanes, N = B/2
+    # (B/4) keys each; every lane sorts its N keys in place (all N outputs are used by the merge).
+    # Network: odd-even merge sort of the next power of two >= N with the extra inputs compile-time
+    # high sentinels folded away (a comparator with a constant input is a renaming).
     lines = ["template <int N> struct SortNet;"]
     counts2 = {}
-    for N in range(36, 65, 4):
-        pos = [("x", i) for i in range(N)] + [("H",)] * (64 - N)
+    for N in [32] + list(range(36, 65, 4)):
+        P2 = 1 << (N - 1).bit_length()  # network of the next power of two (32 for N = 32)
+        pos = [("x", i) for i in range(N)] + [("H",)] * (P2 - N)
         ops = []
         tmp = 0
-        for i, j in oddeven_merge_sort(64):
+        for i, j in oddeven_merge_sort(P2):
             a, b = pos[i], pos[j]
             if a[0] == "H" and b[0] == "H":
                 continue
@@ -136,7 +137,7 @@ def main(path):
         L += ["  }", "};"]
         lines.append("\n".join(L))
         counts2[N] = 2 * len(ops)
-    body.append("// SortNet<N>::run(x): x[0..N-1] ascending (k_median_2l); min/max per N: " + str(counts2) +
+    body.append("// SortNet<N>::run(x): x[0..N-1] ascending (k_median_2l, k_median_4l); min/max per N: " + str(counts2) +
                 "\n" + "\n\n".join(lines))
     hdr = (
         "// median_nets.h -- GENERATED by tools/gen_median_nets.py; do not edit.\n"
