@@ -85,6 +85,7 @@ struct fa_ctx {
   void* zc_dev = nullptr;
   size_t zc_cap = 0;
   hipEvent_t zc_ev = nullptr;
+  unsigned long long zc_seq = 0;  // completion word (first 256 bytes of zc_host) of the one-workgroup path
 };
 
 namespace fa_detail {

@@ -22,6 +22,9 @@
 //    so "acc = t_0" needs no select.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+#include <chrono>
+
 #include <mutex>
 
 #include <algorithm>
@@ -1307,6 +1310,111 @@ int wsum_impl(fa_ctx* ctx, int dtype, int mode, int32_t num_segments, const int6
 }
 }  // namespace
 
+extern "C++" {
+namespace {
+// One workgroup over a whole small round whose buffers sit in mapped host memory: the flattened
+// 16-byte vectors of every segment (Seg.tile_start = the segment's first vector), S vectors per
+// thread and U clients per group with all their loads in flight before any is consumed (each group
+// costs one PCIe round trip), the ordered term/accum of wsum_tile, then every thread's stores are
+// made visible to the host before thread 0 stores `seq` into the completion word.
+constexpr int kHost1Threads = 1024;
+template <int DT, int MODE>
+__global__ void __launch_bounds__(kHost1Threads)
+k_wsum_host1(const InlineDesc dsc, int nseg, int coef_off, int ptr_off, int k, double divisor, int64_t total_vec,
+             unsigned long long* done, unsigned long long seq) {
+  using T = Tr<DT, MODE>;
+  using A = typename T::A;
+  using R = typename T::R;
+  constexpr int V = T::V, S = 2, U = 4;
+  // the tables into LDS with one load per thread (lookups then cost no kernarg round trips)
+  __shared__ u32x4 tab[kInlineBytes / 16];
+  if (threadIdx.x < kInlineBytes / 16) tab[threadIdx.x] = ((const u32x4*)dsc.raw)[threadIdx.x];
+  __syncthreads();
+  const char* b = (const char*)tab;
+  const Seg* segs = (const Seg*)b;
+  const double* coef = (const double*)(b + coef_off);
+  const void* const* ptrs = (const void* const*)(b + ptr_off);
+  const typename T::D d = T::div(divisor);
+  for (int64_t base = 0; base < total_vec; base += (int64_t)kHost1Threads * S) {
+    int64_t g[S];
+    int si[S];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      g[s] = base + s * kHost1Threads + threadIdx.x;
+      si[s] = g[s] < total_vec ? find_seg(segs, nseg, g[s]) : -1;
+    }
+    A acc[S][V];
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[s][v] = T::zero();
+    for (int i0 = 0; i0 < k; i0 += U) {
+      u32x4 r[S][U];
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (si[s] < 0) continue;
+        const Seg& sg = segs[si[s]];
+        const int64_t boff = (g[s] - sg.tile_start) * 16;  // each client's slice is padded to 16 bytes
+#pragma unroll
+        for (int u = 0; u < U; ++u) r[s][u] = ld16<false>((const char*)ptrs[sg.ptr_base + min(i0 + u, k - 1)] + boff);
+      }
+#pragma unroll
+      for (int s = 0; s < S; ++s) {
+        if (si[s] < 0) continue;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (i0 + u < k) {
+            const typename T::C c = T::coef(coef[i0 + u]);
+            R x[V];
+            T::unpack(r[s][u], x);
+#pragma unroll
+            for (int v = 0; v < V; ++v) acc[s][v] = accum<DT, MODE>(acc[s][v], term<DT, MODE>(x[v], c, d));
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+      if (si[s] < 0) continue;
+      const Seg& sg = segs[si[s]];
+      const int64_t e0 = (g[s] - sg.tile_start) * V;
+      if (e0 + V <= sg.numel) {
+        T::stv((char*)sg.out + e0 * T::OUT_BYTES, acc[s]);
+      } else {
+#pragma unroll
+        for (int v = 0; v < V; ++v)
+          if (e0 + v < sg.numel) T::st1(sg.out, e0 + v, acc[s][v]);
+      }
+    }
+  }
+  __threadfence_system();  // this thread's result stores are visible to the host
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+template <int DT>
+void launch_host1(int mode, hipStream_t st, const InlineDesc& dsc, int nseg, int co, int po, int k, double divisor,
+                  int64_t total_vec, unsigned long long* done, unsigned long long seq) {
+  const dim3 g(1), b(kHost1Threads);
+  switch (mode) {
+    case FA_MODE_MUL_W: hipLaunchKernelGGL((k_wsum_host1<DT, FA_MODE_MUL_W>), g, b, 0, st, dsc, nseg, co, po, k, divisor, total_vec, done, seq); break;
+    case FA_MODE_MUL_N_DIV_N: hipLaunchKernelGGL((k_wsum_host1<DT, FA_MODE_MUL_N_DIV_N>), g, b, 0, st, dsc, nseg, co, po, k, divisor, total_vec, done, seq); break;
+    default: hipLaunchKernelGGL((k_wsum_host1<DT, FA_MODE_SUM>), g, b, 0, st, dsc, nseg, co, po, k, divisor, total_vec, done, seq); break;
+  }
+}
+
+bool host1_enabled() {  // FA_HOST1=0: every host round through the device path's kernel + event (A/B)
+  static const int on = [] {
+    const char* e = getenv("FA_HOST1");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  return on != 0;
+}
+constexpr size_t kHost1MaxBytes = 1 << 20;  // input bytes up to which one workgroup serves the round
+constexpr size_t kZcHeader = 256;           // completion word at the start of the mapped buffer
+}  // namespace
+}  // extern "C++"
+
 int fa_weighted_sum_multi(fa_ctx* ctx, int dtype, int mode, int32_t num_segments,
                           const int64_t* seg_numel, int32_t k, const void* const* d_in,
                           const double* coef, double divisor, void* const* d_out, void* hip_stream) {
@@ -1315,8 +1423,12 @@ int fa_weighted_sum_multi(fa_ctx* ctx, int dtype, int mode, int32_t num_segments
 
 // Small host-resident rounds (the reference's quick_start: LR-MNIST, K = 2, 63 KB per client): the
 // launch/copy latencies dominate, so the inputs are packed into ONE mapped pinned buffer and the
-// kernel reads them -- and writes the result -- in place over PCIe (no H2D / D2H copies, one launch,
-// one event wait).  Same kernel, same bits as the device path.
+// kernel reads them -- and writes the result -- in place over PCIe (no H2D / D2H copies, one launch).
+// Rounds whose tables fit the kernel argument and whose inputs are <= kHost1MaxBytes run in ONE
+// workgroup (k_wsum_host1) that ends by storing a sequence number into the mapped buffer; the host
+// spins on that word instead of an event wait (tools/doorbell_probe.hip on MI355X: launch + event
+// 27.2 us, launch + completion word 22.2 us, a resident polling workgroup 18.6 us for cfg1's round).
+// Larger rounds: the device path's kernel + one event wait.  Same per-element arithmetic either way.
 int fa_weighted_sum_host(fa_ctx* ctx, int dtype, int mode, int32_t num_segments, const int64_t* seg_numel,
                          int32_t k, const void* const* h_in, const double* coef, double divisor, void* const* h_out,
                          void* hip_stream) {
@@ -1336,19 +1448,22 @@ int fa_weighted_sum_host(fa_ctx* ctx, int dtype, int mode, int32_t num_segments,
   DeviceGuard g(ctx->device);
   if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
   if (!ctx->zc_ev) FA_HIP(hipEventCreateWithFlags(&ctx->zc_ev, hipEventDisableTiming));
-  if (ctx->zc_cap < total) {
+  if (ctx->zc_cap < total + kZcHeader) {
     if (ctx->zc_host) FA_HIP(hipHostFree(ctx->zc_host));
     ctx->zc_host = ctx->zc_dev = nullptr;
     ctx->zc_cap = 0;
-    const size_t cap = std::max<size_t>(total, 1 << 20);
-    if (hipHostMalloc(&ctx->zc_host, cap, hipHostMallocMapped) != hipSuccess)
+    const size_t cap = std::max<size_t>(total + kZcHeader, 1 << 20);
+    // coherent: the device's reads and its completion word go straight over PCIe, no GPU caching
+    if (hipHostMalloc(&ctx->zc_host, cap, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
       return fail(FA_ERR_NOMEM, "hipHostMalloc(%zu, mapped) failed", cap);
     FA_HIP(hipHostGetDevicePointer(&ctx->zc_dev, ctx->zc_host, 0));
     ctx->zc_cap = cap;
+    memset(ctx->zc_host, 0, kZcHeader);
+    ctx->zc_seq = 0;
   }
   std::vector<const void*> din((size_t)num_segments * k);
   std::vector<void*> dout(num_segments);
-  size_t off = 0;
+  size_t off = kZcHeader;
   char* hb = (char*)ctx->zc_host;
   char* db = (char*)ctx->zc_dev;
   for (int s = 0; s < num_segments; ++s) {
@@ -1363,11 +1478,59 @@ int fa_weighted_sum_host(fa_ctx* ctx, int dtype, int mode, int32_t num_segments,
     dout[s] = db + off;
     off += align16((size_t)seg_numel[s] * out_es);
   }
-  int rc = wsum_impl(ctx, dtype, mode, num_segments, seg_numel, k, din.data(), coef, divisor, dout.data(),
-                     hip_stream, 0);
-  if (rc) return rc;
-  FA_HIP(hipEventRecord(ctx->zc_ev, (hipStream_t)hip_stream));
-  FA_HIP(hipEventSynchronize(ctx->zc_ev));
+  // one workgroup + completion word when the tables fit the kernel argument and the round is small
+  int nseg = 0;
+  int64_t total_vec = 0;
+  for (int s = 0; s < num_segments; ++s)
+    if (seg_numel[s] > 0) ++nseg, total_vec += (seg_numel[s] + V - 1) / V;
+  const size_t seg_b = align16(sizeof(Seg) * nseg), coef_b = align16(sizeof(double) * k);
+  const size_t desc_b = seg_b + coef_b + sizeof(void*) * (size_t)nseg * k;
+  if (host1_enabled() && nseg > 0 && desc_b <= (size_t)kInlineBytes && total <= kHost1MaxBytes) {
+    InlineDesc dsc;
+    Seg* hs = (Seg*)dsc.raw;
+    double* hc = (double*)(dsc.raw + seg_b);
+    const void** hp = (const void**)(dsc.raw + seg_b + coef_b);
+    for (int i = 0; i < k; ++i) hc[i] = coef ? coef[i] : 0.0;
+    int j = 0;
+    int64_t v0 = 0;
+    for (int s = 0; s < num_segments; ++s) {
+      if (seg_numel[s] <= 0) continue;
+      for (int i = 0; i < k; ++i) hp[(size_t)j * k + i] = din[(size_t)s * k + i];
+      hs[j] = Seg{seg_numel[s], v0, dout[s], j * k, 1};
+      v0 += (seg_numel[s] + V - 1) / V;
+      ++j;
+    }
+    const unsigned long long seq = ++ctx->zc_seq;
+    unsigned long long* done_d = (unsigned long long*)ctx->zc_dev;
+    volatile unsigned long long* done_h = (volatile unsigned long long*)ctx->zc_host;
+    hipStream_t st = (hipStream_t)hip_stream;
+    const int co = (int)seg_b, po = (int)(seg_b + coef_b);
+    switch (dtype) {
+      case FA_DTYPE_F32: launch_host1<FA_DTYPE_F32>(mode, st, dsc, nseg, co, po, k, divisor, total_vec, done_d, seq); break;
+      case FA_DTYPE_BF16: launch_host1<FA_DTYPE_BF16>(mode, st, dsc, nseg, co, po, k, divisor, total_vec, done_d, seq); break;
+      case FA_DTYPE_F16: launch_host1<FA_DTYPE_F16>(mode, st, dsc, nseg, co, po, k, divisor, total_vec, done_d, seq); break;
+      case FA_DTYPE_F64: launch_host1<FA_DTYPE_F64>(mode, st, dsc, nseg, co, po, k, divisor, total_vec, done_d, seq); break;
+      default: launch_host1<FA_DTYPE_I64>(mode, st, dsc, nseg, co, po, k, divisor, total_vec, done_d, seq); break;
+    }
+    FA_HIP(hipGetLastError());
+    // spin on the completion word; after 1 s fall back to a stream sync, which reports a fault
+    const auto t0 = std::chrono::steady_clock::now();
+    unsigned spins = 0;
+    while (*done_h != seq) {
+      if ((++spins & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
+        FA_HIP(hipStreamSynchronize(st));
+        if (*done_h != seq) return fail(FA_ERR_HIP, "fa_weighted_sum_host: the round finished without its completion word");
+        break;
+      }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  } else {
+    int rc = wsum_impl(ctx, dtype, mode, num_segments, seg_numel, k, din.data(), coef, divisor, dout.data(),
+                       hip_stream, 0);
+    if (rc) return rc;
+    FA_HIP(hipEventRecord(ctx->zc_ev, (hipStream_t)hip_stream));
+    FA_HIP(hipEventSynchronize(ctx->zc_ev));
+  }
   for (int s = 0; s < num_segments; ++s) {
     const size_t nb = (size_t)seg_numel[s] * out_es;
     if (nb) {

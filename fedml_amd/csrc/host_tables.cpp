@@ -329,7 +329,131 @@ bool match_rows(py::list dicts, py::list keys, torch::Tensor base, torch::Tensor
   return true;
 }
 
+// small_host_round(dicts, keys, mode, coef, divisor, fn, err_fn, ctx, stream, max_bytes) ->
+// OrderedDict | None: a whole small host-resident round (cfg1, the reference's quick_start: K = 2
+// LR-MNIST dicts, 63 KB a client) in one call -- the walk of gather(), the CPU outputs of
+// alloc_outputs() and one call of the C ABI's fa_weighted_sum_host per dtype group, through the
+// function pointer `fn` (libfedagg.so, loaded by the binding), with the GIL released while it runs.
+// The C ABI packs the inputs into its mapped pinned buffer, the device computes, the result is
+// copied into the fresh CPU tensors returned here (never recycled: the caller owns them).  Returns
+// None -- the general path then runs and raises the reference's errors -- unless every value is a
+// contiguous CPU tensor of a C-ABI dtype, the clients agree on every key's dtype and shape, and the
+// round's input bytes are <= max_bytes with K, T <= 4096 (fa_weighted_sum_host's table limits).
+using wsum_host_fn = int (*)(void*, int, int, int32_t, const int64_t*, int32_t, const void* const*, const double*,
+                             double, void* const*, void*);
+using last_error_fn = const char* (*)();
+
+py::object small_host_round(py::list dicts, py::list keys, int mode, py::object coef, double divisor, int64_t fn,
+                            int64_t err_fn, int64_t ctx, int64_t stream, int64_t max_bytes) {
+  const int64_t K = (int64_t)py::len(dicts);
+  const int64_t T = (int64_t)py::len(keys);
+  if (K == 0 || T == 0 || K > 4096 || T > 4096) return py::none();
+  std::vector<double> w((size_t)K, 0.0);
+  if (mode != 2) {  // FA_MODE_SUM = 2: no coefficients
+    if (coef.is_none() || (int64_t)py::len(coef) != K) return py::none();
+    py::sequence cs = coef;
+    for (int64_t i = 0; i < K; ++i) w[i] = cs[i].cast<double>();
+  }
+  std::vector<PyObject*> kv(T);
+  for (int64_t t = 0; t < T; ++t) kv[t] = PyList_GET_ITEM(keys.ptr(), t);
+  std::vector<int64_t> ptr((size_t)(T * K)), numel(T);
+  std::vector<int> code(T);
+  std::vector<at::ScalarType> st(T);
+  std::vector<c10::IntArrayRef> shape(T);
+  std::vector<at::Tensor> first(T);  // client 0's tensors (their sizes() stay valid while held)
+  int64_t in_bytes = 0;
+  for (int64_t i = 0; i < K; ++i) {
+    PyObject* d = PyList_GET_ITEM(dicts.ptr(), i);
+    if (!PyDict_Check(d) || PyDict_GET_SIZE(d) != T) return py::none();
+    Py_ssize_t pos = 0;
+    PyObject *k, *v;
+    for (int64_t t = 0; t < T; ++t) {
+      if (!PyDict_Next(d, &pos, &k, &v)) return py::none();
+      if (k != kv[t]) {
+        const int eq = PyObject_RichCompareBool(k, kv[t], Py_EQ);
+        if (eq < 0) throw py::error_already_set();
+        if (!eq) return py::none();
+      }
+      if (!THPVariable_Check(v)) return py::none();
+      const at::Tensor& x = THPVariable_Unpack(v);
+      if (!x.device().is_cpu() || !x.is_contiguous()) return py::none();
+      if (i == 0) {
+        st[t] = x.scalar_type();
+        code[t] = fa_dtype_code(st[t]);
+        if (code[t] < 0) return py::none();
+        first[t] = x;
+        shape[t] = first[t].sizes();
+        numel[t] = x.numel();
+        in_bytes += numel[t] * (int64_t)x.element_size() * K;
+        if (in_bytes > max_bytes) return py::none();
+      } else if (x.scalar_type() != st[t] || x.sizes() != shape[t]) {
+        return py::none();
+      }
+      ptr[t * K + i] = (int64_t)x.data_ptr();
+    }
+  }
+  // outputs: one CPU allocation, every key on a 256-byte boundary; weighted modes turn int64 into
+  // float32 (PyTorch's int64 * python float)
+  std::vector<at::ScalarType> ost(T);
+  std::vector<int64_t> off(T);
+  int64_t total = 0;
+  for (int64_t t = 0; t < T; ++t) {
+    ost[t] = (code[t] == 4 && mode != 2) ? at::kFloat : st[t];
+    off[t] = total;
+    total += (numel[t] * (int64_t)c10::elementSize(ost[t]) + 255) / 256 * 256;
+  }
+  auto arena = torch::empty({std::max<int64_t>(total, 256)}, torch::TensorOptions().dtype(torch::kUInt8));
+  char* base = (char*)arena.data_ptr();
+  // one C-ABI call per dtype group (key-major tables, keys in their dict order within a group)
+  int rc = 0;
+  {
+    py::gil_scoped_release nogil;
+    std::vector<int64_t> gn, gin, gout;
+    for (int c = 0; c <= 4 && rc == 0; ++c) {
+      gn.clear();
+      gin.clear();
+      gout.clear();
+      for (int64_t t = 0; t < T; ++t) {
+        if (code[t] != c) continue;
+        gn.push_back(numel[t]);
+        for (int64_t i = 0; i < K; ++i) gin.push_back(ptr[t * K + i]);
+        gout.push_back((int64_t)(base + off[t]));
+      }
+      if (gn.empty()) continue;
+      rc = reinterpret_cast<wsum_host_fn>(fn)((void*)ctx, c, mode, (int32_t)gn.size(), gn.data(), (int32_t)K,
+                                              reinterpret_cast<const void* const*>(gin.data()), w.data(), divisor,
+                                              reinterpret_cast<void* const*>(gout.data()), (void*)stream);
+    }
+  }
+  if (rc != 0)
+    throw std::runtime_error(std::string("fa_weighted_sum_host failed (") + std::to_string(rc) +
+                             "): " + reinterpret_cast<last_error_fn>(err_fn)());
+  static PyObject* odict_type = [] {  // collections.OrderedDict, held for the process lifetime
+    PyObject* mod = PyImport_ImportModule("collections");
+    if (!mod) throw py::error_already_set();
+    PyObject* t = PyObject_GetAttrString(mod, "OrderedDict");
+    Py_DECREF(mod);
+    if (!t) throw py::error_already_set();
+    return t;
+  }();
+  py::object out = py::reinterpret_steal<py::object>(PyObject_CallNoArgs(odict_type));
+  if (!out) throw py::error_already_set();
+  const c10::Storage& storage = arena.storage();
+  const c10::DispatchKeySet ks = arena.key_set();
+  for (int64_t t = 0; t < T; ++t) {
+    at::Tensor v = at::detail::make_tensor<c10::TensorImpl>(c10::Storage(storage), ks,
+                                                            caffe2::TypeMeta::fromScalarType(ost[t]));
+    c10::TensorImpl* impl = v.unsafeGetTensorImpl();
+    impl->set_storage_offset(off[t] / (int64_t)c10::elementSize(ost[t]));
+    impl->set_sizes_contiguous(shape[t]);
+    py::object pv = py::reinterpret_steal<py::object>(THPVariable_Wrap(std::move(v)));
+    if (PyObject_SetItem(out.ptr(), kv[t], pv.ptr()) < 0) throw py::error_already_set();
+  }
+  return out;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.def("small_host_round", &small_host_round, "a whole small host-resident round through fa_weighted_sum_host");
   m.def("match_rows", &match_rows, "are these state_dicts the row views of one arena?");
   m.def("pack_range", &pack_range, "multi-threaded packing of host tensors into a pinned staging range");
   m.doc() = "host-side table builder of the fedml_amd aggregation engine (no tensor data access)";

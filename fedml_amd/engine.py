@@ -504,6 +504,16 @@ class AggEngine:
             N.ctypes.cast(out_ptrs.data_ptr(), N._P_vp), self._stream(stream))
         N.check(rc, "fa_weighted_sum_multi")
 
+    def host_round_abi(self):
+        """(fa_weighted_sum_host, fa_last_error, fa_ctx*) as integer addresses, for the one-call small
+        host round (_host.small_host_round), which calls the C ABI directly."""
+        a = getattr(self, "_host_round_abi", None)
+        if a is None:
+            L = N.lib()
+            a = self._host_round_abi = (N.ctypes.cast(L.fa_weighted_sum_host, N.ctypes.c_void_p).value,
+                                        N.ctypes.cast(L.fa_last_error, N.ctypes.c_void_p).value, self._ctx.value)
+        return a
+
     def weighted_sum_host_table(self, dtype_code: int, mode: int, seg_numel: torch.Tensor, k: int,
                                 in_ptrs: torch.Tensor, out_ptrs: torch.Tensor, coef: Optional[Sequence[float]] = None,
                                 divisor: float = 1.0, stream=None) -> None:

@@ -57,6 +57,15 @@ def aggregate(dicts: Sequence[Dict[str, torch.Tensor]], mode: int, coef: Optiona
     keys = list(dicts[0].keys())
     if not keys:
         return OrderedDict()
+    if _HOST_SMALL and not getattr(dicts[0][keys[0]], "is_cuda", True):
+        # small CPU round (cfg1): the whole call in C++ (None: not small / not uniform / not native)
+        eng = engine or get_engine(None)
+        fn, err, ctx = eng.host_round_abi()
+        with eng.lock:
+            out = _host.small_host_round(dicts if isinstance(dicts, list) else list(dicts), keys, mode, coef,
+                                         divisor, fn, err, ctx, 0, _SMALL_HOST_BYTES)
+        if out is not None:
+            return out
     hit = resident_rows(dicts)
     if hit is not None:  # updates adopted into arena rows on arrival: one launch per dtype group
         arena, rows = hit
@@ -94,6 +103,7 @@ def _aggregate_device(keys, ptrs, numel, codes, shapes, dev, k, mode, coef, divi
 
 
 _ELEM = {0: 4, 1: 2, 2: 2, 3: 8, 4: 8}  # bytes per element of each dtype code
+_HOST_SMALL = os.environ.get("FEDML_AMD_HOST_PATH", "packed") == "packed"
 _SMALL_HOST_BYTES = 4 << 20             # CPU rounds up to this size: zero-copy kernel (fa_weighted_sum_host)
 _HOST_MAX_TABLE = 4096                  # fa_weighted_sum_host's limit on num_segments and on k
 
