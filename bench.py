@@ -1322,7 +1322,8 @@ def wl_samask(args, eng, rank, world, timer):
     """§8(f) #4, r03: SecAgg's server mask re-expansion (cross_silo/secagg/sa_fedml_aggregator.py:92-136)
     for N = K clients of ResNet-18 size: every surviving client's numpy MT19937 stream
     (np.random.seed(b_u); randint(0, p, d)) and, for each dropped client, its N - 1 pairwise streams,
-    summed mod p -- fa_mt_randint_sum, one wave per stream.  BGW decoding (a few scalars per client) is
+    summed mod p -- fa_mt_randint_sum (jump-ahead chunks of every stream in parallel; FA_MT_JUMP=0: one
+    wave per stream).  BGW decoding (a few scalars per client) is
     host work outside the step.  ``--variant`` = dropped clients (default 0).  value = latency (ms)."""
     if world > 1:
         raise SystemExit("samask config: single GPU")
@@ -1353,15 +1354,15 @@ def wl_samask(args, eng, rank, world, timer):
         return time.perf_counter() - t0
 
     def parity():
-        n = min(P, 100_000)  # a prefix: the first n draws of a stream do not depend on its length
-        acc = np.zeros(n, dtype=object)
+        # every element (the jump-ahead chunks cover the whole vector): |sum| < len(seeds) * p < 2^63
+        acc = np.zeros(P, dtype=np.int64)
         for s_, g_ in zip(seeds, signs):
             np.random.seed(s_)
-            acc = acc + g_ * np.random.randint(0, p, size=n).astype(object)
-        exp = np.array([int(a) % p for a in acc], dtype=np.int64)
-        ok = np.array_equal(out[:n].cpu().numpy(), exp)
+            acc += g_ * np.random.randint(0, p, size=P).astype(np.int64)
+        exp = np.mod(acc, p)
+        ok = np.array_equal(out.cpu().numpy(), exp)
         return (f"{'bit-exact' if ok else 'MISMATCH'} vs numpy's own legacy streams (np.random.seed + randint, "
-                f"the reference's calls) summed mod p, on the first {n} elements of all {len(seeds)} streams")
+                f"the reference's calls) summed mod p, on all {P} elements of all {len(seeds)} streams")
 
     def cpu(budget_s):
         """The reference's loop body for surviving clients (seed, randint, +=, mod) on a sample of

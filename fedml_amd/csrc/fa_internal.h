@@ -85,7 +85,15 @@ struct fa_ctx {
   void* zc_dev = nullptr;
   size_t zc_cap = 0;
   hipEvent_t zc_ev = nullptr;
-  unsigned long long zc_seq = 0;  // completion word (first 256 bytes of zc_host) of the one-workgroup path
+  unsigned long long zc_seq = 0;  // completion word (first 256 bytes of zc_host) of the host1 path
+  unsigned* zc_counter = nullptr;  // its workgroup counter (device memory)
+  // fa_mt_randint_sum's jump-ahead path: per-call device work space and the jump polynomials
+  void* mt_dev = nullptr;
+  size_t mt_cap = 0;
+  void* mt_poly_dev = nullptr;     // (count) x 312 uint64 words, x^(c J) mod phi for c = 1..count
+  unsigned long long mt_poly_J = 0;
+  int mt_poly_count = 0;
+  int mt_poly_stride = 0;
 };
 
 namespace fa_detail {

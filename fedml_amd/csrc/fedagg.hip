@@ -1146,6 +1146,9 @@ int fa_ctx_destroy(fa_ctx* c) {
   }
   if (c->zc_ev) (void)hipEventDestroy(c->zc_ev);
   if (c->zc_host) (void)hipHostFree(c->zc_host);
+  if (c->mt_dev) (void)hipFree(c->mt_dev);
+  if (c->zc_counter) (void)hipFree(c->zc_counter);
+  if (c->mt_poly_dev) (void)hipFree(c->mt_poly_dev);
   delete c;
   return FA_OK;
 }
@@ -1312,22 +1315,26 @@ int wsum_impl(fa_ctx* ctx, int dtype, int mode, int32_t num_segments, const int6
 
 extern "C++" {
 namespace {
-// One workgroup over a whole small round whose buffers sit in mapped host memory: the flattened
-// 16-byte vectors of every segment (Seg.tile_start = the segment's first vector), S vectors per
-// thread and U clients per group with all their loads in flight before any is consumed (each group
-// costs one PCIe round trip), the ordered term/accum of wsum_tile, then every thread's stores are
-// made visible to the host before thread 0 stores `seq` into the completion word.
-constexpr int kHost1Threads = 1024;
+// A whole small round whose buffers sit in mapped host memory, on G <= kHost1MaxGroups workgroups
+// (the flattened 16-byte vectors of every segment, Seg.tile_start = the segment's first vector; S
+// vectors per thread and U clients per group with all their loads in flight before any is consumed:
+// each group costs one PCIe round trip, and more CUs keep more reads in flight -- cfg1's round takes
+// 25.7 / 17.9 / 14.6 / 13.7 / 15.0 us on 1 / 2 / 4 / 8 / 16 workgroups of 256 threads,
+// profiles/r03n/doorbell_probe.json).  The ordered term/accum of wsum_tile; every thread's stores are
+// made visible to the host, and the last workgroup to finish (a device-memory counter) stores `seq`
+// into the completion word and resets the counter.
+constexpr int kHost1Threads = 256, kHost1MaxGroups = 64;
 template <int DT, int MODE>
 __global__ void __launch_bounds__(kHost1Threads)
 k_wsum_host1(const InlineDesc dsc, int nseg, int coef_off, int ptr_off, int k, double divisor, int64_t total_vec,
-             unsigned long long* done, unsigned long long seq) {
+             unsigned long long* done, unsigned long long seq, unsigned* counter) {
   using T = Tr<DT, MODE>;
   using A = typename T::A;
   using R = typename T::R;
   constexpr int V = T::V, S = 2, U = 4;
   // the tables into LDS with one load per thread (lookups then cost no kernarg round trips)
   __shared__ u32x4 tab[kInlineBytes / 16];
+  static_assert(kInlineBytes / 16 <= kHost1Threads, "one 16-byte load per thread");
   if (threadIdx.x < kInlineBytes / 16) tab[threadIdx.x] = ((const u32x4*)dsc.raw)[threadIdx.x];
   __syncthreads();
   const char* b = (const char*)tab;
@@ -1335,12 +1342,13 @@ k_wsum_host1(const InlineDesc dsc, int nseg, int coef_off, int ptr_off, int k, d
   const double* coef = (const double*)(b + coef_off);
   const void* const* ptrs = (const void* const*)(b + ptr_off);
   const typename T::D d = T::div(divisor);
-  for (int64_t base = 0; base < total_vec; base += (int64_t)kHost1Threads * S) {
+  const int64_t nthr = (int64_t)gridDim.x * kHost1Threads, gt = (int64_t)blockIdx.x * kHost1Threads + threadIdx.x;
+  for (int64_t base = 0; base < total_vec; base += nthr * S) {
     int64_t g[S];
     int si[S];
 #pragma unroll
     for (int s = 0; s < S; ++s) {
-      g[s] = base + s * kHost1Threads + threadIdx.x;
+      g[s] = base + s * nthr + gt;
       si[s] = g[s] < total_vec ? find_seg(segs, nseg, g[s]) : -1;
     }
     A acc[S][V];
@@ -1389,17 +1397,25 @@ k_wsum_host1(const InlineDesc dsc, int nseg, int coef_off, int ptr_off, int k, d
   }
   __threadfence_system();  // this thread's result stores are visible to the host
   __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == gridDim.x - 1) {  // the last workgroup: every other one's stores are visible
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 template <int DT>
 void launch_host1(int mode, hipStream_t st, const InlineDesc& dsc, int nseg, int co, int po, int k, double divisor,
-                  int64_t total_vec, unsigned long long* done, unsigned long long seq) {
-  const dim3 g(1), b(kHost1Threads);
+                  int64_t total_vec, unsigned long long* done, unsigned long long seq, unsigned* counter) {
+  // one vector per thread up to kHost1MaxGroups workgroups
+  const dim3 g((unsigned)std::min<int64_t>(kHost1MaxGroups, std::max<int64_t>(1, (total_vec + kHost1Threads - 1) / kHost1Threads)));
+  const dim3 b(kHost1Threads);
   switch (mode) {
-    case FA_MODE_MUL_W: hipLaunchKernelGGL((k_wsum_host1<DT, FA_MODE_MUL_W>), g, b, 0, st, dsc, nseg, co, po, k, divisor, total_vec, done, seq); break;
-    case FA_MODE_MUL_N_DIV_N: hipLaunchKernelGGL((k_wsum_host1<DT, FA_MODE_MUL_N_DIV_N>), g, b, 0, st, dsc, nseg, co, po, k, divisor, total_vec, done, seq); break;
-    default: hipLaunchKernelGGL((k_wsum_host1<DT, FA_MODE_SUM>), g, b, 0, st, dsc, nseg, co, po, k, divisor, total_vec, done, seq); break;
+    case FA_MODE_MUL_W: hipLaunchKernelGGL((k_wsum_host1<DT, FA_MODE_MUL_W>), g, b, 0, st, dsc, nseg, co, po, k, divisor, total_vec, done, seq, counter); break;
+    case FA_MODE_MUL_N_DIV_N: hipLaunchKernelGGL((k_wsum_host1<DT, FA_MODE_MUL_N_DIV_N>), g, b, 0, st, dsc, nseg, co, po, k, divisor, total_vec, done, seq, counter); break;
+    default: hipLaunchKernelGGL((k_wsum_host1<DT, FA_MODE_SUM>), g, b, 0, st, dsc, nseg, co, po, k, divisor, total_vec, done, seq, counter); break;
   }
 }
 
@@ -1461,6 +1477,10 @@ int fa_weighted_sum_host(fa_ctx* ctx, int dtype, int mode, int32_t num_segments,
     memset(ctx->zc_host, 0, kZcHeader);
     ctx->zc_seq = 0;
   }
+  if (!ctx->zc_counter) {  // the host1 kernel's workgroup counter (device memory, reset by its last user)
+    if (hipMalloc((void**)&ctx->zc_counter, 256) != hipSuccess) return fail(FA_ERR_NOMEM, "hipMalloc(256) failed");
+    FA_HIP(hipMemset(ctx->zc_counter, 0, 256));
+  }
   std::vector<const void*> din((size_t)num_segments * k);
   std::vector<void*> dout(num_segments);
   size_t off = kZcHeader;
@@ -1506,11 +1526,11 @@ int fa_weighted_sum_host(fa_ctx* ctx, int dtype, int mode, int32_t num_segments,
     hipStream_t st = (hipStream_t)hip_stream;
     const int co = (int)seg_b, po = (int)(seg_b + coef_b);
     switch (dtype) {
-      case FA_DTYPE_F32: launch_host1<FA_DTYPE_F32>(mode, st, dsc, nseg, co, po, k, divisor, total_vec, done_d, seq); break;
-      case FA_DTYPE_BF16: launch_host1<FA_DTYPE_BF16>(mode, st, dsc, nseg, co, po, k, divisor, total_vec, done_d, seq); break;
-      case FA_DTYPE_F16: launch_host1<FA_DTYPE_F16>(mode, st, dsc, nseg, co, po, k, divisor, total_vec, done_d, seq); break;
-      case FA_DTYPE_F64: launch_host1<FA_DTYPE_F64>(mode, st, dsc, nseg, co, po, k, divisor, total_vec, done_d, seq); break;
-      default: launch_host1<FA_DTYPE_I64>(mode, st, dsc, nseg, co, po, k, divisor, total_vec, done_d, seq); break;
+      case FA_DTYPE_F32: launch_host1<FA_DTYPE_F32>(mode, st, dsc, nseg, co, po, k, divisor, total_vec, done_d, seq, ctx->zc_counter); break;
+      case FA_DTYPE_BF16: launch_host1<FA_DTYPE_BF16>(mode, st, dsc, nseg, co, po, k, divisor, total_vec, done_d, seq, ctx->zc_counter); break;
+      case FA_DTYPE_F16: launch_host1<FA_DTYPE_F16>(mode, st, dsc, nseg, co, po, k, divisor, total_vec, done_d, seq, ctx->zc_counter); break;
+      case FA_DTYPE_F64: launch_host1<FA_DTYPE_F64>(mode, st, dsc, nseg, co, po, k, divisor, total_vec, done_d, seq, ctx->zc_counter); break;
+      default: launch_host1<FA_DTYPE_I64>(mode, st, dsc, nseg, co, po, k, divisor, total_vec, done_d, seq, ctx->zc_counter); break;
     }
     FA_HIP(hipGetLastError());
     // spin on the completion word; after 1 s fall back to a stream sync, which reports a fault

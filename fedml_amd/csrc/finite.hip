@@ -24,9 +24,11 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <type_traits>
 
 #include "fa_internal.h"
 #include "fedagg_finite.h"
+#include "mt_poly.h"
 
 using namespace fa_detail;
 
@@ -511,6 +513,185 @@ k_mt_fold(unsigned long long* __restrict__ acc, int64_t* __restrict__ total, int
   }
 }
 
+// ---------------------------------------------------------------- jump-ahead expansion (r03)
+// One wave per stream is latency-bound (38.7 ms for 32 streams x 11.7 M draws on a GPU that is
+// mostly idle).  With jump-ahead every stream is cut into C chunks of J words that waves generate in
+// parallel: chunk c starts from the state c*J words past the seed, W_c[j] = XOR_{i: g_i} x_{i+j}
+// with g = x^(cJ) mod phi (mt_poly.h; the host computes and caches the polynomials), x the stream's
+// word sequence from its seed.  Numpy's draws are accepted or rejected one by one, so a first pass
+// counts the accepted draws of every chunk, a scan turns the counts into the chunks' first output
+// positions, and a second pass regenerates each chunk and places its accepted draws there.  The last
+// chunk runs on until the stream has its n draws, so an underestimated C costs time, never bits.
+constexpr int kMtSeqWords = 624 * 34;  // x_0 .. x_21215 >= 19937 + 623 words: every x_{i+j} of a jump
+
+// x_0 .. x_{kMtSeqWords-1} of every stream (one wave each), to global memory
+__global__ void __launch_bounds__(64) k_mt_seq(const uint32_t* __restrict__ seeds, uint32_t* __restrict__ seq) {
+  __shared__ uint32_t mt[2][kMtN];
+  const int lane = threadIdx.x;
+  uint32_t* out = seq + (size_t)blockIdx.x * kMtSeqWords;
+  if (lane == 0) {
+    uint32_t x = seeds[blockIdx.x];
+    for (int i = 0; i < kMtN; ++i) {
+      mt[0][i] = x;
+      x = 1812433253u * (x ^ (x >> 30)) + (uint32_t)(i + 1);
+    }
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int b = 0; b < kMtSeqWords / kMtN; ++b) {
+    for (int i = lane; i < kMtN; i += 64) out[b * kMtN + i] = mt[cur][i];
+    if (b + 1 == kMtSeqWords / kMtN) break;
+    mt_next_block(mt[cur], mt[cur ^ 1], lane);
+    cur ^= 1;
+  }
+}
+
+// W_c for chunk c = blockIdx.x + 1 of stream blockIdx.y: the correlation of the stream's sequence
+// with the set bits of x^(cJ) mod phi, given by the host as a list of bit positions (stride words
+// per chunk: the padded count, 3 unused, the positions padded to a multiple of 16 with kMtJumpSeq,
+// whose window in LDS is all zero).  The sequence (82 KB + the zero pad) and up to kMtPosLds
+// positions sit in LDS; thread t owns words t, t + 256, t + 512 of the window; sixteen positions
+// are read per step (four broadcast 16-byte LDS reads), then up to 48 sequence words.
+constexpr int kMtJumpSeq = 19937 + 624;  // words of the sequence a jump reads
+constexpr int kMtJumpPad = 768;          // zero words after it (the pad position's window)
+constexpr int kMtPosLds = 12288;         // positions staged per round (a longer list takes rounds)
+__global__ void __launch_bounds__(256) k_mt_jump(const uint32_t* __restrict__ seq, const int32_t* __restrict__ pos,
+                                                 int stride, int chunks, uint32_t* __restrict__ windows) {
+  typedef int i32x4 __attribute__((ext_vector_type(4)));
+  __shared__ uint32_t xs[kMtJumpSeq + kMtJumpPad];
+  __shared__ i32x4 pl[kMtPosLds / 4];
+  const int t = threadIdx.x;
+  const int s = blockIdx.y, c = blockIdx.x + 1;
+  const uint32_t* src = seq + (size_t)s * kMtSeqWords;
+  for (int i = t; i < kMtJumpSeq + kMtJumpPad; i += 256) xs[i] = i < kMtJumpSeq ? src[i] : 0u;
+  const int32_t* ps = pos + (size_t)(c - 1) * stride;
+  const int cnt = ps[0];  // a multiple of 16
+  ps += 4;
+  const bool w2 = t + 512 < kMtN;  // threads whose third word exists (t < 112)
+  uint32_t a0 = 0, a1 = 0, a2 = 0;
+  for (int r0 = 0; r0 < cnt; r0 += kMtPosLds) {
+    const int rn = min(kMtPosLds, cnt - r0);
+    __syncthreads();  // the previous round's positions are consumed
+    for (int q = t; q < rn / 4; q += 256) pl[q] = ((const i32x4*)(ps + r0))[q];
+    __syncthreads();
+    for (int k = 0; k < rn / 4; k += 4) {
+      const i32x4 p0 = pl[k], p1 = pl[k + 1], p2 = pl[k + 2], p3 = pl[k + 3];  // broadcast reads
+      const int ii[16] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w,
+                          p2.x, p2.y, p2.z, p2.w, p3.x, p3.y, p3.z, p3.w};
+      uint32_t b0 = 0, b1 = 0, b2 = 0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        b0 ^= xs[ii[q] + t];
+        b1 ^= xs[ii[q] + t + 256];
+      }
+      if (w2) {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) b2 ^= xs[ii[q] + t + 512];
+      }
+      a0 ^= b0;
+      a1 ^= b1;
+      a2 ^= b2;
+    }
+  }
+  uint32_t* out = windows + ((size_t)s * chunks + c) * kMtN;
+  out[t] = a0;
+  out[t + 256] = a1;
+  if (w2) out[t + 512] = a2;
+}
+
+// Pass 1 (PLACE = false): accepted draws of chunks 0 .. chunks-2 of every stream -> counts[s][c].
+// Pass 2 (PLACE = true): chunk c stores its accepted draws, signed (p - v for a negative stream, 0
+// stays 0), into the stream's plane from output position offs[s][c] on (the last chunk until the
+// stream has n): plain coalesced stores, every position of a plane written exactly once (the planes
+// replace k_mt_randint's uint64 atomics, which cost 4.8x the generation in this pass).
+// Chunk 0 starts from the seeded state (x_0..x_623 of seq), chunk c > 0 from W_c; a chunk is
+// jwords words = jwords / 624 blocks.
+template <bool WIDE, bool PLACE>
+__global__ void __launch_bounds__(64)
+k_mt_chunk(const uint32_t* __restrict__ seq, const uint32_t* __restrict__ windows, int chunks, int64_t jwords,
+           uint64_t rng, uint64_t mask, uint64_t p, int64_t n, const int8_t* __restrict__ signs,
+           int64_t* __restrict__ counts, const int64_t* __restrict__ offs, void* __restrict__ planes) {
+  using PT = typename std::conditional<WIDE, uint64_t, uint32_t>::type;
+  PT* plane = (PT*)planes + (size_t)blockIdx.y * n;
+  __shared__ uint32_t mt[2][kMtN];
+  const int lane = threadIdx.x;
+  const int c = blockIdx.x, s = blockIdx.y;
+  const bool last = c == chunks - 1;
+  int64_t count = PLACE ? offs[(size_t)s * chunks + c] : 0;
+  if (PLACE && count >= n) return;  // every output position is taken by earlier chunks
+  const uint32_t* w0 = c == 0 ? seq + (size_t)s * kMtSeqWords : windows + ((size_t)s * chunks + c) * kMtN;
+  for (int i = lane; i < kMtN; i += 64) mt[0][i] = w0[i];
+  __syncthreads();
+  const bool neg = signs[s] < 0;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  constexpr int kVals = WIDE ? kMtN / 2 : kMtN;
+  constexpr int kRounds = (kVals + 63) / 64;
+  int cur = 0;
+  const int64_t blocks = jwords / kMtN;
+  for (int64_t b = 0; (PLACE && last) ? count < n : b < blocks; ++b) {
+    mt_next_block(mt[cur], mt[cur ^ 1], lane);
+    cur ^= 1;
+    const uint32_t* w32 = mt[cur];
+    uint64_t v[kRounds];
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+      const int w = r * 64 + lane;
+      if (w < kVals) {
+        if constexpr (WIDE) v[r] = (uint64_t)mt_temper(w32[2 * w]) << 32 | mt_temper(w32[2 * w + 1]);
+        else v[r] = mt_temper(w32[w]);
+        v[r] &= mask;
+      } else {
+        v[r] = ~0ull;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kRounds; ++r) {
+      const bool ok = v[r] <= rng;
+      const uint64_t bal = __ballot(ok);
+      if constexpr (PLACE) {
+        const int64_t pos = count + __popcll(bal & below);
+        if (ok && pos < n) plane[pos] = (PT)((neg && v[r] != 0) ? p - v[r] : v[r]);
+      }
+      count += __popcll(bal);
+    }
+    if (PLACE && count >= n) break;
+  }
+  if (!PLACE && lane == 0) counts[(size_t)s * chunks + c] = count;
+}
+
+// total[e] = (first ? 0 : total[e]) + sum over the g planes of element e, mod p (planes hold values
+// in [0, p); 32-bit planes sum in uint64 and reduce once, 64-bit planes add modulo p one by one)
+template <bool WIDE>
+__global__ void __launch_bounds__(kBlock)
+k_mt_fold_planes(const void* __restrict__ planes, int g, int64_t n, uint64_t p, int64_t* __restrict__ total, int first) {
+  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (int64_t)gridDim.x * kBlock) {
+    uint64_t t = first ? 0 : (uint64_t)total[e];
+    if constexpr (WIDE) {
+      const uint64_t* pl = (const uint64_t*)planes + e;
+      for (int s = 0; s < g; ++s) {
+        t += __builtin_nontemporal_load(pl + (size_t)s * n);
+        if (t >= p) t -= p;
+      }
+    } else {
+      const uint32_t* pl = (const uint32_t*)planes + e;
+      for (int s = 0; s < g; ++s) t += __builtin_nontemporal_load(pl + (size_t)s * n);
+      t %= p;
+    }
+    total[e] = (int64_t)t;
+  }
+}
+
+// offs[s][c] = sum of counts[s][0..c-1] (exclusive scan over a stream's chunks)
+__global__ void k_mt_scan(const int64_t* __restrict__ counts, int64_t* __restrict__ offs, int streams, int chunks) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= streams) return;
+  int64_t run = 0;
+  for (int c = 0; c < chunks; ++c) {
+    offs[(size_t)s * chunks + c] = run;
+    if (c < chunks - 1) run += counts[(size_t)s * chunks + c];
+  }
+}
+
 }  // namespace
 
 // ============================================================================================ ABI
@@ -745,6 +926,84 @@ int fa_lcc_decode(fa_ctx* ctx, int32_t rows, int32_t k, int64_t m, const int64_t
 }
 
 
+}  // extern "C"
+
+namespace {
+// FA_MT_JUMP=0: every stream sequential (k_mt_randint); FA_MT_JUMP_LOG2=k: chunks of 624 << k words
+bool mt_jump_enabled() {
+  const char* e = getenv("FA_MT_JUMP");
+  return !(e && e[0] == '0');
+}
+// chunk size J = 624 << log2: about 2,048 chunk waves over all streams (8 per CU), in [624 << 2, 624 << 14]
+int mt_jump_log2(double exp_words, int streams) {
+  const char* e = getenv("FA_MT_JUMP_LOG2");
+  if (e) {
+    const int v = atoi(e);
+    return v < 0 ? 0 : v > 20 ? 20 : v;
+  }
+  const double per = exp_words * std::max(1, streams) / (624.0 * 2048.0);
+  int k = 2;
+  while (k < 14 && (double)(1ll << (k + 1)) <= per) ++k;
+  return k;
+}
+
+// The set-bit positions of x^(cJ) mod phi, c = 1..count, on the device (ctx->mt_poly_dev; one row
+// of `stride` int32 per chunk: the padded count, 3 unused, then the positions, padded to a multiple
+// of 16 with kMtJumpSeq; stride a multiple of 4 so that every row starts 16-byte aligned).  Host polynomials are cached per J (mt_poly.h); the device table is rebuilt
+// only when J or the count grows.
+int mt_jump_tables(fa_ctx* ctx, uint64_t J, int count, hipStream_t st) {
+  if (ctx->mt_poly_dev && ctx->mt_poly_J == J && ctx->mt_poly_count >= count) return FA_OK;
+  if (fa_mt::charpoly().empty()) return fail(FA_ERR_INVALID, "fa_mt_randint_sum: MT19937 characteristic polynomial not found");
+  const std::vector<fa_mt::Poly>& g = fa_mt::jump_polys(J, count);
+  std::vector<std::vector<int32_t>> rows((size_t)count);
+  int stride = 0;
+  for (int c = 0; c < count; ++c) {
+    for (int i = 0; i < fa_mt::kDeg; ++i)
+      if (fa_mt::get_bit(g[(size_t)c], i)) rows[(size_t)c].push_back(i);
+    while (rows[(size_t)c].size() % 16) rows[(size_t)c].push_back(kMtJumpSeq);
+    stride = std::max<int>(stride, 4 + (int)rows[(size_t)c].size());  // 4 + a multiple of 16
+  }
+  std::vector<int32_t> tab((size_t)count * stride, 0);
+  for (int c = 0; c < count; ++c) {
+    int32_t* r = &tab[(size_t)c * stride];
+    r[0] = (int32_t)rows[(size_t)c].size();
+    std::copy(rows[(size_t)c].begin(), rows[(size_t)c].end(), r + 4);
+  }
+  FA_HIP(hipStreamSynchronize(st));  // a previous table may still be read by queued kernels
+  if (ctx->mt_poly_dev) FA_HIP(hipFree(ctx->mt_poly_dev));
+  ctx->mt_poly_dev = nullptr;
+  ctx->mt_poly_count = 0;
+  if (hipMalloc(&ctx->mt_poly_dev, tab.size() * sizeof(int32_t)) != hipSuccess)
+    return fail(FA_ERR_NOMEM, "fa_mt_randint_sum: jump table allocation failed");
+  FA_HIP(hipMemcpy(ctx->mt_poly_dev, tab.data(), tab.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  ctx->mt_poly_J = J;
+  ctx->mt_poly_count = count;
+  ctx->mt_poly_stride = stride;
+  return FA_OK;
+}
+
+// device bytes for the per-stream planes of one group (FA_MT_PLANE_MB, default 2 GiB)
+uint64_t mt_plane_budget() {
+  const char* e = getenv("FA_MT_PLANE_MB");
+  const long long mb = e ? atoll(e) : 2048;
+  return (uint64_t)std::max<long long>(1, mb) << 20;
+}
+
+// >= bytes of device work space in ctx->mt_dev (grown, never shrunk)
+int mt_work(fa_ctx* ctx, size_t bytes, hipStream_t st) {
+  if (ctx->mt_cap >= bytes) return FA_OK;
+  FA_HIP(hipStreamSynchronize(st));
+  if (ctx->mt_dev) FA_HIP(hipFree(ctx->mt_dev));
+  ctx->mt_dev = nullptr;
+  ctx->mt_cap = 0;
+  if (hipMalloc(&ctx->mt_dev, bytes) != hipSuccess) return fail(FA_ERR_NOMEM, "fa_mt_randint_sum: %zu bytes of work space", bytes);
+  ctx->mt_cap = bytes;
+  return FA_OK;
+}
+}  // namespace
+
+extern "C" {
+
 size_t fa_mt_randint_sum_scratch_bytes(int64_t n) { return n > 0 ? sizeof(uint64_t) * (size_t)n : 0; }
 
 int fa_mt_randint_sum(fa_ctx* ctx, int32_t num_streams, const uint32_t* seeds, const int8_t* signs, int64_t prime,
@@ -783,6 +1042,52 @@ int fa_mt_randint_sum(fa_ctx* ctx, int32_t num_streams, const uint32_t* seeds, c
   const uint32_t* dseeds = (const uint32_t*)slot->dev;
   const int8_t* dsigns = (const int8_t*)((const char*)slot->dev + seed_b);
   const unsigned fold_blocks = (unsigned)std::min<int64_t>((n + kBlock - 1) / kBlock, 4096);
+  // jump-ahead: C chunks of J words per stream when the stream is long enough for >= 2 of them
+  const double exp_words = (double)n * (wide ? 2.0 : 1.0) * ((double)mask + 1.0) / ((double)rng + 1.0);
+  const uint64_t J = 624ull << mt_jump_log2(exp_words, (int)std::min<uint64_t>(per, (uint64_t)num_streams));
+  const int C = mt_jump_enabled() ? (int)std::min<double>(std::floor(exp_words / (double)J), 4096.0) : 0;
+  if (C >= 2) {
+    rc = mt_jump_tables(ctx, J, C - 1, st);
+    if (rc) return rc;
+    // streams per group: their planes (n values each) within the plane budget
+    const size_t es = wide ? 8 : 4;
+    const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)num_streams, mt_plane_budget() / ((uint64_t)n * es)));
+    const size_t seq_b = align16(sizeof(uint32_t) * kMtSeqWords * G), win_b = align16(sizeof(uint32_t) * kMtN * C * G);
+    const size_t cnt_b = align16(sizeof(int64_t) * C * G), pl_b = (size_t)G * n * es;
+    rc = mt_work(ctx, seq_b + win_b + 2 * cnt_b + pl_b, st);
+    if (rc) return rc;
+    char* w = (char*)ctx->mt_dev;
+    uint32_t* dseq = (uint32_t*)w;
+    uint32_t* dwin = (uint32_t*)(w + seq_b);
+    int64_t* dcnt = (int64_t*)(w + seq_b + win_b);
+    int64_t* doff = (int64_t*)(w + seq_b + win_b + cnt_b);
+    void* dpl = w + seq_b + win_b + 2 * cnt_b;
+    const int32_t* dpos = (const int32_t*)ctx->mt_poly_dev;
+    for (uint64_t s0 = 0; s0 < (uint64_t)num_streams; s0 += G) {
+      const unsigned b = (unsigned)std::min<uint64_t>(G, (uint64_t)num_streams - s0);
+      hipLaunchKernelGGL(k_mt_seq, dim3(b), dim3(64), 0, st, dseeds + s0, dseq);
+      hipLaunchKernelGGL(k_mt_jump, dim3(C - 1, b), dim3(256), 0, st, dseq, dpos, ctx->mt_poly_stride, C, dwin);
+      if (wide) {
+        hipLaunchKernelGGL((k_mt_chunk<true, false>), dim3(C - 1, b), dim3(64), 0, st, dseq, dwin, C, (int64_t)J, rng,
+                           mask, p, n, dsigns + s0, dcnt, (const int64_t*)nullptr, dpl);
+        hipLaunchKernelGGL(k_mt_scan, dim3((b + 63) / 64), dim3(64), 0, st, dcnt, doff, (int)b, C);
+        hipLaunchKernelGGL((k_mt_chunk<true, true>), dim3(C, b), dim3(64), 0, st, dseq, dwin, C, (int64_t)J, rng,
+                           mask, p, n, dsigns + s0, dcnt, (const int64_t*)doff, dpl);
+        hipLaunchKernelGGL((k_mt_fold_planes<true>), dim3(fold_blocks), dim3(kBlock), 0, st, (const void*)dpl, (int)b,
+                           n, p, (int64_t*)d_out, s0 == 0 ? 1 : 0);
+      } else {
+        hipLaunchKernelGGL((k_mt_chunk<false, false>), dim3(C - 1, b), dim3(64), 0, st, dseq, dwin, C, (int64_t)J,
+                           rng, mask, p, n, dsigns + s0, dcnt, (const int64_t*)nullptr, dpl);
+        hipLaunchKernelGGL(k_mt_scan, dim3((b + 63) / 64), dim3(64), 0, st, dcnt, doff, (int)b, C);
+        hipLaunchKernelGGL((k_mt_chunk<false, true>), dim3(C, b), dim3(64), 0, st, dseq, dwin, C, (int64_t)J,
+                           rng, mask, p, n, dsigns + s0, dcnt, (const int64_t*)doff, dpl);
+        hipLaunchKernelGGL((k_mt_fold_planes<false>), dim3(fold_blocks), dim3(kBlock), 0, st, (const void*)dpl,
+                           (int)b, n, p, (int64_t*)d_out, s0 == 0 ? 1 : 0);
+      }
+    }
+    FA_HIP(hipGetLastError());
+    return release(slot, st);
+  }
   int first = 1;
   for (uint64_t s0 = 0; s0 < (uint64_t)num_streams; s0 += per) {
     const unsigned b = (unsigned)std::min<uint64_t>(per, (uint64_t)num_streams - s0);

@@ -209,6 +209,28 @@ def test_mt_randint_sum_vs_numpy(eng, p):
     assert np.array_equal(got, exp)
 
 
+@pytest.mark.parametrize("log2,plane_mb", [(0, None), (3, None), (3, "1")])
+@pytest.mark.parametrize("p", [40961, 2 ** 31 - 1, 2 ** 32 + 15, 2 ** 61 - 1])
+def test_mt_randint_sum_jump_ahead_vs_numpy(eng, p, log2, plane_mb, monkeypatch):
+    """The jump-ahead expansion (chunks of 624 << log2 words started from x^(cJ) mod phi, a counting
+    pass, a scan, a placing pass into per-stream planes and a fold) forced at small chunk sizes --
+    hundreds of chunks per stream, the last one running past its share -- against numpy's own streams,
+    bit for bit, for 32- and 64-bit draws; plane_mb = 1 folds one stream's plane at a time."""
+    monkeypatch.setenv("FA_MT_JUMP_LOG2", str(log2))
+    if plane_mb:
+        monkeypatch.setenv("FA_MT_PLANE_MB", plane_mb)
+    n = 200_003
+    seeds = [0, 1, 2 ** 32 - 1, 987654321, 5, 5, 31337, 2 ** 31, 77, 1234567, 4242]
+    signs = [1, -1, 1, -1, 1, 1, -1, 1, -1, 1, -1]
+    got = eng.mt_randint_sum(seeds, signs, p, n).cpu().numpy()
+    acc = np.zeros(n, dtype=object)
+    for s, g in zip(seeds, signs):
+        np.random.seed(s)
+        acc = acc + g * np.random.randint(0, p, size=n).astype(object)
+    exp = np.array([int(a) % p for a in acc], dtype=np.int64)
+    assert np.array_equal(got, exp)
+
+
 def test_mt_randint_sum_edges(eng):
     from oracle import mt_port
     assert torch.equal(eng.mt_randint_sum([3], [1], 1, 10).cpu(), torch.zeros(10, dtype=torch.int64))  # p = 1

@@ -80,6 +80,52 @@ __global__ void __launch_bounds__(kThreads) k_once(const float* in, float* out, 
   if (threadIdx.x == 0) st_sys(&ctl->done, seq);
 }
 
+// G workgroups, 16-byte loads, each workgroup a contiguous slice; the last one to finish (device
+// counter) stores the completion word
+__global__ void __launch_bounds__(256) k_multi(const float* in, float* out, float w0, float w1, Ctl* ctl,
+                                               unsigned long long seq, unsigned* counter) {
+  constexpr int V4 = P / 4;  // P = 7850 is not a multiple of 4: the last 2 floats separately
+  const float4* a = (const float4*)in;
+  const float4* b = (const float4*)(in + P + 2);  // client 1 starts 16-byte aligned (P + 2 floats pad)
+  float4* o = (float4*)out;
+  const int per = (V4 + gridDim.x - 1) / gridDim.x;
+  const int lo = blockIdx.x * per, hi = min(V4, lo + per);
+  constexpr int R = 8;
+  float4 xa[R], xb[R];
+  for (int base = lo; base < hi; base += 256 * R) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int i = base + r * 256 + (int)threadIdx.x;
+      if (i < hi) { xa[r] = a[i]; xb[r] = b[i]; }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int i = base + r * 256 + (int)threadIdx.x;
+      if (i < hi) {
+        float4 v;
+        v.x = __fadd_rn(__fmul_rn(xa[r].x, w0), __fmul_rn(xb[r].x, w1));
+        v.y = __fadd_rn(__fmul_rn(xa[r].y, w0), __fmul_rn(xb[r].y, w1));
+        v.z = __fadd_rn(__fmul_rn(xa[r].z, w0), __fmul_rn(xb[r].z, w1));
+        v.w = __fadd_rn(__fmul_rn(xa[r].w, w0), __fmul_rn(xb[r].w, w1));
+        o[i] = v;
+      }
+    }
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x < P - 4 * V4) {
+    const int e = 4 * V4 + threadIdx.x;
+    out[e] = __fadd_rn(__fmul_rn(in[e], w0), __fmul_rn(in[P + 2 + e], w1));
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      st_sys(&ctl->done, seq);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kThreads) k_resident(const float* in, float* out, float w0, float w1, Ctl* ctl,
                                                        unsigned long long last, unsigned long long idle_ticks) {
   __shared__ unsigned long long job;
@@ -194,6 +240,30 @@ int main(int argc, char** argv) {
   }
   CK(hipStreamSynchronize(st));
   check("launch+flag");
+  // G workgroups (16-byte loads, padded layout: client 1 at P + 2)
+  unsigned* counter;
+  CK(hipMalloc((void**)&counter, 4));
+  CK(hipMemset(counter, 0, 4));
+  auto pack2 = [&] {
+    memcpy(hin, x0.data(), P * 4);
+    memcpy(hin + P + 2, x1.data(), P * 4);
+  };
+  std::vector<std::pair<int, double>> t_multi;
+  for (int G : {1, 2, 4, 8, 16, 32, 64}) {
+    std::vector<double> t;
+    for (int i = 0; i < iters / 3; ++i) {
+      auto t0 = now();
+      pack2();
+      const unsigned long long s = ++seq;
+      hipLaunchKernelGGL(k_multi, dim3(G), dim3(256), 0, st, din, dout + 4, w0, w1, dctl, s, counter);
+      wait_done(s);
+      memcpy(res.data(), hout + 4, P * 4);
+      t.push_back(us(t0, now()));
+    }
+    CK(hipStreamSynchronize(st));
+    check("multi");
+    t_multi.push_back({G, med(t)});
+  }
   // doorbell: one resident kernel; idle exit after 20 ms (100 MHz ticks)
   ctl->doorbell = seq;
   hipLaunchKernelGGL(k_resident, dim3(1), dim3(kThreads), 0, st, din, dout, w0, w1, dctl, seq, 2000000ull);
@@ -237,8 +307,11 @@ int main(int argc, char** argv) {
     return med(v);
   };
   printf("{\"launch_event_us\": %.2f, \"launch_flag_us\": %.2f, \"doorbell_us\": %.2f, \"doorbell_cold_us\": %.2f, "
-         "\"pack_copy_only_us\": %.2f, \"iters\": %d}\n",
+         "\"pack_copy_only_us\": %.2f, \"iters\": %d, \"launch_flag_by_workgroups_us\": {",
          med(t_ev), med(t_flag), med(t_bell), med(t_cold), pk(), iters);
+  for (size_t i = 0; i < t_multi.size(); ++i)
+    printf("%s\"%d\": %.2f", i ? ", " : "", t_multi[i].first, t_multi[i].second);
+  printf("}}\n");
   CK(hipHostFree(hb));
   return 0;
 }
