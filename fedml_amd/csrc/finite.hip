@@ -547,56 +547,114 @@ __global__ void __launch_bounds__(64) k_mt_seq(const uint32_t* __restrict__ seed
 }
 
 // W_c for chunk c = blockIdx.x + 1 of stream blockIdx.y: the correlation of the stream's sequence
-// with the set bits of x^(cJ) mod phi, given by the host as a list of bit positions (stride words
-// per chunk: the padded count, 3 unused, the positions padded to a multiple of 16 with kMtJumpSeq,
-// whose window in LDS is all zero).  The sequence (82 KB + the zero pad) and up to kMtPosLds
-// positions sit in LDS; thread t owns words t, t + 256, t + 512 of the window; sixteen positions
-// are read per step (four broadcast 16-byte LDS reads), then up to 48 sequence words.
-constexpr int kMtJumpSeq = 19937 + 624;  // words of the sequence a jump reads
-constexpr int kMtJumpPad = 768;          // zero words after it (the pad position's window)
-constexpr int kMtPosLds = 12288;         // positions staged per round (a longer list takes rounds)
-__global__ void __launch_bounds__(256) k_mt_jump(const uint32_t* __restrict__ seq, const int32_t* __restrict__ pos,
-                                                 int stride, int chunks, uint32_t* __restrict__ windows) {
+// with the set bits of x^(cJ) mod phi, given by the host as two lists of bit positions, even then
+// odd, each stored as the index of the aligned word pair it reads, floor(i / 2) (row of `stride` int32
+// per chunk: E, O, 0, 0, E even, O odd; E and O padded to multiples of 32 with the zero-window
+// positions kMtPadEven / kMtPadOdd).  The sequence sits in
+// LDS (85 KB, 8-byte aligned).  Word pairs: for an even position i thread u reads the aligned pair
+// (x_{i+2u}, x_{i+2u+1}) -> words 2u, 2u+1; for an odd i the aligned pair (x_{i+2u-1}, x_{i+2u}) ->
+// words 2u-1, 2u: one ds_read_b64 per thread and position (256 B/clk) instead of two 4-byte reads.
+// 640 threads = two groups of 320 (313 needed: u = 0..312), each taking half of every list; the
+// halves, then the neighbour's odd pair, are combined through LDS at the end.
+constexpr int kMtJumpSeq = 19937 + 624;  // words of the sequence a jump reads (x_0 .. x_20560)
+constexpr int kMtPadEven = 20562;        // pad positions: their windows (the next 626 words) are zero
+constexpr int kMtPadOdd = 20563;
+constexpr int kMtJumpLds = 20562 + 640;  // LDS words of the sequence + the zero region
+constexpr int kMtPosLds = 8192;          // positions staged per round
+constexpr int kMtJumpThreads = 640;
+__global__ void __launch_bounds__(kMtJumpThreads) k_mt_jump(const uint32_t* __restrict__ seq,
+                                                            const int32_t* __restrict__ pos, int stride, int chunks,
+                                                            uint32_t* __restrict__ windows) {
   typedef int i32x4 __attribute__((ext_vector_type(4)));
-  __shared__ uint32_t xs[kMtJumpSeq + kMtJumpPad];
+  typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
+  __shared__ __attribute__((aligned(16))) uint32_t xs[kMtJumpLds];
   __shared__ i32x4 pl[kMtPosLds / 4];
-  const int t = threadIdx.x;
+  __shared__ u32x2v cmb[2][320];
+  const int tid = threadIdx.x;
+  const int grp = tid / 320, u = tid % 320;
   const int s = blockIdx.y, c = blockIdx.x + 1;
-  const uint32_t* src = seq + (size_t)s * kMtSeqWords;
-  for (int i = t; i < kMtJumpSeq + kMtJumpPad; i += 256) xs[i] = i < kMtJumpSeq ? src[i] : 0u;
-  const int32_t* ps = pos + (size_t)(c - 1) * stride;
-  const int cnt = ps[0];  // a multiple of 16
-  ps += 4;
-  const bool w2 = t + 512 < kMtN;  // threads whose third word exists (t < 112)
-  uint32_t a0 = 0, a1 = 0, a2 = 0;
-  for (int r0 = 0; r0 < cnt; r0 += kMtPosLds) {
-    const int rn = min(kMtPosLds, cnt - r0);
-    __syncthreads();  // the previous round's positions are consumed
-    for (int q = t; q < rn / 4; q += 256) pl[q] = ((const i32x4*)(ps + r0))[q];
-    __syncthreads();
-    for (int k = 0; k < rn / 4; k += 4) {
-      const i32x4 p0 = pl[k], p1 = pl[k + 1], p2 = pl[k + 2], p3 = pl[k + 3];  // broadcast reads
-      const int ii[16] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w,
-                          p2.x, p2.y, p2.z, p2.w, p3.x, p3.y, p3.z, p3.w};
-      uint32_t b0 = 0, b1 = 0, b2 = 0;
+  {  // the sequence into LDS: 16-byte loads, all of a thread's in flight before its stores
+    const u32x4* src4 = (const u32x4*)(seq + (size_t)s * kMtSeqWords);  // 84,864-byte rows: aligned
+    u32x4* xs4 = (u32x4*)xs;
+    constexpr int NV = kMtJumpLds / 4, R = (NV + kMtJumpThreads - 1) / kMtJumpThreads;
+    constexpr int NS = (kMtJumpSeq + 3) / 4;  // vectors holding sequence words (the last one partly)
+    u32x4 v[R];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        b0 ^= xs[ii[q] + t];
-        b1 ^= xs[ii[q] + t + 256];
-      }
-      if (w2) {
+    for (int r = 0; r < R; ++r) {
+      const int q = tid + r * kMtJumpThreads;
+      v[r] = q < NS ? src4[q] : u32x4{0u, 0u, 0u, 0u};
+    }
 #pragma unroll
-        for (int q = 0; q < 16; ++q) b2 ^= xs[ii[q] + t + 512];
+    for (int r = 0; r < R; ++r) {
+      const int q = tid + r * kMtJumpThreads;
+      if (q == NS - 1) {  // words past x_20560 are zero
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (4 * q + j >= kMtJumpSeq) v[r][j] = 0u;
       }
-      a0 ^= b0;
-      a1 ^= b1;
-      a2 ^= b2;
+      if (q < NV) xs4[q] = v[r];
     }
   }
-  uint32_t* out = windows + ((size_t)s * chunks + c) * kMtN;
-  out[t] = a0;
-  out[t + 256] = a1;
-  if (w2) out[t + 512] = a2;
+  const int32_t* row = pos + (size_t)(c - 1) * stride;
+  const int E = row[0], O = row[1];
+  const int32_t* lists = row + 4;
+  u32x2v ae = {0u, 0u}, ao = {0u, 0u};
+  const u32x2v* xp = (const u32x2v*)xs;  // the sequence as aligned word pairs
+  // the two lists, one after the other, staged in rounds; group g takes the g-th half of a round
+  for (int pass = 0; pass < 2; ++pass) {
+    const int len = pass ? O : E;
+    const int32_t* lp = lists + (pass ? E : 0);
+    for (int r0 = 0; r0 < len; r0 += kMtPosLds) {
+      const int rn = min(kMtPosLds, len - r0);  // a multiple of 32
+      __syncthreads();  // the previous round's positions (and, first, nothing) are consumed
+      {  // <= kMtPosLds / 4 = 2,048 vectors: up to 4 loads per thread, in flight together
+        const i32x4* lv = (const i32x4*)(lp + r0);
+        i32x4 w[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = tid + r * kMtJumpThreads;
+          if (q < rn / 4) w[r] = lv[q];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int q = tid + r * kMtJumpThreads;
+          if (q < rn / 4) pl[q] = w[r];
+        }
+      }
+      __syncthreads();
+      const int half = rn / 2;  // a multiple of 16
+      const int mine = grp * (half / 4);          // this group's first position vector
+      u32x2v acc = {0u, 0u};
+      for (int k = 0; k < half / 4; k += 4) {
+        const i32x4 p0 = pl[mine + k], p1 = pl[mine + k + 1], p2 = pl[mine + k + 2], p3 = pl[mine + k + 3];  // broadcast
+        const int ii[16] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w,
+                            p2.x, p2.y, p2.z, p2.w, p3.x, p3.y, p3.z, p3.w};
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc ^= xp[ii[q] + u];  // aligned pair: ds_read_b64
+      }
+      if (pass) ao ^= acc;
+      else ae ^= acc;
+    }
+  }
+  // combine the groups' halves, then words 2u = E.x ^ O.y and 2u + 1 = E.y ^ O(u+1).x
+  __syncthreads();
+  if (grp == 1) {
+    cmb[0][u] = ae;
+    cmb[1][u] = ao;
+  }
+  __syncthreads();
+  if (grp == 0) {
+    ae ^= cmb[0][u];
+    ao ^= cmb[1][u];
+  }
+  __syncthreads();
+  if (grp == 0) cmb[1][u] = ao;  // every thread's odd pair, for its left neighbour
+  __syncthreads();
+  if (grp == 0 && u < kMtN / 2) {
+    uint32_t* out = windows + ((size_t)s * chunks + c) * kMtN;
+    out[2 * u] = ae.x ^ ao.y;
+    out[2 * u + 1] = ae.y ^ cmb[1][u + 1].x;
+  }
 }
 
 // Pass 1 (PLACE = false): accepted draws of chunks 0 .. chunks-2 of every stream -> counts[s][c].
@@ -610,9 +668,9 @@ template <bool WIDE, bool PLACE>
 __global__ void __launch_bounds__(64)
 k_mt_chunk(const uint32_t* __restrict__ seq, const uint32_t* __restrict__ windows, int chunks, int64_t jwords,
            uint64_t rng, uint64_t mask, uint64_t p, int64_t n, const int8_t* __restrict__ signs,
-           int64_t* __restrict__ counts, const int64_t* __restrict__ offs, void* __restrict__ planes) {
+           int64_t* __restrict__ counts, const int64_t* __restrict__ offs, void* __restrict__ planes, int64_t pstride) {
   using PT = typename std::conditional<WIDE, uint64_t, uint32_t>::type;
-  PT* plane = (PT*)planes + (size_t)blockIdx.y * n;
+  PT* plane = (PT*)planes + (size_t)blockIdx.y * pstride;
   __shared__ uint32_t mt[2][kMtN];
   const int lane = threadIdx.x;
   const int c = blockIdx.x, s = blockIdx.y;
@@ -660,24 +718,47 @@ k_mt_chunk(const uint32_t* __restrict__ seq, const uint32_t* __restrict__ window
 }
 
 // total[e] = (first ? 0 : total[e]) + sum over the g planes of element e, mod p (planes hold values
-// in [0, p); 32-bit planes sum in uint64 and reduce once, 64-bit planes add modulo p one by one)
+// in [0, p), pstride elements apart, a multiple of 4: 32-bit planes are read as 16-byte vectors of
+// four elements and summed in uint64, reduced once; 64-bit planes add modulo p one by one)
 template <bool WIDE>
 __global__ void __launch_bounds__(kBlock)
-k_mt_fold_planes(const void* __restrict__ planes, int g, int64_t n, uint64_t p, int64_t* __restrict__ total, int first) {
-  for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (int64_t)gridDim.x * kBlock) {
-    uint64_t t = first ? 0 : (uint64_t)total[e];
-    if constexpr (WIDE) {
+k_mt_fold_planes(const void* __restrict__ planes, int g, int64_t n, int64_t pstride, uint64_t p,
+                 int64_t* __restrict__ total, int first) {
+  if constexpr (WIDE) {
+    for (int64_t e = (int64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (int64_t)gridDim.x * kBlock) {
+      uint64_t t = first ? 0 : (uint64_t)total[e];
       const uint64_t* pl = (const uint64_t*)planes + e;
       for (int s = 0; s < g; ++s) {
-        t += __builtin_nontemporal_load(pl + (size_t)s * n);
+        t += __builtin_nontemporal_load(pl + (size_t)s * pstride);
         if (t >= p) t -= p;
       }
-    } else {
-      const uint32_t* pl = (const uint32_t*)planes + e;
-      for (int s = 0; s < g; ++s) t += __builtin_nontemporal_load(pl + (size_t)s * n);
-      t %= p;
+      total[e] = (int64_t)t;
     }
-    total[e] = (int64_t)t;
+  } else {
+    const int64_t nv = (n + 3) / 4;
+    for (int64_t v = (int64_t)blockIdx.x * kBlock + threadIdx.x; v < nv; v += (int64_t)gridDim.x * kBlock) {
+      const int64_t e = 4 * v;
+      uint64_t t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+      const u32x4* pl = (const u32x4*)((const uint32_t*)planes + e);
+      for (int s = 0; s < g; ++s) {
+        const u32x4 x = __builtin_nontemporal_load(pl + (size_t)s * (pstride / 4));
+        t0 += x[0];
+        t1 += x[1];
+        t2 += x[2];
+        t3 += x[3];
+      }
+      const uint64_t tt[4] = {t0, t1, t2, t3};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if (e + j >= n) break;
+        uint64_t t = tt[j] % p;
+        if (!first) {
+          t += (uint64_t)total[e + j];
+          if (t >= p) t -= p;
+        }
+        total[e + j] = (int64_t)t;
+      }
+    }
   }
 }
 
@@ -948,26 +1029,29 @@ int mt_jump_log2(double exp_words, int streams) {
 }
 
 // The set-bit positions of x^(cJ) mod phi, c = 1..count, on the device (ctx->mt_poly_dev; one row
-// of `stride` int32 per chunk: the padded count, 3 unused, then the positions, padded to a multiple
-// of 16 with kMtJumpSeq; stride a multiple of 4 so that every row starts 16-byte aligned).  Host polynomials are cached per J (mt_poly.h); the device table is rebuilt
+// of `stride` int32 per chunk: E, O, 0, 0, the E even positions, the O odd ones, each list padded to a
+// multiple of 32 with kMtPadEven / kMtPadOdd; stride a multiple of 4: every list 16-byte aligned).  Host polynomials are cached per J (mt_poly.h); the device table is rebuilt
 // only when J or the count grows.
 int mt_jump_tables(fa_ctx* ctx, uint64_t J, int count, hipStream_t st) {
   if (ctx->mt_poly_dev && ctx->mt_poly_J == J && ctx->mt_poly_count >= count) return FA_OK;
   if (fa_mt::charpoly().empty()) return fail(FA_ERR_INVALID, "fa_mt_randint_sum: MT19937 characteristic polynomial not found");
   const std::vector<fa_mt::Poly>& g = fa_mt::jump_polys(J, count);
-  std::vector<std::vector<int32_t>> rows((size_t)count);
+  std::vector<std::vector<int32_t>> ev((size_t)count), od((size_t)count);
   int stride = 0;
   for (int c = 0; c < count; ++c) {
     for (int i = 0; i < fa_mt::kDeg; ++i)
-      if (fa_mt::get_bit(g[(size_t)c], i)) rows[(size_t)c].push_back(i);
-    while (rows[(size_t)c].size() % 16) rows[(size_t)c].push_back(kMtJumpSeq);
-    stride = std::max<int>(stride, 4 + (int)rows[(size_t)c].size());  // 4 + a multiple of 16
+      if (fa_mt::get_bit(g[(size_t)c], i)) (i & 1 ? od : ev)[(size_t)c].push_back(i >> 1);  // pair index
+    while (ev[(size_t)c].size() % 32) ev[(size_t)c].push_back(kMtPadEven >> 1);
+    while (od[(size_t)c].size() % 32) od[(size_t)c].push_back(kMtPadOdd >> 1);
+    stride = std::max<int>(stride, 4 + (int)(ev[(size_t)c].size() + od[(size_t)c].size()));  // 4 + a multiple of 32
   }
   std::vector<int32_t> tab((size_t)count * stride, 0);
   for (int c = 0; c < count; ++c) {
     int32_t* r = &tab[(size_t)c * stride];
-    r[0] = (int32_t)rows[(size_t)c].size();
-    std::copy(rows[(size_t)c].begin(), rows[(size_t)c].end(), r + 4);
+    r[0] = (int32_t)ev[(size_t)c].size();
+    r[1] = (int32_t)od[(size_t)c].size();
+    std::copy(ev[(size_t)c].begin(), ev[(size_t)c].end(), r + 4);
+    std::copy(od[(size_t)c].begin(), od[(size_t)c].end(), r + 4 + ev[(size_t)c].size());
   }
   FA_HIP(hipStreamSynchronize(st));  // a previous table may still be read by queued kernels
   if (ctx->mt_poly_dev) FA_HIP(hipFree(ctx->mt_poly_dev));
@@ -1051,9 +1135,10 @@ int fa_mt_randint_sum(fa_ctx* ctx, int32_t num_streams, const uint32_t* seeds, c
     if (rc) return rc;
     // streams per group: their planes (n values each) within the plane budget
     const size_t es = wide ? 8 : 4;
-    const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)num_streams, mt_plane_budget() / ((uint64_t)n * es)));
+    const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)num_streams, mt_plane_budget() / (((uint64_t)n + 3) / 4 * 4 * es)));
     const size_t seq_b = align16(sizeof(uint32_t) * kMtSeqWords * G), win_b = align16(sizeof(uint32_t) * kMtN * C * G);
-    const size_t cnt_b = align16(sizeof(int64_t) * C * G), pl_b = (size_t)G * n * es;
+    const int64_t pstride = (n + 3) / 4 * 4;  // plane stride: every plane 16-byte aligned
+    const size_t cnt_b = align16(sizeof(int64_t) * C * G), pl_b = (size_t)G * pstride * es;
     rc = mt_work(ctx, seq_b + win_b + 2 * cnt_b + pl_b, st);
     if (rc) return rc;
     char* w = (char*)ctx->mt_dev;
@@ -1066,23 +1151,23 @@ int fa_mt_randint_sum(fa_ctx* ctx, int32_t num_streams, const uint32_t* seeds, c
     for (uint64_t s0 = 0; s0 < (uint64_t)num_streams; s0 += G) {
       const unsigned b = (unsigned)std::min<uint64_t>(G, (uint64_t)num_streams - s0);
       hipLaunchKernelGGL(k_mt_seq, dim3(b), dim3(64), 0, st, dseeds + s0, dseq);
-      hipLaunchKernelGGL(k_mt_jump, dim3(C - 1, b), dim3(256), 0, st, dseq, dpos, ctx->mt_poly_stride, C, dwin);
+      hipLaunchKernelGGL(k_mt_jump, dim3(C - 1, b), dim3(kMtJumpThreads), 0, st, dseq, dpos, ctx->mt_poly_stride, C, dwin);
       if (wide) {
         hipLaunchKernelGGL((k_mt_chunk<true, false>), dim3(C - 1, b), dim3(64), 0, st, dseq, dwin, C, (int64_t)J, rng,
-                           mask, p, n, dsigns + s0, dcnt, (const int64_t*)nullptr, dpl);
+                           mask, p, n, dsigns + s0, dcnt, (const int64_t*)nullptr, dpl, pstride);
         hipLaunchKernelGGL(k_mt_scan, dim3((b + 63) / 64), dim3(64), 0, st, dcnt, doff, (int)b, C);
         hipLaunchKernelGGL((k_mt_chunk<true, true>), dim3(C, b), dim3(64), 0, st, dseq, dwin, C, (int64_t)J, rng,
-                           mask, p, n, dsigns + s0, dcnt, (const int64_t*)doff, dpl);
+                           mask, p, n, dsigns + s0, dcnt, (const int64_t*)doff, dpl, pstride);
         hipLaunchKernelGGL((k_mt_fold_planes<true>), dim3(fold_blocks), dim3(kBlock), 0, st, (const void*)dpl, (int)b,
-                           n, p, (int64_t*)d_out, s0 == 0 ? 1 : 0);
+                           n, pstride, p, (int64_t*)d_out, s0 == 0 ? 1 : 0);
       } else {
         hipLaunchKernelGGL((k_mt_chunk<false, false>), dim3(C - 1, b), dim3(64), 0, st, dseq, dwin, C, (int64_t)J,
-                           rng, mask, p, n, dsigns + s0, dcnt, (const int64_t*)nullptr, dpl);
+                           rng, mask, p, n, dsigns + s0, dcnt, (const int64_t*)nullptr, dpl, pstride);
         hipLaunchKernelGGL(k_mt_scan, dim3((b + 63) / 64), dim3(64), 0, st, dcnt, doff, (int)b, C);
         hipLaunchKernelGGL((k_mt_chunk<false, true>), dim3(C, b), dim3(64), 0, st, dseq, dwin, C, (int64_t)J,
-                           rng, mask, p, n, dsigns + s0, dcnt, (const int64_t*)doff, dpl);
+                           rng, mask, p, n, dsigns + s0, dcnt, (const int64_t*)doff, dpl, pstride);
         hipLaunchKernelGGL((k_mt_fold_planes<false>), dim3(fold_blocks), dim3(kBlock), 0, st, (const void*)dpl,
-                           (int)b, n, p, (int64_t*)d_out, s0 == 0 ? 1 : 0);
+                           (int)b, n, pstride, p, (int64_t*)d_out, s0 == 0 ? 1 : 0);
       }
     }
     FA_HIP(hipGetLastError());
