@@ -768,33 +768,34 @@ k_mix(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict__ co
 
 // --------------------------------------------------------------------------------------------
 // Banded mixing (ring-like gossip): every entry of row r reads input (r + off + d) mod num_in with
-// d in {-1, 0, +1} (host-checked).  Rows are walked in order with a register sliding window over
+// d in {-1, 0, +1} (host-checked); NT: non-temporal input loads (the default launch).  Rows are walked in order with a register sliding window over
 // the inputs, so each input tile is loaded ONCE per workgroup (k_mix re-reads neighbours through
 // L2/MALL: +8 % HBM traffic at 256 nodes).  Per group of RG rows the RG new window slots are loaded
 // together; each CSR entry picks its slot by a wave-uniform switch (scalar branches, no VALU select),
 // so the accumulation order is still the CSR order, bit for bit.
-template <int DT, int RG, bool POST>
+template <int DT, int RG, bool POST, bool NT = false>
 __global__ void __launch_bounds__(kBlock)
 k_mix_band(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict__ cols,
            const double* __restrict__ vals, const void* const* __restrict__ in, int num_in, int off,
-           int64_t n, int64_t isst, int64_t osst) {
+           int64_t n, int64_t isst, int64_t osst, int xcd) {
   using T = Tr<DT, FA_MODE_MUL_W>;
   constexpr int V = T::V;
   constexpr int64_t TILE = (int64_t)kBlock * V;
-  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const int64_t bt = xcd ? xcd_tile(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;  // see k_wsum
+  const int64_t base = bt * TILE;
   const float dz = 0.f;
   const int64_t ist = isst ? isst : TILE * T::IN_BYTES, ost = osst ? osst : TILE * T::OUT_BYTES;
   auto wrap = [num_in](int c) { c %= num_in; return c < 0 ? c + num_in : c; };
 
   if (base + TILE <= n) {
-    const int64_t boff = (int64_t)blockIdx.x * ist + (int64_t)threadIdx.x * V * T::IN_BYTES;
-    const int64_t ooff = (int64_t)blockIdx.x * ost + (int64_t)threadIdx.x * V * T::OUT_BYTES;
+    const int64_t boff = bt * ist + (int64_t)threadIdx.x * V * T::IN_BYTES;
+    const int64_t ooff = bt * ost + (int64_t)threadIdx.x * V * T::OUT_BYTES;
     u32x4 win[RG + 2];  // win[s] = input (r0 + off - 1 + s) mod num_in
-    win[0] = ld16<false>((const char*)in[wrap(off - 1)] + boff);
-    win[1] = ld16<false>((const char*)in[wrap(off)] + boff);
+    win[0] = ld16<NT>((const char*)in[wrap(off - 1)] + boff);
+    win[1] = ld16<NT>((const char*)in[wrap(off)] + boff);
     for (int r0 = 0; r0 < nrows; r0 += RG) {
 #pragma unroll
-      for (int g = 0; g < RG; ++g) win[2 + g] = ld16<false>((const char*)in[wrap(r0 + off + 1 + g)] + boff);
+      for (int g = 0; g < RG; ++g) win[2 + g] = ld16<NT>((const char*)in[wrap(r0 + off + 1 + g)] + boff);
 #pragma unroll
       for (int g = 0; g < RG; ++g) {
         if (r0 + g < nrows) {  // wave-uniform
@@ -2057,19 +2058,31 @@ int mix_impl(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t* row
   for (int r = 0; r < rows; ++r) maxdeg = std::max(maxdeg, row_ptr[r + 1] - row_ptr[r]);
   const int band = (aligned && ctx->mix_band) ? band_offset(rows, row_ptr, cols, num_in) : INT32_MIN;
   if (band != INT32_MIN) {
+    // non-temporal input loads by default (r03r interleaved A/B, cfg5 256-node ring: 5.23-5.32 ->
+    // 4.41-4.42 ms; every model is read once per workgroup).  FA_BAND_VAR (A/B measurement): 0 cached
+    // loads, 2 XCD-contiguous tiles, 3 both NT + XCD, 4 NT + XCD + 16-row groups (within 1 % of 1)
+    static const int bv = [] {
+      const char* e = getenv("FA_BAND_VAR");
+      return e ? atoi(e) : 1;
+    }();
+    const int xm = (bv == 2 || bv >= 3) ? 1 : 0;
+#define FA_BAND_K(DT, RG, POST, NT) \
+    hipLaunchKernelGGL((k_mix_band<DT, RG, POST, NT>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, num_in, band, n, isst, osst, xm)
 #define FA_BAND(DT)                                                                                   \
-  if (post_scale)                                                                                     \
-    hipLaunchKernelGGL((k_mix_band<DT, 8, true>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, num_in, band, n, \
-                       isst, osst);                                                                   \
-  else                                                                                                \
-    hipLaunchKernelGGL((k_mix_band<DT, 8, false>), grid, blk, 0, st, drw, rows, dcol, dval, dptr, num_in, band, n, \
-                       isst, osst);
+  if (post_scale) {                                                                                   \
+    if (bv == 1 || bv == 3) FA_BAND_K(DT, 8, true, true); else if (bv == 4) FA_BAND_K(DT, 16, true, true); \
+    else FA_BAND_K(DT, 8, true, false);                                                               \
+  } else {                                                                                            \
+    if (bv == 1 || bv == 3) FA_BAND_K(DT, 8, false, true); else if (bv == 4) FA_BAND_K(DT, 16, false, true); \
+    else FA_BAND_K(DT, 8, false, false);                                                              \
+  }
     switch (dtype) {
       case FA_DTYPE_F32: FA_BAND(FA_DTYPE_F32); break;
       case FA_DTYPE_BF16: FA_BAND(FA_DTYPE_BF16); break;
       case FA_DTYPE_F16: FA_BAND(FA_DTYPE_F16); break;
     }
 #undef FA_BAND
+#undef FA_BAND_K
     FA_HIP(hipGetLastError());
     return release(slot, st);
   }

@@ -1128,14 +1128,15 @@ int fa_mt_randint_sum(fa_ctx* ctx, int32_t num_streams, const uint32_t* seeds, c
   const unsigned fold_blocks = (unsigned)std::min<int64_t>((n + kBlock - 1) / kBlock, 4096);
   // jump-ahead: C chunks of J words per stream when the stream is long enough for >= 2 of them
   const double exp_words = (double)n * (wide ? 2.0 : 1.0) * ((double)mask + 1.0) / ((double)rng + 1.0);
-  const uint64_t J = 624ull << mt_jump_log2(exp_words, (int)std::min<uint64_t>(per, (uint64_t)num_streams));
+  // streams per group: their planes (n values each) within the plane budget; the chunk size is chosen
+  // for the streams of one group (the groups run one after another)
+  const size_t es = wide ? 8 : 4;
+  const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)num_streams, mt_plane_budget() / (((uint64_t)n + 3) / 4 * 4 * es)));
+  const uint64_t J = 624ull << mt_jump_log2(exp_words, (int)G);
   const int C = mt_jump_enabled() ? (int)std::min<double>(std::floor(exp_words / (double)J), 4096.0) : 0;
   if (C >= 2) {
     rc = mt_jump_tables(ctx, J, C - 1, st);
     if (rc) return rc;
-    // streams per group: their planes (n values each) within the plane budget
-    const size_t es = wide ? 8 : 4;
-    const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)num_streams, mt_plane_budget() / (((uint64_t)n + 3) / 4 * 4 * es)));
     const size_t seq_b = align16(sizeof(uint32_t) * kMtSeqWords * G), win_b = align16(sizeof(uint32_t) * kMtN * C * G);
     const int64_t pstride = (n + 3) / 4 * 4;  // plane stride: every plane 16-byte aligned
     const size_t cnt_b = align16(sizeof(int64_t) * C * G), pl_b = (size_t)G * pstride * es;
