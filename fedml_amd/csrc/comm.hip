@@ -328,7 +328,6 @@ int ordered(fa_ctx* ctx, fa_comm* c, bool to_all, const fa_local_step* L, int64_
     }
     rc = order(c, st, c->sa);
     if (rc) return rc;
-    const int64_t L_me = p.psize[ch * world + me], r0 = world * p.roff[ch];
     set_op(c, "chunk %lld/%lld: partials to the owners (point-to-point over every link)", (long long)(ch + 1),
            (long long)p.C);
     xchg_ops(p, world, me, root, to_all, 0, ch, ops);

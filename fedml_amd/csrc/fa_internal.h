@@ -38,6 +38,15 @@ __device__ __forceinline__ int find_seg(const S* __restrict__ segs, int nseg, in
   return lo;
 }
 
+// XCD-contiguous workgroup -> tile map: the dispatcher deals workgroups to the 8 XCDs round-robin;
+// XCD x then walks a contiguous eighth of the tiles (one XCD's L2 and translation caches see a few
+// allocations' neighbourhoods instead of all of them)
+__device__ __forceinline__ int64_t xcd_tile_map(int64_t bid, int64_t tiles) {
+  constexpr int64_t kX = 8;
+  const int64_t x = bid % kX, j = bid / kX, q = tiles / kX, r = tiles % kX;
+  return x * q + (x < r ? x : r) + j;
+}
+
 // Record the calling thread's last error (fa_last_error) and return `code`.
 int fail(int code, const char* fmt, ...);
 const char* last_error();

@@ -383,11 +383,7 @@ __device__ __forceinline__ void wsum_tile(const Seg* __restrict__ segs, int nseg
 // xcd = 1: workgroup -> tile mapping by XCD (the dispatcher deals workgroups to the 8 XCDs
 // round-robin; XCD x then walks a contiguous eighth of the tiles, so one XCD's L2 and address
 // translation caches see a few segments' allocations instead of all of them)
-__device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t tiles) {
-  constexpr int64_t kX = 8;
-  const int64_t x = bid % kX, j = bid / kX, q = tiles / kX, r = tiles % kX;
-  return x * q + min(x, r) + j;
-}
+__device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t tiles) { return xcd_tile_map(bid, tiles); }
 
 bool xcd_map_enabled() {  // FA_XCD_MAP=0: round-robin workgroup -> tile order everywhere (A/B)
   static const int on = [] {

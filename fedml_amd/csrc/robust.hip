@@ -232,14 +232,14 @@ constexpr int k2lCols = kBlock / 2;  // columns per workgroup
 constexpr unsigned kNegInfKey = 0x007FFFFFu, kPosInfKey = 0xFF800000u;  // fkey(-inf), fkey(+inf)
 template <int DT, int N, bool EXACT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MEDIAN_2L_W)))
-k_median_2l(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k) {
+k_median_2l(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int xcd) {
   constexpr int B = 2 * N;
   if constexpr (EXACT) k = B;
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   __shared__ u32x4 xs[N / 4][k2lCols];  // the upper lanes' N sorted keys, [quad][column]
   const int h = __builtin_amdgcn_readfirstlane((int)threadIdx.x / k2lCols);  // half: wave-uniform
   const int c = (int)threadIdx.x % k2lCols;
-  const int64_t tile = blockIdx.x;
+  const int64_t tile = xcd ? xcd_tile_map(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   const MSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
   const int64_t e = (tile - sg.tile_start) * k2lCols + c;
   const bool live = e < sg.numel;
@@ -287,142 +287,6 @@ k_median_2l(const MSeg* __restrict__ segs, int nseg, const void* const* __restri
   if (!live) return;
   const int r = (k - 1) >> 1;
   const bool anynan = nan || cnan;
-  if (anynan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, anynan, sg.out);
-  else MedT<DT>::store(sg.out, e, fkey_inv(kr));
-}
-
-// Four lanes per column, K in (96, 128] (r03): B = 128 keys in quarters of 32, quarter q in wave q
-// of a 256-thread workgroup (64 columns; every load keeps the SGPR-base + 32-bit-offset form).
-//   1. every lane sorts its 32 keys (SortNet<32>, 191 comparators);
-//   2. pairs (0,1) and (2,3) through LDS: the even lane keeps L = min(Q_e[i], Q_o[31-i]), the 32
-//      smallest of the pair, the odd lane U = max(Q_o[i], Q_e[31-i]), the 32 largest; both are
-//      bitonic and a half-cleaner cascade sorts them (80 comparators);
-//   3. sorted A = Q0 u Q1 = [L01, U01] and C = Q2 u Q3 = [L23, U23], so the lower median, rank 63
-//      of the 128 = max_j min(A[j], C[63-j]), splits into max(rank31(L01 u U23), rank31(U01 u L23)):
-//      lane 0 pairs L01 with lane 3's U23, lane 1 U01 with lane 2's L23, lane 1 hands its half to
-//      lane 0 through LDS.
-// The same min/max count as k_median_2l (4 x 382 + 4 x 32 + 4 x 160 + 2 x 63 vs 2 x 1,086 + 128) on
-// 32 keys per lane (k_median_2l: 64 keys, 94 VGPRs).  PH = 2 exchanges step 2 in two halves of 16
-// keys (16 KB of LDS per workgroup instead of 32).  Sentinels, NaN and +-0 rules as k_median_2l.
-constexpr int k4lCols = kBlock / 4;  // columns per workgroup
-#ifndef MEDIAN_4L_W
-#define MEDIAN_4L_W 8
-#endif
-template <int DT, bool EXACT, int PH>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MEDIAN_4L_W)))
-k_median_4l(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k) {
-  constexpr int N = 32, B = 128, QX = N / 4 / PH;  // keys per lane; quads per lane per exchange
-  if constexpr (EXACT) k = B;
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  __shared__ u32x4 xs[4][QX][k4lCols];  // step 2: [lane][quad][column]; step 3 reuses [2..3]
-  __shared__ unsigned rb[2][k4lCols];   // lane 1's half of the median and its NaN flag
-  const int q = __builtin_amdgcn_readfirstlane((int)threadIdx.x / k4lCols);  // quarter: wave-uniform
-  const int c = (int)threadIdx.x % k4lCols;
-  const int64_t tile = blockIdx.x;
-  const MSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
-  const int64_t e = (tile - sg.tile_start) * k4lCols + c;
-  const bool live = e < sg.numel;
-  const int64_t ec = live ? e : sg.numel - 1;
-  const void* const* in = ptrs + sg.ptr_base;
-  const unsigned boff = (unsigned)ec * (unsigned)MedT<DT>::kBytes;
-  const int base = N * q;
-  const int lo_end = k + (B - 1) / 2 - ((k - 1) >> 1);  // slots [k, lo_end) low sentinels, [lo_end, B) high
-  unsigned key[N];
-#pragma unroll
-  for (int t = 0; t < N; ++t) key[t] = __float_as_uint(MedT<DT>::load_off(in[min(base + t, k - 1)], boff));
-#pragma unroll
-  for (int t = 0; t < N; ++t) {
-    const unsigned kk = key[t] ^ ((unsigned)((int)key[t] >> 31) | 0x80000000u);  // fkey
-    if constexpr (EXACT) {
-      key[t] = kk;
-    } else {
-      const unsigned real = 0u - (unsigned)(base + t < k);                 // uniform all-ones / zero
-      const unsigned sent = base + t < lo_end ? kNegInfKey : kPosInfKey;  // uniform
-      key[t] = (kk & real) | (sent & ~real);
-    }
-  }
-  SortNet<N>::run(key);
-  // step 2: lane q pairs its key i with its partner's key 31 - i; even lanes keep the minima (the
-  // two forms are separate code under a wave-uniform branch: no per-key select)
-  unsigned nk[N];
-  auto step2 = [&](auto lo_tag) {
-    constexpr bool LO = decltype(lo_tag)::value;
-#pragma unroll
-    for (int ph = 0; ph < PH; ++ph) {
-      // phase ph publishes keys [h0, h0 + 4 QX) and consumes the partner's same range, which pairs
-      // with own keys 31 - that range
-      const int h0 = ph * 4 * QX;
-      if (ph) __syncthreads();  // the partner has read phase ph-1's quads
-#pragma unroll
-      for (int j = 0; j < QX; ++j)
-        xs[q][j][c] = u32x4{key[h0 + 4 * j], key[h0 + 4 * j + 1], key[h0 + 4 * j + 2], key[h0 + 4 * j + 3]};
-      __syncthreads();
-#pragma unroll
-      for (int j = 0; j < QX; ++j) {
-        const u32x4 b = xs[q ^ 1][j][c];
-        const unsigned pv[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          const int i = N - 1 - (h0 + 4 * j + s);  // partner key h0 + 4j + s pairs with own key i
-          nk[i] = LO ? min(key[i], pv[s]) : max(key[i], pv[s]);
-        }
-      }
-    }
-  };
-  if ((q & 1) == 0) step2(std::true_type{});
-  else step2(std::false_type{});
-  // bitonic -> ascending: half-cleaner cascade
-#pragma unroll
-  for (int s = N / 2; s >= 1; s >>= 1) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      if ((i & s) == 0) {
-        const unsigned a = nk[i], b = nk[i + s];
-        nk[i] = min(a, b);
-        nk[i + s] = max(a, b);
-      }
-    }
-  }
-  __syncthreads();  // every lane has read its partner's step-2 quads
-  // step 3: lanes 2 (L23) and 3 (U23) publish; lane 0 pairs L01 with U23, lane 1 U01 with L23
-  static_assert(4 * QX * PH == N, "exchange layout");
-  unsigned (*xs3)[N / 4][k4lCols][4] = reinterpret_cast<unsigned (*)[N / 4][k4lCols][4]>(&xs[0][0][0]);
-  if (q >= 2) {
-#pragma unroll
-    for (int j = 0; j < N / 4; ++j)
-      *reinterpret_cast<u32x4*>(xs3[q - 2][j][c]) = u32x4{nk[4 * j], nk[4 * j + 1], nk[4 * j + 2], nk[4 * j + 3]};
-  }
-  __syncthreads();
-  // lane 0 reads lane 3's (slot 1), lane 1 lane 2's (slot 0); lanes 2-3 wait at the last barrier
-  // (no wave leaves before it)
-  unsigned kr = 0, nan = 0;
-  if (q < 2) {
-    const int src = q == 0 ? 1 : 0;
-    unsigned cmin = 0xFFFFFFFFu, cmax = 0;
-#pragma unroll
-    for (int j = 0; j < N / 4; ++j) {  // partner keys 4j..4j+3 pair with own keys N-1-4j .. N-4-4j
-      const u32x4 b = *reinterpret_cast<const u32x4*>(xs3[src][j][c]);
-      if (j == 0) cmin = b.x;
-      if (j == N / 4 - 1) cmax = b.w;
-      kr = max(kr, min(nk[N - 1 - 4 * j], b.x));
-      kr = max(kr, min(nk[N - 2 - 4 * j], b.y));
-      kr = max(kr, min(nk[N - 3 - 4 * j], b.z));
-      kr = max(kr, min(nk[N - 4 - 4 * j], b.w));
-    }
-    // a NaN key sorts outside [key(-inf), key(+inf)]: lane 0 sees the extremes of L01 and U23, lane 1
-    // those of U01 and L23 -- between them the global minimum and maximum of each pair
-    nan = (unsigned)(nk[0] < kNegInfKey || nk[N - 1] > kPosInfKey || cmin < kNegInfKey || cmax > kPosInfKey);
-    if (q == 1) {
-      rb[0][c] = kr;
-      rb[1][c] = nan;
-    }
-  }
-  __syncthreads();
-  if (q != 0) return;
-  kr = max(kr, rb[0][c]);
-  if (!live) return;
-  const int r = (k - 1) >> 1;
-  const bool anynan = nan || rb[1][c];
   if (anynan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, anynan, sg.out);
   else MedT<DT>::store(sg.out, e, fkey_inv(kr));
 }
@@ -564,12 +428,11 @@ bool full_enabled() {
   return on != 0;
 }
 
-// Lanes per column for K in (64, 128]: 2 = k_median_2l, 4 = k_median_4l (16 KB exchange), 41 =
-// k_median_4l with the one-shot 32 KB exchange; 1 = one lane (k_median_off).  FA_MEDIAN_LANES
+// Lanes per column for K in (64, 128]: 2 = k_median_2l, 1 = one lane (k_median_off).  FA_MEDIAN_LANES
 // forces a form (read at every call: A/B measurement and tests); FA_MEDIAN_2L=0 keeps one lane.
+// (r03: a four-lanes-per-column form measured 19-30 % slower than k_median_2l and was removed)
 constexpr int kMedian2lMin = 64;   // every K in (64, 128] (r02y: K = 65 and 96 within 2 % either way, the rest faster;
                                    // r02ab: at B = 40..64 the split measured 0-11 % slower, not used)
-constexpr int kMedian4lMin = 128;  // (r03: k_median_4l, not yet the default)
 int median_lanes(int dtype, int k, bool packed, bool off32) {
   static const int mode2 = [] {
     const char* e = getenv("FA_MEDIAN_2L");
@@ -578,30 +441,25 @@ int median_lanes(int dtype, int k, bool packed, bool off32) {
   if (dtype == FA_DTYPE_F64 || packed || !off32 || !full_enabled() || mode2 == 0 || k <= 64 || k > 128) return 1;
   const char* e = getenv("FA_MEDIAN_LANES");
   const int m = e ? atoi(e) : -1;
-  if (m == 1 || m == 2 || m == 4 || m == 41) return m;
-  return k > kMedian4lMin ? 4 : k > kMedian2lMin ? 2 : 1;
+  if (m == 1 || m == 2) return m;
+  return k > kMedian2lMin ? 2 : 1;
 }
 
 template <int DT>
 void launch_median(int k, bool packed, bool off32, int lanes, dim3 grid, hipStream_t st, const MSeg* ds,
                    int nseg, const void* const* dp) {
   if constexpr (DT != FA_DTYPE_F64) {
-    if (lanes == 4 || lanes == 41) {
-      if (k == 128) {
-        if (lanes == 4) hipLaunchKernelGGL((k_median_4l<DT, true, 2>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);
-        else hipLaunchKernelGGL((k_median_4l<DT, true, 1>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);
-      } else {
-        if (lanes == 4) hipLaunchKernelGGL((k_median_4l<DT, false, 2>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);
-        else hipLaunchKernelGGL((k_median_4l<DT, false, 1>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);
-      }
-      return;
-    }
     if (lanes == 2) {
+      // FA_MEDIAN_XCD=1: XCD-contiguous tile map (A/B measurement)
+      static const int xm = [] {
+        const char* e = getenv("FA_MEDIAN_XCD");
+        return e && e[0] == '1' ? 1 : 0;
+      }();
       switch ((k + 7) / 8) {  // B = K rounded up to 8, N = B / 2 keys per lane
 #define FA_M2(Q)                                                                                                  \
   case Q:                                                                                                       \
-    if (k == 8 * Q) hipLaunchKernelGGL((k_median_2l<DT, 4 * Q, true>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k); \
-    else hipLaunchKernelGGL((k_median_2l<DT, 4 * Q, false>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k);          \
+    if (k == 8 * Q) hipLaunchKernelGGL((k_median_2l<DT, 4 * Q, true>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k, xm); \
+    else hipLaunchKernelGGL((k_median_2l<DT, 4 * Q, false>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k, xm);          \
     return;
         FA_M2(9) FA_M2(10) FA_M2(11) FA_M2(12) FA_M2(13) FA_M2(14) FA_M2(15) FA_M2(16)
 #undef FA_M2
@@ -662,7 +520,7 @@ int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t*
   bool off32 = true;
   for (int s = 0; s < num_segments; ++s) off32 = off32 && seg_numel[s] * es <= (int64_t)0xFFFFFFFFll;
   const int lanes = median_lanes(dtype, k, packed, off32);
-  const int64_t tile_elems = packed ? 2 * kBlock : lanes == 2 ? k2lCols : lanes >= 4 ? k4lCols : kBlock;
+  const int64_t tile_elems = packed ? 2 * kBlock : lanes == 2 ? k2lCols : kBlock;
   int nseg = 0;
   int64_t tiles = 0;
   for (int s = 0; s < num_segments; ++s) {
@@ -732,7 +590,6 @@ namespace {
 constexpr int kPE = 64;       // longest float32 run (coordinates); small-K esplit cap
 constexpr int kMaxPairK = 128;
 constexpr int kMaxPairThreads = 1024;
-constexpr int kNP = 8;        // split heuristic: staged coordinates per lane (chunks of >= 64 below)
 constexpr int kNPS = 16;      // k_pairdist: elements of one client staged per thread and chunk
 constexpr int kNPL = 8;       // k_pairdist_lane: coordinates of one client staged per lane and chunk
 

@@ -99,8 +99,13 @@ int fa_lcc_decode(fa_ctx *ctx, int32_t rows, int32_t k, int64_t m, const int64_t
  * which is what the reference's loop of masks, `np.mod(mask + temp, p)` and `aggregated_mask +=`
  * leaves (modular sums; every intermediate stays below 2 p).  seeds / signs are HOST arrays of
  * num_streams entries (seed in [0, 2^32), sign +1 or -1).  d_scratch: at least
- * fa_mt_randint_sum_scratch_bytes(n) bytes of device memory.  One workgroup of one wave expands
- * each stream (MT19937 is sequential per stream); the streams run in parallel.
+ * fa_mt_randint_sum_scratch_bytes(n) bytes of device memory.  Streams of at least two chunks
+ * (chunk = 624 << k words, k chosen per call) are expanded by MT19937 jump-ahead: every chunk of
+ * every stream starts from its own jumped state (x^(cJ) mod the characteristic polynomial, computed
+ * and cached on the host at the first call for a chunk size) and runs in parallel; the context then
+ * holds device work space for the chunk windows and one plane of n values per stream of a group (the
+ * group sized to FA_MT_PLANE_MB, default 2048 MiB), kept for reuse until fa_ctx_destroy.  Shorter
+ * streams: one wave per stream.  FA_MT_JUMP=0 forces the one-wave form (identical results).
  */
 int fa_mt_randint_sum(fa_ctx *ctx, int32_t num_streams, const uint32_t *seeds, const int8_t *signs,
                       int64_t prime, int64_t n, void *d_out, void *d_scratch, size_t scratch_bytes,
