@@ -1633,7 +1633,12 @@ int pair_impl(fa_ctx* ctx, int dtype, int mode, int32_t nseg0, const int64_t* nu
     if (strides[g] < 0 || strides[g] % FA_TILE_BYTES)
       return fail(FA_ERR_INVALID, "tile_stride must be 0 (row-major) or a positive multiple of %d (got %lld)",
                   FA_TILE_BYTES, (long long)strides[g]);
-  const bool k16 = k <= 16;
+  // two 4-KiB slots per client and workgroup up to K = 16 (FA_PAIR_S=2 forces them for any K: A/B)
+  static const bool s2 = [] {
+    const char* e = getenv("FA_PAIR_S");
+    return e && e[0] == '2';
+  }();
+  const bool k16 = k <= 16 || s2;
   const int nsg[2] = {nseg0, nseg1};
   const int64_t* numel[2] = {numel0, numel1};
   const void* const* din[2] = {d_in0, d_in1};

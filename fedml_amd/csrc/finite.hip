@@ -550,8 +550,8 @@ __global__ void __launch_bounds__(64) k_mt_seq(const uint32_t* __restrict__ seed
 // with the set bits of x^(cJ) mod phi, given by the host as two lists of bit positions, even then
 // odd, each stored as the index of the aligned word pair it reads, floor(i / 2) (row of `stride` int32
 // per chunk: E, O, 0, 0, E even, O odd; E and O padded to multiples of 32 with the zero-window
-// positions kMtPadEven / kMtPadOdd).  The sequence sits in
-// LDS (85 KB, 8-byte aligned).  Word pairs: for an even position i thread u reads the aligned pair
+// positions kMtPadEven / kMtPadOdd).  The sequence sits in LDS (85 KB, 8-byte aligned); the positions
+// are read by scalar loads.  Word pairs: for an even position i thread u reads the aligned pair
 // (x_{i+2u}, x_{i+2u+1}) -> words 2u, 2u+1; for an odd i the aligned pair (x_{i+2u-1}, x_{i+2u}) ->
 // words 2u-1, 2u: one ds_read_b64 per thread and position (256 B/clk) instead of two 4-byte reads.
 // 640 threads = two groups of 320 (313 needed: u = 0..312), each taking half of every list; the
@@ -560,18 +560,15 @@ constexpr int kMtJumpSeq = 19937 + 624;  // words of the sequence a jump reads (
 constexpr int kMtPadEven = 20562;        // pad positions: their windows (the next 626 words) are zero
 constexpr int kMtPadOdd = 20563;
 constexpr int kMtJumpLds = 20562 + 640;  // LDS words of the sequence + the zero region
-constexpr int kMtPosLds = 8192;          // positions staged per round
 constexpr int kMtJumpThreads = 640;
 __global__ void __launch_bounds__(kMtJumpThreads) k_mt_jump(const uint32_t* __restrict__ seq,
                                                             const int32_t* __restrict__ pos, int stride, int chunks,
                                                             uint32_t* __restrict__ windows) {
-  typedef int i32x4 __attribute__((ext_vector_type(4)));
   typedef uint32_t u32x2v __attribute__((ext_vector_type(2)));
   __shared__ __attribute__((aligned(16))) uint32_t xs[kMtJumpLds];
-  __shared__ i32x4 pl[kMtPosLds / 4];
   __shared__ u32x2v cmb[2][320];
   const int tid = threadIdx.x;
-  const int grp = tid / 320, u = tid % 320;
+  const int grp = __builtin_amdgcn_readfirstlane(tid / 320), u = tid % 320;  // 320 = 5 whole waves
   const int s = blockIdx.y, c = blockIdx.x + 1;
   {  // the sequence into LDS: 16-byte loads, all of a thread's in flight before its stores
     const u32x4* src4 = (const u32x4*)(seq + (size_t)s * kMtSeqWords);  // 84,864-byte rows: aligned
@@ -595,46 +592,31 @@ __global__ void __launch_bounds__(kMtJumpThreads) k_mt_jump(const uint32_t* __re
       if (q < NV) xs4[q] = v[r];
     }
   }
+  __syncthreads();  // the sequence is in LDS
   const int32_t* row = pos + (size_t)(c - 1) * stride;
   const int E = row[0], O = row[1];
   const int32_t* lists = row + 4;
   u32x2v ae = {0u, 0u}, ao = {0u, 0u};
   const u32x2v* xp = (const u32x2v*)xs;  // the sequence as aligned word pairs
-  // the two lists, one after the other, staged in rounds; group g takes the g-th half of a round
+  // the two lists, one after the other; group g takes the g-th half of each
   for (int pass = 0; pass < 2; ++pass) {
     const int len = pass ? O : E;
     const int32_t* lp = lists + (pass ? E : 0);
-    for (int r0 = 0; r0 < len; r0 += kMtPosLds) {
-      const int rn = min(kMtPosLds, len - r0);  // a multiple of 32
-      __syncthreads();  // the previous round's positions (and, first, nothing) are consumed
-      {  // <= kMtPosLds / 4 = 2,048 vectors: up to 4 loads per thread, in flight together
-        const i32x4* lv = (const i32x4*)(lp + r0);
-        i32x4 w[4];
+    // positions by scalar loads (uniform addresses, 16 per s_load_dwordx16): no LDS cycles for them
+    // (r03u interleaved A/B: 2.60-2.62 ms with the positions staged in LDS and read as broadcasts,
+    // 2.53-2.54 ms this way)
+    const int half = len / 2;  // a multiple of 16
+    const int32_t* gp = lp + grp * half;
+    u32x2v acc = {0u, 0u};
+    for (int k = 0; k < half; k += 16) {
+      int ii[16];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int q = tid + r * kMtJumpThreads;
-          if (q < rn / 4) w[r] = lv[q];
-        }
+      for (int q = 0; q < 16; ++q) ii[q] = gp[k + q];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int q = tid + r * kMtJumpThreads;
-          if (q < rn / 4) pl[q] = w[r];
-        }
-      }
-      __syncthreads();
-      const int half = rn / 2;  // a multiple of 16
-      const int mine = grp * (half / 4);          // this group's first position vector
-      u32x2v acc = {0u, 0u};
-      for (int k = 0; k < half / 4; k += 4) {
-        const i32x4 p0 = pl[mine + k], p1 = pl[mine + k + 1], p2 = pl[mine + k + 2], p3 = pl[mine + k + 3];  // broadcast
-        const int ii[16] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w,
-                            p2.x, p2.y, p2.z, p2.w, p3.x, p3.y, p3.z, p3.w};
-#pragma unroll
-        for (int q = 0; q < 16; ++q) acc ^= xp[ii[q] + u];  // aligned pair: ds_read_b64
-      }
-      if (pass) ao ^= acc;
-      else ae ^= acc;
+      for (int q = 0; q < 16; ++q) acc ^= xp[ii[q] + u];  // aligned pair: ds_read_b64
     }
+    if (pass) ao ^= acc;
+    else ae ^= acc;
   }
   // combine the groups' halves, then words 2u = E.x ^ O.y and 2u + 1 = E.y ^ O(u+1).x
   __syncthreads();
