@@ -120,17 +120,28 @@ def launch_cmd(n, argv, port, script=None):
 def launch_ranks(n, argv, timeout_s, script=None):
     """``python bench.py --gpus N`` without an outer launcher: start the N ranks as CHILD processes
     (torch.distributed.run, one rank per GPU) -- nothing here has touched the GPU, and the parent
-    never execs -- relay their output (rank 0 prints the JSON line), and return the worst rc.  A
-    run that outlives ``timeout_s`` is killed as a process group and returns 124."""
+    never execs -- relay their output (rank 0's JSON line to stdout, any other line the ranks print
+    to stderr), and return the worst rc.  A run that outlives ``timeout_s`` is killed as a process
+    group and returns 124."""
     import signal
     import subprocess
     env = dict(os.environ)
     env.setdefault("MASTER_ADDR", "127.0.0.1")
     env.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")  # a collective timeout tears the rank down
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")      # dmabuf IPC (the host driver's only mode)
-    p = subprocess.Popen(launch_cmd(n, argv, _free_port(), script), env=env, start_new_session=True)
+    import threading
+    p = subprocess.Popen(launch_cmd(n, argv, _free_port(), script), env=env, start_new_session=True,
+                         stdout=subprocess.PIPE, text=True, bufsize=1)
+
+    def relay():  # the JSON line (rank 0) to stdout; whatever else a rank prints (gloo banners) to stderr
+        for line in p.stdout:
+            (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+            (sys.stdout if line.lstrip().startswith("{") else sys.stderr).flush()
+    pump = threading.Thread(target=relay, daemon=True)
+    pump.start()
     try:
         rc = p.wait(timeout=timeout_s)
+        pump.join(timeout=10)
     except subprocess.TimeoutExpired:
         print(f"bench.py: the {n}-rank run exceeded {timeout_s:.0f} s; killing its process group",
               file=sys.stderr, flush=True)
