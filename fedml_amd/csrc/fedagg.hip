@@ -1536,7 +1536,10 @@ int fa_weighted_sum_host(fa_ctx* ctx, int dtype, int mode, int32_t num_segments,
     while (*done_h != seq) {
       if ((++spins & 1023u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {
         FA_HIP(hipStreamSynchronize(st));
-        if (*done_h != seq) return fail(FA_ERR_HIP, "fa_weighted_sum_host: the round finished without its completion word");
+        if (*done_h != seq) {  // reset the workgroup counter so that the next round starts clean
+          (void)hipMemset(ctx->zc_counter, 0, 256);
+          return fail(FA_ERR_HIP, "fa_weighted_sum_host: the round finished without its completion word");
+        }
         break;
       }
     }

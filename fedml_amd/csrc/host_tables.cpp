@@ -361,6 +361,8 @@ py::object small_host_round(py::list dicts, py::list keys, int mode, py::object 
   std::vector<at::ScalarType> st(T);
   std::vector<c10::IntArrayRef> shape(T);
   std::vector<at::Tensor> first(T);  // client 0's tensors (their sizes() stay valid while held)
+  std::vector<at::Tensor> keep;       // every input, referenced while the GIL is released below
+  keep.reserve((size_t)(K * T));
   int64_t in_bytes = 0;
   for (int64_t i = 0; i < K; ++i) {
     PyObject* d = PyList_GET_ITEM(dicts.ptr(), i);
@@ -390,6 +392,7 @@ py::object small_host_round(py::list dicts, py::list keys, int mode, py::object 
         return py::none();
       }
       ptr[t * K + i] = (int64_t)x.data_ptr();
+      keep.push_back(x);
     }
   }
   // outputs: one CPU allocation, every key on a 256-byte boundary; weighted modes turn int64 into
