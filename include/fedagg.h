@@ -276,9 +276,13 @@ int fa_stream_destroy(void *stream);
  * key-major; h_out: nseg host pointers), SYNCHRONOUS: the inputs are packed into one mapped pinned
  * buffer owned by ctx, the kernel reads them and writes the results in place over PCIe (no
  * separate H2D/D2H copies), the call waits for it on hip_stream and copies the results out.
- * Replaces the reference loop (agg_operator.py:37-44) for small CPU-resident rounds, where
+ * Rounds up to 1 MiB whose tables fit the kernel argument (3 KB) run on up to 64 workgroups that
+ * end by storing a sequence number into the mapped buffer; the call spins on that word (a second
+ * after the launch it falls back to a stream sync, which reports a fault) instead of an event
+ * wait.  Replaces the reference loop (agg_operator.py:37-44) for small CPU-resident rounds, where
  * launch and copy latencies dominate (cfg1: LR-MNIST, K = 2, 63 KB per client).  Same
- * arithmetic and bits as fa_weighted_sum_multi.
+ * arithmetic and bits as fa_weighted_sum_multi.  Calls on one ctx must not overlap (as every
+ * entry point: one thread per context at a time).
  */
 int fa_weighted_sum_host(fa_ctx *ctx, int dtype, int mode, int32_t num_segments, const int64_t *seg_numel,
                          int32_t k, const void *const *h_in, const double *coef, double divisor,
