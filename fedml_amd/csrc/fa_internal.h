@@ -99,10 +99,12 @@ struct fa_ctx {
   // fa_mt_randint_sum's jump-ahead path: per-call device work space and the jump polynomials
   void* mt_dev = nullptr;
   size_t mt_cap = 0;
-  void* mt_poly_dev = nullptr;     // (count) x 312 uint64 words, x^(c J) mod phi for c = 1..count
+  void* mt_poly_dev = nullptr;     // (count) rows of set-bit pair positions of x^(c J) mod phi, c = 1..count
   unsigned long long mt_poly_J = 0;
   int mt_poly_count = 0;
   int mt_poly_stride = 0;
+  hipEvent_t mt_ev = nullptr;  // the last jump-path call's kernels have finished with mt_dev / mt_poly_dev
+  bool mt_live = false;        // mt_ev has been recorded
 };
 
 namespace fa_detail {

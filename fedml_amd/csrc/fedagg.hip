@@ -1143,6 +1143,8 @@ int fa_ctx_destroy(fa_ctx* c) {
   }
   if (c->zc_ev) (void)hipEventDestroy(c->zc_ev);
   if (c->zc_host) (void)hipHostFree(c->zc_host);
+  if (c->mt_live) (void)hipEventSynchronize(c->mt_ev);
+  if (c->mt_ev) (void)hipEventDestroy(c->mt_ev);
   if (c->mt_dev) (void)hipFree(c->mt_dev);
   if (c->zc_counter) (void)hipFree(c->zc_counter);
   if (c->mt_poly_dev) (void)hipFree(c->mt_poly_dev);

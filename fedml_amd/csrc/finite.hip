@@ -1036,6 +1036,7 @@ int mt_jump_tables(fa_ctx* ctx, uint64_t J, int count, hipStream_t st) {
     std::copy(od[(size_t)c].begin(), od[(size_t)c].end(), r + 4 + ev[(size_t)c].size());
   }
   FA_HIP(hipStreamSynchronize(st));  // a previous table may still be read by queued kernels
+  if (ctx->mt_live) FA_HIP(hipEventSynchronize(ctx->mt_ev));  // ... also on another stream
   if (ctx->mt_poly_dev) FA_HIP(hipFree(ctx->mt_poly_dev));
   ctx->mt_poly_dev = nullptr;
   ctx->mt_poly_count = 0;
@@ -1059,6 +1060,7 @@ uint64_t mt_plane_budget() {
 int mt_work(fa_ctx* ctx, size_t bytes, hipStream_t st) {
   if (ctx->mt_cap >= bytes) return FA_OK;
   FA_HIP(hipStreamSynchronize(st));
+  if (ctx->mt_live) FA_HIP(hipEventSynchronize(ctx->mt_ev));
   if (ctx->mt_dev) FA_HIP(hipFree(ctx->mt_dev));
   ctx->mt_dev = nullptr;
   ctx->mt_cap = 0;
@@ -1092,7 +1094,6 @@ int fa_mt_randint_sum(fa_ctx* ctx, int32_t num_streams, const uint32_t* seeds, c
   const bool wide = rng > 0xFFFFFFFFull;
   FA_HIP(hipMemsetAsync(d_out, 0, sizeof(int64_t) * (size_t)n, st));
   if (num_streams == 0 || rng == 0) return FA_OK;  // randint(0, 1) draws nothing and is all zeros
-  FA_HIP(hipMemsetAsync(d_scratch, 0, sizeof(uint64_t) * (size_t)n, st));
   // streams per batch: a batch's sum of values in [0, p) must not wrap 64 bits
   const uint64_t per = std::min<uint64_t>((uint64_t)num_streams, UINT64_MAX / rng);
   const size_t seed_b = align16(sizeof(uint32_t) * num_streams);
@@ -1124,6 +1125,13 @@ int fa_mt_randint_sum(fa_ctx* ctx, int32_t num_streams, const uint32_t* seeds, c
     const size_t cnt_b = align16(sizeof(int64_t) * C * G), pl_b = (size_t)G * pstride * es;
     rc = mt_work(ctx, seq_b + win_b + 2 * cnt_b + pl_b, st);
     if (rc) return rc;
+    // the work space is shared by every call on this ctx: a previous call queued on another stream
+    // must be done with it before these kernels overwrite it
+    if (!ctx->mt_ev && hipEventCreateWithFlags(&ctx->mt_ev, hipEventDisableTiming) != hipSuccess) {
+      ctx->mt_ev = nullptr;
+      return fail(FA_ERR_HIP, "fa_mt_randint_sum: hipEventCreate failed");
+    }
+    if (ctx->mt_live) FA_HIP(hipStreamWaitEvent(st, ctx->mt_ev, 0));
     char* w = (char*)ctx->mt_dev;
     uint32_t* dseq = (uint32_t*)w;
     uint32_t* dwin = (uint32_t*)(w + seq_b);
@@ -1154,8 +1162,11 @@ int fa_mt_randint_sum(fa_ctx* ctx, int32_t num_streams, const uint32_t* seeds, c
       }
     }
     FA_HIP(hipGetLastError());
+    FA_HIP(hipEventRecord(ctx->mt_ev, st));
+    ctx->mt_live = true;
     return release(slot, st);
   }
+  FA_HIP(hipMemsetAsync(d_scratch, 0, sizeof(uint64_t) * (size_t)n, st));
   int first = 1;
   for (uint64_t s0 = 0; s0 < (uint64_t)num_streams; s0 += per) {
     const unsigned b = (unsigned)std::min<uint64_t>(per, (uint64_t)num_streams - s0);

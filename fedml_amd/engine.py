@@ -121,6 +121,20 @@ class AggEngine:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         return N.ctypes.c_void_p(s.cuda_stream)
 
+    def _scratch(self, name: str, need: int, stream=None) -> torch.Tensor:
+        """Device scratch of >= need bytes, cached per (name, stream): calls queued on different
+        streams never share one, and a buffer replaced while a kernel on ``stream`` may still read it
+        is only reused by the allocator after that stream's queued work (record_stream)."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        cache = self.__dict__.setdefault("_scratch_cache", {})
+        key = (name, s.cuda_stream)
+        t = cache.get(key)
+        if t is None or t.numel() < need:
+            t = torch.empty(max(int(need), 1), dtype=torch.uint8, device=self.device)
+            t.record_stream(s)
+            cache[key] = t
+        return t
+
     # ------------------------------------------------------------------ weighted sums
     def weighted_sum(self, xs: Sequence[torch.Tensor], mode: int, coef: Optional[Sequence[float]] = None,
                      divisor: float = 1.0, out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
@@ -813,9 +827,7 @@ class AggEngine:
         sg = (N.ctypes.c_int8 * max(S, 1))(*[int(v) for v in signs])
         with self.lock:
             need = self._lib.fa_mt_randint_sum_scratch_bytes(n)
-            scratch = getattr(self, "_mt_scratch", None)
-            if need and (scratch is None or scratch.numel() < need):
-                scratch = self._mt_scratch = torch.empty(need, dtype=torch.uint8, device=self.device)
+            scratch = self._scratch("mt", need, stream) if need else None
             rc = self._lib.fa_mt_randint_sum(self._ctx, S, sd, sg, int(prime), n, out.data_ptr(),
                                              scratch.data_ptr() if need else None, need, self._stream(stream))
         N.check(rc, "fa_mt_randint_sum")
@@ -900,9 +912,7 @@ class AggEngine:
         nl = N.i64_array([seg[0].numel() for seg in segments])
         with self.lock:
             need = self._lib.fa_pairwise_sqdist_scratch_bytes(len(segments), nl, k)
-            scratch = getattr(self, "_pd_scratch", None)
-            if scratch is None or scratch.numel() < need:
-                scratch = self._pd_scratch = torch.empty(max(need, 1), dtype=torch.uint8, device=self.device)
+            scratch = self._scratch("pd", need, stream)
             d = torch.empty((k, k), dtype=torch.float64, device=self.device)
             rc = self._lib.fa_pairwise_sqdist_rt(self._ctx, _DIFF_DT[diff_dtype], len(segments), nl, k,
                                                  N.ptr_array(in_ptrs), d.data_ptr(), scratch.data_ptr(),

@@ -231,6 +231,27 @@ def test_mt_randint_sum_jump_ahead_vs_numpy(eng, p, log2, plane_mb, monkeypatch)
     assert np.array_equal(got, exp)
 
 
+@pytest.mark.parametrize("jump", ["1", "0"])
+def test_mt_randint_sum_two_streams(eng, jump, monkeypatch):
+    """Calls queued on two streams of one engine share neither work space nor scratch: each stream's
+    results equal numpy's, whichever path (jump-ahead or sequential) runs."""
+    monkeypatch.setenv("FA_MT_JUMP", jump)
+    monkeypatch.setenv("FA_MT_JUMP_LOG2", "0")
+    p, sizes = 2 ** 31 - 1, [150_001, 90_007, 150_001, 120_011]
+    streams = [torch.cuda.Stream(device=eng.device), torch.cuda.Stream(device=eng.device)]
+    outs = []
+    for i, n in enumerate(sizes):
+        seeds, signs = [100 + i, 7 * i + 1, 2 ** 32 - 1 - i], [1, -1, 1]
+        outs.append((seeds, signs, n, eng.mt_randint_sum(seeds, signs, p, n, stream=streams[i % 2])))
+    torch.cuda.synchronize()
+    for seeds, signs, n, got in outs:
+        acc = np.zeros(n, dtype=object)
+        for s, g in zip(seeds, signs):
+            np.random.seed(s)
+            acc = acc + g * np.random.randint(0, p, size=n).astype(object)
+        assert np.array_equal(got.cpu().numpy(), np.array([int(a) % p for a in acc], dtype=np.int64))
+
+
 def test_mt_randint_sum_edges(eng):
     from oracle import mt_port
     assert torch.equal(eng.mt_randint_sum([3], [1], 1, 10).cpu(), torch.zeros(10, dtype=torch.int64))  # p = 1
