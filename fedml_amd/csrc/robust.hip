@@ -170,11 +170,17 @@ __device__ __forceinline__ void median_col(const void* const* in, int k, int64_t
 // form below compiles `i < k ? key : sentinel` and `nan || ...` (k a runtime value) into an
 // exec-mask branch with its own s_waitcnt per client -- ~3,000 scalar and branch instructions ahead
 // of B = 128's 2,175 min/max -- and keeps a 64-bit VGPR address per client (B = 128: 158 VGPRs).
-// Here the sentinels are uniform bit masks (and/or, no branch), the NaN test an integer OR, and
-// every load is `uniform base (SGPRs) + ONE shared 32-bit byte offset` (global_load ... saddr).
-// Measured (r02j): K = 128 1.58 -> 1.45 ms, K = 96 1.11 -> 0.88, K = 64 0.62 -> 0.59, K = 32 0.278
-// -> 0.272 ms; bit-exact (same network, same keys).
-// EXACT (k == B, no sentinels): the masks are dropped at compile time (K = 128: 1.53 -> 1.45 ms).
+// Here the sentinels are uniform selects (no branch) and every load is `uniform base (SGPRs) + ONE
+// shared 32-bit byte offset` (global_load ... saddr).  Measured (r02j): K = 128 1.58 -> 1.45 ms,
+// K = 96 1.11 -> 0.88, K = 64 0.62 -> 0.59, K = 32 0.278 -> 0.272 ms; bit-exact (same network).
+// EXACT (k == B, no sentinels): the selects are dropped at compile time (K = 128: 1.53 -> 1.45 ms).
+// Float keys (r03): the network runs on the loaded floats with IEEE 754-2019 minimum / maximum
+// (median_nets.h, v_minimum3_f32 / v_maximum3_f32): their order is the uint32 keys' order on every
+// non-NaN value (-0 < +0 included), so the same bits are selected, and a NaN anywhere in the column
+// makes the selected value NaN (every input reaches the selected output) -- no per-key conversion
+// or NaN test (5-6 VALU a key in the uint32-key form, commit 9aaf2ea).  Sentinels are -inf / +inf (a
+// tie with a real infinity selects the same bits).  Interleaved A/B (profiles/r03ac): K = 64 0.606 ->
+// 0.535 ms, K = 32 unchanged.
 template <int DT, int B, bool EXACT, int W = (B > 64 ? 2 : (B > 56 ? 3 : (B > 32 ? 4 : 5)))>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W)))
 k_median_off(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k) {
@@ -187,28 +193,19 @@ k_median_off(const MSeg* __restrict__ segs, int nseg, const void* const* __restr
   const void* const* in = ptrs + sg.ptr_base;
   const unsigned boff = (unsigned)ec * (unsigned)MedT<DT>::kBytes;
   const int lo_end = k + (B - 1) / 2 - ((k - 1) >> 1);  // sentinels [k, lo_end) low, [lo_end, B) high
-  unsigned key[B];
+  float x[B];
 #pragma unroll
-  for (int i = 0; i < B; ++i) key[i] = __float_as_uint(MedT<DT>::load_off(in[min(i, k - 1)], boff));
-  unsigned nanbits = 0;
+  for (int i = 0; i < B; ++i) x[i] = MedT<DT>::load_off(in[min(i, k - 1)], boff);
+  if constexpr (!EXACT) {
 #pragma unroll
-  for (int i = 0; i < B; ++i) {
-    const unsigned kk = key[i] ^ ((unsigned)((int)key[i] >> 31) | 0x80000000u);  // fkey
-    if constexpr (EXACT) {
-      nanbits |= (unsigned)((key[i] & 0x7FFFFFFFu) > 0x7F800000u);
-      key[i] = kk;
-    } else {
-      const unsigned real = 0u - (unsigned)(i < k);        // uniform all-ones / zero
-      const unsigned sent = i < lo_end ? 0u : 0xFFFFFFFFu;  // uniform
-      nanbits |= real & (unsigned)((key[i] & 0x7FFFFFFFu) > 0x7F800000u);
-      key[i] = (kk & real) | (sent & ~real);
-    }
+    for (int i = 0; i < B; ++i) x[i] = i < k ? x[i] : (i < lo_end ? -__builtin_inff() : __builtin_inff());
   }
-  const unsigned kr = select_mid<B>(key);
+  const float kr = select_mid<B>(x);
   if (!live) return;
   const int r = (k - 1) >> 1;
-  if (nanbits || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, nanbits != 0, sg.out);
-  else MedT<DT>::store(sg.out, e, fkey_inv(kr));
+  const bool nan = kr != kr;
+  if (nan || kr == 0.0f) store_rare<DT>(in, k, e, r, nan, sg.out);
+  else MedT<DT>::store(sg.out, e, kr);
 }
 
 // Two lanes per column, K in (64, 128] (r02).  k_median_off at B = 128 holds 128 keys per lane:
@@ -221,15 +218,15 @@ k_median_off(const MSeg* __restrict__ segs, int nseg, const void* const* __restr
 // B = 128's pruned selection network), the upper lanes hand their sorted keys to the lower lanes
 // through LDS, and the lower median -- rank N-1 of the 2N keys -- is max_j min(A[j], C[N-1-j]) (the N
 // pairwise minima of a sorted A and a reversed sorted C are the N smallest keys).  Padding as
-// k_median_off, all of it in the upper half, but the sentinels are the keys of -inf and +inf (a tie
-// with a real infinity selects the same bits), so a NaN shows as a sorted key outside [key(-inf),
-// key(+inf)] -- two compares per lane instead of one per key.  N keys + the merge fit 128 VGPRs
+// k_median_off, all of it in the upper half, sentinels -inf / +inf.  Float keys as k_median_off (r03):
+// a NaN in either half turns that half's sorted keys NaN and so the merged value (r02's uint32 keys
+// found a NaN as a sorted key outside [key(-inf), key(+inf)]; K = 100 1.009 -> 0.955 ms, K = 128
+// within 1 %, profiles/r03ac).  N keys + the merge fit 128 VGPRs
 // (4 waves per SIMD).  Same keys and rare-case rules as k_median_off: bit-exact.
 constexpr int k2lCols = kBlock / 2;  // columns per workgroup
 #ifndef MEDIAN_2L_W
 #define MEDIAN_2L_W (N <= 40 ? 8 : N <= 48 ? 6 : 5)
 #endif
-constexpr unsigned kNegInfKey = 0x007FFFFFu, kPosInfKey = 0xFF800000u;  // fkey(-inf), fkey(+inf)
 template <int DT, int N, bool EXACT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MEDIAN_2L_W)))
 k_median_2l(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int xcd) {
@@ -248,47 +245,37 @@ k_median_2l(const MSeg* __restrict__ segs, int nseg, const void* const* __restri
   const unsigned boff = (unsigned)ec * (unsigned)MedT<DT>::kBytes;
   const int base = N * h;
   const int lo_end = k + (B - 1) / 2 - ((k - 1) >> 1);  // slots [k, lo_end) low sentinels, [lo_end, B) high
-  unsigned key[N];
+  float x[N];
 #pragma unroll
-  for (int t = 0; t < N; ++t) key[t] = __float_as_uint(MedT<DT>::load_off(in[min(base + t, k - 1)], boff));
+  for (int t = 0; t < N; ++t) x[t] = MedT<DT>::load_off(in[min(base + t, k - 1)], boff);
+  if constexpr (!EXACT) {
 #pragma unroll
-  for (int t = 0; t < N; ++t) {
-    const unsigned kk = key[t] ^ ((unsigned)((int)key[t] >> 31) | 0x80000000u);  // fkey
-    if constexpr (EXACT) {
-      key[t] = kk;
-    } else if (t < N - 8) {
-      key[t] = kk;  // K > B - 8: only the upper half's last 8 slots can hold sentinels
-    } else {
-      const unsigned real = 0u - (unsigned)(base + t < k);                 // uniform all-ones / zero
-      const unsigned sent = base + t < lo_end ? kNegInfKey : kPosInfKey;  // uniform
-      key[t] = (kk & real) | (sent & ~real);
-    }
+    for (int t = N - 8; t < N; ++t)  // K > B - 8: only the upper half's last 8 slots can hold sentinels
+      x[t] = base + t < k ? x[t] : (base + t < lo_end ? -__builtin_inff() : __builtin_inff());
   }
-  SortNet<N>::run(key);
-  const bool nan = key[0] < kNegInfKey || key[N - 1] > kPosInfKey;  // a NaN key sorts outside the infinities
+  SortNet<N>::run(x);  // a NaN input turns every sorted output NaN
   if (h == 1) {
 #pragma unroll
-    for (int q = 0; q < N / 4; ++q) xs[q][c] = u32x4{key[4 * q], key[4 * q + 1], key[4 * q + 2], key[4 * q + 3]};
+    for (int q = 0; q < N / 4; ++q)
+      xs[q][c] = u32x4{__float_as_uint(x[4 * q]), __float_as_uint(x[4 * q + 1]), __float_as_uint(x[4 * q + 2]),
+                       __float_as_uint(x[4 * q + 3])};
   }
   __syncthreads();
   if (h == 1) return;
-  unsigned kr = 0;
-  // the upper half's NaN shows in its own sorted extremes (no flag array: N x 512 B of LDS per
-  // workgroup, so five 128-column workgroups share a CU at N = 64)
-  const bool cnan = xs[0][c].x < kNegInfKey || xs[N / 4 - 1][c].w > kPosInfKey;
+  float kr = -__builtin_inff();
 #pragma unroll
-  for (int q = 0; q < N / 4; ++q) {  // partner keys 4q..4q+3 pair with own keys N-1-4q .. N-4-4q
+  for (int q = 0; q < N / 4; ++q) {
     const u32x4 b = xs[q][c];
-    kr = max(kr, min(key[N - 1 - 4 * q], b.x));
-    kr = max(kr, min(key[N - 2 - 4 * q], b.y));
-    kr = max(kr, min(key[N - 3 - 4 * q], b.z));
-    kr = max(kr, min(key[N - 4 - 4 * q], b.w));
+    kr = kmax(kr, kmin(x[N - 1 - 4 * q], __uint_as_float(b.x)));
+    kr = kmax(kr, kmin(x[N - 2 - 4 * q], __uint_as_float(b.y)));
+    kr = kmax(kr, kmin(x[N - 3 - 4 * q], __uint_as_float(b.z)));
+    kr = kmax(kr, kmin(x[N - 4 - 4 * q], __uint_as_float(b.w)));
   }
   if (!live) return;
   const int r = (k - 1) >> 1;
-  const bool anynan = nan || cnan;
-  if (anynan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, anynan, sg.out);
-  else MedT<DT>::store(sg.out, e, fkey_inv(kr));
+  const bool nan = kr != kr;
+  if (nan || kr == 0.0f) store_rare<DT>(in, k, e, r, nan, sg.out);
+  else MedT<DT>::store(sg.out, e, kr);
 }
 
 // (B > 64: median_col's body written out -- called through median_col, B = 128 took 256 VGPRs,

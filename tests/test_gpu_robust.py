@@ -153,6 +153,52 @@ def test_median_two_lanes_per_column(eng, dtype, k):
         assert torch.equal(o.cpu().view(iv), exp.view(iv))
 
 
+def _special_columns(g, k, n, dtype):
+    """Columns mixing normal values with the bit patterns a float-key network could mishandle:
+    subnormals of both signs (denormal flushing would change the selected bits), signalling and
+    negative / payload NaNs, +-0, +-inf and the largest finite values."""
+    fb = dtype
+    if dtype == torch.float32:
+        pats = [0x00000001, 0x007FFFFF, 0x80000001, 0x807FFFFF, 0x00400000, 0x80400000, 0x7F800001, 0xFFC00000,
+                0x7FC12345, 0x00000000, 0x80000000, 0x7F800000, 0xFF800000, 0x7F7FFFFF, 0xFF7FFFFF]
+    elif dtype == torch.bfloat16:
+        pats = [0x0001, 0x007F, 0x8001, 0x807F, 0x0040, 0x7F81, 0xFFC0, 0x0000, 0x8000, 0x7F80, 0xFF80, 0x7F7F, 0xFF7F]
+    else:
+        pats = [0x0001, 0x03FF, 0x8001, 0x83FF, 0x0200, 0x7C01, 0xFE00, 0x0000, 0x8000, 0x7C00, 0xFC00, 0x7BFF, 0xFBFF]
+    w = (np.uint32, np.int32) if dtype == torch.float32 else (np.uint16, np.int16)
+    pats = torch.from_numpy(np.array(pats, dtype=w[0]).view(w[1]))
+    xs = []
+    for i in range(k):
+        v = (torch.randn(n, generator=g) * 1e-3).to(fb)
+        u = torch.rand(n, generator=g)
+        # most columns: subnormals / extremes only (no NaN) so the network, not the rescan, selects
+        sel = torch.randint(0, len(pats), (n,), generator=g)
+        special = pats[sel].view(fb)
+        nan = (special != special)
+        pick = (u < 0.6) & ~nan | (u < 0.002)
+        xs.append(torch.where(pick, special, v))
+    return xs
+
+
+@pytest.mark.parametrize("lanes", ["1", "2"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("k", [7, 8, 32, 33, 64, 72, 100, 127, 128])
+def test_median_special_values_float_keys(eng, dtype, k, lanes, monkeypatch):
+    """The float-key networks (IEEE minimum / maximum, NaN-propagating; k_median_off, k_median_2l)
+    select the same bits as the oracle on subnormals of both signs (a flushing min / max would
+    change them), signalling / negative / payload NaNs, +-0, +-inf and +-max, one and two lanes per
+    column."""
+    from oracle import orc
+    monkeypatch.setenv("FA_MEDIAN_LANES", lanes)
+    g = torch.Generator().manual_seed(1000 + k)
+    xs = _special_columns(g, k, 4099, dtype)
+    off = torch.zeros(1, dtype=dtype, device=DEV)  # 2-byte views: 16-bit types take the one-per-lane kernels
+    segs = [torch.cat([off, x.to(DEV)])[1:] if dtype != torch.float32 else x.to(DEV) for x in xs]
+    got = eng.coord_median([segs])[0].cpu()
+    iv = torch.int32 if dtype == torch.float32 else torch.int16
+    assert torch.equal(got.view(iv), orc.coord_median(xs).view(iv))
+
+
 def test_median_all_zero_columns(eng):
     """Columns of only +-0 in every sign pattern: ATen returns the zero of rank (K-1)/2 by index."""
     from oracle import orc

@@ -142,15 +142,20 @@ def main(path):
     hdr = (
         "// median_nets.h -- GENERATED by tools/gen_median_nets.py; do not edit.\n"
         "// MidNet<B>::run(keys): the key at rank (B-1)/2 of B keys, by a pruned Batcher odd-even merge\n"
-        "// network of the next power of two with compile-time sentinels folded away.  Keys: uint32\n"
-        "// (one coordinate per lane) or two uint16 keys packed in 32 bits (two coordinates per lane,\n"
-        "// v_pk_min_u16 / v_pk_max_u16).  Used by k_median (robust.hip).\n"
+        "// network of the next power of two with compile-time sentinels folded away.  Keys: uint32 or\n"
+        "// float (one coordinate per lane) or two uint16 keys packed in 32 bits (two coordinates per lane,\n"
+        "// v_pk_min_u16 / v_pk_max_u16).  Used by the k_median kernels (robust.hip).\n"
         "#pragma once\n\n"
         "typedef unsigned short fa_u16x2 __attribute__((ext_vector_type(2)));\n"
         "__device__ __forceinline__ unsigned kmin(unsigned a, unsigned b) { return min(a, b); }\n"
         "__device__ __forceinline__ unsigned kmax(unsigned a, unsigned b) { return max(a, b); }\n"
         "__device__ __forceinline__ fa_u16x2 kmin(fa_u16x2 a, fa_u16x2 b) { return __builtin_elementwise_min(a, b); }\n"
-        "__device__ __forceinline__ fa_u16x2 kmax(fa_u16x2 a, fa_u16x2 b) { return __builtin_elementwise_max(a, b); }\n\n"
+        "__device__ __forceinline__ fa_u16x2 kmax(fa_u16x2 a, fa_u16x2 b) { return __builtin_elementwise_max(a, b); }\n"
+        "// float keys (r03): IEEE 754-2019 minimum / maximum -- one v_minimum3_f32 / v_maximum3_f32 on gfx950,\n"
+        "// no input canonicalisation, -0 < +0, and a NaN input turns both outputs NaN, so a column with a NaN\n"
+        "// selects NaN (every input reaches the selected output) -- no per-key conversion or NaN test.\n"
+        "__device__ __forceinline__ float kmin(float a, float b) { return __builtin_elementwise_minimum(a, b); }\n"
+        "__device__ __forceinline__ float kmax(float a, float b) { return __builtin_elementwise_maximum(a, b); }\n\n"
         "template <int B> struct MidNet;\n\n"
     )
     with open(path, "w") as f:
