@@ -180,20 +180,23 @@ def _special_columns(g, k, n, dtype):
     return xs
 
 
-@pytest.mark.parametrize("lanes", ["1", "2"])
+@pytest.mark.parametrize("layout", ["lanes1", "lanes2", "packed"])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("k", [7, 8, 32, 33, 64, 72, 100, 127, 128])
-def test_median_special_values_float_keys(eng, dtype, k, lanes, monkeypatch):
+def test_median_special_values_float_keys(eng, dtype, k, layout, monkeypatch):
     """The float-key networks (IEEE minimum / maximum, NaN-propagating; k_median_off, k_median_2l)
     select the same bits as the oracle on subnormals of both signs (a flushing min / max would
     change them), signalling / negative / payload NaNs, +-0, +-inf and +-max, one and two lanes per
-    column."""
+    column; "packed": 4-byte aligned 16-bit columns, two per lane on uint16 keys (k_median_pk, K <= 64)."""
     from oracle import orc
-    monkeypatch.setenv("FA_MEDIAN_LANES", lanes)
+    if layout == "packed" and dtype == torch.float32:
+        pytest.skip("no packed form for float32")
+    monkeypatch.setenv("FA_MEDIAN_LANES", "2" if layout == "lanes2" else "1")
     g = torch.Generator().manual_seed(1000 + k)
     xs = _special_columns(g, k, 4099, dtype)
     off = torch.zeros(1, dtype=dtype, device=DEV)  # 2-byte views: 16-bit types take the one-per-lane kernels
-    segs = [torch.cat([off, x.to(DEV)])[1:] if dtype != torch.float32 else x.to(DEV) for x in xs]
+    segs = [torch.cat([off, x.to(DEV)])[1:] if dtype != torch.float32 and layout != "packed" else x.to(DEV)
+            for x in xs]
     got = eng.coord_median([segs])[0].cpu()
     iv = torch.int32 if dtype == torch.float32 else torch.int16
     assert torch.equal(got.view(iv), orc.coord_median(xs).view(iv))
