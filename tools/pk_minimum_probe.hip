@@ -19,6 +19,14 @@ __global__ void k_pk(const h2* a, const h2* b, h2* mn, h2* mx, int n) {
   mx[i] = __builtin_elementwise_maximum(a[i], b[i]);
 }
 
+// three distinct operands: the compiler fuses min(min(a, b), c) into one v_pk_minimum3_f16
+__global__ void k_pk3(const h2* a, const h2* b, const h2* c, h2* mn, h2* mx, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  mn[i] = __builtin_elementwise_minimum(__builtin_elementwise_minimum(a[i], b[i]), c[i]);
+  mx[i] = __builtin_elementwise_maximum(__builtin_elementwise_maximum(a[i], b[i]), c[i]);
+}
+
 static float h2f(unsigned short u) {
   _Float16 h;
   memcpy(&h, &u, 2);
@@ -71,5 +79,31 @@ int main() {
     }
   }
   printf("{\"pairs\": %d, \"min_mismatch\": %d, \"max_mismatch\": %d}\n", 2 * n, bad_mn, bad_mx);
+  // three operands: reference = two chained two-operand results (already checked above)
+  std::vector<unsigned short> C(2 * n);
+  for (int i = 0; i < 2 * n; ++i) C[i] = rand() % 3 ? pats[rand() % 10] : (unsigned short)rand();
+  void *dc, *dmn3, *dmx3;
+  (void)hipMalloc(&dc, 4 * n);
+  (void)hipMalloc(&dmn3, 4 * n);
+  (void)hipMalloc(&dmx3, 4 * n);
+  (void)hipMemcpy(dc, C.data(), 4 * n, hipMemcpyHostToDevice);
+  hipLaunchKernelGGL(k_pk3, dim3(n / 256), dim3(256), 0, 0, (const h2*)da, (const h2*)db, (const h2*)dc, (h2*)dmn3,
+                     (h2*)dmx3, n);
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  std::vector<unsigned short> MN3(2 * n), MX3(2 * n);
+  (void)hipMemcpy(MN3.data(), dmn3, 4 * n, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(MX3.data(), dmx3, 4 * n, hipMemcpyDeviceToHost);
+  int bad3n = 0, bad3x = 0;
+  shown = 0;
+  for (int i = 0; i < 2 * n; ++i) {
+    const bool okn = ref(MN[i], C[i], true, MN3[i]), okx = ref(MX[i], C[i], false, MX3[i]);
+    bad3n += !okn;
+    bad3x += !okx;
+    if ((!okn || !okx) && shown < 8) {
+      printf("3-op half %d: a=%04x b=%04x c=%04x min3=%04x max3=%04x\n", i & 1, A[i], B[i], C[i], MN3[i], MX3[i]);
+      ++shown;
+    }
+  }
+  printf("{\"triples\": %d, \"min3_mismatch\": %d, \"max3_mismatch\": %d}\n", 2 * n, bad3n, bad3x);
   return 0;
 }
