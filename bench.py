@@ -80,6 +80,13 @@ def parse():
                    help="N > 1 over RCCL: native = the whole step in one fa_group_reduce call of libfedagg "
                         "(include/fedagg_comm.h, its own RCCL communicators); torch = the same algorithm issued "
                         "per chunk through torch.distributed (group_reduce.py; always used over gloo)")
+    p.add_argument("--self-launch", action="store_true",
+                   help="start the ranks through torch.distributed.run even at --gpus 1 (the chain the multi-GPU "
+                        "driver runs: parent -> launcher -> rank -> RCCL init -> native exchange)")
+    p.add_argument("--loopback", action="store_true",
+                   help="metric / hier: run the group -> global exchange even at one rank, native ordered exchanges "
+                        "with FA_XCHG_LOOPBACK (every rank owns a piece, its own piece goes through RCCL as a self "
+                        "send / receive) -- at --gpus 1 it executes the whole N > 1 exchange body on one GPU")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     p.add_argument("--check-samples", type=int, default=65536)
@@ -107,6 +114,36 @@ def _free_port():
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def visible_gpu_count():
+    """GPUs this process may use, counted WITHOUT initialising HIP -- the launcher parent must not touch
+    the GPU before its ranks start (torch.cuda.device_count() may fall back to hipGetDeviceCount when
+    amdsmi discovery fails).  KFD topology nodes with SIMDs whose render node this process can open,
+    capped by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set; without a
+    KFD topology, the render nodes this process can open."""
+    import glob
+    n = 0
+    nodes = glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties")
+    for prop in nodes:
+        try:
+            with open(prop) as f:
+                kv = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
+        except OSError:
+            continue
+        if int(kv.get("simd_count", "0")) <= 0:
+            continue  # a CPU node
+        minor = kv.get("drm_render_minor")
+        dev = f"/dev/dri/renderD{minor}" if minor is not None else None
+        if dev is None or os.access(dev, os.R_OK | os.W_OK):
+            n += 1
+    if not nodes:
+        n = sum(1 for d in glob.glob("/dev/dri/renderD*") if os.access(d, os.R_OK | os.W_OK))
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
 
 
 def launch_cmd(n, argv, port, script=None):
@@ -203,13 +240,15 @@ def init_dist(args):
                          "with --nproc-per-node N)")
     if world > 1 and args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.loopback and args.config not in ("metric", "hier"):
+        raise SystemExit("--loopback: the metric and hier configs run the group -> global exchange")
     # FEDML_AMD_BENCH_REHEARSAL=1: rehearse the N > 1 code path with every rank on device 0 over gloo
     # (RCCL refuses two ranks on one GPU); numbers from such a run are not measurements
     rehearsal = os.environ.get("FEDML_AMD_BENCH_REHEARSAL") == "1"
     if rehearsal:
         local = 0
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 or args.loopback:
         import datetime
 
         import torch.distributed as dist
@@ -404,9 +443,11 @@ def reducer(args, eng, timer, **kw):
         # the product path: one fa_group_reduce call per step (include/fedagg_comm.h), its local-step
         # kernels HIP-event timed inside the library
         red = GroupReducer(collective=args.collective, chunks=args.chunks, stream=masked_stream(eng, args),
-                           native=True, timing=True)
+                           native=True, timing=True, loopback=args.loopback)
         timer.natives.append(red)
         return red
+    if args.loopback:
+        raise SystemExit("--loopback: the native exchange over RCCL only (--exchange-impl native, nccl backend)")
 
     def untimed_sum(xs_, mode, coef, div, o):
         return eng.weighted_sum(xs_, mode, coef, div, out=o)
@@ -430,7 +471,7 @@ def sum_over_ranks(v, world):
 
 
 def collective_note(args, world):
-    if world == 1:
+    if world == 1 and not args.loopback:
         return ""
     return {"ordered": "the whole global model on rank 0, rank-ordered sum (bit-exact)",
             "ordered_all": "the whole global model on every rank, rank-ordered sum (bit-exact)",
@@ -457,7 +498,7 @@ def wl_metric(args, eng, rank, world, timer):
         xs = make_arena_rows(mine, P) if args.layout == "arena" else make_flat_clients(mine, P)
     out = torch.empty(P, device="cuda")
     res = {}
-    if world > 1:
+    if world > 1 or args.loopback:
         def timed_sum(xs_, mode, coef, div, o):
             with timer:
                 return eng.weighted_sum(xs_, mode, coef, div, out=o)
@@ -498,7 +539,7 @@ def wl_metric(args, eng, rank, world, timer):
             return None
         from oracle import orc
         tiles = sample_tiles(P, max(1, args.check_samples // 1024), 99)
-        if world == 1:
+        if world == 1 and not args.loopback:
             sampled = list(tiled_pick(buf, tiles, P)[rows]) if tiled else [flat_pick(x, tiles, P) for x in xs]
             exp = orc.weighted_sum(sampled, MUL_W, w)
             bad = count_bad(flat_pick(out, tiles, P), exp)
@@ -966,7 +1007,8 @@ def wl_hier(args, eng, rank, world, timer):
     N = sum(counts)
     my_groups = split(G, rank, world)
     clients = [i for g in my_groups for i in range(g * M, (g + 1) * M)]
-    tiled = args.layout == "tiled" and world == 1  # multi-rank hierarchical: flat rows (GroupReducer slices)
+    # multi-rank hierarchical: flat rows (GroupReducer slices)
+    tiled = args.layout == "tiled" and world == 1 and not args.loopback
     if tiled:
         arena = make_tiled_arena(clients, P)
         buf, rows, xs = arena.bufs[torch.float32], list(range(len(clients))), None
@@ -983,7 +1025,7 @@ def wl_hier(args, eng, rank, world, timer):
         with timer:
             return eng.weighted_sum_grouped(xs_, mode, coef, div, gp, gm, gc, gd, out=o)
 
-    if world > 1:
+    if world > 1 or args.loopback:
         red = reducer(args, eng, timer, local_grouped=timed_grouped)
 
         def step():
@@ -1136,11 +1178,32 @@ def wl_gossip(args, eng, rank, world, timer):
                               "the survey's 4*n*P*4 accounting would be 2x these figures")
 
 
+def pcie_probe(nbytes=1 << 30, reps=5):
+    """Pinned H2D and D2H copy rates (GB/s, best of ``reps``) of one ``nbytes`` buffer: the PCIe
+    ceiling the host-path line is read against."""
+    h = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    out = {}
+    for name, (dst, src) in {"h2d": (d, h), "d2h": (h, d)}.items():
+        best = float("inf")
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            dst.copy_(src, non_blocking=True)
+            torch.cuda.synchronize()
+            best = min(best, time.perf_counter() - t0)
+        out[f"pinned_{name}_GBs"] = round(nbytes / best / 1e9, 2)
+    return out
+
+
 def wl_host(args, eng, rank, world, timer):
-    """Host path (SURVEY.md §8(d) 'Host path'): client updates start in pageable host memory (as
-    unpickled from MPI / socket receive buffers), are packed into pinned staging and copied H2D into
-    the ClientArena (copy stream, overlapped with packing the next client), aggregated, and the
-    averaged model is copied back D2H for broadcast.  Step = ingest K clients + FedAvg + D2H."""
+    """Host path (SURVEY.md §8(d) 'Host path'; the reference receives updates into MPI / socket
+    buffers, core/distributed/communication/mpi/mpi_receive_thread.py:25): client updates start in
+    host memory -- pageable (as unpickled from receive buffers) or, with --pinned, already in pinned
+    receive buffers -- are copied H2D into the ClientArena (pageable: packed into pinned staging on the
+    way, overlapped with the next client's copy), aggregated, and the averaged model is copied back
+    D2H for broadcast.  Step = ingest K clients + FedAvg + D2H; value = the aggregate's algorithmic
+    bytes / that step time (the PCIe-inclusive rate, never the device-resident metric)."""
     from fedml_amd.arena import ArenaLayout, ClientArena
     from fedml_amd.engine import MUL_W
     K = args.clients or 128
@@ -1149,11 +1212,13 @@ def wl_host(args, eng, rank, world, timer):
     N = sum(counts)
     w = [c / N for c in counts]
     g = torch.Generator().manual_seed(0)
-    host = [{"w": torch.randn(P, generator=g)} for _ in range(K)]
-    if args.pinned:
-        host = [{"w": h["w"].pin_memory()} for h in host]
+    base = torch.randn(P + K, generator=g)
+    # distinct clients without K full randn passes (a metric-size run holds 64 GB of updates)
+    host = [{"w": (base[i:i + P].pin_memory() if args.pinned else base[i:i + P].clone())} for i in range(K)]
+    del base
     arena = ClientArena(ArenaLayout([("w", (P,), torch.float32)]), capacity=K)
     result = torch.empty(P, pin_memory=True)
+    pcie = pcie_probe()
 
     def step():
         for i in range(K):
@@ -1161,10 +1226,30 @@ def wl_host(args, eng, rank, world, timer):
         with timer:
             avg = arena.aggregate(MUL_W, w)
         result.copy_(avg["w"], non_blocking=True)
+        torch.cuda.current_stream().synchronize()  # the model is on the host for broadcast
 
-    return dict(name=f"fedavg_host_ingest_{'pinned' if args.pinned else 'pageable'}_K{K}_P{P}_fp32", dtype="fp32", step=step, parity=lambda: None,
-                bytes_total=K * P * 4 + P * 4, launch_bytes=K * P * 4 + P * 4, clients=K, params=P, cpu_K=None,
-                roofline_note="value includes pageable->pinned packing, H2D over PCIe and the D2H of the result")
+    def parity():
+        """The oracle's ordered FedAvg of the HOST updates on 64 sampled 4-KiB tiles vs the host result."""
+        if args.check_samples <= 0:
+            return None
+        from oracle import orc
+        tiles = sample_tiles(P, max(1, args.check_samples // 1024), 97)
+        cols = [torch.cat([h["w"][t * 1024:min((t + 1) * 1024, P)] for t in tiles]) for h in host]
+        exp = orc.weighted_sum(cols, MUL_W, w)
+        got = torch.cat([result[t * 1024:min((t + 1) * 1024, P)] for t in tiles])
+        bad = count_bad(got, exp)
+        return f"{'bit-exact' if bad == 0 else f'{bad} MISMATCHES'} vs oracle on {exp.numel()} sampled elements"
+
+    pcie_floor_ms = ((K * P * 4) / (pcie["pinned_h2d_GBs"] * 1e9) + P * 4 / (pcie["pinned_d2h_GBs"] * 1e9)) * 1e3
+    return dict(name=f"fedavg_host_ingest_{'pinned' if args.pinned else 'pageable'}_K{K}_P{P}_fp32", dtype="fp32",
+                step=step, parity=parity, bytes_total=K * P * 4 + P * 4, launch_bytes=K * P * 4 + P * 4, clients=K,
+                params=P, cpu_K=None,
+                data=f"synthetic N(0,1) client updates in {'pinned' if args.pinned else 'pageable'} HOST memory "
+                     "(client i = window i of one random vector), n_i ~ U{50..600} (seed 7)",
+                extra_line={"pcie": dict(pcie, floor_ms_per_step=round(pcie_floor_ms, 2),
+                                         note="K*P*4 B H2D + P*4 B D2H at the pinned copy rates")},
+                roofline_note="value includes the H2D of every update (pageable: packed through pinned staging), "
+                              "the aggregation and the D2H of the result; `pcie` holds this box's pinned copy rates")
 
 
 def wl_fedopt(args, eng, rank, world, timer):
@@ -1412,7 +1497,10 @@ def _robust_cpu(fn, K, Pc, budget_s, nbytes, what, digits=2):
 
 def wl_median(args, eng, rank, world, timer):
     """§8(f) #3: coordinate-wise median (coordinate_wise_median_defense.py:18-44) of K client
-    weight vectors of ResNet-18 size: one fa_coord_median launch (a selection per coordinate)."""
+    weight vectors of ResNet-18 size: one fa_coord_median launch (a selection per coordinate).
+    --layout tiled (default): the clients in a tile-interleaved ClientArena (fa_coord_median_tiled,
+    the layout the FedAvg kernels read at the metric's rate); arena / tensors: K rows of one
+    allocation (client-major, fa_coord_median)."""
     if world > 1:
         raise SystemExit("median config: single GPU")
     K = args.clients or 32
@@ -1425,13 +1513,25 @@ def wl_median(args, eng, rank, world, timer):
         for i, x in enumerate(xs):
             arena[i, :P].copy_(x)
         xs = [arena[i, :P] for i in range(K)]
+    tiled = args.layout == "tiled"
+    if tiled:
+        from fedml_amd.arena import ArenaLayout, ClientArena
+        ta = ClientArena(ArenaLayout([("w", (P,), dt)]), capacity=K, zero=False, tiled=True)
+        for i, x in enumerate(xs):
+            ta.write(i, {"w": x})
+        torch.cuda.synchronize()
+        ta._scratch.clear()
+        buf, rows = ta.bufs[dt], list(range(K))
     es = xs[0].element_size()
     ibits = {4: torch.int32, 2: torch.int16}[es]
     out = torch.empty(P, dtype=dt, device="cuda")
 
     def step():
         with timer:
-            eng.coord_median([xs], outs=[out])
+            if tiled:
+                eng.coord_median_tiled(buf, rows, n=P, out=out)
+            else:
+                eng.coord_median([xs], outs=[out])
 
     def parity():
         if args.check_samples <= 0:
@@ -1449,9 +1549,11 @@ def wl_median(args, eng, rank, world, timer):
         return _robust_cpu(robust_port.median_port, K, Pc, budget_s, K * Pc * 4 + Pc * 4,
                            "oracle/robust_port.median_port (cat + torch.median, coordinate_wise_median_defense.py:26-31)")
 
-    return dict(name=f"coord_median_K{K}_P{P}_{args.dtype}", dtype=args.dtype, step=step, parity=parity,
+    return dict(name=f"coord_median_K{K}_P{P}_{args.dtype}" + ("_tiled" if tiled else ""), dtype=args.dtype,
+                step=step, parity=parity,
                 bytes_total=(K * P + P) * es, launch_bytes=(K * P + P) * es, clients=K, params=P, cpu_K=K, cpu=cpu,
-                data="synthetic N(0,1) client weight vectors, resident in HBM (rows 256-byte aligned)")
+                data="synthetic N(0,1) client weight vectors, resident in HBM (" +
+                     ("tile-interleaved ClientArena rows)" if tiled else "rows 256-byte aligned)"))
 
 
 def wl_krum(args, eng, rank, world, timer):
@@ -1666,10 +1768,10 @@ def cpu_probe(args):
 
 def main():
     args = parse()
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    if (args.gpus > 1 or args.self_launch) and "WORLD_SIZE" not in os.environ:
         # no outer launcher: start the N ranks as child processes before anything touches the GPU
         if os.environ.get("FEDML_AMD_BENCH_REHEARSAL") != "1" and not os.environ.get("FEDML_AMD_BENCH_CPU_PROBE"):
-            have = torch.cuda.device_count()  # counts devices without initialising HIP on this image
+            have = visible_gpu_count()  # sysfs / device nodes only: no HIP call in the parent
             if have < args.gpus:
                 raise SystemExit(f"--gpus {args.gpus}: only {have} HIP device(s) visible "
                                  "(FEDML_AMD_BENCH_REHEARSAL=1 rehearses the N-rank path on one device over gloo)")
@@ -1753,7 +1855,9 @@ def main():
                                        + (" (native fa_group_reduce)" if timer.natives else " (torch.distributed)")
                                        + f" in {args.chunks} chunks"
                                        + (f", local partials on {args.cu_mask} CUs" if args.cu_mask else "")
-                                       if world > 1 else ""),
+                                       + (", loopback (own pieces through RCCL self send/recv)" if args.loopback
+                                          else "")
+                                       if world > 1 or args.loopback else ""),
                        "kernel_variant": args.variant, "layout": args.layout},
             "roofline": roofline_block(wl, world, value, unit, achieved, kernel_ms, launch_bytes),
             "cpu_baseline": cpu,
@@ -1761,6 +1865,7 @@ def main():
         }
         if wl.get("roofline_note"):
             line["roofline"]["note"] = wl["roofline_note"]
+        line.update(wl.get("extra_line", {}))
         if wl.get("latency"):
             line["latency_ms"] = {"mean": round(float(np.mean(lat)) * 1e3, 4),
                                   "median": round(float(np.median(lat)) * 1e3, 4),
@@ -1770,7 +1875,7 @@ def main():
                 line["latency_ms"]["all_arrive_at_once"] = wl["extra"]["b2b_ms"]
         print(json.dumps(line), flush=True)
     stage("teardown")
-    if world > 1:
+    if world > 1 or args.loopback:
         import torch.distributed as dist
         dist.destroy_process_group()
     stage.done()

@@ -36,15 +36,17 @@ EXPORTED_SYMBOLS = (
     "fa_finite_sum", "fa_finite_sum_tiled", "fa_finite_quantize", "fa_lcc_decode", "fa_mt_randint_sum",
     "fa_mt_randint_sum_scratch_bytes",
     # include/fedagg_robust.h
-    "fa_coord_median", "fa_pairwise_sqdist", "fa_pairwise_sqdist_rt", "fa_pairwise_sqdist_scratch_bytes",
+    "fa_coord_median", "fa_coord_median_tiled", "fa_pairwise_sqdist", "fa_pairwise_sqdist_rt", "fa_pairwise_sqdist_scratch_bytes",
     # include/fedagg_comm.h
     "fa_comm_unique_id", "fa_comm_init", "fa_comm_wrap", "fa_comm_destroy", "fa_comm_size", "fa_local_out_dtype",
     "fa_group_plan", "fa_group_ops", "fa_group_reduce_scratch_bytes", "fa_group_reduce", "fa_comm_set_timing", "fa_comm_local_time",
-    "fa_comm_last_op",
+    "fa_comm_last_op", "fa_group_plan_ex", "fa_group_ops_ex", "fa_comm_op_counts",
 )
 
 # enum fa_exchange / fa_local_kind (include/fedagg_comm.h)
 XCHG_ORDERED, XCHG_ORDERED_ALL, XCHG_REDUCE, XCHG_ALL_REDUCE, XCHG_REDUCE_SCATTER = 0, 1, 2, 3, 4
+XCHG_LOOPBACK = 0x100                    # OR'ed into an ordered exchange
+XFLAG_DELIVER_ALL, XFLAG_LOOPBACK = 1, 2  # fa_group_plan_ex / fa_group_ops_ex flags
 LOCAL_FLAT, LOCAL_TILED, LOCAL_GROUPED, LOCAL_GROUPED_TILED, LOCAL_PARTIAL = 0, 1, 2, 3, 4
 COMM_ID_BYTES = 128
 
@@ -155,6 +157,9 @@ def _declare(L):
     L.fa_mt_randint_sum_scratch_bytes.argtypes = [ctypes.c_int64]
     L.fa_coord_median.restype = ctypes.c_int
     L.fa_coord_median.argtypes = [_vp, ctypes.c_int, ctypes.c_int32, _P_i64, ctypes.c_int32, _P_vp, _P_vp, _vp]
+    L.fa_coord_median_tiled.restype = ctypes.c_int
+    L.fa_coord_median_tiled.argtypes = [_vp, ctypes.c_int, ctypes.c_int32, _P_i64, ctypes.c_int32, _P_vp,
+                                        ctypes.c_int64, _P_vp, _vp]
     L.fa_pairwise_sqdist.restype = ctypes.c_int
     L.fa_pairwise_sqdist.argtypes = [_vp, ctypes.c_int32, _P_i64, ctypes.c_int32, _P_vp, _vp, _vp, ctypes.c_size_t, _vp]
     L.fa_pairwise_sqdist_rt.restype = ctypes.c_int
@@ -190,6 +195,15 @@ def _declare(L):
     L.fa_group_ops.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                ctypes.c_int32, ctypes.c_int, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P_i32,
                                _P_i32, _P_i32, _P_i64, _P_i64]
+    L.fa_group_plan_ex.restype = ctypes.c_int
+    L.fa_group_plan_ex.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                   ctypes.c_int32, ctypes.c_int32, _P_i64, _P_i64, _P_i64, _P_i64]
+    L.fa_group_ops_ex.restype = ctypes.c_int
+    L.fa_group_ops_ex.argtypes = [ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                  ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                  _P_i32, _P_i32, _P_i32, _P_i64, _P_i64]
+    L.fa_comm_op_counts.restype = ctypes.c_int
+    L.fa_comm_op_counts.argtypes = [_vp, _P_i64]
     L.fa_group_reduce_scratch_bytes.restype = ctypes.c_int
     L.fa_group_reduce_scratch_bytes.argtypes = [_vp, ctypes.c_int, _P_ls, ctypes.c_int64, ctypes.c_int32,
                                                 ctypes.c_int32, ctypes.c_int32, _P_i64]

@@ -217,7 +217,14 @@ class ClientArena:
         """Row i is about to be overwritten: every row view handed out by an earlier adopt(i) that is
         still alive (a caller kept the update dict, or one of its tensors) is moved to a private copy
         first (``t.set_(t.clone())``, on the compute stream, which the overwrite is ordered after), so
-        it keeps its values -- in the reference each update owns its tensors."""
+        it keeps its values -- in the reference each update owns its tensors.
+
+        Scope: the protection covers the tensor OBJECTS adopt() handed out (the dict's entries, and
+        the dict itself).  A view derived from one of them (``t.reshape(-1)``, ``t[0]``, ``t.T``) is a
+        view of the arena row, not of the private copy; it follows the row once that is
+        overwritten.  Callers that keep such a view across rounds clone it (the arena's storage is
+        shared by every row, so it cannot tell which row a derived view points into).  Results of
+        ``ArrivalIngest.to_host`` have no such limit (their guard counts references on the storage)."""
         refs = self._handed.pop(i, None)
         if not refs:
             return
@@ -392,6 +399,31 @@ class ClientArena:
                                                           n=self.layout.group_numel[dt], out=o)
             else:
                 outs[dt] = self.engine.weighted_sum_rows(buf, clients, mode, coef, divisor, out=o)
+        return self.layout.carve(outs)
+
+    def median(self, clients: Optional[Sequence[int]] = None,
+               out: Optional[Dict[torch.dtype, torch.Tensor]] = None) -> "OrderedDict[str, torch.Tensor]":
+        """Coordinate-wise median over the given client rows (default: all), one launch per dtype
+        group (coordinate_wise_median_defense.py:18-44's torch.median(dim=-1) per coordinate; a
+        selection, bit for bit): tiled arenas through fa_coord_median_tiled (the layout whose K tiles
+        of a workgroup are one contiguous run), client-major arenas over the row views.  Float groups
+        only (the reference's median runs over weight tensors).  Returns per-key views."""
+        clients = list(range(self.capacity)) if clients is None else list(clients)
+        if not clients:
+            raise RuntimeError("torch.cat(): expected a non-empty list of Tensors")
+        if any(dt not in (torch.float32, torch.bfloat16, torch.float16, torch.float64) for dt in self.bufs):
+            raise TypeError("median: the arena holds a non-float dtype group")
+        self._wait_ingest()
+        outs: Dict[torch.dtype, torch.Tensor] = {}
+        for dt, buf in self.bufs.items():
+            o = out[dt] if out is not None else None
+            n = self.layout.group_numel[dt]
+            if self.tiled:
+                outs[dt] = self.engine.coord_median_tiled(buf, clients, n=n, out=o)
+            else:
+                o = o if o is not None else torch.empty(n, dtype=dt, device=buf.device)
+                self.engine.coord_median([[buf[i][:n] for i in clients]], outs=[o])
+                outs[dt] = o
         return self.layout.carve(outs)
 
     def _pair_groups(self) -> Optional[torch.dtype]:

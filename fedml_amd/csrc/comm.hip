@@ -42,6 +42,7 @@ struct fa_comm {
   int64_t launches = 0;
   mutable std::mutex mu;                   // guards last_op (read by a watchdog thread)
   char last_op[192] = {0};
+  int64_t nops[2][2] = {{0, 0}, {0, 0}};   // point-to-point ops issued: [communicator][send, recv]
 };
 
 namespace {
@@ -122,7 +123,8 @@ struct Plan {
   int64_t mine = 0;                             // elements of all this rank's pieces
 };
 
-void make_plan(int64_t n, int32_t chunks, int32_t align, int world, int root, int me, Plan* p) {
+// loop (FA_XCHG_LOOPBACK): every rank, root included, owns one of `world` pieces.
+void make_plan(int64_t n, int32_t chunks, int32_t align, int world, int root, int me, bool loop, Plan* p) {
   p->C = num_chunks(n, chunks, align);
   p->lo.resize(p->C); p->hi.resize(p->C);
   p->pstart.assign(p->C * world, 0); p->psize.assign(p->C * world, 0);
@@ -134,9 +136,9 @@ void make_plan(int64_t n, int32_t chunks, int32_t align, int world, int root, in
     for (int r = 0; r < world; ++r) p->pstart[c * world + r] = a;
     int o = 0;
     for (int r = 0; r < world; ++r) {
-      if (r == root) continue;
+      if (r == root && !loop) continue;
       int64_t plo, phi;
-      bounds(L, world - 1, align, o++, &plo, &phi);
+      bounds(L, loop ? world : world - 1, align, o++, &plo, &phi);
       p->pstart[c * world + r] = a + plo;
       p->psize[c * world + r] = phi - plo;
     }
@@ -157,20 +159,24 @@ struct P2p {
 // The ops of rank `me` in chunk ch: phase 0 = partials to the owners (communicator 1), phase 1 = the
 // summed pieces to the root / to every rank (communicator 2).  A pure function of the plan: every
 // rank derives its sends and its peers' matching receives from the same plan (fa_group_ops exports it
-// for the CPU test that pairs them up and replays the data movement).
-void xchg_ops(const Plan& p, int world, int me, int root, bool to_all, int phase, int64_t ch, std::vector<P2p>& ops) {
+// for the CPU test that pairs them up and replays the data movement).  With `loop` a rank's own piece
+// travels too (self send / receive in the same group) and the owner's sum lands in FA_XBUF_SUM, from
+// where the delivery sends it -- to the root, or to every rank, itself included.
+void xchg_ops(const Plan& p, int world, int me, int root, bool to_all, bool loop, int phase, int64_t ch,
+              std::vector<P2p>& ops) {
   ops.clear();
   const int64_t L_me = p.psize[ch * world + me], s_me = p.pstart[ch * world + me];
   const int64_t r0 = world * p.roff[ch];
   for (int r = 0; r < world; ++r) {
-    if (r == me) continue;
+    if (r == me && !loop) continue;
     const int64_t Lr = p.psize[ch * world + r], sr = p.pstart[ch * world + r];
     if (phase == 0) {
       if (Lr) ops.push_back(P2p{r, true, FA_XBUF_SEND, sr, Lr});
       if (L_me) ops.push_back(P2p{r, false, FA_XBUF_RECV, r0 + r * L_me, L_me});
     } else {
       if ((to_all || me == root) && Lr) ops.push_back(P2p{r, false, FA_XBUF_OUT, sr, Lr});
-      if (L_me && (to_all || r == root)) ops.push_back(P2p{r, true, FA_XBUF_OUT, s_me, L_me});
+      if (L_me && (to_all || r == root))
+        ops.push_back(loop ? P2p{r, true, FA_XBUF_SUM, p.roff[ch], L_me} : P2p{r, true, FA_XBUF_OUT, s_me, L_me});
     }
   }
 }
@@ -178,20 +184,21 @@ void xchg_ops(const Plan& p, int world, int me, int root, bool to_all, int phase
 int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 struct Scratch {
-  int64_t send = 0, recv = 0, stage = 0, total = 0;  // byte offsets / total
+  int64_t send = 0, recv = 0, sum = 0, stage = 0, total = 0;  // byte offsets / total
 };
 
-int scratch_layout(int exchange, const fa_local_step* L, int64_t n, int32_t chunks, int32_t align, int world,
-                   int root, int me, int osz, Scratch* s) {
-  s->send = s->recv = s->stage = s->total = 0;
+int scratch_layout(int exchange, bool loop, const fa_local_step* L, int64_t n, int32_t chunks, int32_t align,
+                   int world, int root, int me, int osz, Scratch* s) {
+  s->send = s->recv = s->sum = s->stage = s->total = 0;
   if (exchange == FA_XCHG_ORDERED || exchange == FA_XCHG_ORDERED_ALL) {
-    if (world <= 1) return FA_OK;  // nothing to exchange
+    if (world <= 1 && !loop) return FA_OK;  // nothing to exchange
     Plan p;
-    make_plan(n, chunks, align, world, root, me, &p);
+    make_plan(n, chunks, align, world, root, me, loop, &p);
     const int64_t send_b = L->kind == FA_LOCAL_PARTIAL ? 0 : round_up(n * osz, 256);
     s->send = 0;
     s->recv = send_b;
-    s->total = send_b + round_up(world * p.mine * osz, 256);
+    s->sum = send_b + round_up(world * p.mine * osz, 256);
+    s->total = s->sum + (loop ? round_up(p.mine * osz, 256) : 0);
   } else if (exchange == FA_XCHG_REDUCE_SCATTER) {
     const int64_t S = (n + (int64_t)world * align - 1) / ((int64_t)world * align) * align;
     s->stage = 0;
@@ -268,16 +275,18 @@ int run_local(fa_ctx* ctx, fa_comm* c, const fa_local_step* L, int64_t a, int64_
   return FA_OK;
 }
 
-int ordered(fa_ctx* ctx, fa_comm* c, bool to_all, const fa_local_step* L, int64_t n, int32_t chunks,
+int ordered(fa_ctx* ctx, fa_comm* c, bool to_all, bool loop, const fa_local_step* L, int64_t n, int32_t chunks,
             int32_t align, int root, char* out, char* scratch, hipStream_t st, int osz, ncclDataType_t nt) {
   const int world = c->world, me = c->rank;
   Plan p;
-  make_plan(n, chunks, align, world, root, me, &p);
+  make_plan(n, chunks, align, world, root, me, loop, &p);
   Scratch sl;
-  scratch_layout(to_all ? FA_XCHG_ORDERED_ALL : FA_XCHG_ORDERED, L, n, chunks, align, world, root, me, osz, &sl);
+  scratch_layout(to_all ? FA_XCHG_ORDERED_ALL : FA_XCHG_ORDERED, loop, L, n, chunks, align, world, root, me, osz,
+                 &sl);
   const bool partial = L->kind == FA_LOCAL_PARTIAL;
   const char* send = partial ? (const char*)L->d_partial : scratch + sl.send;
   char* recv = scratch + sl.recv;
+  char* sums = scratch + sl.sum;  // loop: the owner's summed pieces, sent from here
   std::vector<const void*> ptrs, sum_in(world);
   std::vector<hipEvent_t> after_a2a(p.C);
 
@@ -287,13 +296,16 @@ int ordered(fa_ctx* ctx, fa_comm* c, bool to_all, const fa_local_step* L, int64_
   if (rc) return rc;
 
   std::vector<P2p> ops;
-  char* bufs[3] = {(char*)send, recv, out};
-  auto issue = [&](const std::vector<P2p>& list, ncclComm_t comm, hipStream_t s, const char* what) -> int {
+  char* bufs[4] = {(char*)send, recv, out, sums};
+  auto issue = [&](const std::vector<P2p>& list, int which, const char* what) -> int {
+    ncclComm_t comm = which ? c->c2 : c->c1;
+    hipStream_t s = which ? c->sb : c->sa;
     ncclResult_t res = ncclGroupStart();
     for (size_t q = 0; q < list.size() && res == ncclSuccess; ++q) {
       const P2p& o = list[q];
       char* ptr = bufs[o.buf] + o.offset * osz;
       res = o.send ? ncclSend(ptr, (size_t)o.count, nt, o.peer, comm, s) : ncclRecv(ptr, (size_t)o.count, nt, o.peer, comm, s);
+      if (res == ncclSuccess) c->nops[which][o.send ? 0 : 1]++;
     }
     const ncclResult_t end = ncclGroupEnd();  // closes the group whatever happened inside it
     if (res != ncclSuccess) return fail(FA_ERR_COMM, "%s send/recv: %s", what, ncclGetErrorString(res));
@@ -306,18 +318,19 @@ int ordered(fa_ctx* ctx, fa_comm* c, bool to_all, const fa_local_step* L, int64_
     const int64_t r0 = world * p.roff[ch];
     if (L_me) {  // a rank with no piece (the root) neither waits for its sends nor orders its receives
       FA_HIP(hipStreamWaitEvent(st, after_a2a[ch], 0));  // behind the S(um)'s own stream, not the host
-      for (int r = 0; r < world; ++r)
-        sum_in[r] = r == me ? (const void*)(send + s_me * osz) : (const void*)(recv + (r0 + r * L_me) * osz);
+      for (int r = 0; r < world; ++r)  // loop: the own partial came through RCCL like the others
+        sum_in[r] = r == me && !loop ? (const void*)(send + s_me * osz) : (const void*)(recv + (r0 + r * L_me) * osz);
+      char* dst = loop ? sums + p.roff[ch] * osz : out + s_me * osz;
       int rc2 = fa_weighted_sum(ctx, fa_local_out_dtype(L->dtype, L->mode), FA_MODE_SUM, L_me, world, sum_in.data(),
-                                nullptr, 1.0, out + s_me * osz, st);
+                                nullptr, 1.0, dst, st);
       if (rc2) return rc2;
       rc2 = order(c, st, c->sb);
       if (rc2) return rc2;
     }
     set_op(c, "chunk %lld/%lld: delivery of the summed pieces %s", (long long)(ch + 1), (long long)p.C,
            to_all ? "to every rank" : "to the root");
-    xchg_ops(p, world, me, root, to_all, 1, ch, ops);
-    return issue(ops, c->c2, c->sb, "delivery");
+    xchg_ops(p, world, me, root, to_all, loop, 1, ch, ops);
+    return issue(ops, 1, "delivery");
   };
 
   for (int64_t ch = 0; ch < p.C; ++ch) {
@@ -330,8 +343,8 @@ int ordered(fa_ctx* ctx, fa_comm* c, bool to_all, const fa_local_step* L, int64_
     if (rc) return rc;
     set_op(c, "chunk %lld/%lld: partials to the owners (point-to-point over every link)", (long long)(ch + 1),
            (long long)p.C);
-    xchg_ops(p, world, me, root, to_all, 0, ch, ops);
-    rc = issue(ops, c->c1, c->sa, "owner");
+    xchg_ops(p, world, me, root, to_all, loop, 0, ch, ops);
+    rc = issue(ops, 0, "owner");
     if (rc) return rc;
     rc = event(c, &after_a2a[ch]);
     if (rc) return rc;
@@ -519,12 +532,14 @@ int fa_comm_size(const fa_comm* c, int* world, int* rank) {
   return FA_OK;
 }
 
-int fa_group_plan(int64_t n, int32_t chunks, int32_t align, int32_t world, int32_t root, int32_t max_chunks,
-                  int64_t* chunk_lo, int64_t* chunk_hi, int64_t* piece_start, int64_t* piece_size) {
-  if (n < 0 || chunks < 1 || align < 1 || world < 1 || root < 0 || root >= world || !chunk_lo || !chunk_hi)
+int fa_group_plan_ex(int64_t n, int32_t chunks, int32_t align, int32_t world, int32_t root, int32_t flags,
+                     int32_t max_chunks, int64_t* chunk_lo, int64_t* chunk_hi, int64_t* piece_start,
+                     int64_t* piece_size) {
+  if (n < 0 || chunks < 1 || align < 1 || world < 1 || root < 0 || root >= world || !chunk_lo || !chunk_hi ||
+      (flags & ~(FA_XFLAG_DELIVER_ALL | FA_XFLAG_LOOPBACK)))
     return fail(FA_ERR_INVALID, "fa_group_plan: invalid arguments");
   Plan p;
-  make_plan(n, chunks, align, world, root, 0, &p);
+  make_plan(n, chunks, align, world, root, 0, (flags & FA_XFLAG_LOOPBACK) != 0, &p);
   if (p.C > max_chunks) return fail(FA_ERR_INVALID, "fa_group_plan: %lld chunks > max_chunks %d", (long long)p.C, max_chunks);
   for (int64_t c = 0; c < p.C; ++c) {
     chunk_lo[c] = p.lo[c];
@@ -537,17 +552,23 @@ int fa_group_plan(int64_t n, int32_t chunks, int32_t align, int32_t world, int32
   return (int)p.C;
 }
 
-int fa_group_ops(int64_t n, int32_t chunks, int32_t align, int32_t world, int32_t rank, int32_t root, int deliver_all,
-                 int32_t phase, int32_t chunk, int32_t max_ops, int32_t* peer, int32_t* is_send, int32_t* buf,
-                 int64_t* offset, int64_t* count) {
+int fa_group_plan(int64_t n, int32_t chunks, int32_t align, int32_t world, int32_t root, int32_t max_chunks,
+                  int64_t* chunk_lo, int64_t* chunk_hi, int64_t* piece_start, int64_t* piece_size) {
+  return fa_group_plan_ex(n, chunks, align, world, root, 0, max_chunks, chunk_lo, chunk_hi, piece_start, piece_size);
+}
+
+int fa_group_ops_ex(int64_t n, int32_t chunks, int32_t align, int32_t world, int32_t rank, int32_t root,
+                    int32_t flags, int32_t phase, int32_t chunk, int32_t max_ops, int32_t* peer, int32_t* is_send,
+                    int32_t* buf, int64_t* offset, int64_t* count) {
   if (n < 0 || chunks < 1 || align < 1 || world < 1 || rank < 0 || rank >= world || root < 0 || root >= world ||
-      (phase != 0 && phase != 1) || chunk < 0)
+      (phase != 0 && phase != 1) || chunk < 0 || (flags & ~(FA_XFLAG_DELIVER_ALL | FA_XFLAG_LOOPBACK)))
     return fail(FA_ERR_INVALID, "fa_group_ops: invalid arguments");
+  const bool loop = (flags & FA_XFLAG_LOOPBACK) != 0;
   Plan p;
-  make_plan(n, chunks, align, world, root, rank, &p);
+  make_plan(n, chunks, align, world, root, rank, loop, &p);
   if (chunk >= p.C) return fail(FA_ERR_INVALID, "fa_group_ops: chunk %d of %lld", chunk, (long long)p.C);
   std::vector<P2p> ops;
-  if (world > 1) xchg_ops(p, world, rank, root, deliver_all != 0, phase, chunk, ops);
+  if (world > 1 || loop) xchg_ops(p, world, rank, root, (flags & FA_XFLAG_DELIVER_ALL) != 0, loop, phase, chunk, ops);
   if ((int64_t)ops.size() > max_ops) return fail(FA_ERR_INVALID, "fa_group_ops: %zu ops > max_ops", ops.size());
   for (size_t q = 0; q < ops.size(); ++q) {
     if (peer) peer[q] = ops[q].peer;
@@ -559,16 +580,25 @@ int fa_group_ops(int64_t n, int32_t chunks, int32_t align, int32_t world, int32_
   return (int)ops.size();
 }
 
+int fa_group_ops(int64_t n, int32_t chunks, int32_t align, int32_t world, int32_t rank, int32_t root, int deliver_all,
+                 int32_t phase, int32_t chunk, int32_t max_ops, int32_t* peer, int32_t* is_send, int32_t* buf,
+                 int64_t* offset, int64_t* count) {
+  return fa_group_ops_ex(n, chunks, align, world, rank, root, deliver_all ? FA_XFLAG_DELIVER_ALL : 0, phase, chunk,
+                         max_ops, peer, is_send, buf, offset, count);
+}
+
 int fa_group_reduce_scratch_bytes(const fa_comm* c, int exchange, const fa_local_step* L, int64_t n,
                                   int32_t chunks, int32_t align, int32_t root, int64_t* bytes) {
   if (!c || !bytes) return fail(FA_ERR_INVALID, "fa_group_reduce_scratch_bytes: NULL argument");
   int rc = check_local(L);
   if (rc) return rc;
+  const bool loop = (exchange & FA_XCHG_LOOPBACK) != 0;
+  exchange &= ~FA_XCHG_LOOPBACK;
   if (n < 0 || chunks < 1 || align < 1 || root < 0 || root >= c->world)
     return fail(FA_ERR_INVALID, "fa_group_reduce_scratch_bytes: invalid n/chunks/align/root");
   Scratch s;
-  scratch_layout(exchange, L, n, chunks, align, c->world, root, c->rank, esize(fa_local_out_dtype(L->dtype, L->mode)),
-                 &s);
+  scratch_layout(exchange, loop, L, n, chunks, align, c->world, root, c->rank,
+                 esize(fa_local_out_dtype(L->dtype, L->mode)), &s);
   *bytes = s.total;
   return FA_OK;
 }
@@ -579,8 +609,12 @@ int fa_group_reduce(fa_ctx* ctx, fa_comm* c, int exchange, const fa_local_step* 
   if (!ctx || !c) return fail(FA_ERR_INVALID, "fa_group_reduce: ctx/comm is NULL");
   int rc = check_local(L);
   if (rc) return rc;
+  const bool loop = (exchange & FA_XCHG_LOOPBACK) != 0;
+  exchange &= ~FA_XCHG_LOOPBACK;
   if (exchange < FA_XCHG_ORDERED || exchange > FA_XCHG_REDUCE_SCATTER)
     return fail(FA_ERR_INVALID, "fa_group_reduce: unknown exchange %d", exchange);
+  if (loop && exchange != FA_XCHG_ORDERED && exchange != FA_XCHG_ORDERED_ALL)
+    return fail(FA_ERR_INVALID, "fa_group_reduce: FA_XCHG_LOOPBACK applies to the ordered exchanges only");
   if (n < 0 || chunks < 1 || align < 1 || root < 0 || root >= c->world)
     return fail(FA_ERR_INVALID, "fa_group_reduce: invalid n/chunks/align/root");
   if (n > 0 && !d_out) return fail(FA_ERR_INVALID, "fa_group_reduce: d_out is NULL");
@@ -594,7 +628,7 @@ int fa_group_reduce(fa_ctx* ctx, fa_comm* c, int exchange, const fa_local_step* 
                                align, (long long)E);
   }
   Scratch s;
-  scratch_layout(exchange, L, n, chunks, align, c->world, root, c->rank, osz, &s);
+  scratch_layout(exchange, loop, L, n, chunks, align, c->world, root, c->rank, osz, &s);
   if (s.total > 0 && (!d_scratch || scratch_bytes < s.total))
     return fail(FA_ERR_INVALID, "fa_group_reduce: scratch of %lld bytes < %lld needed", (long long)scratch_bytes,
                 (long long)s.total);
@@ -605,7 +639,7 @@ int fa_group_reduce(fa_ctx* ctx, fa_comm* c, int exchange, const fa_local_step* 
   c->next_ev = 0;
   char* out = (char*)d_out;
   std::vector<const void*> ptrs;
-  if (c->world == 1 && (exchange == FA_XCHG_ORDERED || exchange == FA_XCHG_ORDERED_ALL)) {
+  if (c->world == 1 && !loop && (exchange == FA_XCHG_ORDERED || exchange == FA_XCHG_ORDERED_ALL)) {
     // no owners: the local step (or the partial) is the result; the RCCL exchanges still run their
     // collectives at world 1 (a copy), so one GPU exercises their stream ordering
     const int64_t C = num_chunks(n, chunks, align);
@@ -626,7 +660,8 @@ int fa_group_reduce(fa_ctx* ctx, fa_comm* c, int exchange, const fa_local_step* 
   switch (exchange) {
     case FA_XCHG_ORDERED:
     case FA_XCHG_ORDERED_ALL:
-      return ordered(ctx, c, exchange == FA_XCHG_ORDERED_ALL, L, n, chunks, align, root, out, scratch, st, osz, nt);
+      return ordered(ctx, c, exchange == FA_XCHG_ORDERED_ALL, loop, L, n, chunks, align, root, out, scratch, st, osz,
+                     nt);
     case FA_XCHG_REDUCE:
     case FA_XCHG_ALL_REDUCE:
       return reduce_like(ctx, c, exchange, L, n, chunks, align, root, out, st, osz, nt);
@@ -656,6 +691,12 @@ int fa_comm_local_time(fa_comm* c, int reset, double* ms, int64_t* launches) {
     c->local_ms = 0.0;
     c->launches = 0;
   }
+  return FA_OK;
+}
+
+int fa_comm_op_counts(const fa_comm* c, int64_t* counts) {
+  if (!c || !counts) return fail(FA_ERR_INVALID, "fa_comm_op_counts: NULL argument");
+  for (int i = 0; i < 4; ++i) counts[i] = c->nops[i / 2][i % 2];
   return FA_OK;
 }
 

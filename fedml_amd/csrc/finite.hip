@@ -1017,7 +1017,7 @@ int mt_jump_log2(double exp_words, int streams) {
 int mt_jump_tables(fa_ctx* ctx, uint64_t J, int count, hipStream_t st) {
   if (ctx->mt_poly_dev && ctx->mt_poly_J == J && ctx->mt_poly_count >= count) return FA_OK;
   if (fa_mt::charpoly().empty()) return fail(FA_ERR_INVALID, "fa_mt_randint_sum: MT19937 characteristic polynomial not found");
-  const std::vector<fa_mt::Poly>& g = fa_mt::jump_polys(J, count);
+  const std::vector<fa_mt::Poly> g = fa_mt::jump_polys(J, count);
   std::vector<std::vector<int32_t>> ev((size_t)count), od((size_t)count);
   int stride = 0;
   for (int c = 0; c < count; ++c) {
@@ -1098,16 +1098,6 @@ int fa_mt_randint_sum(fa_ctx* ctx, int32_t num_streams, const uint32_t* seeds, c
   const uint64_t per = std::min<uint64_t>((uint64_t)num_streams, UINT64_MAX / rng);
   const size_t seed_b = align16(sizeof(uint32_t) * num_streams);
   const size_t tab = seed_b + align16((size_t)num_streams);
-  fa_ctx::Slot* slot = nullptr;
-  int rc = acquire_slot(ctx, tab, &slot);
-  if (rc) return rc;
-  char* h = (char*)slot->host;
-  memcpy(h, seeds, sizeof(uint32_t) * num_streams);
-  memcpy(h + seed_b, signs, (size_t)num_streams);
-  rc = stage(slot, tab, st);
-  if (rc) return rc;
-  const uint32_t* dseeds = (const uint32_t*)slot->dev;
-  const int8_t* dsigns = (const int8_t*)((const char*)slot->dev + seed_b);
   const unsigned fold_blocks = (unsigned)std::min<int64_t>((n + kBlock - 1) / kBlock, 4096);
   // jump-ahead: C chunks of J words per stream when the stream is long enough for >= 2 of them
   const double exp_words = (double)n * (wide ? 2.0 : 1.0) * ((double)mask + 1.0) / ((double)rng + 1.0);
@@ -1117,21 +1107,37 @@ int fa_mt_randint_sum(fa_ctx* ctx, int32_t num_streams, const uint32_t* seeds, c
   const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)num_streams, mt_plane_budget() / (((uint64_t)n + 3) / 4 * 4 * es)));
   const uint64_t J = 624ull << mt_jump_log2(exp_words, (int)G);
   const int C = mt_jump_enabled() ? (int)std::min<double>(std::floor(exp_words / (double)J), 4096.0) : 0;
-  if (C >= 2) {
+  const size_t seq_b = align16(sizeof(uint32_t) * kMtSeqWords * G), win_b = align16(sizeof(uint32_t) * kMtN * C * G);
+  const int64_t pstride = (n + 3) / 4 * 4;  // plane stride: every plane 16-byte aligned
+  const size_t cnt_b = align16(sizeof(int64_t) * C * G), pl_b = (size_t)G * pstride * es;
+  int rc;
+  if (C >= 2) {  // everything that can fail before the staging slot is taken (a taken slot is always released)
     rc = mt_jump_tables(ctx, J, C - 1, st);
     if (rc) return rc;
-    const size_t seq_b = align16(sizeof(uint32_t) * kMtSeqWords * G), win_b = align16(sizeof(uint32_t) * kMtN * C * G);
-    const int64_t pstride = (n + 3) / 4 * 4;  // plane stride: every plane 16-byte aligned
-    const size_t cnt_b = align16(sizeof(int64_t) * C * G), pl_b = (size_t)G * pstride * es;
     rc = mt_work(ctx, seq_b + win_b + 2 * cnt_b + pl_b, st);
     if (rc) return rc;
-    // the work space is shared by every call on this ctx: a previous call queued on another stream
-    // must be done with it before these kernels overwrite it
     if (!ctx->mt_ev && hipEventCreateWithFlags(&ctx->mt_ev, hipEventDisableTiming) != hipSuccess) {
       ctx->mt_ev = nullptr;
       return fail(FA_ERR_HIP, "fa_mt_randint_sum: hipEventCreate failed");
     }
-    if (ctx->mt_live) FA_HIP(hipStreamWaitEvent(st, ctx->mt_ev, 0));
+  }
+  fa_ctx::Slot* slot = nullptr;
+  rc = acquire_slot(ctx, tab, &slot);
+  if (rc) return rc;
+  char* h = (char*)slot->host;
+  memcpy(h, seeds, sizeof(uint32_t) * num_streams);
+  memcpy(h + seed_b, signs, (size_t)num_streams);
+  rc = stage(slot, tab, st);
+  if (rc) return rc;
+  const uint32_t* dseeds = (const uint32_t*)slot->dev;
+  const int8_t* dsigns = (const int8_t*)((const char*)slot->dev + seed_b);
+  if (C >= 2) {
+    // the work space is shared by every call on this ctx: a previous call queued on another stream
+    // must be done with it before these kernels overwrite it
+    if (ctx->mt_live && hipStreamWaitEvent(st, ctx->mt_ev, 0) != hipSuccess) {
+      (void)release(slot, st);
+      return fail(FA_ERR_HIP, "fa_mt_randint_sum: hipStreamWaitEvent failed");
+    }
     char* w = (char*)ctx->mt_dev;
     uint32_t* dseq = (uint32_t*)w;
     uint32_t* dwin = (uint32_t*)(w + seq_b);
@@ -1161,12 +1167,19 @@ int fa_mt_randint_sum(fa_ctx* ctx, int32_t num_streams, const uint32_t* seeds, c
                            (int)b, n, pstride, p, (int64_t*)d_out, s0 == 0 ? 1 : 0);
       }
     }
-    FA_HIP(hipGetLastError());
-    FA_HIP(hipEventRecord(ctx->mt_ev, st));
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipEventRecord(ctx->mt_ev, st);
+    if (e != hipSuccess) {
+      (void)release(slot, st);
+      return fail(FA_ERR_HIP, "fa_mt_randint_sum: %s", hipGetErrorString(e));
+    }
     ctx->mt_live = true;
     return release(slot, st);
   }
-  FA_HIP(hipMemsetAsync(d_scratch, 0, sizeof(uint64_t) * (size_t)n, st));
+  if (hipMemsetAsync(d_scratch, 0, sizeof(uint64_t) * (size_t)n, st) != hipSuccess) {
+    (void)release(slot, st);
+    return fail(FA_ERR_HIP, "fa_mt_randint_sum: hipMemsetAsync of the scratch failed");
+  }
   int first = 1;
   for (uint64_t s0 = 0; s0 < (uint64_t)num_streams; s0 += per) {
     const unsigned b = (unsigned)std::min<uint64_t>(per, (uint64_t)num_streams - s0);
@@ -1180,7 +1193,11 @@ int fa_mt_randint_sum(fa_ctx* ctx, int32_t num_streams, const uint32_t* seeds, c
                        (int64_t*)d_out, n, p, first);
     first = 0;
   }
-  FA_HIP(hipGetLastError());
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    (void)release(slot, st);
+    return fail(FA_ERR_HIP, "fa_mt_randint_sum: %s", hipGetErrorString(e));
+  }
   return release(slot, st);
 }
 

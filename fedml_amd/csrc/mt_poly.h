@@ -187,8 +187,10 @@ inline Poly xpow(uint64_t e) {
   return r;
 }
 
-// Jump polynomials x^(c*J) mod phi for c = 1..count, cached per J (they depend on J only).
-inline const std::vector<Poly>& jump_polys(uint64_t J, int count) {
+// Jump polynomials x^(c*J) mod phi for c = 1..count, cached per J (they depend on J only).  Returns a
+// COPY of the first `count`, made under the lock: another context may grow the cache (and move its
+// storage) while the caller reads them.
+inline std::vector<Poly> jump_polys(uint64_t J, int count) {
   static std::mutex mu;
   static std::vector<std::pair<uint64_t, std::vector<Poly>>> cache;
   std::lock_guard<std::mutex> lk(mu);
@@ -204,7 +206,7 @@ inline const std::vector<Poly>& jump_polys(uint64_t J, int count) {
     const Poly g1 = (*v)[0];
     while ((int)v->size() < count) v->push_back(mulmod(v->back(), g1));
   }
-  return *v;
+  return std::vector<Poly>(v->begin(), v->begin() + std::max(0, count));
 }
 
 }  // namespace fa_mt

@@ -59,6 +59,9 @@ template <> struct MedT<FA_DTYPE_F32> {
   __device__ static float load_off(const void* p, unsigned off) { return gld_nt_off<float>(p, off); }
   __device__ static void store(void* p, int64_t e, float v) { ((float*)p)[e] = v; }
   __device__ static void store_bits(void* p, int64_t e, const void* src) { ((unsigned*)p)[e] = ((const unsigned*)src)[e]; }
+  __device__ static void store_bits_off(void* p, int64_t e, const void* src, unsigned off) {
+    ((unsigned*)p)[e] = gld_nt_off<unsigned>(src, off);
+  }
 };
 template <> struct MedT<FA_DTYPE_BF16> {
   static constexpr int kBytes = 2;
@@ -74,6 +77,9 @@ template <> struct MedT<FA_DTYPE_BF16> {
   __device__ static void store_bits(void* p, int64_t e, const void* src) {
     ((unsigned short*)p)[e] = ((const unsigned short*)src)[e];
   }
+  __device__ static void store_bits_off(void* p, int64_t e, const void* src, unsigned off) {
+    ((unsigned short*)p)[e] = gld_nt_off<unsigned short>(src, off);
+  }
 };
 template <> struct MedT<FA_DTYPE_F16> {
   static constexpr int kBytes = 2;
@@ -88,6 +94,9 @@ template <> struct MedT<FA_DTYPE_F16> {
   }
   __device__ static void store_bits(void* p, int64_t e, const void* src) {
     ((unsigned short*)p)[e] = ((const unsigned short*)src)[e];
+  }
+  __device__ static void store_bits_off(void* p, int64_t e, const void* src, unsigned off) {
+    ((unsigned short*)p)[e] = gld_nt_off<unsigned short>(src, off);
   }
 };
 
@@ -106,29 +115,44 @@ struct MSeg {
   int64_t numel;
   int64_t tile_start;
   void* out;
+  int64_t tstride;  // 0: flat client segments; > 0: tile-interleaved inputs, bytes between a client's tiles
   int32_t ptr_base;
   int32_t pad;
 };
-static_assert(sizeof(MSeg) == 32, "MSeg layout");
+static_assert(sizeof(MSeg) == 40, "MSeg layout");
+
+// Byte offset of a workgroup's first column e0 from a client's segment start: flat segments e0 * SZ;
+// tiled inputs (tstride > 0, FA_TILE_BYTES tiles of E elements; fedml_amd/arena.py tiled=True)
+// (e0 / E) * tstride + (e0 % E) * SZ.  A workgroup's columns never straddle a tile (its column count
+// divides E), so a client's element is `uniform base (SGPRs: pointer + this offset) + the lane's
+// 32-bit byte offset` in both layouts -- every load keeps global_load's saddr form, for any segment size.
+template <int SZ>
+__device__ __forceinline__ int64_t col_base(int64_t e0, int64_t tstride) {
+  constexpr int64_t E = FA_TILE_BYTES / SZ;
+  return tstride ? (e0 / E) * tstride + (e0 % E) * SZ : e0 * SZ;
+}
+__device__ __forceinline__ const void* at(const void* p, int64_t ub) { return (const char*)p + ub; }
 
 // Rare cases, resolved by an in-order rescan of the column: a NaN anywhere -> ATen returns the
 // FIRST NaN; a zero selected -> the selected rank r falls in the block of (equal) zeros, which ATen
 // orders by client index -> the (r - #negatives)-th zero in client order.
+// Client i's element of this lane: at(in[i], ub) + boff (col_base); the result goes to out[e].
 template <int DT>
-__device__ __forceinline__ void store_rare(const void* const* in, int k, int64_t e, int r, bool nan, void* out) {
+__device__ __forceinline__ void store_rare(const void* const* in, int64_t ub, unsigned boff, int k, int64_t e, int r,
+                                           bool nan, void* out) {
   if (nan) {
     for (int i = 0; i < k; ++i) {
-      const float x = MedT<DT>::load(in[i], e);
-      if (x != x) { MedT<DT>::store_bits(out, e, in[i]); return; }
+      const float x = MedT<DT>::load_off(at(in[i], ub), boff);
+      if (x != x) { MedT<DT>::store_bits_off(out, e, at(in[i], ub), boff); return; }
     }
   }
   int negc = 0;
-  for (int i = 0; i < k; ++i) negc += MedT<DT>::load(in[i], e) < 0.0f;
+  for (int i = 0; i < k; ++i) negc += MedT<DT>::load_off(at(in[i], ub), boff) < 0.0f;
   int seen = 0;
   for (int i = 0; i < k; ++i) {
-    const float x = MedT<DT>::load(in[i], e);
+    const float x = MedT<DT>::load_off(at(in[i], ub), boff);
     if (x == 0.0f) {
-      if (seen == r - negc) { MedT<DT>::store_bits(out, e, in[i]); return; }
+      if (seen == r - negc) { MedT<DT>::store_bits_off(out, e, at(in[i], ub), boff); return; }
       ++seen;
     }
   }
@@ -143,14 +167,14 @@ __device__ __forceinline__ void store_rare(const void* const* in, int k, int64_t
 // load is unconditional) before any is consumed, keys + sentinels, the network, the rare-case rescan
 // (k_median_pk's odd last coordinate).
 template <int DT, int B>
-__device__ __forceinline__ void median_col(const void* const* in, int k, int64_t e, int64_t ec, bool live,
-                                           void* out) {
+__device__ __forceinline__ void median_col(const void* const* in, int64_t ub, unsigned boff, int k, int64_t e,
+                                           bool live, void* out) {
   const void* p[B];
 #pragma unroll
-  for (int i = 0; i < B; ++i) p[i] = in[min(i, k - 1)];
+  for (int i = 0; i < B; ++i) p[i] = at(in[min(i, k - 1)], ub);
   float x[B];
 #pragma unroll
-  for (int i = 0; i < B; ++i) x[i] = MedT<DT>::load(p[i], ec);  // clamped: every load unconditional
+  for (int i = 0; i < B; ++i) x[i] = MedT<DT>::load_off(p[i], boff);  // clamped: every load unconditional
   const int lo_end = k + (B - 1) / 2 - ((k - 1) >> 1);          // sentinels [k, lo_end) are low
   unsigned key[B];
   bool nan = false;
@@ -162,7 +186,7 @@ __device__ __forceinline__ void median_col(const void* const* in, int k, int64_t
   const unsigned kr = select_mid<B>(key);
   if (!live) return;
   const int r = (k - 1) >> 1;
-  if (nan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, nan, out);
+  if (nan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, ub, boff, k, e, r, nan, out);
   else MedT<DT>::store(out, e, fkey_inv(kr));
 }
 
@@ -187,15 +211,16 @@ k_median_off(const MSeg* __restrict__ segs, int nseg, const void* const* __restr
   if constexpr (EXACT) k = B;
   const int64_t tile = blockIdx.x;
   const MSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
-  const int64_t e = (tile - sg.tile_start) * kBlock + threadIdx.x;
+  const int64_t e0 = (tile - sg.tile_start) * kBlock, e = e0 + threadIdx.x;
   const bool live = e < sg.numel;
   const int64_t ec = live ? e : sg.numel - 1;
   const void* const* in = ptrs + sg.ptr_base;
-  const unsigned boff = (unsigned)ec * (unsigned)MedT<DT>::kBytes;
+  const int64_t ub = col_base<MedT<DT>::kBytes>(e0, sg.tstride);
+  const unsigned boff = (unsigned)(ec - e0) * (unsigned)MedT<DT>::kBytes;
   const int lo_end = k + (B - 1) / 2 - ((k - 1) >> 1);  // sentinels [k, lo_end) low, [lo_end, B) high
   float x[B];
 #pragma unroll
-  for (int i = 0; i < B; ++i) x[i] = MedT<DT>::load_off(in[min(i, k - 1)], boff);
+  for (int i = 0; i < B; ++i) x[i] = MedT<DT>::load_off(at(in[min(i, k - 1)], ub), boff);
   if constexpr (!EXACT) {
 #pragma unroll
     for (int i = 0; i < B; ++i) x[i] = i < k ? x[i] : (i < lo_end ? -__builtin_inff() : __builtin_inff());
@@ -204,7 +229,7 @@ k_median_off(const MSeg* __restrict__ segs, int nseg, const void* const* __restr
   if (!live) return;
   const int r = (k - 1) >> 1;
   const bool nan = kr != kr;
-  if (nan || kr == 0.0f) store_rare<DT>(in, k, e, r, nan, sg.out);
+  if (nan || kr == 0.0f) store_rare<DT>(in, ub, boff, k, e, r, nan, sg.out);
   else MedT<DT>::store(sg.out, e, kr);
 }
 
@@ -238,16 +263,17 @@ k_median_2l(const MSeg* __restrict__ segs, int nseg, const void* const* __restri
   const int c = (int)threadIdx.x % k2lCols;
   const int64_t tile = xcd ? xcd_tile_map(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
   const MSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
-  const int64_t e = (tile - sg.tile_start) * k2lCols + c;
+  const int64_t e0 = (tile - sg.tile_start) * k2lCols, e = e0 + c;
   const bool live = e < sg.numel;
   const int64_t ec = live ? e : sg.numel - 1;
   const void* const* in = ptrs + sg.ptr_base;
-  const unsigned boff = (unsigned)ec * (unsigned)MedT<DT>::kBytes;
+  const int64_t ub = col_base<MedT<DT>::kBytes>(e0, sg.tstride);
+  const unsigned boff = (unsigned)(ec - e0) * (unsigned)MedT<DT>::kBytes;
   const int base = N * h;
   const int lo_end = k + (B - 1) / 2 - ((k - 1) >> 1);  // slots [k, lo_end) low sentinels, [lo_end, B) high
   float x[N];
 #pragma unroll
-  for (int t = 0; t < N; ++t) x[t] = MedT<DT>::load_off(in[min(base + t, k - 1)], boff);
+  for (int t = 0; t < N; ++t) x[t] = MedT<DT>::load_off(at(in[min(base + t, k - 1)], ub), boff);
   if constexpr (!EXACT) {
 #pragma unroll
     for (int t = N - 8; t < N; ++t)  // K > B - 8: only the upper half's last 8 slots can hold sentinels
@@ -274,7 +300,7 @@ k_median_2l(const MSeg* __restrict__ segs, int nseg, const void* const* __restri
   if (!live) return;
   const int r = (k - 1) >> 1;
   const bool nan = kr != kr;
-  if (nan || kr == 0.0f) store_rare<DT>(in, k, e, r, nan, sg.out);
+  if (nan || kr == 0.0f) store_rare<DT>(in, ub, boff, k, e, r, nan, sg.out);
   else MedT<DT>::store(sg.out, e, kr);
 }
 
@@ -285,20 +311,22 @@ __global__ void __launch_bounds__(kBlock)
 k_median(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k) {
   const int64_t tile = blockIdx.x;
   const MSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
-  const int64_t e = (tile - sg.tile_start) * kBlock + threadIdx.x;
+  const int64_t e0 = (tile - sg.tile_start) * kBlock, e = e0 + threadIdx.x;
   const bool live = e < sg.numel;
   const int64_t ec = live ? e : sg.numel - 1;
   const void* const* in = ptrs + sg.ptr_base;
+  const int64_t ub = col_base<MedT<DT>::kBytes>(e0, sg.tstride);
+  const unsigned boff = (unsigned)(ec - e0) * (unsigned)MedT<DT>::kBytes;
   if constexpr (B <= 64) {  // measured faster through median_col up to 64 (K = 64: 0.74 -> 0.64 ms)
-    median_col<DT, B>(in, k, e, ec, live, sg.out);
+    median_col<DT, B>(in, ub, boff, k, e, live, sg.out);
     return;
   }
   const void* p[B];
 #pragma unroll
-  for (int i = 0; i < B; ++i) p[i] = in[min(i, k - 1)];
+  for (int i = 0; i < B; ++i) p[i] = at(in[min(i, k - 1)], ub);
   float x[B];
 #pragma unroll
-  for (int i = 0; i < B; ++i) x[i] = MedT<DT>::load(p[i], ec);  // clamped: every load unconditional
+  for (int i = 0; i < B; ++i) x[i] = MedT<DT>::load_off(p[i], boff);  // clamped: every load unconditional
   const int lo_end = k + (B - 1) / 2 - ((k - 1) >> 1);          // sentinels [k, lo_end) are low
   unsigned key[B];
   bool nan = false;
@@ -310,7 +338,7 @@ k_median(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict_
   const unsigned kr = select_mid<B>(key);
   if (!live) return;
   const int r = (k - 1) >> 1;
-  if (nan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, k, e, r, nan, sg.out);
+  if (nan || kr == kPosZeroKey || kr == kNegZeroKey) store_rare<DT>(in, ub, boff, k, e, r, nan, sg.out);
   else MedT<DT>::store(sg.out, e, fkey_inv(kr));
 }
 
@@ -329,19 +357,21 @@ __global__ void __launch_bounds__(kBlock)
 k_median_pk(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k) {
   const int64_t tile = blockIdx.x;
   const MSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
-  const int64_t e = ((tile - sg.tile_start) * kBlock + threadIdx.x) * 2;
+  const int64_t e0 = (tile - sg.tile_start) * kBlock * 2, e = e0 + threadIdx.x * 2;
   if (e >= sg.numel) return;
   const void* const* in = ptrs + sg.ptr_base;
+  const int64_t ub = col_base<2>(e0, sg.tstride);
+  const unsigned boff = (unsigned)(e - e0) * 2u;
   if (e + 1 == sg.numel) {  // odd segment length: the last coordinate alone
-    median_col<DT, B>(in, k, e, e, true, sg.out);
+    median_col<DT, B>(in, ub, boff, k, e, true, sg.out);
     return;
   }
   const void* p[B];
 #pragma unroll
-  for (int i = 0; i < B; ++i) p[i] = in[min(i, k - 1)];
+  for (int i = 0; i < B; ++i) p[i] = at(in[min(i, k - 1)], ub);
   unsigned w[B];
 #pragma unroll
-  for (int i = 0; i < B; ++i) w[i] = gld_nt<unsigned>(p[i], e >> 1);
+  for (int i = 0; i < B; ++i) w[i] = gld_nt_off<unsigned>(p[i], boff);
   const int lo_end = k + (B - 1) / 2 - ((k - 1) >> 1);
   fa_u16x2 key[B];
   bool nan0 = false, nan1 = false;
@@ -362,47 +392,52 @@ k_median_pk(const MSeg* __restrict__ segs, int nseg, const void* const* __restri
     ((unsigned*)sg.out)[e >> 1] = k16_inv(k0) | (k16_inv(k1) << 16);
     return;
   }
-  if (rare0) store_rare<DT>(in, k, e, r, nan0, sg.out);
+  if (rare0) store_rare<DT>(in, ub, boff, k, e, r, nan0, sg.out);
   else ((unsigned short*)sg.out)[e] = (unsigned short)k16_inv(k0);
-  if (rare1) store_rare<DT>(in, k, e + 1, r, nan1, sg.out);
+  if (rare1) store_rare<DT>(in, ub, boff + 2u, k, e + 1, r, nan1, sg.out);
   else ((unsigned short*)sg.out)[e + 1] = (unsigned short)k16_inv(k1);
 }
 
 // Any K (and float64): rank counting, ATen's order (value, client index), NaN first.
 template <typename T> __device__ __forceinline__ T ldv(const void* p, int64_t e) { return ((const T*)p)[e]; }
 
+// client element at(p, ub) + lane offset c (elements), as a double
 template <int DT>
-__device__ __forceinline__ double load_d(const void* p, int64_t e) {
-  if constexpr (DT == FA_DTYPE_F64) return gld<double>(p, e);
-  else return (double)MedT<DT>::load(p, e);
+__device__ __forceinline__ double load_d(const void* p, int64_t c) {
+  if constexpr (DT == FA_DTYPE_F64) return gld<double>(p, c);
+  else return (double)MedT<DT>::load(p, c);
 }
 template <int DT>
-__device__ __forceinline__ void copy_bits(void* out, int64_t e, const void* src) {
-  if constexpr (DT == FA_DTYPE_F64) ((unsigned long long*)out)[e] = ((const unsigned long long*)src)[e];
-  else MedT<DT>::store_bits(out, e, src);
+__device__ __forceinline__ void copy_bits(void* out, int64_t e, const void* src, int64_t c) {
+  if constexpr (DT == FA_DTYPE_F64) ((unsigned long long*)out)[e] = ((const unsigned long long*)src)[c];
+  else MedT<DT>::store_bits_off(out, e, src, (unsigned)c * (unsigned)MedT<DT>::kBytes);
 }
+template <int DT> constexpr int elem_bytes() { if constexpr (DT == FA_DTYPE_F64) return 8; else return MedT<DT>::kBytes; }
 
 template <int DT>
 __global__ void __launch_bounds__(kBlock)
 k_median_rank(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k) {
   const int64_t tile = blockIdx.x;
   const MSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
-  const int64_t e = (tile - sg.tile_start) * kBlock + threadIdx.x;
+  const int64_t e0 = (tile - sg.tile_start) * kBlock, e = e0 + threadIdx.x;
   if (e >= sg.numel) return;
   const void* const* in = ptrs + sg.ptr_base;
+  const int64_t ub = col_base<elem_bytes<DT>()>(e0, sg.tstride);
+  const int64_t c = e - e0;
   for (int i = 0; i < k; ++i) {
-    if (load_d<DT>(in[i], e) != load_d<DT>(in[i], e)) { copy_bits<DT>(sg.out, e, in[i]); return; }
+    const double xi = load_d<DT>(at(in[i], ub), c);
+    if (xi != xi) { copy_bits<DT>(sg.out, e, at(in[i], ub), c); return; }
   }
   const int r = (k - 1) >> 1;
   for (int i = 0; i < k; ++i) {
-    const double xi = load_d<DT>(in[i], e);
+    const double xi = load_d<DT>(at(in[i], ub), c);
     int less = 0, eq_before = 0;
     for (int j = 0; j < k; ++j) {
-      const double xj = load_d<DT>(in[j], e);
+      const double xj = load_d<DT>(at(in[j], ub), c);
       less += xj < xi;
       eq_before += (xj == xi) && (j < i);
     }
-    if (less + eq_before == r) { copy_bits<DT>(sg.out, e, in[i]); return; }
+    if (less + eq_before == r) { copy_bits<DT>(sg.out, e, at(in[i], ub), c); return; }
   }
 }
 
@@ -484,15 +519,17 @@ void launch_median(int k, bool packed, bool off32, int lanes, dim3 grid, hipStre
 }  // namespace
 
 // ============================================================================================ ABI
-extern "C" {
-
-int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t* seg_numel, int32_t k,
-                    const void* const* d_in, void* const* d_out, void* hip_stream) {
+namespace {
+int median_impl(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t* seg_numel, int32_t k,
+                const void* const* d_in, int64_t tstride, void* const* d_out, void* hip_stream) {
   if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
   if (k <= 0 || num_segments <= 0 || !seg_numel || !d_in || !d_out)
     return fail(FA_ERR_INVALID, "fa_coord_median: invalid arguments");
   if (dtype != FA_DTYPE_F32 && dtype != FA_DTYPE_BF16 && dtype != FA_DTYPE_F16 && dtype != FA_DTYPE_F64)
     return fail(FA_ERR_DTYPE, "fa_coord_median: dtype %d not supported (F32, BF16, F16, F64)", dtype);
+  if (tstride < 0 || tstride % FA_TILE_BYTES)
+    return fail(FA_ERR_INVALID, "fa_coord_median_tiled: tile_stride must be a positive multiple of %d (got %lld)",
+                FA_TILE_BYTES, (long long)tstride);
   // bf16 / f16 with 4-byte aligned pointers, K <= 64: two coordinates per lane (k_median_pk;
   // bf16 K = 16 / 32 / 64: 0.127 / 0.251 / 0.655 -> 0.106 / 0.205 / 0.572 ms.  K = 128 took 2.44 ms
   // packed vs 1.51 ms one per lane: 128 live keys + 128 pointers exceed the register file)
@@ -502,10 +539,10 @@ int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t*
     packed = d_out[s] && (uintptr_t)d_out[s] % 4 == 0;
     for (int i = 0; i < k && packed; ++i) packed = (uintptr_t)d_in[(int64_t)s * k + i] % 4 == 0;
   }
-  // k_median_off addresses a client's element by a 32-bit byte offset: every segment must fit
-  const int64_t es = dtype == FA_DTYPE_F32 ? 4 : dtype == FA_DTYPE_F64 ? 8 : 2;
-  bool off32 = true;
-  for (int s = 0; s < num_segments; ++s) off32 = off32 && seg_numel[s] * es <= (int64_t)0xFFFFFFFFll;
+  // every kernel addresses a client's element as a uniform 64-bit base (the workgroup's first column,
+  // col_base) + a 32-bit lane offset, so any segment size takes the branch-free forms (r03: segments
+  // over 4 GB took the generic k_median)
+  const bool off32 = true;
   const int lanes = median_lanes(dtype, k, packed, off32);
   const int64_t tile_elems = packed ? 2 * kBlock : lanes == 2 ? k2lCols : kBlock;
   int nseg = 0;
@@ -538,7 +575,7 @@ int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t*
     const int64_t n = seg_numel[s];
     if (n == 0) continue;
     for (int i = 0; i < k; ++i) hp[(int64_t)j * k + i] = d_in[(int64_t)s * k + i];
-    hs[j] = MSeg{n, t0, d_out[s], j * k, 0};
+    hs[j] = MSeg{n, t0, d_out[s], tstride, j * k, 0};
     t0 += (n + tile_elems - 1) / tile_elems;
     ++j;
   }
@@ -554,8 +591,26 @@ int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t*
     case FA_DTYPE_F16: launch_median<FA_DTYPE_F16>(k, packed, off32, lanes, grid, st, ds, nseg, dp); break;
     default: launch_median<FA_DTYPE_F64>(k, packed, off32, lanes, grid, st, ds, nseg, dp); break;
   }
-  FA_HIP(hipGetLastError());
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    (void)release(slot, st);
+    return fail(FA_ERR_HIP, "fa_coord_median: %s", hipGetErrorString(e));
+  }
   return release(slot, st);
+}
+}  // namespace
+
+extern "C" {
+
+int fa_coord_median(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t* seg_numel, int32_t k,
+                    const void* const* d_in, void* const* d_out, void* hip_stream) {
+  return median_impl(ctx, dtype, num_segments, seg_numel, k, d_in, 0, d_out, hip_stream);
+}
+
+int fa_coord_median_tiled(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t* seg_numel, int32_t k,
+                          const void* const* d_in, int64_t tile_stride, void* const* d_out, void* hip_stream) {
+  if (tile_stride <= 0) return fail(FA_ERR_INVALID, "fa_coord_median_tiled: tile_stride must be > 0");
+  return median_impl(ctx, dtype, num_segments, seg_numel, k, d_in, tile_stride, d_out, hip_stream);
 }
 
 }  // extern "C"

@@ -101,7 +101,7 @@ class GroupReducer:
     def __init__(self, group=None, collective: str = "ordered", dst: int = 0, chunks: int = 8,
                  local_sum: Optional[LocalSum] = None, local_grouped: Optional[Callable] = None,
                  stream: Optional[torch.cuda.Stream] = None, combine_sum: Optional[LocalSum] = None,
-                 native: Optional[bool] = None, timing: bool = False):
+                 native: Optional[bool] = None, timing: bool = False, loopback: bool = False):
         if collective not in COLLECTIVES:
             raise ValueError(f"unknown collective {collective!r}")
         self.group = group
@@ -127,13 +127,17 @@ class GroupReducer:
         # (include/fedagg_comm.h) over libfedagg's own RCCL communicators; the torch.distributed form
         # below is the same algorithm for CPU (gloo) tests and the one-GPU rehearsal, or with an
         # injected local reduction
+        # loopback (native only): the ordered exchanges with a piece for every rank, the own piece sent
+        # to itself through RCCL (FA_XCHG_LOOPBACK) -- runs the whole exchange even at world 1
         if native is None:
-            native = (local_sum is None and combine_sum is None and local_grouped is None and self.world > 1
-                      and dist.get_backend(group) == "nccl")
+            native = (local_sum is None and combine_sum is None and local_grouped is None
+                      and (self.world > 1 or loopback) and dist.get_backend(group) == "nccl")
+        if loopback and not native:
+            raise ValueError("loopback: only the native exchange (RCCL) has it")
         self.native = None
         if native:
             from .native_exchange import NativeExchange
-            self.native = NativeExchange(_native_comm(group), collective, dst, chunks)
+            self.native = NativeExchange(_native_comm(group), collective, dst, chunks, loopback=loopback)
             self.native.comm.set_timing(timing)
         elif collective in ("ordered", "ordered_all") and self.world > 1:
             self._group2 = _second_group(group)

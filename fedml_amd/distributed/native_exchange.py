@@ -24,14 +24,15 @@ EXCHANGE_CODE = {"ordered": N.XCHG_ORDERED, "ordered_all": N.XCHG_ORDERED_ALL, "
                  "all_reduce": N.XCHG_ALL_REDUCE, "reduce_scatter": N.XCHG_REDUCE_SCATTER}
 
 
-def group_plan(n: int, chunks: int, align: int, world: int, root: int):
-    """fa_group_plan: [(lo, hi, [piece (start, size) per rank])] per chunk -- the C library's plan
-    (a pure function, also callable without a GPU)."""
+def group_plan(n: int, chunks: int, align: int, world: int, root: int, loopback: bool = False):
+    """fa_group_plan_ex: [(lo, hi, [piece (start, size) per rank])] per chunk -- the C library's plan
+    (a pure function, also callable without a GPU).  ``loopback``: the root owns a piece too."""
     L = N.lib()
     cap = max(1, chunks)
     lo, hi = (ctypes.c_int64 * cap)(), (ctypes.c_int64 * cap)()
     ps, pz = (ctypes.c_int64 * (cap * world))(), (ctypes.c_int64 * (cap * world))()
-    c = L.fa_group_plan(int(n), int(chunks), int(align), int(world), int(root), cap, lo, hi, ps, pz)
+    c = L.fa_group_plan_ex(int(n), int(chunks), int(align), int(world), int(root),
+                           N.XFLAG_LOOPBACK if loopback else 0, cap, lo, hi, ps, pz)
     if c < 0:
         N.check(c, "fa_group_plan")
     return [(lo[i], hi[i], [(ps[i * world + r], pz[i * world + r]) for r in range(world)]) for i in range(c)]
@@ -75,6 +76,12 @@ class NativeComm:
                 "fa_comm_local_time")
         return ms.value, cnt.value
 
+    def op_counts(self) -> Tuple[int, int, int, int]:
+        """(sends, receives) issued on communicator 1, then on communicator 2, since creation."""
+        c = (ctypes.c_int64 * 4)()
+        N.check(self._lib.fa_comm_op_counts(self._h, c), "fa_comm_op_counts")
+        return tuple(c)
+
     def last_op(self) -> str:
         buf = ctypes.create_string_buffer(256)
         if self._lib.fa_comm_last_op(self._h, buf, 256) != N.FA_OK:
@@ -96,12 +103,17 @@ class NativeComm:
 class NativeExchange:
     """fa_group_reduce over a NativeComm: the local-step descriptors and the scratch buffer."""
 
-    def __init__(self, comm: NativeComm, collective: str, root: int = 0, chunks: int = 8):
+    def __init__(self, comm: NativeComm, collective: str, root: int = 0, chunks: int = 8, loopback: bool = False):
         if collective not in EXCHANGE_CODE:
             raise ValueError(f"unknown collective {collective!r}")
+        if loopback and collective not in ("ordered", "ordered_all"):
+            raise ValueError("loopback applies to the ordered exchanges only")
         self.comm = comm
         self.collective = collective
-        self.code = EXCHANGE_CODE[collective]
+        self.loopback = bool(loopback)
+        # FA_XCHG_LOOPBACK: every rank (root included) owns a piece and sends its own piece to itself
+        # through RCCL -- at world 1 the whole ordered exchange runs on one GPU
+        self.code = EXCHANGE_CODE[collective] | (N.XCHG_LOOPBACK if loopback else 0)
         self.root = root
         self.chunks = chunks
         self._scratch = None
@@ -186,8 +198,9 @@ class NativeExchange:
 
     def owned(self, n: int, align: int) -> List[tuple]:
         """The pieces this rank summed in the ordered exchanges (its d_out holds them)."""
-        if self.code not in (N.XCHG_ORDERED, N.XCHG_ORDERED_ALL) or self.comm.world == 1:
+        if self.collective not in ("ordered", "ordered_all") or (self.comm.world == 1 and not self.loopback):
             return []
         me = self.comm.rank
         return [(pc[me][0], pc[me][0] + pc[me][1])
-                for _, _, pc in group_plan(n, self.chunks, align, self.comm.world, self.root) if pc[me][1]]
+                for _, _, pc in group_plan(n, self.chunks, align, self.comm.world, self.root, self.loopback)
+                if pc[me][1]]

@@ -867,6 +867,26 @@ class AggEngine:
         N.check(rc, "fa_coord_median")
         return results
 
+    def coord_median_tiled(self, buf: torch.Tensor, rows: Sequence[int], n: Optional[int] = None,
+                           out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """Coordinate-wise median over rows of a TILE-INTERLEAVED arena group ``buf`` [tiles, capacity,
+        E] (fa_coord_median_tiled): the same selection, bit for bit, as ``coord_median`` over the
+        logical rows, read in the layout whose K tiles of a workgroup are one contiguous run."""
+        if buf.dtype not in (torch.float32, torch.bfloat16, torch.float16, torch.float64):
+            raise TypeError(f"coord_median_tiled: unsupported dtype {buf.dtype}")
+        n, ptrs, stride = self._tiled_args(buf, rows, 0, n, "coord_median_tiled")
+        if out is None:
+            out = torch.empty(n, dtype=buf.dtype, device=self.device)
+        elif out.dtype != buf.dtype or out.numel() != n or not out.is_contiguous():
+            raise ValueError(f"coord_median_tiled: output must be a contiguous {buf.dtype} tensor of {n} elements")
+        _require_device(out, self.device, "output")
+        if n == 0:
+            return out
+        rc = self._lib.fa_coord_median_tiled(self._ctx, DTYPE_CODE[buf.dtype], 1, N.i64_array([n]), len(rows), ptrs,
+                                             stride, N.ptr_array([out.data_ptr()]), self._stream(stream))
+        N.check(rc, "fa_coord_median_tiled")
+        return out
+
     MAX_PAIR_K = 128  # kMaxPairK (fedml_amd/csrc/robust.hip): clients per fa_pairwise_sqdist launch
 
     def pairwise_sqdist(self, segments: Sequence[Sequence[torch.Tensor]], stream=None,

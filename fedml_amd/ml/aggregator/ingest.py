@@ -21,7 +21,6 @@ row views to private copies before the row is overwritten (ClientArena._detach).
 """
 from __future__ import annotations
 
-import weakref
 from collections import OrderedDict
 from typing import Dict, Optional
 
@@ -39,7 +38,6 @@ class ArrivalIngest:
         self.parity = 0
         self._host: Dict[int, "OrderedDict[str, torch.Tensor]"] = {}
         self._flat_host: Dict[int, list] = {}  # per round parity: pinned flat buffers, one per dtype group
-        self._handed: Dict[tuple, list] = {}    # (form, parity) -> weakrefs of the result tensors returned
 
     @staticmethod
     def wants(device) -> bool:
@@ -83,15 +81,13 @@ class ArrivalIngest:
         bufs = self._host.get(self.parity)
         if bufs is None or list(bufs.keys()) != list(averaged.keys()) or any(
                 bufs[k].shape != v.shape or bufs[k].dtype != v.dtype for k, v in averaged.items()) or \
-                _held(self._handed.get(("dict", self.parity))):
+                _storage_held(bufs.values()):
             bufs = self._host[self.parity] = OrderedDict(
                 (k, torch.empty(v.shape, dtype=v.dtype, pin_memory=True)) for k, v in averaged.items())
         for k, v in averaged.items():
             bufs[k].copy_(v, non_blocking=True)
         torch.cuda.current_stream(next(iter(averaged.values())).device).synchronize()
-        out = OrderedDict((k, t.view(t.shape)) for k, t in bufs.items())  # caller-side tensor objects
-        self._handed[("dict", self.parity)] = [weakref.ref(t) for t in out.values()]
-        return out
+        return OrderedDict((k, t.view(t.shape)) for k, t in bufs.items())  # caller-side tensor objects
 
 
     def _to_host_flat(self, averaged):
@@ -112,7 +108,7 @@ class ArrivalIngest:
             return None
         dev = next(iter(averaged.values())).device
         cache = self._flat_host.setdefault(self.parity, [])
-        if _held(self._handed.get(("flat", self.parity))):
+        if _storage_held(cache):
             # the caller still holds (part of) the result these buffers carried two rounds ago: leave
             # them to it and take fresh ones (the reference returns a dict that stays valid)
             cache = self._flat_host[self.parity] = []
@@ -130,13 +126,15 @@ class ArrivalIngest:
             for k, hv in zip(keys, _host.carve(host, [o - lo for o in offs], list(shapes))):
                 views[k] = hv
         torch.cuda.current_stream(dev).synchronize()
-        self._handed[("flat", self.parity)] = [weakref.ref(v) for v in views.values()]
         return OrderedDict((k, views[k]) for k in averaged.keys())
 
 
-def _held(refs) -> bool:
-    """Is any tensor of an earlier result still referenced outside the ingest?"""
-    return bool(refs) and any(r() is not None for r in refs)
+def _storage_held(bufs) -> bool:
+    """Is the storage of any of these (the ingest's own pinned buffers) still referenced from outside --
+    by a tensor handed out from it or by ANY view derived from one (reshape, slice, ``.T``)?  Counted
+    on the storage itself, not on the handed-out tensor objects: the buffer's own tensor and this
+    probe's storage object account for 2 references."""
+    return any(torch._C._storage_Use_Count(b.untyped_storage()._cdata) > 2 for b in bufs if b is not None)
 
 
 def _numel(shape) -> int:

@@ -57,7 +57,7 @@ def aggregate(dicts: Sequence[Dict[str, torch.Tensor]], mode: int, coef: Optiona
     keys = list(dicts[0].keys())
     if not keys:
         return OrderedDict()
-    if _HOST_SMALL and not getattr(dicts[0][keys[0]], "is_cuda", True):
+    if _host_small() and not getattr(dicts[0][keys[0]], "is_cuda", True):
         # small CPU round (cfg1): the whole call in C++ (None: not small / not uniform / not native)
         eng = engine or get_engine(None)
         fn, err, ctx = eng.host_round_abi()
@@ -77,7 +77,7 @@ def aggregate(dicts: Sequence[Dict[str, torch.Tensor]], mode: int, coef: Optiona
     if ptrs is not None and int(codes.min()) >= 0:
         if dev.startswith("cuda"):
             return _aggregate_device(keys, ptrs, numel, codes, shapes, dev, len(dicts), mode, coef, divisor, engine)
-        if dev == "cpu" and os.environ.get("FEDML_AMD_HOST_PATH", "packed") == "packed":
+        if dev == "cpu" and _host_small():
             nbytes = sum(n * _ELEM[c] for n, c in zip(numel.tolist(), codes.tolist())) * len(dicts)
             # the zero-copy kernel takes at most _HOST_MAX_TABLE keys and clients (fa_weighted_sum_host)
             if nbytes <= _SMALL_HOST_BYTES and len(keys) <= _HOST_MAX_TABLE and len(dicts) <= _HOST_MAX_TABLE:
@@ -103,7 +103,14 @@ def _aggregate_device(keys, ptrs, numel, codes, shapes, dev, k, mode, coef, divi
 
 
 _ELEM = {0: 4, 1: 2, 2: 2, 3: 8, 4: 8}  # bytes per element of each dtype code
-_HOST_SMALL = os.environ.get("FEDML_AMD_HOST_PATH", "packed") == "packed"
+
+
+def _host_small() -> bool:
+    """FEDML_AMD_HOST_PATH=packed (default): small CPU rounds take the zero-copy kernel.  Read per call,
+    so every check of it agrees with the variable's current value."""
+    return os.environ.get("FEDML_AMD_HOST_PATH", "packed") == "packed"
+
+
 _SMALL_HOST_BYTES = 4 << 20             # CPU rounds up to this size: zero-copy kernel (fa_weighted_sum_host)
 _HOST_MAX_TABLE = 4096                  # fa_weighted_sum_host's limit on num_segments and on k
 

@@ -68,6 +68,15 @@ enum fa_exchange {
     FA_XCHG_REDUCE_SCATTER = 4
 };
 
+/* OR'ed into an ordered exchange (fa_group_reduce, fa_group_reduce_scratch_bytes): every rank, root
+ * included, owns one of `world` pieces, and a rank's own partial piece goes through RCCL as a self
+ * send / receive like everyone else's; each owner sums the received pieces in rank order into a
+ * scratch area and the delivery sends them from there (to root, or to every rank, itself
+ * included).  Same result bits as without it.  At world 1 it runs the whole exchange -- grouped
+ * ncclSend/ncclRecv on both communicators, the event ordering, the owner's SUM, the second stream --
+ * through RCCL on one GPU (what a one-GPU box can verify of the N > 1 path). */
+#define FA_XCHG_LOOPBACK 0x100
+
 /* The local (group) step whose result is exchanged. */
 enum fa_local_kind {
     FA_LOCAL_FLAT = 0,           /* fa_weighted_sum over d_in[i] (n elements each)               */
@@ -122,7 +131,11 @@ int fa_group_plan(int64_t n, int32_t chunks, int32_t align, int32_t world, int32
                   int64_t *chunk_lo, int64_t *chunk_hi, int64_t *piece_start, int64_t *piece_size);
 
 /* Buffers of the ordered exchange's point-to-point operations (fa_group_ops). */
-enum fa_xchg_buf { FA_XBUF_SEND = 0, FA_XBUF_RECV = 1, FA_XBUF_OUT = 2 };
+enum fa_xchg_buf { FA_XBUF_SEND = 0, FA_XBUF_RECV = 1, FA_XBUF_OUT = 2, FA_XBUF_SUM = 3 };
+
+/* Flags of fa_group_plan_ex / fa_group_ops_ex. */
+#define FA_XFLAG_DELIVER_ALL 1 /* FA_XCHG_ORDERED_ALL */
+#define FA_XFLAG_LOOPBACK 2    /* FA_XCHG_LOOPBACK: every rank owns a piece, own pieces sent to self */
 
 /*
  * The point-to-point operations rank `rank` issues for chunk `chunk` of the ordered exchanges
@@ -136,6 +149,14 @@ enum fa_xchg_buf { FA_XBUF_SEND = 0, FA_XBUF_RECV = 1, FA_XBUF_OUT = 2 };
 int fa_group_ops(int64_t n, int32_t chunks, int32_t align, int32_t world, int32_t rank, int32_t root, int deliver_all,
                  int32_t phase, int32_t chunk, int32_t max_ops, int32_t *peer, int32_t *is_send, int32_t *buf,
                  int64_t *offset, int64_t *count);
+/* The same two with FA_XFLAG_* flags (FA_XBUF_SUM: the owner's summed pieces of a LOOPBACK exchange,
+ * this rank's pieces back to back in chunk order). */
+int fa_group_plan_ex(int64_t n, int32_t chunks, int32_t align, int32_t world, int32_t root, int32_t flags,
+                     int32_t max_chunks, int64_t *chunk_lo, int64_t *chunk_hi, int64_t *piece_start,
+                     int64_t *piece_size);
+int fa_group_ops_ex(int64_t n, int32_t chunks, int32_t align, int32_t world, int32_t rank, int32_t root,
+                    int32_t flags, int32_t phase, int32_t chunk, int32_t max_ops, int32_t *peer, int32_t *is_send,
+                    int32_t *buf, int64_t *offset, int64_t *count);
 
 /* Bytes of device scratch fa_group_reduce needs for these arguments (on this rank). */
 int fa_group_reduce_scratch_bytes(const fa_comm *comm, int exchange, const fa_local_step *local, int64_t n,
@@ -157,6 +178,9 @@ int fa_group_reduce(fa_ctx *ctx, fa_comm *comm, int exchange, const fa_local_ste
  * (ms) and count since the last reset. */
 int fa_comm_set_timing(fa_comm *comm, int enable);
 int fa_comm_local_time(fa_comm *comm, int reset, double *ms, int64_t *launches);
+/* Point-to-point operations this fa_comm has issued since it was created: counts[0..3] = sends and
+ * receives on communicator 1, sends and receives on communicator 2. */
+int fa_comm_op_counts(const fa_comm *comm, int64_t *counts);
 /* The last exchange operation this fa_comm issued, as text (hang diagnostics); "" if none. */
 int fa_comm_last_op(const fa_comm *comm, char *buf, int64_t buf_bytes);
 

@@ -5,6 +5,7 @@
  *
  *   fa_coord_median     core/security/defense/coordinate_wise_median_defense.py:26-31
  *                       torch.median(torch.cat(client vectors, -1), dim=-1).values
+ *   fa_coord_median_tiled  the same over tile-interleaved arena rows
  *   fa_pairwise_sqdist  core/security/defense/krum_defense.py:52-66 (_compute_krum_score's
  *                       compute_euclidean_distance(v_i, v_j) ** 2 for every pair)
  *   fa_pairwise_sqdist_rt  the same for bfloat16 / float16 models (differences in the model dtype)
@@ -37,6 +38,15 @@ extern "C" {
  */
 int fa_coord_median(fa_ctx *ctx, int dtype, int32_t num_segments, const int64_t *seg_numel, int32_t k,
                     const void *const *d_in, void *const *d_out, void *hip_stream);
+/*
+ * The same over TILE-INTERLEAVED client rows (fedml_amd/arena.py ClientArena(tiled=True), the
+ * layout fa_weighted_sum_tiled reads): element e of client i's segment s is at
+ * d_in[s * k + i] + (e / E) * tile_stride + (e % E) * sizeof(dtype), E = FA_TILE_BYTES / sizeof(dtype);
+ * every d_in pointer is the start of a tile; tile_stride a positive multiple of FA_TILE_BYTES.
+ * Same results, bit for bit, as fa_coord_median over the logical rows.
+ */
+int fa_coord_median_tiled(fa_ctx *ctx, int dtype, int32_t num_segments, const int64_t *seg_numel, int32_t k,
+                          const void *const *d_in, int64_t tile_stride, void *const *d_out, void *hip_stream);
 
 /*
  * Pairwise squared Euclidean distances of k float32 client vectors (2 <= k <= 128), each given

@@ -73,3 +73,56 @@ def test_roofline_block_multi_gpu_is_whole_step():
     assert one["frac"] == round(6650.0 / bench.HBM_PEAK_GBS, 4) and "local_kernel" not in one
     if one["traffic"] is not None:
         assert "not measured in this run" in one["traffic_source"]
+
+
+def test_self_launch_at_one_rank():
+    """--self-launch forces the launcher chain at --gpus 1 (what the driver's scaling run executes)."""
+    r = _run(["--gpus", "1", "--self-launch", "--steps", "1", "--warmup", "0"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1 and lines[0]["n_gpus"] == 1
+
+
+def test_prelaunch_device_count_never_touches_hip(monkeypatch):
+    """The parent counts GPUs from sysfs / device nodes: with every HIP-backed count made to raise,
+    main() still reaches the launcher (stubbed) -- nothing initialises HIP before the ranks start."""
+    import torch
+    import bench
+
+    def boom(*a, **k):
+        raise AssertionError("HIP device count called in the launcher parent")
+    monkeypatch.setattr(torch.cuda, "device_count", boom)
+    monkeypatch.setattr(torch._C, "_cuda_getDeviceCount", boom, raising=False)
+    monkeypatch.setattr(torch.cuda, "is_available", boom)
+    monkeypatch.setattr(torch.cuda, "init", boom)
+    assert isinstance(bench.visible_gpu_count(), int)
+    calls = []
+    monkeypatch.setattr(bench, "visible_gpu_count", lambda: 8)
+    monkeypatch.setattr(bench, "launch_ranks", lambda n, argv, t, script=None: calls.append((n, list(argv))) or 0)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv("FEDML_AMD_BENCH_CPU_PROBE", raising=False)
+    monkeypatch.delenv("FEDML_AMD_BENCH_REHEARSAL", raising=False)
+    for argv in (["--gpus", "8"], ["--gpus", "1", "--self-launch", "--loopback"]):
+        monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
+        with pytest.raises(SystemExit) as e:
+            bench.main()
+        assert e.value.code == 0
+    assert calls == [(8, ["--gpus", "8"]), (1, ["--gpus", "1", "--self-launch", "--loopback"])]
+
+
+def test_prelaunch_refuses_more_ranks_than_gpus(monkeypatch):
+    import bench
+    monkeypatch.setattr(bench, "visible_gpu_count", lambda: 1)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv("FEDML_AMD_BENCH_CPU_PROBE", raising=False)
+    monkeypatch.delenv("FEDML_AMD_BENCH_REHEARSAL", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert "only 1" in str(e.value.code)
+
+
+def test_visible_gpu_count_honours_visible_devices(monkeypatch):
+    import bench
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    assert bench.visible_gpu_count() == 0

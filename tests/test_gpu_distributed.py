@@ -185,3 +185,86 @@ def test_native_comm_last_op_and_plan(pg):
     red.fedavg([torch.ones(5000, device="cuda")], [1.0])
     torch.cuda.synchronize()
     assert "ncclReduce" in red.native.comm.last_op()
+
+
+# ----------------------------------------------------------------------------- loopback: the ordered body on one GPU
+def _loop_inputs(dtype, K, P, seed):
+    g = torch.Generator().manual_seed(seed)
+    if dtype == torch.int64:
+        xs = [torch.randint(-2**62, 2**62, (P,), generator=g, dtype=torch.int64) for _ in range(K)]
+    else:
+        xs = [torch.randn(P, generator=g).to(dtype) for _ in range(K)]
+    counts = [int(v) for v in torch.randint(50, 601, (K,), generator=g)]
+    return xs, counts
+
+
+def _same_bits(got, exp):
+    ib = {4: torch.int32, 2: torch.int16, 8: torch.int64}[exp.element_size()]
+    return got.dtype == exp.dtype and torch.equal(got.cpu().view(ib), exp.view(ib))
+
+
+@pytest.mark.parametrize("collective", ["ordered", "ordered_all"])
+@pytest.mark.parametrize("layout", ["flat", "tiled", "grouped"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.int64])
+@pytest.mark.parametrize("chunks", [1, 4])
+def test_native_loopback_ordered_exchange(pg, collective, layout, dtype, chunks):
+    """FA_XCHG_LOOPBACK at world 1: the default N > 1 exchange body (comm.hip ordered(): grouped
+    ncclSend / ncclRecv on communicator 1, the after-exchange events, the owner's rank-ordered SUM,
+    the delivery on communicator 2's stream) runs through RCCL on one GPU, the own piece going
+    through a self send / receive.  Bit-exact vs the oracle; both communicators carried every chunk.
+    Reference: python/fedml/simulation/nccl/base_framework/common.py:196-228."""
+    from oracle import orc
+    from fedml_amd.arena import ArenaLayout, ClientArena
+    from fedml_amd.distributed.group_reduce import GroupReducer
+    from fedml_amd.engine import get_engine
+    if layout == "grouped" and dtype == torch.int64:
+        pytest.skip("the grouped (hierarchical) kernel takes float dtypes only (fa_weighted_sum_grouped)")
+    K, P = 6, 4096 * 9 + 77
+    xs, counts = _loop_inputs(dtype, K, P, seed=31 + chunks)
+    N = sum(counts)
+    w = [c / N for c in counts]
+    red = GroupReducer(collective=collective, chunks=chunks, native=True, loopback=True)
+    assert red.native is not None and red.native.loopback
+    before = red.native.comm.op_counts()
+    if layout == "flat":
+        if dtype == torch.int64:
+            got, exp = red.sum([x.cuda() for x in xs]), orc.weighted_sum(xs, 2)
+        else:
+            got, exp = red.fedavg([x.cuda() for x in xs], w), orc.weighted_sum(xs, 0, w)
+        align = 256
+    elif layout == "tiled":
+        arena = ClientArena(ArenaLayout([("w", (P,), dtype)]), K, device="cuda:0", tiled=True)
+        for i, x in enumerate(xs):
+            arena.write(i, {"w": x.cuda()})
+        got = red.fedavg_tiled(get_engine(0), arena.bufs[dtype], list(range(K)), w, P)
+        exp = orc.weighted_sum(xs, 0, w)
+        align = 4096 // xs[0].element_size()
+    else:
+        got = red.hierarchical([x.cuda() for x in xs], counts, 3 * N)
+        exp = orc.weighted_sum([orc.weighted_sum(xs, 0, w)], 1, [N], float(3 * N))
+        align = 256
+    torch.cuda.synchronize()
+    assert _same_bits(got[:P], exp)
+    after = red.native.comm.op_counts()
+    C = min(chunks, -(-P // align))
+    d = [a - b for a, b in zip(after, before)]
+    assert d == [C, C, C, C], f"sends/recvs on c1, c2: {d}"  # one self send + receive per chunk and phase
+    assert red.owned == [(0, P)] or sum(hi - lo for lo, hi in red.owned) == P
+    assert "delivery" in red.native.comm.last_op()
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_native_loopback_partial_and_repeat(pg, chunks):
+    """A caller's partial (FA_LOCAL_PARTIAL) through the loopback exchange, three calls in a row on
+    the same communicators (event pool reuse), the scratch reused across calls."""
+    from oracle import orc
+    from fedml_amd.distributed.native_exchange import NativeExchange
+    from fedml_amd.distributed.group_reduce import GroupReducer
+    red = GroupReducer(collective="ordered", chunks=chunks, native=True, loopback=True)
+    for it in range(3):
+        g = torch.Generator().manual_seed(100 + it)
+        x = torch.randn(50_000 + it * 1000, generator=g)
+        part = x.cuda()
+        got = red.native.run(NativeExchange.partial(part), part.numel(), 256)
+        torch.cuda.synchronize()
+        assert _same_bits(got, orc.weighted_sum([x], 2))

@@ -294,3 +294,31 @@ def test_arena_adopt_detaches_held_views():
     assert torch.equal(t_held, keep) and torch.equal(d0["w"], keep)
     assert d0["w"].data_ptr() != d1["w"].data_ptr()
     assert resident_rows([d1]) is not None and resident_rows([d0]) is None
+
+
+def test_to_host_result_kept_only_through_derived_views():
+    """a caller that keeps only a reshape / slice / transpose of a pinned host result (not
+    the returned tensor objects) still sees that round's values after rounds r+1 and r+2 -- the guard
+    counts references on the pinned storage, not the handed-out tensor objects."""
+    from oracle import orc
+    srv = _server(3)
+    g = torch.Generator().manual_seed(41)
+    kept = []
+    for rnd in range(4):
+        ds = [OrderedDict(a=torch.randn(64, 33, generator=g), n=torch.randint(0, 9, (2,), generator=g))
+              for _ in range(3)]
+        xs = {k: [d[k].clone() for d in ds] for k in ds[0]}
+        for i, d in enumerate(ds):
+            srv.add_local_trained_result(i, d, 10 * (i + 1))
+        assert srv.check_whether_all_receive()
+        srv.aggregate()
+        host = srv.get_global_model_params_host()
+        exp = {k: orc.weighted_sum(xs[k], MUL_W, [10 / 60, 20 / 60, 30 / 60]) for k in xs}
+        if rnd < 2:  # keep derived views only; the dict and its tensors are dropped
+            kept.append(((host["a"].reshape(-1)[7:], host["a"].T, host["n"][1:]), exp))
+        del host
+    torch.cuda.synchronize()
+    for r, ((flat, tr, n1), exp) in enumerate(kept):
+        assert _bits(flat, exp["a"].reshape(-1)[7:]), f"round {r}: reshape/slice view changed"
+        assert _bits(tr.contiguous(), exp["a"].T.contiguous()), f"round {r}: transposed view changed"
+        assert torch.equal(n1, exp["n"][1:]), f"round {r}: int64 slice changed"

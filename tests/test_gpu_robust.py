@@ -414,3 +414,103 @@ def test_pairwise_f64_models_vs_reference(eng, path):
     raw = list(zip(meta["n"], cl))
     sel = d.defend_before_aggregation(raw)
     assert [next(i for i, (_, c) in enumerate(raw) if c is sc) for _, sc in sel] == meta["selected"]
+
+
+# ----------------------------------------------------------------------------- median over the tiled arena
+def _tiled_rows(xs, dtype, cap_extra=2):
+    """The clients as rows of a tile-interleaved ClientArena group (fedml_amd/arena.py tiled=True),
+    with spare rows so the row pointers are not the first ``K`` of the capacity."""
+    from fedml_amd.arena import ArenaLayout, ClientArena
+    n = xs[0].numel()
+    arena = ClientArena(ArenaLayout([("w", (n,), dtype)]), len(xs) + cap_extra, device=DEV, tiled=True)
+    rows = list(range(cap_extra, cap_extra + len(xs)))
+    for r, x in zip(rows, xs):
+        arena.write(r, {"w": x.to(DEV)})
+    return arena, rows
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
+@pytest.mark.parametrize("k", [1, 2, 5, 8, 32, 33, 64, 65, 100, 128, 129])
+def test_median_tiled_vs_oracle(eng, dtype, k):
+    """fa_coord_median_tiled over tile-interleaved arena rows: every kernel form (one lane, two lanes,
+    packed 16-bit, rank counting for float64 and K > 128) addresses element e of a row at
+    (e / E) * tile_stride + (e % E) * size -- bit-exact to the oracle, NaN / +-0 / ties / +-inf included,
+    with lengths that end inside a tile and a workgroup."""
+    from oracle import orc
+    g = torch.Generator().manual_seed(500 + k)
+    n = 3 * 4096 // (8 if dtype == torch.float64 else 4) + 777 if k <= 128 else 2100
+    xs = _column_data(g, k, n, dtype, zeros=0.15)
+    arena, rows = _tiled_rows(xs, dtype)
+    got = eng.coord_median_tiled(arena.bufs[dtype], rows, n=n).cpu()
+    exp = orc.coord_median(xs)
+    iv = {8: torch.int64, 4: torch.int32, 2: torch.int16}[exp.element_size()]
+    assert torch.equal(got.view(iv), exp.view(iv))
+
+
+@pytest.mark.parametrize("layout", ["lanes1", "lanes2"])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("k", [7, 32, 64, 72, 100, 128])
+def test_median_tiled_special_values(eng, dtype, k, layout, monkeypatch):
+    """The tiled addressing on the float-key networks' hard cases (subnormals, NaN payloads, +-0,
+    +-inf, +-max) and through the rare-case rescan (which re-reads the column in the tiled layout)."""
+    from oracle import orc
+    monkeypatch.setenv("FA_MEDIAN_LANES", "2" if layout == "lanes2" else "1")
+    g = torch.Generator().manual_seed(2000 + k)
+    xs = _special_columns(g, k, 5000, dtype)
+    arena, rows = _tiled_rows(xs, dtype, cap_extra=1)
+    got = eng.coord_median_tiled(arena.bufs[dtype], rows, n=5000).cpu()
+    iv = torch.int32 if dtype == torch.float32 else torch.int16
+    assert torch.equal(got.view(iv), orc.coord_median(xs).view(iv))
+
+
+def test_median_tiled_equals_flat_large(eng):
+    """A model-sized case (K = 40, 3.1 M coordinates): tiled and flat inputs give the same bits."""
+    g = torch.Generator(device=DEV).manual_seed(3)
+    n = 3_100_003
+    xs = [torch.randn(n, generator=g, device=DEV) for _ in range(40)]
+    arena, rows = _tiled_rows(xs, torch.float32, cap_extra=0)
+    a = eng.coord_median_tiled(arena.bufs[torch.float32], rows, n=n)
+    b = eng.coord_median([xs])[0]
+    assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+
+
+@pytest.mark.parametrize("tiled", [False, True])
+def test_arena_median_per_key(eng, tiled):
+    """ClientArena.median: one launch per dtype group over the rows (tiled: fa_coord_median_tiled),
+    per-key views equal to the oracle's median of each key."""
+    from oracle import orc
+    from fedml_amd.arena import ArenaLayout, ClientArena
+    g = torch.Generator().manual_seed(12)
+    shapes = [("conv.weight", (16, 3, 3, 3)), ("conv.bias", (16,)), ("fc.weight", (10, 300)), ("fc.bias", (10,))]
+    K = 9
+    ds = [OrderedDict((k, _column_data(g, 1, int(np.prod(s)), torch.float32)[0].view(s)) for k, s in shapes)
+          for _ in range(K)]
+    arena = ClientArena(ArenaLayout([(k, s, torch.float32) for k, s in shapes]), K + 1, device=DEV, tiled=tiled)
+    for i, d in enumerate(ds):
+        arena.write(i + 1, OrderedDict((k, v.to(DEV)) for k, v in d.items()))
+    med = arena.median(list(range(1, K + 1)))
+    for k, _ in shapes:
+        exp = orc.coord_median([d[k].reshape(-1) for d in ds])
+        assert torch.equal(med[k].cpu().reshape(-1).view(torch.int32), exp.view(torch.int32)), k
+
+
+def test_median_defense_on_adopted_rows(eng):
+    """The defense on updates adopted into arena rows (what the round drivers hold) takes the
+    arena path and returns the same bits as on separate tensors."""
+    from fedml_amd.arena import ClientArena, resident_rows
+    from fedml_amd.core.security.defense.coordinate_wise_median_defense import CoordinateWiseMedianDefense
+    g = torch.Generator().manual_seed(13)
+    K = 11
+    mk = lambda: OrderedDict(w=torch.randn(40, 30, generator=g), b=torch.randn(30, generator=g))  # noqa: E731
+    ds = [mk() for _ in range(K)]
+    sep = [OrderedDict((k, v.to(DEV)) for k, v in d.items()) for d in ds]
+    adopted = [OrderedDict((k, v.to(DEV)) for k, v in d.items()) for d in ds]
+    arena = ClientArena.for_model(adopted[0], K, device=DEV)
+    for i, d in enumerate(adopted):
+        arena.adopt(i, d)
+    assert resident_rows(adopted) is not None
+    d = CoordinateWiseMedianDefense(types.SimpleNamespace())
+    a = d.defend_on_aggregation([(1.0, x) for x in adopted])
+    b = d.defend_on_aggregation([(1.0, x) for x in sep])
+    for k in a:
+        assert torch.equal(a[k].cpu().view(torch.int32), b[k].cpu().view(torch.int32)), k

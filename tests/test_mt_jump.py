@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_mt_jump_polynomials(tmp_path):
     exe = str(tmp_path / "mt_jump_check")
     subprocess.run(["g++", "-O2", "-std=c++17", "-I", os.path.join(ROOT, "fedml_amd", "csrc"),
-                    os.path.join(ROOT, "tools", "mt_jump_check.cpp"), "-o", exe], check=True)
+                    os.path.join(ROOT, "tools", "mt_jump_check.cpp"), "-o", exe, "-pthread"], check=True)
     out = subprocess.run([exe, "4"], check=True, capture_output=True, text=True, timeout=120).stdout
     res = json.loads(out.strip().splitlines()[-1])
     assert res["ok"] and res["phi_weight"] == 135  # MT19937's characteristic polynomial has 135 terms

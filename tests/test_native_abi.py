@@ -167,3 +167,19 @@ def test_match_rows_checks_dtype_and_shape():
     assert not _host.match_rows([{"w": buf[1, :12].view(3, 4).view(torch.int32), "b": buf[1, 12:16]}], ["w", "b"],
                                 base, stride, [1], meta, moff)
     assert not _host.match_rows([ok], ["w", "b"], base, stride, [0], meta, moff)
+
+
+def test_storage_held_counts_derived_views():
+    """ingest._storage_held: a buffer is held while ANY tensor on its storage lives outside it --
+    the handed-out view, or one derived from it after the original is gone."""
+    import torch
+    from fedml_amd.ml.aggregator.ingest import _storage_held
+    buf = torch.zeros(100)
+    assert not _storage_held([buf])
+    v = buf[10:20].view(2, 5)
+    assert _storage_held([buf])
+    d = v.reshape(-1)[3:].T if v.dim() == 1 else v.reshape(-1)[3:]
+    del v
+    assert _storage_held([buf])  # only the derived view remains
+    del d
+    assert not _storage_held([buf])

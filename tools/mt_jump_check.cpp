@@ -9,6 +9,8 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include <thread>
+
 #include "mt_poly.h"
 
 using namespace fa_mt;
@@ -79,6 +81,21 @@ int main(int argc, char** argv) {
       printf("FAIL: jump_polys(%llu)[%d] != x^(c J)\n", (unsigned long long)J, c);
       return 1;
     }
+  // 4. two threads (two contexts' calls) growing the cache for different J at once: each gets its own
+  //    copy, equal to the sequential powers (the copy is taken under the cache's lock)
+  {
+    const uint64_t Ja = 624 * 3, Jb = 624 * 11;
+    std::vector<Poly> ra, rb;
+    std::thread ta([&] { for (int c = 1; c <= 24; c += 3) ra = jump_polys(Ja, c); });
+    std::thread tb([&] { for (int c = 1; c <= 24; c += 3) rb = jump_polys(Jb, c); });
+    ta.join();
+    tb.join();
+    for (int c = 1; c <= 22; ++c)
+      if (ra[(size_t)c - 1] != xpow((uint64_t)c * Ja) || rb[(size_t)c - 1] != xpow((uint64_t)c * Jb)) {
+        printf("FAIL: concurrent jump_polys differ at c = %d\n", c);
+        return 1;
+      }
+  }
   auto t2 = std::chrono::steady_clock::now();
   const int n = argc > 1 ? atoi(argv[1]) : 0;  // optional: time n polynomials of the device chunk size
   double tp = 0;
