@@ -20,3 +20,13 @@ cat gpurun_out/r04a/selflaunch_loopback_hier.json
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > gpurun_out/r04a/bench_default.json 2> gpurun_out/r04a/bench_default.err \
   || { echo "bench FAIL"; tail -20 gpurun_out/r04a/bench_default.err; exit 1; }
 cat gpurun_out/r04a/bench_default.json
+for rep in 1 2; do
+  for lay in tiled arena; do
+    for K in 32 128; do
+      timeout -k 10 300 python bench.py --config median --clients $K --layout $lay --steps 20 --warmup 3 --no-cpu-baseline \
+        > gpurun_out/r04a/median_${lay}_K${K}_r${rep}.json 2> gpurun_out/r04a/median_${lay}_K${K}_r${rep}.err \
+        || { echo "median FAIL"; tail -20 gpurun_out/r04a/median_${lay}_K${K}_r${rep}.err; exit 1; }
+      python -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);r=d['roofline'];print(sys.argv[1],d['value'],r['kernel_avg_ms'],r['frac'],d['parity'])" gpurun_out/r04a/median_${lay}_K${K}_r${rep}.json
+    done
+  done
+done
