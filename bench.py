@@ -119,29 +119,28 @@ def _free_port():
 def visible_gpu_count():
     """GPUs this process may use, counted WITHOUT initialising HIP -- the launcher parent must not touch
     the GPU before its ranks start (torch.cuda.device_count() may fall back to hipGetDeviceCount when
-    amdsmi discovery fails).  KFD topology nodes with SIMDs whose render node this process can open,
-    capped by ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set; without a
-    KFD topology, the render nodes this process can open."""
+    amdsmi discovery fails).  KFD topology nodes with SIMDs whose render node this process can open;
+    if none can be read, the render nodes this process can open; capped by ROCR_VISIBLE_DEVICES /
+    HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set.  0 = could not tell."""
     import glob
     n = 0
-    nodes = glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties")
-    for prop in nodes:
+    for prop in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
         try:
             with open(prop) as f:
                 kv = dict(line.split()[:2] for line in f if len(line.split()) >= 2)
         except OSError:
-            continue
+            continue  # a node this container may not see
         if int(kv.get("simd_count", "0")) <= 0:
             continue  # a CPU node
         minor = kv.get("drm_render_minor")
         dev = f"/dev/dri/renderD{minor}" if minor is not None else None
-        if dev is None or os.access(dev, os.R_OK | os.W_OK):
+        if dev is None or not os.path.exists(dev) or os.access(dev, os.R_OK | os.W_OK):
             n += 1
-    if not nodes:
+    if n == 0:
         n = sum(1 for d in glob.glob("/dev/dri/renderD*") if os.access(d, os.R_OK | os.W_OK))
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         v = os.environ.get(var)
-        if v is not None:
+        if v is not None and n > 0:
             n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
     return n
 
@@ -1772,7 +1771,7 @@ def main():
         # no outer launcher: start the N ranks as child processes before anything touches the GPU
         if os.environ.get("FEDML_AMD_BENCH_REHEARSAL") != "1" and not os.environ.get("FEDML_AMD_BENCH_CPU_PROBE"):
             have = visible_gpu_count()  # sysfs / device nodes only: no HIP call in the parent
-            if have < args.gpus:
+            if 0 < have < args.gpus:  # 0: could not tell -- the ranks then report for themselves
                 raise SystemExit(f"--gpus {args.gpus}: only {have} HIP device(s) visible "
                                  "(FEDML_AMD_BENCH_REHEARSAL=1 rehearses the N-rank path on one device over gloo)")
         sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout))

@@ -6,6 +6,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <vector>
 
 #include "fedagg.h"
 
@@ -87,6 +88,8 @@ struct fa_ctx {
     hipEvent_t ev = nullptr;
     hipEvent_t staged = nullptr;  // the table copy on the side stream has landed (stage())
     bool pending = false;
+    std::vector<char> shadow;     // the bytes `dev` holds, for stage(..., reuse) (valid if shadow_ok)
+    bool shadow_ok = false;
   } slots[fa_detail::kSlots];
   int next = 0;
   // fa_weighted_sum_host: one mapped pinned buffer the kernel reads and writes in place over PCIe
@@ -113,7 +116,10 @@ namespace fa_detail {
 // still in flight (kSlots calls ago).
 int acquire_slot(fa_ctx* ctx, size_t bytes, fa_ctx::Slot** out);
 // Copy the slot's first `bytes` host bytes to its device buffer (async on `st`).
-int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st);
+// reuse: the caller's kernels only READ the table; if the slot's device buffer already holds exactly
+// these bytes (the same table staged through this slot before), the copy -- and the caller stream's
+// wait for it -- is skipped.
+int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st, bool reuse = false);
 // Mark the slot busy until the work queued on `st` so far has finished.
 int release(fa_ctx::Slot* s, hipStream_t st);
 

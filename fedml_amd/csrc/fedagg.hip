@@ -1010,6 +1010,7 @@ int acquire_slot(fa_ctx* ctx, size_t bytes, fa_ctx::Slot** out) {
     if (s.dev) FA_HIP(hipFree(s.dev));
     s.host = s.dev = nullptr;
     s.cap = 0;
+    s.shadow_ok = false;
     // mapped: the staging copy is a kernel on the caller's stream reading it over PCIe (stage())
     if (hipHostMalloc(&s.host, cap, hipHostMallocMapped) != hipSuccess)
       return fail(FA_ERR_NOMEM, "hipHostMalloc(%zu) failed", cap);
@@ -1061,7 +1062,28 @@ hipStream_t side_stream() {
 }
 }  // namespace
 
-int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st) {
+// r04: a state_dict round over the SAME client tensors as the slot's last use (the bench's steps, and
+// rounds whose updates the caching allocator places at the same addresses) stages a byte-identical
+// table; its copy and the cross-queue wait behind it cost ~14 us of GPU idle per call at cfg2's 3,904
+// pointers (profiles/r04b: 19.8 us between k_wsum_pair kernels vs ~6 us without a staged table).
+// FA_STAGE_REUSE=0: always copy (A/B).
+namespace {
+bool stage_reuse_enabled() {
+  const char* e = getenv("FA_STAGE_REUSE");
+  return !(e && e[0] == '0');
+}
+}  // namespace
+
+int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st, bool reuse) {
+  reuse = reuse && stage_reuse_enabled();
+  if (reuse && s->shadow_ok && s->shadow.size() == bytes && memcmp(s->host, s->shadow.data(), bytes) == 0)
+    return FA_OK;  // acquire_slot waited for the slot's last reader, which waited for that copy
+  if (reuse) {
+    s->shadow.assign((const char*)s->host, (const char*)s->host + bytes);
+    s->shadow_ok = true;
+  } else {
+    s->shadow_ok = false;
+  }
   if (s->hmap && bytes <= (256u << 10) && stage_kernel_enabled()) {
     const int n16 = (int)((bytes + 15) / 16);  // slots are >= 16 KB and 16-byte multiples
     const int blocks = std::max(1, std::min(64, (n16 + kBlock - 1) / kBlock));
@@ -1292,7 +1314,7 @@ int wsum_impl(fa_ctx* ctx, int dtype, int mode, int32_t num_segments, const int6
     FA_HIP(hipGetLastError());
     return FA_OK;
   }
-  rc = stage(slot, bytes, st);
+  rc = stage(slot, bytes, st, true);
   if (rc) return rc;
   char* d = (char*)slot->dev;
   const Seg* ds = (const Seg*)d;
@@ -1710,7 +1732,7 @@ int pair_impl(fa_ctx* ctx, int dtype, int mode, int32_t nseg0, const int64_t* nu
   }
   const char* dev = nullptr;
   if (!inl) {
-    rc = stage(slot, L.bytes, st);
+    rc = stage(slot, L.bytes, st, true);
     if (rc) return rc;
     dev = (const char*)slot->dev;
   }

@@ -122,7 +122,36 @@ def test_prelaunch_refuses_more_ranks_than_gpus(monkeypatch):
     assert "only 1" in str(e.value.code)
 
 
-def test_visible_gpu_count_honours_visible_devices(monkeypatch):
+def test_visible_gpu_count_honours_visible_devices(monkeypatch, tmp_path):
+    import glob as _glob
     import bench
-    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
-    assert bench.visible_gpu_count() == 0
+    # a fake KFD topology: a CPU node, two GPU nodes (render nodes absent here: counted)
+    root = tmp_path / "nodes"
+    for i, simd in enumerate([0, 1024, 1024]):
+        d = root / str(i)
+        d.mkdir(parents=True)
+        (d / "properties").write_text(f"simd_count {simd}\ndrm_render_minor {128 + i}\n")
+    real = _glob.glob
+    monkeypatch.setattr(_glob, "glob", lambda pat: real(str(root / "*" / "properties"))
+                        if pat.startswith("/sys/class/kfd") else [])
+    monkeypatch.delenv("ROCR_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("CUDA_VISIBLE_DEVICES", raising=False)
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES", raising=False)
+    assert bench.visible_gpu_count() == 2
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
+    assert bench.visible_gpu_count() == 1
+
+
+def test_unknown_gpu_count_does_not_refuse(monkeypatch):
+    """0 = the parent could not tell (no readable topology): it launches and lets the ranks report."""
+    import bench
+    monkeypatch.setattr(bench, "visible_gpu_count", lambda: 0)
+    calls = []
+    monkeypatch.setattr(bench, "launch_ranks", lambda n, argv, t, script=None: calls.append(n) or 0)
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv("FEDML_AMD_BENCH_CPU_PROBE", raising=False)
+    monkeypatch.delenv("FEDML_AMD_BENCH_REHEARSAL", raising=False)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "8"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert e.value.code == 0 and calls == [8]

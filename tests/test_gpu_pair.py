@@ -178,3 +178,42 @@ def test_state_dict_pair_multi_vs_oracle(fdt, mode, k):
         exp = orc.weighted_sum([d[name].cpu() for d in dicts], mode, coef, div)
         assert got[name].shape == torch.Size(shape) and got[name].dtype == exp.dtype, name
         assert bits_equal(got[name].cpu(), exp), name
+
+
+def test_staged_table_reuse_across_calls(monkeypatch):
+    """r04: a read-only descriptor table identical to the one a staging slot already holds is not
+    copied again (fa_detail::stage reuse).  Interleave rounds over two sets of separate-tensor dicts
+    (same table -> reuse; other table -> copy), in-place updates of the same tensors between calls
+    (same pointers, new data), and a PushSum mix (its kernel writes its staged table: no reuse after
+    it) -- every result bit-exact to the oracle, with reuse on and off."""
+    from collections import OrderedDict as OD
+    from oracle import orc
+    from fedml_amd.engine import get_engine
+    from fedml_amd.ml.aggregator.state_dict_agg import MUL_W, aggregate
+    eng = get_engine(0)
+    g = torch.Generator().manual_seed(77)
+    shapes = [("a", (300, 7)), ("b", (64,)), ("c", (5, 5, 3)), ("n", (1,))]
+    K = 9
+
+    def mk():
+        return [OD((k, (torch.randint(0, 50, s, generator=g) if k == "n" else torch.randn(s, generator=g)).cuda())
+                   for k, s in shapes) for _ in range(K)]
+    for reuse in ("1", "0"):
+        monkeypatch.setenv("FA_STAGE_REUSE", reuse)
+        A, B = mk(), mk()
+        w = [1.0 / K] * K
+        for it in range(12):
+            ds = A if it % 3 else B
+            if it == 5:
+                for d in A:  # same pointers, new values
+                    d["a"].add_(1.0)
+            if it == 7:
+                xs = [torch.randn(4099, generator=g).cuda() for _ in range(3)]
+                eng.pushsum(xs, [0, 2, 4, 6], [0, 1, 1, 2, 0, 2], [0.5] * 6, torch.ones(3, device="cuda"))
+            out = aggregate(ds, MUL_W, w)
+            torch.cuda.synchronize()
+            for k, _ in shapes:
+                exp = orc.weighted_sum([d[k].cpu().reshape(-1) for d in ds], MUL_W, w)
+                got = out[k].cpu().reshape(-1)
+                ib = {4: torch.int32, 8: torch.int64}[got.element_size()]
+                assert torch.equal(got.view(ib), exp.view(ib)), (reuse, it, k)
