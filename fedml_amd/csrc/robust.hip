@@ -1146,269 +1146,6 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
                 partial + (int64_t)blockIdx.x * ((int64_t)k * (k - 1) / 2));
 }
 
-// ---------------------------------------------------------------------------------------------
-// r04: octet x quad register tiles (k_pairdist_oq).  The 4x4 tiles above do 16 packed sub+fma per two
-// 16-byte LDS reads, and a 16-wave workgroup per CU syncs 16 waves per chunk (r03 PMC at K = 128: VALU
-// busy 67 % of cycles, 74 % of its instructions the useful sub / fma; SQ_WAIT_ANY 0.47).  Here a thread
-// owns an 8 x 4 tile: the 8 clients of octet p (two 16-byte reads) against the 4 of quad q (one read)
-// -- 32 pairs, 16 packed sub + 16 packed fma per coordinate, 3 reads instead of 4 for the same pairs.
-// Tiles: for octet p, quad 2p+1 (its own upper half: the 16 pairs p0 x p1 and the 6 inside p1) and
-// every quad of the octets above it (32 pairs each) -- no^2 tiles for no = ceil(K / 8) octets (K = 128:
-// 256 = one 4-wave workgroup, every lane busy); the 6 pairs inside each octet's lower quad p0 are a
-// small second phase over all threads (Within, as the 4x4 kernel's).  Padding clients (k..kp8-1) are
-// staged as zeros and their pairs dropped.
-// LDS: [chunk coordinate e][client], S floats a row (S = 32 * ceil(kp8 / 32): a row holds whole
-// multiples of 8 quads), quad Q of row e stored at quad Q ^ h(e), h(e) = (e / 4) % 8 -- the staging
-// stores (32 lanes = 4 clients x 8 four-coordinate groups) then hit 32 distinct banks, and the pair
-// loop's reads of one row by lanes with distinct quads stay on distinct 16-byte bank slots.  Lanes are
-// renumbered so that each ds_read_b128 lane group of 16 (MI355X_MICROARCH.md §LDS) holds 16 consecutive
-// tiles of ONE coordinate slice (one row), and the host orders the tiles so that a group's b-quads are
-// distinct mod 16 where it can (tools: bank model in DESIGN.md §4).
-// Staging: lane-load j of a chunk = client 4 * (j / (4G)) + j % 4, coordinates 4 * ((j % 4G) / 4) .. + 3
-// (G = C / 4 groups a row): a wave's 64 loads cover 4 clients x 256 contiguous bytes.
-// Sums as before: float32 runs of <= kPE coordinates (packed pairs), float64 across runs; the
-// slices of a tile and the within-octet threads are added in a fixed order (deterministic).
-__constant__ unsigned char kB128LaneRank[64] = {
-    0, 1, 2, 3, 16, 17, 18, 19, 20, 21, 22, 23, 4, 5, 6, 7, 24, 25, 26, 27, 8, 9, 10, 11,
-    12, 13, 14, 15, 28, 29, 30, 31, 32, 33, 34, 35, 48, 49, 50, 51, 52, 53, 54, 55, 36, 37, 38, 39,
-    56, 57, 58, 59, 40, 41, 42, 43, 44, 45, 46, 47, 60, 61, 62, 63};
-
-template <int S>
-__device__ __forceinline__ int oq_col(int quad, int e) { return 4 * (quad ^ ((e >> 2) & 7)); }
-
-// One coordinate of an octet x quad tile: a = the octet's 8 clients, b = the quad's 4.
-template <int RT>
-__device__ __forceinline__ void oq_tile(const float4 a0, const float4 a1, const float4 b, f32x2 (&acc)[16]) {
-  const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-  const f32x2 b01 = {b.x, b.y}, b23 = {b.z, b.w};
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const f32x2 au = {av[u], av[u]};
-    const f32x2 d0 = round_diff<RT>(au - b01), d1 = round_diff<RT>(au - b23);
-    acc[2 * u] = __builtin_elementwise_fma(d0, d0, acc[2 * u]);
-    acc[2 * u + 1] = __builtin_elementwise_fma(d1, d1, acc[2 * u + 1]);
-  }
-}
-
-// The within-quad pairs of every octet's lower quad p0 (quad 2 * db): thread t, octet db = t % no,
-// coordinates e = de0, de0 + dg, ... of the chunk (dg = threads per octet) -- Within's arithmetic on the
-// swizzled rows.
-template <int S, int RT>
-__device__ __forceinline__ void oq_inner(Within<RT>& wb, const float* lb, int pe, int e0, int dg, int db) {
-  for (int e = e0; e < pe; e += dg) {
-    const float4 v = *(const float4*)&lb[e * S + oq_col<S>(2 * db, e)];
-    const f32x2 x = round_diff<RT>(f32x2{v.x, v.x} - f32x2{v.y, v.z});  // (0,1) (0,2)
-    const f32x2 y = round_diff<RT>(f32x2{v.x, v.y} - f32x2{v.w, v.z});  // (0,3) (1,2)
-    const f32x2 z = round_diff<RT>(f32x2{v.y, v.z} - f32x2{v.w, v.w});  // (1,3) (2,3)
-    wb.acc[0] = __builtin_elementwise_fma(x, x, wb.acc[0]);
-    wb.acc[1] = __builtin_elementwise_fma(y, y, wb.acc[1]);
-    wb.acc[2] = __builtin_elementwise_fma(z, z, wb.acc[2]);
-  }
-}
-
-template <int S, int RT, bool VEC, int NL, bool PF>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
-k_pairdist_oq(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int kp8,
-              int64_t nchunks, int ntiles, int es, int ce, const unsigned short* __restrict__ tile_pq,
-              double* __restrict__ partial) {
-  extern __shared__ float lds[];                 // [2][pe][S], then (epilogue) the reductions
-  const int pe = ce * es;                        // coordinates a chunk
-  const int no = kp8 / 8;
-  const int t = threadIdx.x;
-  const int tv = (t & ~63) | kB128LaneRank[t & 63];  // b128 lane groups hold consecutive tiles
-  const bool pact = tv < ntiles * es;
-  const int tile = pact ? tv % ntiles : 0, es_me = pact ? tv / ntiles : 0;
-  const unsigned pq = tile_pq[tile];
-  const int p = (int)(pq & 0xFF), q = (int)(pq >> 8);
-  const int nth = (int)blockDim.x;
-  const int dg = nth / no;                       // within-quad phase: threads per octet
-  const bool dact = t < dg * no;
-  const int db = t % no, de0 = t / no;
-  Within<RT> wb;
-  wb.init();
-  double accd[32];
-  f32x2 acc[16];
-  int run = 0;
-#pragma unroll
-  for (int u = 0; u < 32; ++u) accd[u] = 0.0;
-#pragma unroll
-  for (int u = 0; u < 16; ++u) acc[u] = f32x2{0.0f, 0.0f};
-  auto flush = [&]() {
-#pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      accd[2 * u] += (double)acc[u].x;
-      accd[2 * u + 1] += (double)acc[u].y;
-      acc[u] = f32x2{0.0f, 0.0f};
-    }
-    run = 0;
-  };
-  // staging: NL lane-loads per thread and chunk, j = t + m * nth
-  const int G = pe / 4, L = kp8 * G;
-  float4 v[NL];
-  int cseg = -1;
-  int64_t snum = 0, sbase = 0;
-  auto load = [&](int64_t ch) {
-    const int si = nseg > 1 ? find_seg(segs, nseg, ch) : 0;
-    const PSeg sg = segs[si];
-    if (si != cseg) {
-      cseg = si;
-      snum = sg.numel;
-      sbase = sg.ptr_base;
-    }
-    const int64_t b0 = (ch - sg.tile_start) * pe;
-#pragma unroll
-    for (int m = 0; m < NL; ++m) {
-      const int j = t + m * nth;
-      const int r = j % (4 * G);
-      const int c = 4 * (j / (4 * G)) + (r & 3), g = r >> 2;
-      const int64_t e = b0 + 4 * g;
-      float4 x = {0.0f, 0.0f, 0.0f, 0.0f};
-      if (j < L && c < k) {
-        const float* src = (const float*)ptrs[sbase + c];
-        if (VEC && e + 4 <= snum) {
-          typedef float f32x4v __attribute__((ext_vector_type(4)));
-          const f32x4v y = __builtin_nontemporal_load((const __attribute__((address_space(1))) f32x4v*)(src + e));
-          x = float4{y.x, y.y, y.z, y.w};
-        } else {
-          x.x = e < snum ? gld<float>(src, e) : 0.0f;
-          x.y = e + 1 < snum ? gld<float>(src, e + 1) : 0.0f;
-          x.z = e + 2 < snum ? gld<float>(src, e + 2) : 0.0f;
-          x.w = e + 3 < snum ? gld<float>(src, e + 3) : 0.0f;
-        }
-      }
-      v[m] = x;
-    }
-  };
-  const int bufsz = pe * S;
-  auto put = [&](int buf) {
-    float* l = lds + buf * bufsz;
-#pragma unroll
-    for (int m = 0; m < NL; ++m) {
-      const int j = t + m * nth;
-      if (j < L) {
-        const int r = j % (4 * G);
-        const int c = 4 * (j / (4 * G)) + (r & 3), g = r >> 2;
-        const int e = 4 * g;  // h(e .. e + 3) = g % 8
-        const int cc = oq_col<S>(c >> 2, e) + (c & 3);
-        l[(e + 0) * S + cc] = v[m].x;
-        l[(e + 1) * S + cc] = v[m].y;
-        l[(e + 2) * S + cc] = v[m].z;
-        l[(e + 3) * S + cc] = v[m].w;
-      }
-    }
-  };
-  const int64_t c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
-  if (c0 < c1) {
-    load(c0);
-    put(0);
-    if (c0 + 1 < c1) load(c0 + 1);
-  }
-  __syncthreads();
-  int cur = 0;
-  const int ebeg = es_me * ce;
-  for (int64_t ch = c0; ch < c1; ++ch, cur ^= 1) {
-    const float* lb = lds + cur * bufsz;
-    if (pact && !PF) {
-      for (int e4 = ebeg; e4 < ebeg + ce; e4 += 4) {  // 4 rows share the swizzle
-        const float* r0 = lb + e4 * S;
-        const int ca0 = oq_col<S>(2 * p, e4), ca1 = oq_col<S>(2 * p + 1, e4), cb = oq_col<S>(q, e4);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float4 a0 = *(const float4*)(r0 + i * S + ca0);
-          const float4 a1 = *(const float4*)(r0 + i * S + ca1);
-          const float4 b = *(const float4*)(r0 + i * S + cb);
-          oq_tile<RT>(a0, a1, b, acc);
-        }
-      }
-    } else if (pact) {
-      // PF: the next row's three 16-byte reads are issued before this row's 32 packed sub + fma (a
-      // scheduling barrier keeps the compiler from sinking them back to their use), so at two waves
-      // per SIMD the LDS latency hides behind the arithmetic
-      const float* r0 = lb + ebeg * S;
-      int ca0 = oq_col<S>(2 * p, ebeg), ca1 = oq_col<S>(2 * p + 1, ebeg), cb = oq_col<S>(q, ebeg);
-      float4 a0 = *(const float4*)(r0 + ca0), a1 = *(const float4*)(r0 + ca1), b = *(const float4*)(r0 + cb);
-      for (int e4 = ebeg; e4 < ebeg + ce; e4 += 4) {
-        const bool more = e4 + 4 < ebeg + ce;
-        const int na0 = oq_col<S>(2 * p, e4 + 4), na1 = oq_col<S>(2 * p + 1, e4 + 4), nb = oq_col<S>(q, e4 + 4);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float4 x0, x1, y;
-          if (i < 3) {
-            const float* rn = r0 + (i + 1) * S;
-            x0 = *(const float4*)(rn + ca0);
-            x1 = *(const float4*)(rn + ca1);
-            y = *(const float4*)(rn + cb);
-          } else {
-            const float* rn = r0 + (more ? 4 * S : 0);
-            x0 = *(const float4*)(rn + (more ? na0 : ca0));
-            x1 = *(const float4*)(rn + (more ? na1 : ca1));
-            y = *(const float4*)(rn + (more ? nb : cb));
-          }
-          __builtin_amdgcn_sched_barrier(0);
-          oq_tile<RT>(a0, a1, b, acc);
-          a0 = x0;
-          a1 = x1;
-          b = y;
-        }
-        r0 += 4 * S;
-        ca0 = na0;
-        ca1 = na1;
-        cb = nb;
-      }
-    }
-    run += ce;
-    if (run + ce > kPE) flush();  // float runs of <= kPE coordinates, then float64
-    if (dact) oq_inner<S, RT>(wb, lb, pe, de0, dg, db);
-    wb.step((pe + dg - 1) / dg);
-    if (ch + 1 < c1) {
-      put(cur ^ 1);  // buffer cur ^ 1 was last read before the previous barrier
-      if (ch + 2 < c1) load(ch + 2);
-    }
-    __syncthreads();
-  }
-  flush();
-  wb.flush();
-  // epilogue: the tiles' slices added in slice order (es > 1), useful slots to this block's partials;
-  // then the within-quad pairs, the dg threads of an octet in thread order
-  double* out = partial + (int64_t)blockIdx.x * ((int64_t)k * (k - 1) / 2);
-  double* red = (double*)lds;
-  auto emit = [&](int tl, int u, int vv, double val) {
-    const unsigned pq2 = tile_pq[tl];
-    const int pp = (int)(pq2 & 0xFF), qq = (int)(pq2 >> 8);
-    const int a = 8 * pp + u, b = 4 * qq + vv;
-    if (a < b && b < k) out[pair_index(a, b, k)] = val;
-  };
-  if (es == 1) {
-    if (pact) {
-#pragma unroll
-      for (int u = 0; u < 32; ++u) emit(tile, u / 4, u % 4, accd[u]);
-    }
-  } else {
-    __syncthreads();
-    for (int s2 = 0; s2 < es; ++s2) {
-      if (pact && es_me == s2) {
-#pragma unroll
-        for (int u = 0; u < 32; ++u) red[tile * 32 + u] = (s2 == 0 ? 0.0 : red[tile * 32 + u]) + accd[u];
-      }
-      __syncthreads();
-    }
-    for (int idx = t; idx < ntiles * 32; idx += nth) emit(idx / 32, (idx % 32) / 4, idx % 4, red[idx]);
-  }
-  __syncthreads();  // LDS reused for the within-quad sums
-  if (dact) {
-#pragma unroll
-    for (int u = 0; u < 6; ++u) red[t * 6 + u] = wb.accd[u];
-  }
-  __syncthreads();
-  for (int idx = t; idx < no * 6; idx += nth) {
-    const int b = idx / 6, u = idx % 6;
-    double sum = 0.0;
-    for (int g = 0; g < dg; ++g) sum += red[(g * no + b) * 6 + u];
-    const int i = 8 * b + (u < 3 ? 0 : u < 5 ? 1 : 2), j = 8 * b + (u < 3 ? u + 1 : u < 5 ? u - 1 : 3);
-    if (j < k) out[pair_index(i, j, k)] = sum;
-  }
-}
-
 // float64 models (krum_defense.py:50-66 over vectorize_weight's float64 vector, common/utils.py:8-30):
 // every difference and square in float64, as the reference computes them (no float32 step).  A rare
 // path, written for clarity: a workgroup stages kC64 coordinates of all k clients in LDS ([e][client]
@@ -1495,85 +1232,6 @@ k_pairdist_reduce(const double* __restrict__ partial, int nblocks, int k, double
     for (int i = threadIdx.x; i < k; i += kBlock) d[(int64_t)i * k + i] = 0.0;
 }
 
-
-// k_pairdist_oq's work split (see the kernel): tiles, slices, chunk rows, staging loads per thread.
-struct OqSplit { int kp8, no, ntiles, es, nth, ce, pe, S, nl; size_t lds; };
-OqSplit oq_split(int k) {
-  OqSplit o;
-  o.kp8 = (k + 7) & ~7;
-  o.no = o.kp8 / 8;
-  o.ntiles = o.no * o.no;
-  o.S = 32 * ((o.kp8 + 31) / 32);
-  auto waves = [](int th) { return (th + 63) / 64 * 64; };
-  // slices: the most whose waves stay >= 90 % busy within 256 threads (512 when 256 cannot reach it)
-  o.es = 1;
-  for (int e = 1; waves(e * o.ntiles) <= 256; ++e)
-    if ((double)(e * o.ntiles) / waves(e * o.ntiles) >= 0.9) o.es = e;
-  if ((double)(o.es * o.ntiles) / waves(o.es * o.ntiles) < 0.9)
-    for (int e = 1; waves(e * o.ntiles) <= 512; ++e)
-      if ((double)(e * o.ntiles) / waves(e * o.ntiles) >= 0.9) o.es = e;
-  for (;;) {
-    o.nth = waves(o.ntiles * o.es);
-    // at most 4 staging loads (16 B) per thread and chunk, rows in multiples of 4 (one swizzle)
-    const int pe_max = 16 * o.nth / o.kp8;
-    o.ce = std::min(kPE / 2, (pe_max / o.es) & ~3);
-    if (o.ce >= 4 || o.es == 1) break;
-    o.es = std::max(1, o.es / 2);
-  }
-  o.ce = std::max(o.ce, 4);
-  // LDS: two chunk buffers within ~52 KB for 256-thread groups (three per CU at <= 168 VGPRs)
-  const size_t cap = o.nth <= 256 ? 52 * 1024 : 150 * 1024;
-  while (o.ce > 4 && 2 * sizeof(float) * (size_t)o.ce * o.es * o.S > cap) o.ce -= 4;
-  o.pe = o.ce * o.es;
-  o.nl = (o.kp8 * (o.pe / 4) + o.nth - 1) / o.nth;
-  size_t lds = 2 * sizeof(float) * (size_t)o.pe * o.S;
-  if (o.es > 1) lds = std::max(lds, sizeof(double) * 32 * (size_t)o.ntiles);
-  o.lds = std::max(lds, sizeof(double) * 6 * (size_t)o.nth);
-  return o;
-}
-
-// The tile list, ordered so that each 16-tile group (one ds_read_b128 lane group) reads distinct quads
-// mod 16 -- 16-byte bank slots -- where a greedy pass finds them (K = 128: b reads 1.5 -> 1.3 cycles of
-// the conflict-free 1 in the bank model).  Entry = p | q << 8.
-void oq_tiles(int no, std::vector<unsigned short>& out) {
-  std::vector<std::pair<int, int>> all;
-  for (int p = 0; p < no; ++p) {
-    all.push_back({p, 2 * p + 1});
-    for (int q = 2 * p + 2; q < 2 * no; ++q) all.push_back({p, q});
-  }
-  std::vector<char> used(all.size(), 0);
-  out.clear();
-  size_t left = all.size();
-  while (left) {
-    unsigned qmask = 0;
-    std::vector<size_t> grp;
-    for (size_t i = 0; i < all.size() && grp.size() < 16; ++i) {
-      if (used[i] || (qmask >> (all[i].second % 16) & 1u)) continue;
-      grp.push_back(i);
-      qmask |= 1u << (all[i].second % 16);
-    }
-    for (size_t i = 0; i < all.size() && grp.size() < 16; ++i)
-      if (!used[i] && std::find(grp.begin(), grp.end(), i) == grp.end()) grp.push_back(i);
-    for (size_t i : grp) {
-      used[i] = 1;
-      out.push_back((unsigned short)(all[i].first | (all[i].second << 8)));
-      --left;
-    }
-  }
-}
-
-// FA_PAIR_OQ_PF=0/1: k_pairdist_oq without / with the explicit next-row LDS prefetch (A/B); default on
-bool oq_pf() {
-  const char* e = getenv("FA_PAIR_OQ_PF");
-  return !(e && e[0] == '0');
-}
-
-// FA_PAIR_OQ=0: the 4x4-tile kernels (A/B measurement); read at every call
-bool oq_enabled() {
-  const char* e = getenv("FA_PAIR_OQ");
-  return !(e && e[0] == '0');
-}
-
 }  // namespace
 
 extern "C" {
@@ -1598,9 +1256,7 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
   if (k < 2 || k > kMaxPairK || num_segments <= 0 || !seg_numel || !d_in || !d_dist)
     return fail(FA_ERR_INVALID, "fa_pairwise_sqdist: invalid arguments (2 <= k <= %d)", kMaxPairK);
   const PairSplit q = pair_split(k);
-  const bool oq = !f64 && oq_enabled();
-  const OqSplit o = oq_split(k);
-  const int kp = q.kp, ntiles = q.ntiles, esplit = q.esplit, pe = oq ? o.pe : q.pe;
+  const int kp = q.kp, ntiles = q.ntiles, esplit = q.esplit, pe = q.pe;
   if (q.nthreads > kMaxPairThreads) return fail(FA_ERR_INVALID, "fa_pairwise_sqdist: k too large");
   int nseg = 0;
   int64_t nchunks = 0, nchunks64 = 0;
@@ -1629,16 +1285,12 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
   }
   const size_t seg_bytes = align16(sizeof(PSeg) * nseg);
   const size_t ptr_bytes = sizeof(void*) * (size_t)nseg * k;
-  std::vector<unsigned short> tl;
-  if (oq) oq_tiles(o.no, tl);
-  const size_t tile_bytes = align16(sizeof(unsigned short) * tl.size());
   fa_ctx::Slot* slot = nullptr;
-  int rc = acquire_slot(ctx, seg_bytes + align16(ptr_bytes) + tile_bytes, &slot);
+  int rc = acquire_slot(ctx, seg_bytes + ptr_bytes, &slot);
   if (rc) return rc;
   char* h = (char*)slot->host;
   PSeg* hs = (PSeg*)h;
   const void** hp = (const void**)(h + seg_bytes);
-  if (oq) memcpy(h + seg_bytes + align16(ptr_bytes), tl.data(), sizeof(unsigned short) * tl.size());
   int j = 0;
   int64_t c0 = 0;
   const int64_t cpe = f64 ? kC64 : pe;  // coordinates per chunk
@@ -1650,7 +1302,7 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
     c0 += (n + cpe - 1) / cpe;
     ++j;
   }
-  rc = stage(slot, seg_bytes + align16(ptr_bytes) + tile_bytes, st);
+  rc = stage(slot, seg_bytes + ptr_bytes, st);
   if (rc) return rc;
   const char* dv = (const char*)slot->dev;
   // FA_PAIR_PF=1: the next coordinate's LDS reads issued before this one's arithmetic.  Off by default:
@@ -1661,29 +1313,7 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
     const char* e = getenv("FA_PAIR_PF");
     return e && e[0] == '1' ? 1 : 0;
   }();
-  if (oq) {
-    bool vec = true;  // 16-byte loads: every client segment 16-byte aligned (chunk starts are multiples of 4)
-    for (int i = 0; i < j * k; ++i) vec = vec && ((uintptr_t)hp[i] % 16 == 0);
-    const unsigned short* dtl = (const unsigned short*)(dv + seg_bytes + align16(ptr_bytes));
-#define FA_OQ3(S_, R, V, NL_) if (oq_pf()) FA_OQ4(S_, R, V, NL_, true); else FA_OQ4(S_, R, V, NL_, false)
-#define FA_OQ4(S_, R, V, NL_, PF_) hipLaunchKernelGGL((k_pairdist_oq<S_, R, V, NL_, PF_>), dim3((unsigned)nblocks), dim3((unsigned)o.nth), \
-      o.lds, st, (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, o.kp8, nchunks, o.ntiles, o.es, o.ce, dtl,   \
-      (double*)d_scratch)
-#define FA_OQ2(S_, R, V) if (o.nl <= 2) FA_OQ3(S_, R, V, 2); else FA_OQ3(S_, R, V, 4)
-#define FA_OQ1(S_, R) if (vec) FA_OQ2(S_, R, true); else FA_OQ2(S_, R, false)
-#define FA_OQ(S_) if (rt == 1) FA_OQ1(S_, 1); else if (rt == 2) FA_OQ1(S_, 2); else FA_OQ1(S_, 0)
-    switch (o.S) {
-      case 32: FA_OQ(32); break;
-      case 64: FA_OQ(64); break;
-      case 96: FA_OQ(96); break;
-      default: FA_OQ(128); break;
-    }
-#undef FA_OQ
-#undef FA_OQ1
-#undef FA_OQ2
-#undef FA_OQ3
-#undef FA_OQ4
-  } else if (f64) {
+  if (f64) {
     hipLaunchKernelGGL(k_pairdist_f64, dim3((unsigned)nblocks), dim3(kBlock), sizeof(double) * kC64 * k, st,
                        (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, nchunks64, (double*)d_scratch);
   } else if (q.lane) {
@@ -1727,14 +1357,6 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
 }
 
 size_t fa_pairwise_sqdist_scratch_bytes(int32_t num_segments, const int64_t* seg_numel, int32_t k) {
-  if (k >= 2 && num_segments > 0 && seg_numel && k <= kMaxPairK && oq_enabled()) {
-    const OqSplit o = oq_split(k);
-    int64_t nchunks = 0;
-    for (int s = 0; s < num_segments; ++s)
-      if (seg_numel[s] > 0) nchunks += (seg_numel[s] + o.pe - 1) / o.pe;
-    const int64_t nblocks = std::max<int64_t>(1, std::min<int64_t>(nchunks, pair_split(k).nblocks));
-    return sizeof(double) * (size_t)((int64_t)k * (k - 1) / 2) * (size_t)nblocks;
-  }
   if (k < 2 || num_segments <= 0 || !seg_numel) return 0;
   const PairSplit q = pair_split(k);
   int64_t nchunks = 0;
