@@ -87,6 +87,9 @@ def parse():
                    help="metric / hier: run the group -> global exchange even at one rank, native ordered exchanges "
                         "with FA_XCHG_LOOPBACK (every rank owns a piece, its own piece goes through RCCL as a self "
                         "send / receive) -- at --gpus 1 it executes the whole N > 1 exchange body on one GPU")
+    p.add_argument("--soak-seconds", type=float, default=5.0,
+                   help="one GPU: after the timed steps, keep stepping (untimed by the line's value) for this long and "
+                        "report the sustained rate beside it (clock / thermal steadiness; 0 = off)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     p.add_argument("--check-samples", type=int, default=65536)
@@ -1808,6 +1811,22 @@ def main():
     torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
     timer.stop()
+    sustained = None
+    if args.soak_seconds > 0 and world == 1 and not wl.get("latency") and wl.get("bytes_total"):
+        stage("soak")
+        n_soak = 0
+        torch.cuda.synchronize()
+        t_s = time.perf_counter()
+        while time.perf_counter() - t_s < args.soak_seconds:
+            for _ in range(max(1, args.steps)):
+                wl["step"]()
+            torch.cuda.synchronize()
+            n_soak += max(1, args.steps)
+        dt_s = time.perf_counter() - t_s
+        sustained = {"seconds": round(dt_s, 2), "steps": n_soak,
+                     "value": round(wl["bytes_total"] * n_soak / dt_s / 1e9, 2), "unit": "GB/s",
+                     "ms_per_step": round(dt_s / n_soak * 1e3, 4),
+                     "note": "the same step repeated after the timed region (not part of `value`)"}
     stage("parity check")
     ms_per_step = elapsed / args.steps * 1e3
     if wl.get("latency"):  # the step returns its own latency (s); value = mean (or median) latency in ms
@@ -1865,6 +1884,8 @@ def main():
         if wl.get("roofline_note"):
             line["roofline"]["note"] = wl["roofline_note"]
         line.update(wl.get("extra_line", {}))
+        if sustained is not None:
+            line["sustained"] = sustained
         if wl.get("latency"):
             line["latency_ms"] = {"mean": round(float(np.mean(lat)) * 1e3, 4),
                                   "median": round(float(np.median(lat)) * 1e3, 4),
