@@ -21,12 +21,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
-#include <utility>
 
 #include "fa_internal.h"
 #include "fedagg_robust.h"
 #include "median_nets.h"
-#include "pair_seg.h"
 
 using namespace fa_detail;
 
@@ -631,8 +629,7 @@ int fa_coord_median_tiled(fa_ctx* ctx, int dtype, int32_t num_segments, const in
 // adds them in block order (deterministic).
 namespace {
 
-constexpr int kPE = kPairRun;  // longest float32 run (coordinates); small-K esplit cap
-constexpr int kRotDefaultMaxK = 0;  // float32-run K taking k_pairdist_rot by default (none: r04f-k, not faster)
+constexpr int kPE = 64;       // longest float32 run (coordinates); small-K esplit cap
 constexpr int kMaxPairK = 128;
 constexpr int kMaxPairThreads = 1024;
 constexpr int kNPS = 16;      // k_pairdist: elements of one client staged per thread and chunk
@@ -727,7 +724,14 @@ size_t pair_lds_bytes(const PairSplit& q) {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// PSeg: pair_seg.h (shared with pairrot.hip)
+struct PSeg {
+  int64_t numel;
+  int64_t tile_start;   // first chunk of this segment (find_seg keys on it)
+  int32_t ptr_base;
+  int32_t pad;
+  int64_t pad2;
+};
+static_assert(sizeof(PSeg) == 32, "PSeg layout");
 
 // The reference's difference `v_i - v_j` is computed in the vectorized model's dtype
 // (krum_defense.py:52-60: torch.cat of the weights, then `(v1 - v2).norm()`): for bfloat16 / float16
@@ -1254,14 +1258,8 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
   const PairSplit q = pair_split(k);
   const int kp = q.kp, ntiles = q.ntiles, esplit = q.esplit, pe = q.pe;
   if (q.nthreads > kMaxPairThreads) return fail(FA_ERR_INVALID, "fa_pairwise_sqdist: k too large");
-  // FA_PAIR_ROT=0 / 1: the tile kernels / k_pairdist_rot for every float32-run K (A/B switch)
-  static const int rot_env = [] {
-    const char* e = getenv("FA_PAIR_ROT");
-    return e && (e[0] == '0' || e[0] == '1') ? e[0] - '0' : -1;
-  }();
-  const bool rot = !f64 && (rot_env < 0 ? k <= kRotDefaultMaxK : rot_env == 1);  // k_pairdist_rot (pairrot.hip)
   int nseg = 0;
-  int64_t nchunks = 0, nchunks64 = 0, nunits = 0;
+  int64_t nchunks = 0, nchunks64 = 0;
   for (int s = 0; s < num_segments; ++s) {
     if (seg_numel[s] < 0) return fail(FA_ERR_INVALID, "segment %d has negative numel", s);
     if (seg_numel[s] == 0) continue;
@@ -1270,7 +1268,6 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
     ++nseg;
     nchunks += (seg_numel[s] + pe - 1) / pe;
     nchunks64 += (seg_numel[s] + kC64 - 1) / kC64;
-    nunits += (seg_numel[s] + kRotUnit - 1) / kRotUnit;
   }
   const int64_t npairs = (int64_t)k * (k - 1) / 2;
   // workgroups: the same count for every diff dtype (fa_pairwise_sqdist_scratch_bytes sizes the
@@ -1296,7 +1293,7 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
   const void** hp = (const void**)(h + seg_bytes);
   int j = 0;
   int64_t c0 = 0;
-  const int64_t cpe = f64 ? kC64 : rot ? kRotUnit : pe;  // coordinates per chunk
+  const int64_t cpe = f64 ? kC64 : pe;  // coordinates per chunk
   for (int s = 0; s < num_segments; ++s) {
     const int64_t n = seg_numel[s];
     if (n == 0) continue;
@@ -1319,15 +1316,6 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
   if (f64) {
     hipLaunchKernelGGL(k_pairdist_f64, dim3((unsigned)nblocks), dim3(kBlock), sizeof(double) * kC64 * k, st,
                        (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, nchunks64, (double*)d_scratch);
-  } else if (rot) {
-    bool vec = true;  // 16-byte loads: every client segment 16-byte aligned (unit rows start at 4-float multiples)
-    for (int i = 0; i < j * k; ++i) vec = vec && ((uintptr_t)hp[i] % 16 == 0);
-    const int e = launch_pairdist_rot(k, rt, vec, nblocks, (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes),
-                                      nunits, (double*)d_scratch, st);
-    if (e != hipSuccess) {
-      release(slot, st);
-      return fail(FA_ERR_HIP, "k_pairdist_rot launch: %s", hipGetErrorString((hipError_t)e));
-    }
   } else if (q.lane) {
     const size_t lds = pair_lds_bytes(q);
     bool vec = true;  // 16-byte loads: every client segment 16-byte aligned (chunk starts are multiples of 8)
