@@ -223,7 +223,7 @@ def test_median_multi_segment(eng):
         assert bits_equal(o.cpu(), orc.coord_median(c) if c[0].numel() else torch.empty(0))
 
 
-@pytest.mark.parametrize("k", [2, 3, 5, 8, 16, 31, 48, 64, 80, 97, 100, 128])
+@pytest.mark.parametrize("k", [2, 3, 5, 8, 15, 16, 17, 24, 31, 32, 33, 48, 64, 80, 97, 100, 128])
 def test_pairwise_sqdist_vs_oracle(eng, k):
     from oracle import orc
     g = torch.Generator().manual_seed(k)
@@ -235,7 +235,7 @@ def test_pairwise_sqdist_vs_oracle(eng, k):
     np.testing.assert_allclose(D.numpy(), ref.numpy(), rtol=1e-6)
 
 
-@pytest.mark.parametrize("k,off", [(4, 1), (8, 3), (33, 1), (100, 2), (128, 1)])
+@pytest.mark.parametrize("k,off", [(4, 1), (8, 3), (20, 2), (32, 1), (33, 1), (100, 2), (128, 1)])
 def test_pairwise_sqdist_unaligned_views(eng, k, off):
     """Client vectors at 4-byte (not 16-byte) offsets take the scalar staging loads; one segment
     whose length ends mid-chunk, another spanning many chunks (double-buffered pipeline)."""

@@ -5,7 +5,7 @@ import csv
 import sys
 
 
-def summary(path, name_filter="k_pairdist"):
+def summary(path, name_filter="k_pairdist"):  # every kernel whose name contains the filter
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     for r in csv.DictReader(open(path)):
         if name_filter in r["Kernel_Name"]:

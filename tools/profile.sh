@@ -7,7 +7,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 TAG=${1:-r01}
 shift || true
-BENCH_ARGS=${BENCH_ARGS:-"--steps 5 --warmup 2 --no-cpu-baseline --check-samples 0"}
+BENCH_ARGS=${BENCH_ARGS:-"--steps 5 --warmup 2 --no-cpu-baseline --check-samples 0 --soak-seconds 0"}
 OUT=/tmp/prof_$TAG  # raw traces stay off gpurun_out (copied back only if < 64 MiB)
 mkdir -p $OUT
 fault() { case "$1" in 124|134|137|139) return 0;; *) return 1;; esac; }
