@@ -1010,184 +1010,6 @@ k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __re
                 partial + (int64_t)blockIdx.x * ((int64_t)k * (k - 1) / 2));
 }
 
-// K <= 32 (r04): circulant pairs, wave-private staging -- no workgroup barrier in the main loop.
-// KC = 16 or 32 client slots (clients k..KC-1 staged as zeros).  Lane (ci, g) = (lane % KC, lane / KC)
-// owns the KC/2 pairs (ci, (ci + d) mod KC), d = 1..KC/2 -- every unordered pair exactly once, the
-// d = KC/2 pairs on ci < KC/2 only -- so all 64 lanes run the same instruction stream (the 4x4 tiles
-// need a second, within-block phase and 36 tiles do not divide a wave).  A wave streams chunks of
-// kCC = 32 coordinates: 8-lane runs load one 128-byte line of one client (KC / 8 16-byte loads per
-// lane), the registers go to the wave's own LDS rows [client][coordinate] after the previous chunk's
-// reads, and lane group g takes coordinate pairs g, g + NG, ...: one ds_read_b64 of the partner's two
-// coordinates per packed sub + fma (v_pk_add_f32 / v_pk_fma_f32, the fastest VALU form measured for
-// this step: tools/dpp_rate_probe.hip).  Row stride kCC + 64 / KC floats (34 / 36): the 32 (KC = 32)
-// or 16 x 2 (KC = 16) lanes of a half-wave read rows whose 8-byte words fall on distinct banks.
-// 32-coordinate chunks keep the staging registers (KC / 8 x 4) and client pointers (KC / 8) within
-// 128 VGPRs beside the 2 x KC / 2 float32 and KC / 2 float64 sums.  float32 runs of <= kPE coordinates per
-// component, then float64; the lane groups and waves are added in a fixed order.
-constexpr int kCC = 32;
-// NW waves per workgroup and per SIMD (1,024 workgroups fill the chip once); FA_PAIR_CIRC_W=3 (<= 168
-// VGPRs) for A/B against the default 4 (<= 128)
-template <int KC, bool VEC, int RT, int NW>
-__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW)))
-k_pairdist_circ(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k,
-                int64_t nchunks, double* __restrict__ partial) {
-  constexpr int S = kCC + 64 / KC;   // LDS row stride (floats)
-  constexpr int NG = 64 / KC;        // lane groups (coordinate pairs interleaved over them)
-  constexpr int ND = KC / 2;         // pairs per lane
-  constexpr int NP = kCC / 2 / NG;   // coordinate pairs per lane and chunk
-  constexpr int NJ = KC / 8;         // 16-byte staging loads per lane and chunk
-  constexpr int LPC = kCC / 4;       // lanes per client row in one staging load
-  constexpr int NR = KC + ND;        // LDS rows: clients 0..KC-1, then 0..ND-1 again (no wrap-around)
-  extern __shared__ float lds[];     // [waves][NR][S]; the epilogue reuses it
-  const int lane = threadIdx.x & 63;
-  const int wid = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
-  const int W = (int)blockDim.x >> 6;
-  float* my = lds + wid * NR * S;
-  const int ci = lane % KC, g = lane / KC;
-  f32x2 acc[ND];
-  double accd[ND];
-#pragma unroll
-  for (int d = 0; d < ND; ++d) {
-    acc[d] = f32x2{0.0f, 0.0f};
-    accd[d] = 0.0;
-  }
-  int run = 0;
-  auto flush = [&]() {
-#pragma unroll
-    for (int d = 0; d < ND; ++d) {
-      accd[d] += (double)acc[d].x + (double)acc[d].y;
-      acc[d] = f32x2{0.0f, 0.0f};
-    }
-    run = 0;
-  };
-  // staging: load j, lane L -> flat float4 f = 64 j + L: client f / LPC, coordinates 4 (f % LPC) .. + 3
-  int sc[NJ];
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) sc[j] = (64 * j + lane) / LPC;
-  const int sp = lane % LPC;
-  typedef const __attribute__((address_space(1))) float* gptr;
-  typedef float f32x4 __attribute__((ext_vector_type(4)));
-  auto compute = [&]() {
-#pragma unroll 1
-    for (int n = 0; n < NP; ++n) {
-      const int p = g + n * NG;  // coordinate pair 2p, 2p + 1 of the chunk
-      const float* q = my + ci * S + 2 * p;
-      const f32x2 a = *(const f32x2*)q;
-#pragma unroll
-      for (int d = 1; d <= ND; ++d) {
-        // partner (ci + d) mod KC: row ci + d of the duplicated rows -- a constant offset from q, so the
-        // ds_read_b64 carries it as its immediate (no address arithmetic per pair: r04o PMC, 40 % of the
-        // VALU instructions were row-index math with the wrap-around)
-        const f32x2 b = *(const f32x2*)(q + d * S);
-        const f32x2 t = round_diff<RT>(a - b);
-        acc[d - 1] = __builtin_elementwise_fma(t, t, acc[d - 1]);
-        // at most 8 partner reads in flight: all 16 hoisted (32 VGPRs) spill at KC = 32
-        if (d % 8 == 0) __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    run += NP;
-    if (run + NP > kPE) flush();
-  };
-  auto put = [&](const f32x4 (&v)[NJ]) {
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      float* q = &my[sc[j] * S + 4 * sp];  // 8-byte aligned (S even): two 8-byte stores
-      *(f32x2*)q = f32x2{v[j].x, v[j].y};
-      *(f32x2*)(q + 2) = f32x2{v[j].z, v[j].w};
-      if (sc[j] < ND) {  // the copy row KC + sc[j] (loads j < NJ / 2 only: uniform)
-        *(f32x2*)(q + KC * S) = f32x2{v[j].x, v[j].y};
-        *(f32x2*)(q + KC * S + 2) = f32x2{v[j].z, v[j].w};
-      }
-    }
-  };
-  // workgroup: a contiguous run of chunks [c0, c1); wave w every W-th of them.  Per segment: the client
-  // pointers once (clients past k read client 0 and are replaced by zeros), whole chunks by
-  // unconditional loads one chunk ahead, the partial last chunk by guarded loads.
-  const int64_t c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
-  for (int si = nseg > 1 && c0 < c1 ? find_seg(segs, nseg, c0) : 0; si < nseg && c0 < c1; ++si) {
-    const PSeg sg = segs[si];
-    if (sg.tile_start >= c1) break;
-    const int64_t nfull = sg.numel / kCC, send = sg.tile_start + (sg.numel + kCC - 1) / kCC;
-    const int64_t lo = std::max(c0, sg.tile_start), hi = std::min(c1, send);
-    if (lo >= hi) continue;
-    const float* src[NJ];
-    bool live[NJ];
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      live[j] = sc[j] < k;
-      src[j] = (const float*)ptrs[sg.ptr_base + (live[j] ? sc[j] : 0)];
-    }
-    const int64_t first = lo + (((wid - (lo - c0)) % W) + W) % W;  // my first chunk in [lo, hi)
-    const int64_t fend = std::min(hi, sg.tile_start + nfull);
-    const int64_t n = first < fend ? (fend - 1 - first) / W + 1 : 0;
-    auto load = [&](int64_t t, f32x4 (&v)[NJ]) {  // my t-th whole chunk (clamped to n - 1)
-      t = t < n ? t : n - 1;
-      const int64_t e0 = (first + t * W - sg.tile_start) * kCC + 4 * sp;
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        f32x4 x;
-        if constexpr (VEC) {
-          x = *(const __attribute__((address_space(1))) f32x4*)(src[j] + e0);
-        } else {
-          x = f32x4{((gptr)src[j])[e0], ((gptr)src[j])[e0 + 1], ((gptr)src[j])[e0 + 2], ((gptr)src[j])[e0 + 3]};
-        }
-        v[j] = live[j] ? x : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
-      }
-    };
-    if (n > 0) {
-      f32x4 v[NJ];
-      load(0, v);
-      for (int64_t t = 0; t < n; ++t) {
-        put(v);          // the previous chunk's reads are done: this wave's own rows, in program order
-        load(t + 1, v);  // clamped: the last iteration re-reads its chunk (a cache hit), no branch
-        compute();
-      }
-    }
-    const int64_t tail = sg.tile_start + nfull;
-    if (nfull * kCC < sg.numel && tail >= lo && tail < hi && (tail - c0) % W == wid) {
-      const int64_t e0 = nfull * kCC + 4 * sp;
-      f32x4 v[NJ];
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        float x[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const bool in = e0 + u < sg.numel;
-          const float y = ((gptr)src[j])[in ? e0 + u : sg.numel - 1];
-          x[u] = in && live[j] ? y : 0.0f;
-        }
-        v[j] = f32x4{x[0], x[1], x[2], x[3]};
-      }
-      put(v);
-      compute();
-    }
-  }
-  flush();
-  // lane groups (same pairs, other coordinates) in a fixed order, then the waves through LDS
-#pragma unroll
-  for (int d = 0; d < ND; ++d) {
-    double x = accd[d];
-    if constexpr (NG == 4) x += __shfl_xor(x, 16);
-    x += __shfl_xor(x, 32);
-    accd[d] = x;
-  }
-  __syncthreads();  // every wave is done with its staging rows
-  double* red = (double*)lds;  // [waves][KC][ND]
-  if (g == 0) {
-#pragma unroll
-    for (int d = 0; d < ND; ++d) red[(wid * KC + ci) * ND + d] = accd[d];
-  }
-  __syncthreads();
-  double* out = partial + (int64_t)blockIdx.x * ((int64_t)k * (k - 1) / 2);
-  for (int idx = threadIdx.x; idx < KC * ND; idx += (int)blockDim.x) {
-    const int i = idx / ND, d = idx % ND + 1, j = (i + d) % KC;
-    if (i >= k || j >= k || (d == ND && i >= ND)) continue;
-    double s = 0.0;
-    for (int w = 0; w < W; ++w) s += red[(w * KC + i) * ND + d - 1];
-    out[pair_index(i < j ? i : j, i < j ? j : i, k)] = s;
-  }
-}
-
 // waves_per_eu(4): <= 128 VGPRs, the budget at which a CU holds 16 waves (MI355X_MICROARCH.md: waves
 // per CU halve at 64 / 128 VGPRs) -- two 8-wave workgroups of 512 threads (K = 128)
 template <int KPAD, int RT, bool PF>
@@ -1436,14 +1258,8 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
   const PairSplit q = pair_split(k);
   const int kp = q.kp, ntiles = q.ntiles, esplit = q.esplit, pe = q.pe;
   if (q.nthreads > kMaxPairThreads) return fail(FA_ERR_INVALID, "fa_pairwise_sqdist: k too large");
-  // K <= 32: k_pairdist_circ (r04); FA_PAIR_CIRC=0 keeps k_pairdist_lane (A/B switch)
-  static const bool circ_on = [] {
-    const char* e = getenv("FA_PAIR_CIRC");
-    return !(e && e[0] == '0');
-  }();
-  const bool circ = !f64 && k <= 32 && circ_on;
   int nseg = 0;
-  int64_t nchunks = 0, nchunks64 = 0, nchunksc = 0;
+  int64_t nchunks = 0, nchunks64 = 0;
   for (int s = 0; s < num_segments; ++s) {
     if (seg_numel[s] < 0) return fail(FA_ERR_INVALID, "segment %d has negative numel", s);
     if (seg_numel[s] == 0) continue;
@@ -1452,7 +1268,6 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
     ++nseg;
     nchunks += (seg_numel[s] + pe - 1) / pe;
     nchunks64 += (seg_numel[s] + kC64 - 1) / kC64;
-    nchunksc += (seg_numel[s] + kCC - 1) / kCC;
   }
   const int64_t npairs = (int64_t)k * (k - 1) / 2;
   // workgroups: the same count for every diff dtype (fa_pairwise_sqdist_scratch_bytes sizes the
@@ -1478,7 +1293,7 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
   const void** hp = (const void**)(h + seg_bytes);
   int j = 0;
   int64_t c0 = 0;
-  const int64_t cpe = f64 ? kC64 : circ ? kCC : pe;  // coordinates per chunk
+  const int64_t cpe = f64 ? kC64 : pe;  // coordinates per chunk
   for (int s = 0; s < num_segments; ++s) {
     const int64_t n = seg_numel[s];
     if (n == 0) continue;
@@ -1501,26 +1316,6 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
   if (f64) {
     hipLaunchKernelGGL(k_pairdist_f64, dim3((unsigned)nblocks), dim3(kBlock), sizeof(double) * kC64 * k, st,
                        (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, nchunks64, (double*)d_scratch);
-  } else if (circ) {
-    bool vec = true;  // 16-byte loads: every client segment 16-byte aligned (chunk pieces start at 4-float multiples)
-    for (int i = 0; i < j * k; ++i) vec = vec && ((uintptr_t)hp[i] % 16 == 0);
-    static const int cw = [] {
-      const char* e = getenv("FA_PAIR_CIRC_W");
-      return e && e[0] == '3' ? 3 : 4;
-    }();
-#define FA_PDC2(KC, V, R, NW) hipLaunchKernelGGL((k_pairdist_circ<KC, V, R, NW>), dim3((unsigned)nblocks), dim3(64 * NW),  \
-      sizeof(float) * NW * (KC + KC / 2) * (kCC + 64 / KC), st, (const PSeg*)dv, nseg,                                  \
-      (const void* const*)(dv + seg_bytes), k, nchunksc, (double*)d_scratch)
-#define FA_PDC(KC, V, R) if (cw == 3) FA_PDC2(KC, V, R, 3); else FA_PDC2(KC, V, R, 4)
-#define FA_PDCR(KC, V) if (rt == 1) FA_PDC(KC, V, 1); else if (rt == 2) FA_PDC(KC, V, 2); else FA_PDC(KC, V, 0)
-    if (k <= 16) {
-      if (vec) FA_PDCR(16, true); else FA_PDCR(16, false);
-    } else {
-      if (vec) FA_PDCR(32, true); else FA_PDCR(32, false);
-    }
-#undef FA_PDCR
-#undef FA_PDC
-#undef FA_PDC2
   } else if (q.lane) {
     const size_t lds = pair_lds_bytes(q);
     bool vec = true;  // 16-byte loads: every client segment 16-byte aligned (chunk starts are multiples of 8)
