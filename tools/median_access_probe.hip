@@ -3,6 +3,7 @@
 // all K loads issued before any is used) versus 16 bytes (4 coordinates) of each client?  No network:
 // the loaded values are reduced by a min (data-dependent, so nothing is dropped) and one value per
 // coordinate is stored.  Output: one JSON line per form with the average kernel time over reps.
+// r04: the same 4-byte-per-lane pattern on the tiled ClientArena layout (run_tiled).
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -47,6 +48,53 @@ __global__ void __launch_bounds__(256) k_w16(const float* const* __restrict__ ro
 #pragma unroll
   for (int i = 1; i < K; ++i) m = __builtin_elementwise_minimum(m, ldnt((const f4*)(rows[i] + e)));  // loads hoisted by the compiler
   *(f4*)(out + e) = m;
+}
+
+// the tiled ClientArena layout [tiles][K][E] (E = 1024 floats): column e of client i at
+// (e / E) * K * E + i * E + e % E -- a workgroup's 256 columns lie in one tile, its K rows 4 KiB apart
+template <int K>
+__global__ void __launch_bounds__(256) k_w4t(const float* __restrict__ arena, int64_t n, float* __restrict__ out) {
+  constexpr int64_t E = 1024;
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  const float* base = arena + (e / E) * K * E + e % E;
+  float x[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) x[i] = ldnt(base + i * E);
+  float m = x[0];
+#pragma unroll
+  for (int i = 1; i < K; ++i) m = __builtin_elementwise_minimum(m, x[i]);
+  out[e] = m;
+}
+
+template <int K>
+void run_tiled(int64_t n, int reps) {
+  constexpr int64_t E = 1024;
+  const int64_t tiles = (n + E - 1) / E;
+  float* arena;
+  CK(hipMalloc(&arena, tiles * K * E * sizeof(float)));
+  CK(hipMemset(arena, 0x3f, tiles * K * E * sizeof(float)));
+  float* out;
+  CK(hipMalloc(&out, n * sizeof(float)));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  const unsigned grid = (unsigned)((n + 255) / 256);
+  auto launch = [&] { hipLaunchKernelGGL(k_w4t<K>, dim3(grid), dim3(256), 0, 0, (const float*)arena, n, out); };
+  for (int w = 0; w < 3; ++w) launch();
+  CK(hipDeviceSynchronize());
+  CK(hipEventRecord(a, 0));
+  for (int r = 0; r < reps; ++r) launch();
+  CK(hipEventRecord(b, 0));
+  CK(hipEventSynchronize(b));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, a, b));
+  ms /= reps;
+  const double bytes = (double)n * 4.0 * (K + 1);
+  printf("{\"K\": %d, \"form\": \"4B/lane tiled\", \"ms\": %.4f, \"GBps\": %.1f}\n", K, ms, bytes / (ms * 1e-3) / 1e9);
+  fflush(stdout);
+  CK(hipFree(arena));
+  CK(hipFree(out));
 }
 
 template <int K>
@@ -96,5 +144,7 @@ int main(int argc, char** argv) {
   run<32>(n, reps);
   run<64>(n, reps);
   run<128>(n, reps);
+  run_tiled<32>(n, reps);
+  run_tiled<128>(n, reps);
   return 0;
 }
