@@ -304,97 +304,6 @@ k_median_2l(const MSeg* __restrict__ segs, int nseg, const void* const* __restri
   else MedT<DT>::store(sg.out, e, kr);
 }
 
-// r04: k_median_2l with its loads one column block AHEAD of its network.  A workgroup takes `reps`
-// consecutive blocks of k2lCols columns; while a lane sorts block t's N keys (x), block t + 1's N
-// loads are in flight into a second register set (y) -- the r04q probe put k_median_2l at 0.82 of its
-// own read pattern's rate on the tiled layout, the network's latency not hidden behind loads.  Every
-// block's keys, sentinels, merge and rare-case rules
-// are k_median_2l's, so the result is the same bits.  The next block's index is clamped to the last
-// one (its loads always issue: exact vmcnt waits, no load under a branch).  Two key sets (2N VGPRs)
-// leave 2-3 waves / SIMD.
-// N >= 48: 2 waves / SIMD (<= 256 VGPRs; at 168 the two key sets spilled), else 3
-template <int DT, int N, bool EXACT>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(N >= 48 ? 2 : 3)))
-k_median_2lp(const MSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int64_t ntiles,
-             int reps) {
-  constexpr int B = 2 * N;
-  if constexpr (EXACT) k = B;
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  __shared__ u32x4 xs[N / 4][k2lCols];
-  const int h = __builtin_amdgcn_readfirstlane((int)threadIdx.x / k2lCols);  // half: wave-uniform
-  const int c = (int)threadIdx.x % k2lCols;
-  const int base = N * h;
-  const int lo_end = k + (B - 1) / 2 - ((k - 1) >> 1);
-  const int64_t t0 = (int64_t)blockIdx.x * reps;
-  const int64_t t1 = t0 + reps < ntiles ? t0 + reps : ntiles;
-  // one block's addressing
-  struct Blk {
-    const void* const* in;
-    int64_t ub, e;
-    unsigned boff;
-    bool live;
-    void* out;
-  };
-  auto blk = [&](int64_t tile) {
-    const MSeg sg = segs[nseg > 1 ? find_seg(segs, nseg, tile) : 0];
-    const int64_t e0 = (tile - sg.tile_start) * k2lCols, e = e0 + c;
-    const bool live = e < sg.numel;
-    const int64_t ec = live ? e : sg.numel - 1;
-    return Blk{ptrs + sg.ptr_base, col_base<MedT<DT>::kBytes>(e0, sg.tstride), e,
-               (unsigned)(ec - e0) * (unsigned)MedT<DT>::kBytes, live, sg.out};
-  };
-  auto load = [&](const Blk& b, float (&v)[N]) {
-#pragma unroll
-    for (int t = 0; t < N; ++t) v[t] = MedT<DT>::load_off(at(b.in[min(base + t, k - 1)], b.ub), b.boff);
-  };
-  auto finish = [&](const Blk& b, float (&x)[N]) {  // k_median_2l's body after the loads
-    if constexpr (!EXACT) {
-#pragma unroll
-      for (int t = N - 8; t < N; ++t)
-        x[t] = base + t < k ? x[t] : (base + t < lo_end ? -__builtin_inff() : __builtin_inff());
-    }
-    SortNet<N>::run(x);
-    if (h == 1) {
-#pragma unroll
-      for (int q = 0; q < N / 4; ++q)
-        xs[q][c] = u32x4{__float_as_uint(x[4 * q]), __float_as_uint(x[4 * q + 1]), __float_as_uint(x[4 * q + 2]),
-                         __float_as_uint(x[4 * q + 3])};
-    }
-    __syncthreads();
-    if (h == 0) {
-      float kr = -__builtin_inff();
-#pragma unroll
-      for (int q = 0; q < N / 4; ++q) {
-        const u32x4 u = xs[q][c];
-        kr = kmax(kr, kmin(x[N - 1 - 4 * q], __uint_as_float(u.x)));
-        kr = kmax(kr, kmin(x[N - 2 - 4 * q], __uint_as_float(u.y)));
-        kr = kmax(kr, kmin(x[N - 3 - 4 * q], __uint_as_float(u.z)));
-        kr = kmax(kr, kmin(x[N - 4 - 4 * q], __uint_as_float(u.w)));
-      }
-      if (b.live) {
-        const int r = (k - 1) >> 1;
-        const bool nan = kr != kr;
-        if (nan || kr == 0.0f) store_rare<DT>(b.in, b.ub, b.boff, k, b.e, r, nan, b.out);
-        else MedT<DT>::store(b.out, b.e, kr);
-      }
-    }
-    __syncthreads();  // xs is rewritten by the next block
-  };
-  if (t0 >= t1) return;
-  float x[N], y[N];
-  Blk bx = blk(t0), by;
-  load(bx, x);
-  for (int64_t t = t0; t < t1; t += 2) {
-    by = blk(t + 1 < t1 ? t + 1 : t1 - 1);
-    load(by, y);
-    finish(bx, x);
-    if (t + 1 >= t1) break;
-    bx = blk(t + 2 < t1 ? t + 2 : t1 - 1);
-    load(bx, x);
-    finish(by, y);
-  }
-}
-
 // (B > 64: median_col's body written out -- called through median_col, B = 128 took 256 VGPRs,
 // 1 wave/SIMD, 1.6 -> 2.2 ms; B <= 64 the other way round)
 template <int DT, int B>
@@ -568,27 +477,10 @@ void launch_median(int k, bool packed, bool off32, int lanes, dim3 grid, hipStre
         const char* e = getenv("FA_MEDIAN_XCD");
         return e && e[0] == '1' ? 1 : 0;
       }();
-      // FA_MEDIAN_2LP=0: k_median_2l (one column block per workgroup) instead of the load-ahead
-      // k_median_2lp; FA_MEDIAN_2LP_REPS: its blocks per workgroup (A/B measurement)
-      static const int lp = [] {
-        const char* e = getenv("FA_MEDIAN_2LP");
-        return e && e[0] == '0' ? 0 : 1;
-      }();
-      static const int lreps = [] {
-        const char* e = getenv("FA_MEDIAN_2LP_REPS");
-        const int v = e ? atoi(e) : 0;
-        return v >= 2 && v <= 4096 ? v : 8;
-      }();
-      const int64_t ntiles = grid.x;
-      const dim3 lgrid((unsigned)((ntiles + lreps - 1) / lreps));
       switch ((k + 7) / 8) {  // B = K rounded up to 8, N = B / 2 keys per lane
 #define FA_M2(Q)                                                                                                  \
   case Q:                                                                                                       \
-    if (lp && k == 8 * Q)                                                                                         \
-      hipLaunchKernelGGL((k_median_2lp<DT, 4 * Q, true>), lgrid, dim3(kBlock), 0, st, ds, nseg, dp, k, ntiles, lreps); \
-    else if (lp)                                                                                                  \
-      hipLaunchKernelGGL((k_median_2lp<DT, 4 * Q, false>), lgrid, dim3(kBlock), 0, st, ds, nseg, dp, k, ntiles, lreps); \
-    else if (k == 8 * Q) hipLaunchKernelGGL((k_median_2l<DT, 4 * Q, true>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k, xm); \
+    if (k == 8 * Q) hipLaunchKernelGGL((k_median_2l<DT, 4 * Q, true>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k, xm); \
     else hipLaunchKernelGGL((k_median_2l<DT, 4 * Q, false>), grid, dim3(kBlock), 0, st, ds, nseg, dp, k, xm);          \
     return;
         FA_M2(9) FA_M2(10) FA_M2(11) FA_M2(12) FA_M2(13) FA_M2(14) FA_M2(15) FA_M2(16)
