@@ -724,30 +724,6 @@ size_t pair_lds_bytes(const PairSplit& q) {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// k_pairdist_ring's shape (kp > 32): at most 8 compute waves (the most coordinate slices that fit),
-// 4 loader waves, a 4-slot ring of chunks of ce <= kPE coordinates per slice within 150 KB of LDS,
-// pe a multiple of 4 (16-byte pieces), PPL 16-byte pieces per loader lane and chunk (8 / 12 / 16).
-struct RingSplit { int esplit, ncw, ce, pe, ppl, nthreads; size_t lds; bool ok; };
-constexpr int kRingNS = 4, kRingNLW = 4;
-RingSplit ring_split(int kp, int kpad, int ntiles) {
-  RingSplit r{};
-  auto waves = [](int th) { return (th + 63) / 64; };
-  r.esplit = 1;
-  for (int e = 1; waves(e * ntiles) <= 8; ++e) r.esplit = e;
-  r.ncw = waves(r.esplit * ntiles);
-  const int S = kpad + 4;
-  r.ce = 64;
-  while (r.ce > 1 && ((size_t)kRingNS * r.esplit * r.ce * S * 4 + 64 > 150 * 1024 || (r.esplit * r.ce) % 4)) --r.ce;
-  r.pe = r.esplit * r.ce;
-  const int pieces = kp * r.pe / 4, per = (pieces + kRingNLW * 64 - 1) / (kRingNLW * 64);
-  r.ppl = per <= 8 ? 8 : per <= 12 ? 12 : 16;
-  r.nthreads = 64 * (r.ncw + kRingNLW);
-  r.lds = std::max((size_t)kRingNS * r.pe * S * 4 + 64, std::max(sizeof(double) * 16 * (size_t)ntiles,
-                                                                 sizeof(double) * 6 * (size_t)r.nthreads));
-  r.ok = per <= 16 && r.pe % 4 == 0 && r.nthreads <= kMaxPairThreads && r.lds <= 160 * 1024;
-  return r;
-}
-
 struct PSeg {
   int64_t numel;
   int64_t tile_start;   // first chunk of this segment (find_seg keys on it)
@@ -1170,163 +1146,6 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
                 partial + (int64_t)blockIdx.x * ((int64_t)k * (k - 1) / 2));
 }
 
-// ---------------------------------------------------------------------------------------------------
-// k_pairdist_ring (r04, kp > 32; FA_PAIR_RING=1): k_pairdist's tiles and within-block phase, with the
-// staging taken off the compute waves.  NLW loader waves fill an NS-slot LDS ring ([slot][pe][S]
-// floats, the [e][client] layout of k_pairdist) while the compute waves work on older slots; the
-// hand-off is two monotonic LDS counters per slot instead of a workgroup barrier per chunk:
-//   fill[s]: loader waves that finished writing their part of the slot's current chunk (+1 each),
-//   done[s]: compute waves that finished reading it (+1 each).
-// Chunk j lives in slot j % NS: its loaders wait for done[s] >= NCW * (j / NS) (chunk j - NS read),
-// its readers for fill[s] >= NLW * (j / NS + 1).  Every wait is bounded (kRingSpin polls with
-// s_sleep); a wave that times out stops taking chunks and still reaches the epilogue's barriers, so
-// the grid always drains (the result is then wrong and the parity tests say so).  Same float32 runs
-// (ce <= kPE coordinates per chunk), float64 flushes, fixed-order epilogue as k_pairdist.
-constexpr int kRingSpin = 1 << 20;
-__device__ __forceinline__ bool ring_wait(int* p, int v) {
-  for (int n = 0; n < kRingSpin; ++n) {
-    if (__hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= v) return true;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return false;
-}
-__device__ __forceinline__ void ring_signal(int* p) {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this wave's LDS reads / writes of the slot done
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(p, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-template <int KPAD, int RT, bool VEC, int NS, int NLW, int PPL>
-__global__ void __launch_bounds__(64 * (8 + NLW))  // <= 12 waves: 168 VGPRs at 3 waves / SIMD
-k_pairdist_ring(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int kp,
-                int64_t nchunks, int ntiles, int esplit, int ce, int ncw, double* __restrict__ partial) {
-  constexpr int S = KPAD + 4;
-  extern __shared__ float lds[];  // [NS][pe][S], then fill[NS], done[NS]
-  const int pe = ce * esplit;
-  const int nb = kp / 4;
-  const int nct = ncw * 64;                      // compute threads; the loader waves follow
-  const int t = threadIdx.x;
-  const int bufsz = pe * S;
-  int* fill = (int*)(lds + NS * bufsz);
-  int* done = fill + NS;
-  if (t < 2 * NS) fill[t] = 0;                   // fill and done are adjacent
-  __syncthreads();
-  const int64_t c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
-  const int nj = (int)(c1 - c0);
-  // compute roles (k_pairdist's)
-  const bool comp = t < nct;
-  const bool pact = t < ntiles * esplit;
-  const int es = pact ? t / ntiles : 0;
-  const int tile = pact ? t % ntiles : 0;
-  int bi = 0, bj = 1;
-  if (pact) tile_blocks(tile, nb, bi, bj);
-  const int dg = nct / nb;
-  const bool dact = t < dg * nb;
-  const int db = t % nb, de0 = t / nb;
-  Within<RT> wb;
-  wb.init();
-  double accd[16];
-  f32x2 acc[8];
-  int run = 0;
-#pragma unroll
-  for (int u = 0; u < 16; ++u) accd[u] = 0.0;
-#pragma unroll
-  for (int u = 0; u < 8; ++u) acc[u] = f32x2{0.0f, 0.0f};
-  auto flush = [&]() {
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      accd[2 * u] += (double)acc[u].x;
-      accd[2 * u + 1] += (double)acc[u].y;
-      acc[u] = f32x2{0.0f, 0.0f};
-    }
-    run = 0;
-  };
-  if (comp) {
-    const int off_a = es * ce * S + 4 * bi, off_b = es * ce * S + 4 * bj;
-    for (int j = 0; j < nj; ++j) {
-      const int s = j % NS;
-      if (!ring_wait(&fill[s], NLW * (j / NS + 1))) break;
-      const float* lb = lds + s * bufsz;
-      if (pact) {
-        const float* pa = lb + off_a;
-        const float* pb = lb + off_b;
-#pragma unroll 2
-        for (int i = 0; i < ce; ++i) pair_tile<RT>(*(const float4*)(pa + i * S), *(const float4*)(pb + i * S), acc);
-      }
-      run += ce;
-      if (run + ce > kPE) flush();
-      if (dact) wb.add(lb, S, pe, de0, dg, db);
-      wb.step((pe + dg - 1) / dg);
-      ring_signal(&done[s]);
-    }
-  } else {
-    // loader: piece p = lane + NL * i (i < PPL) of a chunk's kp * pe / 4 float4 pieces -> client
-    // p / (pe / 4), coordinates 4 (p % (pe / 4)) .. + 3; client pointers cached per segment
-    const int l = t - nct, NL = NLW * 64;
-    const int qpc = pe / 4;                      // pieces per client row
-    const int npieces = kp * qpc;
-    int pc[PPL], pq[PPL];
-#pragma unroll
-    for (int i = 0; i < PPL; ++i) {
-      const int p = l + NL * i;
-      pc[i] = p < npieces ? p / qpc : kp;        // kp: no piece
-      pq[i] = p < npieces ? p % qpc : 0;
-    }
-    int cseg = -1;
-    const float* src[PPL];
-    int64_t snum = 0, sstart = 0;
-    typedef const __attribute__((address_space(1))) float* gptr;
-    for (int j = 0; j < nj; ++j) {
-      const int s = j % NS;
-      if (!ring_wait(&done[s], ncw * (j / NS))) break;
-      const int64_t ch = c0 + j;
-      const int si = nseg > 1 ? find_seg(segs, nseg, ch) : 0;
-      if (si != cseg) {
-        cseg = si;
-        const PSeg sg = segs[si];
-        snum = sg.numel;
-        sstart = sg.tile_start;
-#pragma unroll
-        for (int i = 0; i < PPL; ++i) src[i] = (const float*)ptrs[sg.ptr_base + (pc[i] < k ? pc[i] : 0)];
-      }
-      const int64_t b0 = (ch - sstart) * pe;
-      const int lim = (int)std::min<int64_t>(pe, snum - b0);  // coordinates of this chunk in the segment
-      float4 v[PPL];
-#pragma unroll
-      for (int i = 0; i < PPL; ++i) {
-        const int e = 4 * pq[i];
-        const bool any = pc[i] < k && e < lim;
-        if (VEC && any && e + 4 <= lim) {
-          typedef float f32x4 __attribute__((ext_vector_type(4)));
-          const f32x4 w = *(const __attribute__((address_space(1))) f32x4*)(src[i] + b0 + e);
-          v[i] = float4{w.x, w.y, w.z, w.w};
-        } else {
-          float x[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) x[u] = any && e + u < lim ? ((gptr)src[i])[b0 + e + u] : 0.0f;
-          v[i] = float4{x[0], x[1], x[2], x[3]};
-        }
-      }
-      float* lb = lds + s * bufsz;
-#pragma unroll
-      for (int i = 0; i < PPL; ++i) {
-        if (pc[i] < kp) {                        // clients k..kp-1 are written as zeros
-          float* q = lb + 4 * pq[i] * S + pc[i];
-          q[0] = v[i].x;
-          q[S] = v[i].y;
-          q[2 * S] = v[i].z;
-          q[3 * S] = v[i].w;
-        }
-      }
-      ring_signal(&fill[s]);
-    }
-  }
-  flush();
-  wb.flush();
-  __syncthreads();  // the ring is free: the epilogue reuses the LDS
-  pair_epilogue(lds, accd, pact, es, tile, bi, bj, ntiles, esplit, nb, k, wb.accd, dact, dg,
-                partial + (int64_t)blockIdx.x * ((int64_t)k * (k - 1) / 2));
-}
-
 // float64 models (krum_defense.py:50-66 over vectorize_weight's float64 vector, common/utils.py:8-30):
 // every difference and square in float64, as the reference computes them (no float32 step).  A rare
 // path, written for clarity: a workgroup stages kC64 coordinates of all k clients in LDS ([e][client]
@@ -1450,18 +1269,6 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
     nchunks += (seg_numel[s] + pe - 1) / pe;
     nchunks64 += (seg_numel[s] + kC64 - 1) / kC64;
   }
-  // kp > 32: k_pairdist_ring with FA_PAIR_RING=1 (A/B)
-  static const bool ring_on = [] {
-    const char* e = getenv("FA_PAIR_RING");
-    return e && e[0] == '1';
-  }();
-  RingSplit rq{};
-  if (!f64 && !q.lane && ring_on) rq = ring_split(kp, q.kpad, ntiles);
-  const bool ring = rq.ok;
-  int64_t nchunksr = 0;
-  if (ring)
-    for (int s = 0; s < num_segments; ++s)
-      if (seg_numel[s] > 0) nchunksr += (seg_numel[s] + rq.pe - 1) / rq.pe;
   const int64_t npairs = (int64_t)k * (k - 1) / 2;
   // workgroups: the same count for every diff dtype (fa_pairwise_sqdist_scratch_bytes sizes the
   // partials by it), float64 chunks spread over them
@@ -1486,7 +1293,7 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
   const void** hp = (const void**)(h + seg_bytes);
   int j = 0;
   int64_t c0 = 0;
-  const int64_t cpe = f64 ? kC64 : ring ? rq.pe : pe;  // coordinates per chunk
+  const int64_t cpe = f64 ? kC64 : pe;  // coordinates per chunk
   for (int s = 0; s < num_segments; ++s) {
     const int64_t n = seg_numel[s];
     if (n == 0) continue;
@@ -1526,24 +1333,6 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
 #undef FA_PDL
 #undef FA_PDL1
 #undef FA_PDL2
-  } else if (ring) {
-    bool vec = true;
-    for (int i = 0; i < j * k; ++i) vec = vec && ((uintptr_t)hp[i] % 16 == 0);
-#define FA_PR3(KPAD, R, V, PPL) hipLaunchKernelGGL((k_pairdist_ring<KPAD, R, V, kRingNS, kRingNLW, PPL>), dim3((unsigned)nblocks), \
-      dim3((unsigned)rq.nthreads), rq.lds, st, (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunksr, \
-      ntiles, rq.esplit, rq.ce, rq.ncw, (double*)d_scratch)
-#define FA_PR2(KPAD, R, V) if (rq.ppl == 8) FA_PR3(KPAD, R, V, 8); else if (rq.ppl == 12) FA_PR3(KPAD, R, V, 12); else FA_PR3(KPAD, R, V, 16)
-#define FA_PR1(KPAD, R) if (vec) FA_PR2(KPAD, R, true); else FA_PR2(KPAD, R, false)
-#define FA_PRR(KPAD) if (rt == 1) FA_PR1(KPAD, 1); else if (rt == 2) FA_PR1(KPAD, 2); else FA_PR1(KPAD, 0)
-    switch (q.kpad) {
-      case 64: FA_PRR(64); break;
-      case 96: FA_PRR(96); break;
-      default: FA_PRR(128); break;
-    }
-#undef FA_PRR
-#undef FA_PR1
-#undef FA_PR2
-#undef FA_PR3
   } else {
     const size_t lds = pair_lds_bytes(q);
 #define FA_PD(KPAD, R) if (pf) FA_PD2(KPAD, R, true); else FA_PD2(KPAD, R, false)
