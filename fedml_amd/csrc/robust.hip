@@ -765,12 +765,14 @@ __device__ __forceinline__ int64_t pair_index(int i, int j, int k) {  // i < j
 // sub and fused multiply-add as the scalar form, half the VALU issue slots.
 template <int RT>
 __device__ __forceinline__ void pair_tile(const float4 a, const float4 b, f32x2 (&acc)[8]) {
-  const float av[4] = {a.x, a.y, a.z, a.w};
+  // a's lanes broadcast by shuffles of its two halves (op_sel on the packed subtraction, no v_mov)
+  const f32x2 a01 = {a.x, a.y}, a23 = {a.z, a.w};
   const f32x2 b01 = {b.x, b.y}, b23 = {b.z, b.w};
+  const f32x2 ax[4] = {__builtin_shufflevector(a01, a01, 0, 0), __builtin_shufflevector(a01, a01, 1, 1),
+                       __builtin_shufflevector(a23, a23, 0, 0), __builtin_shufflevector(a23, a23, 1, 1)};
 #pragma unroll
   for (int x = 0; x < 4; ++x) {
-    const f32x2 ax = {av[x], av[x]};
-    const f32x2 d0 = round_diff<RT>(ax - b01), d1 = round_diff<RT>(ax - b23);
+    const f32x2 d0 = round_diff<RT>(ax[x] - b01), d1 = round_diff<RT>(ax[x] - b23);
     acc[2 * x] = __builtin_elementwise_fma(d0, d0, acc[2 * x]);
     acc[2 * x + 1] = __builtin_elementwise_fma(d1, d1, acc[2 * x + 1]);
   }
@@ -979,7 +981,7 @@ k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __re
       const float* pb = lb + 4 * bj;
       float4 a = *(const float4*)&pa[e_lo * stride];
       float4 b = *(const float4*)&pb[e_lo * stride];
-#pragma unroll 2
+#pragma unroll 4
       for (int e = e_lo; e < e_hi; ++e) {
         float4 an = a, bn = b;
         if constexpr (PF) {
@@ -1115,7 +1117,7 @@ k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restric
     if (pact) {
       float4 a = *(const float4*)pa;
       float4 b = *(const float4*)pb;
-#pragma unroll 2
+#pragma unroll 4
       for (int i = 0; i < ce; ++i) {
         float4 an = a, bn = b;
         if constexpr (PF) {  // next coordinate's reads in flight during this one's arithmetic
