@@ -1,0 +1,16 @@
+# r04y: the grouped (hier) kernel with 16 clients' loads in flight per wave (FA_GROUPED_U=16) vs 8 --
+# grouped GPU tests with U=16, then hier at P = 10.49 / 11.70 / 12.58 M, 2 interleaved reps.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r04y; mkdir -p $O
+FA_GROUPED_U=16 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests -k "group or hier or seq" > $O/pytest_u16.txt 2>&1 \
+  || { echo "pytest u16 FAIL"; tail -40 $O/pytest_u16.txt; exit 1; }
+tail -1 $O/pytest_u16.txt
+line() { python -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);r=d.get('roofline') or {};print(sys.argv[1],d['value'],d['unit'],d['ms_per_step'],r.get('kernel_avg_ms'),r.get('frac'),'|',(d.get('parity') or '')[:30])" $1; }
+b() { n=$1; shift; timeout -k 10 200 python bench.py "$@" --steps 20 --warmup 3 --no-cpu-baseline --soak-seconds 0 > $O/$n.json 2> $O/$n.err || { echo "FAIL $n"; tail -8 $O/$n.err; exit 1; }; line $O/$n.json; }
+for rep in 1 2; do
+  for P in 11699132 12582912 10485760; do
+    b hier_P${P}_u8_r$rep --config hier --params $P --check-samples 0
+    FA_GROUPED_U=16 b hier_P${P}_u16_r$rep --config hier --params $P --check-samples 0
+  done
+done
+FA_GROUPED_U=16 b hier_u16_parity --config hier
