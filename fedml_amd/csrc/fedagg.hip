@@ -373,6 +373,9 @@ __device__ __forceinline__ void wsum_tile(const Seg* __restrict__ segs, int nseg
     for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
       A acc = T::zero();
       const int64_t pe = B::phys(e, sst);
+      // unrolled: the loads of 8 clients issue before their chain of accumulations (a long client list
+      // issued one load per round trip: r04x / r04aa, the 512-client hier tail tile ran ~0.25 ms alone)
+#pragma unroll 8
       for (int i = 0; i < k; ++i)
         acc = accum<DT, MODE>(acc, term<DT, MODE>(T::ld1(in[i], pe), T::coef(coef[i]), d));
       T::st1(sg.out, e, acc);
@@ -397,7 +400,9 @@ template <int DT, int MODE, int U, int S, bool NT, bool PF>
 __global__ void __launch_bounds__(kBlock)
 k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
        const void* const* __restrict__ ptrs, int k, double divisor, int64_t sstr, int xcd) {
-  const int64_t t = xcd ? xcd_tile(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;
+  const int64_t t = xcd ? xcd_tile(blockIdx.x, gridDim.x)
+                       : nseg == 1 ? (blockIdx.x == 0 ? (int64_t)gridDim.x - 1 : (int64_t)blockIdx.x - 1)  // see k_wsum_inl
+                                   : (int64_t)blockIdx.x;
   wsum_tile<DT, MODE, U, S, NT, PF>(segs, nseg, coef, ptrs, k, divisor, sstr, t);
 }
 
@@ -415,8 +420,10 @@ template <int DT, int MODE, int U, int S, bool NT, bool PF>
 __global__ void __launch_bounds__(kBlock)
 k_wsum_inl(const InlineDesc dsc, int nseg, int coef_off, int ptr_off, int k, double divisor, int64_t sstr) {
   const char* b = dsc.raw;
+  // one segment: workgroup 0 takes the last tile (ragged: the scalar path), so it overlaps the stream
+  const int64_t t = nseg == 1 ? (blockIdx.x == 0 ? (int64_t)gridDim.x - 1 : (int64_t)blockIdx.x - 1) : (int64_t)blockIdx.x;
   wsum_tile<DT, MODE, U, S, NT, PF>((const Seg*)b, nseg, (const double*)(b + coef_off),
-                                    (const void* const*)(b + ptr_off), k, divisor, sstr, blockIdx.x);
+                                    (const void* const*)(b + ptr_off), k, divisor, sstr, t);
 }
 
 // A float dtype group and the state_dict's int64 group (BatchNorm num_batches_tracked counters,
@@ -478,7 +485,10 @@ k_wsum_grouped(const Seg* __restrict__ segs, const double* __restrict__ coef,
   using A = typename B::A;
   constexpr int V = T::V;
   constexpr int64_t TILE = (int64_t)kBlock * V;
-  const int64_t tile = blockIdx.x;
+  // workgroup 0 takes the LAST tile (ragged: the scalar path, one pass over every client per element)
+  // so that it overlaps the stream instead of running alone at the end -- r04aa: cfg4 (512 clients,
+  // 11.70 M coordinates) 3.80 -> 3.55 ms; the size had run as slow as 12.58 M (profiles/r04x)
+  const int64_t tile = blockIdx.x == 0 ? (int64_t)gridDim.x - 1 : (int64_t)blockIdx.x - 1;
   const Seg sg = segs[0];
   const int64_t base = tile * TILE;
   const void* const* in = ptrs;
@@ -519,6 +529,7 @@ k_wsum_grouped(const Seg* __restrict__ segs, const double* __restrict__ coef,
       for (int g = 0; g < ngroups; ++g) {
         const GroupDesc gd = groups[g];
         A acc = T::zero();
+#pragma unroll 8
         for (int i = gd.begin; i < gd.end; ++i)
           acc = accum<DT, MODE>(acc, term<DT, MODE>(T::ld1(in[i], pe), T::coef(coef[i]), d));
         out = accum<DT, MODE>(out, epilogue(acc, gd));

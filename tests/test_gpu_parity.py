@@ -232,6 +232,37 @@ def test_grouped_two_level_vs_oracle(eng, dtype, mode, gmode, P):
     assert bits_equal(got.cpu(), exp)
 
 
+@pytest.mark.parametrize("mode,gmode", [(MUL_W, MUL_W), (SUM, SUM), (MUL_N_DIV_N, MUL_N_DIV_N)])
+@pytest.mark.parametrize("P", [3_122_193, 2_400_000])
+def test_grouped_multi_round_vs_oracle(eng, mode, gmode, P):
+    """More than one round of resident workgroups (> 8 x CUs tiles of 1,024 floats), a partial last
+    round and a ragged last tile, which workgroup 0 takes (r04): fa_weighted_sum_grouped bit-identical
+    to the levels as separate ordered reductions over the WHOLE output."""
+    from oracle import orc
+    g = torch.Generator().manual_seed(P + mode)
+    gptr = [0, 3, 8, 9, 16]
+    K = gptr[-1]
+    xs = [torch.randn(P, generator=g) for _ in range(K)]
+    counts = [int(v) for v in torch.randint(50, 601, (K,), generator=g)]
+    coef = [c / sum(counts) for c in counts] if mode == MUL_W else counts
+    div = float(sum(counts))
+    gcoef = [0.3, 1.7, 2.0, 0.01] if gmode == MUL_W else [11, 7, 3, 5]
+    gdiv = [26.0, 26.0, 13.0, 7.0]
+    terms = []
+    for j in range(len(gptr) - 1):
+        Gj = orc.weighted_sum(xs[gptr[j]:gptr[j + 1]], mode, coef[gptr[j]:gptr[j + 1]], div)
+        if gmode == SUM:
+            terms.append(Gj)
+        elif gmode == MUL_W:
+            terms.append(orc.weighted_sum([Gj], MUL_W, [gcoef[j]]))
+        else:
+            terms.append(orc.weighted_sum([Gj], MUL_N_DIV_N, [gcoef[j]], gdiv[j]))
+    exp = orc.weighted_sum(terms, SUM)
+    got = eng.weighted_sum_grouped([x.cuda() for x in xs], mode, coef, div, gptr, gmode,
+                                   gcoef if gmode != SUM else None, gdiv if gmode == MUL_N_DIV_N else None)
+    assert bits_equal(got.cpu(), exp)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16], ids=str)
 @pytest.mark.parametrize("layout", ["ring", "halo"])
 def test_banded_mix_kernel_equals_general(dtype, layout):
