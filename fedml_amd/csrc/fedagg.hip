@@ -396,13 +396,17 @@ bool xcd_map_enabled() {  // FA_XCD_MAP=0: round-robin workgroup -> tile order e
   return on != 0;
 }
 
+// one segment: workgroup 0 takes the last tile (ragged: the scalar path, one pass over every client
+// per element) so that it overlaps the stream instead of running alone after it (r04aa / r04ab)
+__device__ __forceinline__ int64_t tail_first(int nseg) {
+  return nseg == 1 ? (blockIdx.x == 0 ? (int64_t)gridDim.x - 1 : (int64_t)blockIdx.x - 1) : (int64_t)blockIdx.x;
+}
+
 template <int DT, int MODE, int U, int S, bool NT, bool PF>
 __global__ void __launch_bounds__(kBlock)
 k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
        const void* const* __restrict__ ptrs, int k, double divisor, int64_t sstr, int xcd) {
-  const int64_t t = xcd ? xcd_tile(blockIdx.x, gridDim.x)
-                       : nseg == 1 ? (blockIdx.x == 0 ? (int64_t)gridDim.x - 1 : (int64_t)blockIdx.x - 1)  // see k_wsum_inl
-                                   : (int64_t)blockIdx.x;
+  const int64_t t = xcd ? xcd_tile(blockIdx.x, gridDim.x) : tail_first(nseg);
   wsum_tile<DT, MODE, U, S, NT, PF>(segs, nseg, coef, ptrs, k, divisor, sstr, t);
 }
 
@@ -420,8 +424,7 @@ template <int DT, int MODE, int U, int S, bool NT, bool PF>
 __global__ void __launch_bounds__(kBlock)
 k_wsum_inl(const InlineDesc dsc, int nseg, int coef_off, int ptr_off, int k, double divisor, int64_t sstr) {
   const char* b = dsc.raw;
-  // one segment: workgroup 0 takes the last tile (ragged: the scalar path), so it overlaps the stream
-  const int64_t t = nseg == 1 ? (blockIdx.x == 0 ? (int64_t)gridDim.x - 1 : (int64_t)blockIdx.x - 1) : (int64_t)blockIdx.x;
+  const int64_t t = tail_first(nseg);
   wsum_tile<DT, MODE, U, S, NT, PF>((const Seg*)b, nseg, (const double*)(b + coef_off),
                                     (const void* const*)(b + ptr_off), k, divisor, sstr, t);
 }
@@ -641,6 +644,7 @@ __device__ __forceinline__ void fedavg_sgd_tile(const Seg* __restrict__ segs, in
     for (int64_t e = base + threadIdx.x; e < end; e += kBlock) {
       const int64_t pe = B::phys(e, sst);
       float acc = -0.0f;
+#pragma unroll 8
       for (int i = 0; i < k; ++i)
         acc = accum<FA_DTYPE_F32, FA_MODE_MUL_W>(
             acc, term<FA_DTYPE_F32, FA_MODE_MUL_W>(T::ld1(in[i], pe), T::coef(coef[i]), d));
@@ -664,7 +668,7 @@ k_fedavg_sgd(const Seg* __restrict__ segs, int nseg, const double* __restrict__ 
              float mom, float damp1, float wd, int flags, int64_t sstr, void* const* __restrict__ bufs2,
              RmsArgs ra) {
   fedavg_sgd_tile<U, NT, OPT>(segs, nseg, coef, ptrs, k, bufs, neg_lr, mom, damp1, wd, flags, sstr, bufs2, ra,
-                              blockIdx.x);
+                              tail_first(nseg));
 }
 
 // the same with its tables (Seg[nseg] | coef[k] | bufs[nseg] | bufs2[nseg] | ptrs[nseg * k]) as the
@@ -676,7 +680,7 @@ k_fedavg_sgd_inl(const InlineDesc dsc, int nseg, int coef_off, int buf_off, int 
   const char* b = dsc.raw;
   fedavg_sgd_tile<U, NT, OPT>((const Seg*)b, nseg, (const double*)(b + coef_off), (const void* const*)(b + ptr_off),
                               k, (void* const*)(b + buf_off), neg_lr, mom, damp1, wd, flags, sstr,
-                              (void* const*)(b + buf2_off), ra, blockIdx.x);
+                              (void* const*)(b + buf2_off), ra, tail_first(nseg));
 }
 
 // --------------------------------------------------------------------------------------------
@@ -694,14 +698,15 @@ k_mix(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict__ co
   using T = Tr<DT, FA_MODE_MUL_W>;
   constexpr int V = T::V;
   constexpr int64_t TILE = (int64_t)kBlock * V;
-  const int64_t base = (int64_t)blockIdx.x * TILE;
+  const int64_t bt = tail_first(1);  // the ragged last tile (scalar path over every row) first
+  const int64_t base = bt * TILE;
   const float dz = 0.f;
   // 4-KiB slot strides of the inputs / outputs: TILE * bytes (flat) or an arena's tile stride
   const int64_t ist = isst ? isst : TILE * T::IN_BYTES, ost = osst ? osst : TILE * T::OUT_BYTES;
 
   if (aligned && base + TILE <= n) {
-    const int64_t boff = (int64_t)blockIdx.x * ist + (int64_t)threadIdx.x * V * T::IN_BYTES;
-    const int64_t ooff = (int64_t)blockIdx.x * ost + (int64_t)threadIdx.x * V * T::OUT_BYTES;
+    const int64_t boff = bt * ist + (int64_t)threadIdx.x * V * T::IN_BYTES;
+    const int64_t ooff = bt * ost + (int64_t)threadIdx.x * V * T::OUT_BYTES;
     for (int r0 = 0; r0 < nrows; r0 += RG) {
       int beg[RG], end[RG];
       int maxd = 0;
@@ -788,7 +793,9 @@ k_mix_band(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict
   using T = Tr<DT, FA_MODE_MUL_W>;
   constexpr int V = T::V;
   constexpr int64_t TILE = (int64_t)kBlock * V;
-  const int64_t bt = xcd ? xcd_tile(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;  // see k_wsum
+  const int64_t bt0 = xcd ? xcd_tile(blockIdx.x, gridDim.x) : (int64_t)blockIdx.x;  // see k_wsum
+  // workgroup 0 (tile 0 under either map) takes the last, ragged tile: its scalar path walks every row
+  const int64_t bt = bt0 == 0 ? (int64_t)gridDim.x - 1 : bt0 - 1;
   const int64_t base = bt * TILE;
   const float dz = 0.f;
   const int64_t ist = isst ? isst : TILE * T::IN_BYTES, ost = osst ? osst : TILE * T::OUT_BYTES;

@@ -1,0 +1,16 @@
+# r04ac: ragged-tile-first in the FedOpt (k_fedavg_sgd) and mixing (k_mix, k_mix_band) kernels
+# (libfedagg_new.so) vs a08b639 (libfedagg_base.so): FedOpt / gossip / mixing GPU tests on new, then
+# gossip and fedopt 3 interleaved pairs.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r04ac; mkdir -p $O
+use() { cp fedml_amd/libfedagg_$1.so fedml_amd/libfedagg.so; }
+use new
+timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests -k "mix or gossip or fedopt or sgd or rmsprop or pushsum or band" > $O/pytest_new.txt 2>&1 \
+  || { echo "pytest new FAIL"; tail -40 $O/pytest_new.txt; exit 1; }
+tail -1 $O/pytest_new.txt
+line() { python -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);r=d.get('roofline') or {};print(sys.argv[1],d['value'],d['unit'],d['ms_per_step'],r.get('kernel_avg_ms'),r.get('frac'),'|',(d.get('parity') or '')[:30])" $1; }
+b() { n=$1; shift; timeout -k 10 300 python bench.py "$@" --steps 20 --warmup 3 --no-cpu-baseline --soak-seconds 0 > $O/$n.json 2> $O/$n.err || { echo "FAIL $n"; tail -8 $O/$n.err; exit 1; }; line $O/$n.json; }
+for rep in 1 2 3; do
+  for v in base new; do use $v; b gossip_${v}_r$rep --config gossip; b fedopt_${v}_r$rep --config fedopt --layout tiled; done
+done
+use new
