@@ -22,7 +22,38 @@ import sys
 BUCKETS = list(range(8, 129, 8))
 
 
-def oddeven_merge_sort(n):
+# A 16-key sorting network of 60 comparators (Green's construction: four hypercube layers, then 28
+# comparators), against Batcher's 63.  Used as the base case of the merge sort below: the 32-key sort
+# becomes 2 x 60 + 65 = 185 comparators (Batcher 191), the 64-key sort 531 (Batcher 543).  Checked
+# exhaustively over all 2^16 0-1 inputs by verify_g16() (0-1 principle) on every generation.
+G16 = [(0, 13), (1, 12), (2, 15), (3, 14), (4, 8), (5, 6), (7, 11), (9, 10),
+       (0, 5), (1, 7), (2, 9), (3, 4), (6, 13), (8, 14), (10, 15), (11, 12),
+       (0, 1), (2, 3), (4, 5), (6, 8), (7, 9), (10, 11), (12, 13), (14, 15),
+       (0, 2), (1, 3), (4, 10), (5, 11), (6, 7), (8, 9), (12, 14), (13, 15),
+       (1, 2), (3, 12), (4, 6), (5, 7), (8, 10), (9, 11), (13, 14),
+       (1, 4), (2, 6), (5, 8), (7, 10), (9, 13), (11, 14),
+       (2, 4), (3, 6), (9, 12), (11, 13),
+       (3, 5), (6, 8), (7, 9), (10, 12),
+       (3, 4), (5, 6), (7, 8), (9, 10), (11, 12),
+       (6, 7), (8, 9)]
+
+
+# Base case of the merge sort: G16 (True) or Batcher's own 16-key sort (False, the committed
+# median_nets.h until the G16 form is measured on the GPU: `--g16` writes it).
+BASE16 = "--g16" in sys.argv
+
+
+def verify_g16():
+    n = 16
+    for v in range(1 << n):
+        bits = [(v >> i) & 1 for i in range(n)]
+        for i, j in G16:
+            if bits[i] > bits[j]:
+                bits[i], bits[j] = bits[j], bits[i]
+        assert all(bits[i] <= bits[i + 1] for i in range(n - 1)), v
+
+
+def oddeven_merge_sort(n, base16=BASE16):
     comps = []
 
     def merge(lo, hi, r):
@@ -35,7 +66,9 @@ def oddeven_merge_sort(n):
             comps.append((lo, lo + r))
 
     def sort(lo, hi):
-        if hi - lo >= 1:
+        if base16 and hi - lo + 1 == 16:
+            comps.extend((lo + a, lo + b) for a, b in G16)
+        elif hi - lo >= 1:
             mid = lo + (hi - lo) // 2
             sort(lo, mid)
             sort(mid + 1, hi)
@@ -93,9 +126,38 @@ def emit(B):
     return "\n".join(lines), len(need)
 
 
+def check_midnet(B, cols=4096, seed=0):
+    """Evaluates the pruned network on random columns with many ties: the rank-(B-1)//2 key."""
+    import numpy as np
+    nodes, need, out = network(B)
+    rng = np.random.default_rng(seed + B)
+    x = rng.integers(0, 7, size=(B, cols)).astype(np.float64)
+    x[:, : cols // 2] = rng.standard_normal((B, cols // 2))
+    val = {}
+    get = lambda o: x[o[1]] if o[0] == "x" else val[o[1]]
+    for i in sorted(need):
+        op, a, b = nodes[i]
+        val[i] = (np.minimum if op == "min" else np.maximum)(get(a), get(b))
+    assert (get(out) == np.sort(x, axis=0)[(B - 1) // 2]).all(), B
+
+
+def check_sortnet(N, ops, pos, cols=4096, seed=0):
+    import numpy as np
+    rng = np.random.default_rng(seed + 1000 + N)
+    x = rng.integers(0, 5, size=(N, cols)).astype(np.float64)
+    x[:, : cols // 2] = rng.standard_normal((N, cols // 2))
+    val = {}
+    get = lambda o: x[o[1]] if o[0] == "x" else val[o[1]][0 if o[2] == "min" else 1]
+    for a, b, t in ops:
+        val[t] = (np.minimum(get(a), get(b)), np.maximum(get(a), get(b)))
+    assert (np.stack([get(pos[i]) for i in range(N)]) == np.sort(x, axis=0)).all(), N
+
+
 def main(path):
+    verify_g16()
     body, counts = [], {}
     for B in BUCKETS:
+        check_midnet(B)
         code, ops = emit(B)
         counts[B] = ops
         body.append(f"// B = {B}: {ops} min/max ops\n" + code)
@@ -123,6 +185,7 @@ def main(path):
             pos[i], pos[j] = ("t", tmp, "min"), ("t", tmp, "max")
             tmp += 1
         assert all(pos[i][0] != "H" for i in range(N))
+        check_sortnet(N, ops, pos)
         # emit in SSA over named temporaries; the outputs are copied back to x[0..N-1]
         ref = lambda o: f"x[{o[1]}]" if o[0] == "x" else ("i" if o[2] == "min" else "a") + str(o[1])
         L = [f"template <> struct SortNet<{N}> {{",
@@ -142,7 +205,9 @@ def main(path):
     hdr = (
         "// median_nets.h -- GENERATED by tools/gen_median_nets.py; do not edit.\n"
         "// MidNet<B>::run(keys): the key at rank (B-1)/2 of B keys, by a pruned Batcher odd-even merge\n"
-        "// network of the next power of two with compile-time sentinels folded away.  Keys: uint32 or\n"
+        + ("// network of the next power of two (16-key blocks: a 60-comparator network) with compile-time\n"
+           "// sentinels folded away.  Keys: uint32 or\n" if BASE16 else
+           "// network of the next power of two with compile-time sentinels folded away.  Keys: uint32 or\n") +
         "// float (one coordinate per lane) or two uint16 keys packed in 32 bits (two coordinates per lane,\n"
         "// v_pk_min_u16 / v_pk_max_u16).  Used by the k_median kernels (robust.hip).\n"
         "#pragma once\n\n"
@@ -165,4 +230,5 @@ def main(path):
 
 if __name__ == "__main__":
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    main(sys.argv[1] if len(sys.argv) > 1 else os.path.join(root, "fedml_amd", "csrc", "median_nets.h"))
+    args = [a for a in sys.argv[1:] if a != "--g16"]
+    main(args[0] if args else os.path.join(root, "fedml_amd", "csrc", "median_nets.h"))
