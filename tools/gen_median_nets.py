@@ -38,9 +38,10 @@ G16 = [(0, 13), (1, 12), (2, 15), (3, 14), (4, 8), (5, 6), (7, 11), (9, 10),
        (6, 7), (8, 9)]
 
 
-# Base case of the merge sort: G16 (True) or Batcher's own 16-key sort (False, the committed
-# median_nets.h until the G16 form is measured on the GPU: `--g16` writes it).
-BASE16 = "--g16" in sys.argv
+# Base case of the merge sort: G16 (default; r04ae, 3 interleaved pairs: median K = 128 1.156-1.164
+# -> 1.090-1.095 ms, K = 32 0.2675-0.269 -> 0.262-0.265, bit-exact) or Batcher's own 16-key sort
+# (`--batcher`, the r01-r04 networks).
+BASE16 = "--batcher" not in sys.argv
 
 
 def verify_g16():
@@ -230,5 +231,5 @@ def main(path):
 
 if __name__ == "__main__":
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    args = [a for a in sys.argv[1:] if a != "--g16"]
+    args = [a for a in sys.argv[1:] if a != "--batcher"]
     main(args[0] if args else os.path.join(root, "fedml_amd", "csrc", "median_nets.h"))

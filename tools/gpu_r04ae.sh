@@ -17,4 +17,4 @@ for rep in 1 2 3; do
   done
 done
 use base
-CONFIGS="metric hier gossip" bash tools/gpu_r04ad.sh
+[ -z "$EVIDENCE" ] || CONFIGS="metric hier gossip" bash tools/gpu_r04ad.sh
