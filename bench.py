@@ -43,6 +43,18 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# FEDML_AMD_BENCH_REHEARSAL=cpu (tests only): the N-rank metric / hier / gossip code paths -- launcher,
+# gloo process group, GroupReducer / DistributedGossip, per-rank parity -- on the CPU, with the local
+# reductions of an engine the TEST injects (FEDML_AMD_BENCH_ENGINE=module:factory, e.g.
+# tests/rehearsal_engine.py).  The product has no CPU path: without an injected engine this mode
+# refuses to run, and its lines are rehearsals, not measurements.
+CPU_REHEARSAL = os.environ.get("FEDML_AMD_BENCH_REHEARSAL") == "cpu"
+DEV = "cpu" if CPU_REHEARSAL else "cuda"
+
+
+def sync():
+    if not CPU_REHEARSAL:
+        torch.cuda.synchronize()
 METRIC = "device-resident aggregate GB/s, K=128 × 125M fp32 params; 1/2/4/8 GPU"
 RESNET18_P = 11_699_132
 
@@ -124,7 +136,8 @@ def visible_gpu_count():
     the GPU before its ranks start (torch.cuda.device_count() may fall back to hipGetDeviceCount when
     amdsmi discovery fails).  KFD topology nodes with SIMDs whose render node this process can open;
     if none can be read, the render nodes this process can open; capped by ROCR_VISIBLE_DEVICES /
-    HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set.  0 = could not tell."""
+    HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES when set (an explicitly EMPTY mask = 0 devices).
+    None = could not tell (neither the topology nor a render node readable, no mask)."""
     import glob
     n = 0
     for prop in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
@@ -141,11 +154,17 @@ def visible_gpu_count():
             n += 1
     if n == 0:
         n = sum(1 for d in glob.glob("/dev/dri/renderD*") if os.access(d, os.R_OK | os.W_OK))
+    known = n > 0
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
         v = os.environ.get(var)
-        if v is not None and n > 0:
-            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
-    return n
+        if v is None:
+            continue
+        m = len([x for x in v.split(",") if x.strip() != ""])
+        if m == 0:
+            return 0  # set and empty: no device is visible, whatever the topology says
+        if known:
+            n = min(n, m)
+    return n if known else None
 
 
 def launch_cmd(n, argv, port, script=None):
@@ -246,10 +265,13 @@ def init_dist(args):
         raise SystemExit("--loopback: the metric and hier configs run the group -> global exchange")
     # FEDML_AMD_BENCH_REHEARSAL=1: rehearse the N > 1 code path with every rank on device 0 over gloo
     # (RCCL refuses two ranks on one GPU); numbers from such a run are not measurements
-    rehearsal = os.environ.get("FEDML_AMD_BENCH_REHEARSAL") == "1"
+    rehearsal = os.environ.get("FEDML_AMD_BENCH_REHEARSAL") in ("1", "cpu")
+    if CPU_REHEARSAL and args.config not in ("metric", "hier", "gossip"):
+        raise SystemExit("FEDML_AMD_BENCH_REHEARSAL=cpu: the metric, hier and gossip configs only")
     if rehearsal:
         local = 0
-    torch.cuda.set_device(local)
+    if not CPU_REHEARSAL:
+        torch.cuda.set_device(local)
     if world > 1 or args.loopback:
         import datetime
 
@@ -271,13 +293,13 @@ def masked_stream(eng, args):
     streams every step).  Returns None: the GroupReducer then uses the current stream.  Only ONE
     such stream per process -- HIP multiplexes streams onto 4 hardware queues per process, and
     extra CU-masked queues serialised launches (tools/host_overhead.py)."""
-    if not args.cu_mask:
+    if not args.cu_mask or CPU_REHEARSAL:
         return None
     total = torch.cuda.get_device_properties(eng.device).multi_processor_count
     if args.cu_mask >= total:
         return None
     ms = eng.cu_masked_stream(args.cu_mask)
-    torch.cuda.synchronize()
+    sync()
     torch.cuda.set_stream(ms)
     return None
 
@@ -292,7 +314,7 @@ def max_over_ranks(x, world):
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    t = torch.tensor([x], dtype=torch.float64, device=DEV)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -306,32 +328,49 @@ def client_counts(K):
 def make_flat_clients(idx, P, dtype=torch.float32):
     out = []
     for i in idx:
-        g = torch.Generator(device="cuda").manual_seed(1000 + i)
-        out.append(torch.randn(P, generator=g, device="cuda", dtype=torch.float32).to(dtype))
+        g = torch.Generator(device=DEV).manual_seed(1000 + i)
+        out.append(torch.randn(P, generator=g, device=DEV, dtype=torch.float32).to(dtype))
     return out
 
 
 def make_arena_rows(idx, P, dtype=torch.float32):
     """Client updates as rows of ONE ClientArena allocation (same values as make_flat_clients)."""
+    if CPU_REHEARSAL:  # rows of one host allocation (a ClientArena is device memory)
+        rows = torch.empty(len(idx), P, dtype=dtype)
+        for j, i in enumerate(idx):
+            g = torch.Generator(device=DEV).manual_seed(1000 + i)
+            rows[j].copy_(torch.randn(P, generator=g, device=DEV, dtype=torch.float32).to(dtype))
+        return list(rows)
     from fedml_amd.arena import ArenaLayout, ClientArena
     arena = ClientArena(ArenaLayout([("w", (P,), dtype)]), capacity=len(idx), zero=False)
     rows = []
     for j, i in enumerate(idx):
-        g = torch.Generator(device="cuda").manual_seed(1000 + i)
+        g = torch.Generator(device=DEV).manual_seed(1000 + i)
         row = arena.bufs[dtype][j][:P]
-        row.copy_(torch.randn(P, generator=g, device="cuda", dtype=torch.float32).to(dtype))
+        row.copy_(torch.randn(P, generator=g, device=DEV, dtype=torch.float32).to(dtype))
         rows.append(row)
     return rows
 
 
 def make_tiled_arena(idx, P, dtype=torch.float32):
     """Client updates in a TILE-INTERLEAVED ClientArena (same values as make_flat_clients)."""
+    if CPU_REHEARSAL:  # the same [tiles, capacity, E] group layout in host memory (E: 4 KiB of fp32)
+        import types
+        E = 1024
+        nt = -(-P // E)
+        buf = torch.zeros(nt, len(idx), E, dtype=dtype)
+        for j, i in enumerate(idx):
+            g = torch.Generator(device=DEV).manual_seed(1000 + i)
+            f = torch.zeros(nt * E, dtype=dtype)
+            f[:P] = torch.randn(P, generator=g, device=DEV, dtype=torch.float32).to(dtype)
+            buf[:, j, :] = f.view(nt, E)
+        return types.SimpleNamespace(bufs={dtype: buf})
     from fedml_amd.arena import ArenaLayout, ClientArena
     arena = ClientArena(ArenaLayout([("w", (P,), dtype)]), capacity=len(idx), zero=False, tiled=True)
     for j, i in enumerate(idx):
-        g = torch.Generator(device="cuda").manual_seed(1000 + i)
-        arena.write(j, {"w": torch.randn(P, generator=g, device="cuda", dtype=torch.float32).to(dtype)})
-    torch.cuda.synchronize()
+        g = torch.Generator(device=DEV).manual_seed(1000 + i)
+        arena.write(j, {"w": torch.randn(P, generator=g, device=DEV, dtype=torch.float32).to(dtype)})
+    sync()
     arena._scratch.clear()
     return arena
 
@@ -368,14 +407,14 @@ def load_layout(name):
 def make_layout_clients(idx, layout):
     dicts = []
     for i in idx:
-        g = torch.Generator(device="cuda").manual_seed(1000 + i)
+        g = torch.Generator(device=DEV).manual_seed(1000 + i)
         d = {}
         for name, shape, dt in layout:
             dt = getattr(torch, dt)
             if dt == torch.int64:
-                d[name] = torch.randint(0, 100, tuple(shape), generator=g, device="cuda", dtype=dt)
+                d[name] = torch.randint(0, 100, tuple(shape), generator=g, device=DEV, dtype=dt)
             else:
-                d[name] = torch.randn(tuple(shape), generator=g, device="cuda").to(dt)
+                d[name] = torch.randn(tuple(shape), generator=g, device=DEV).to(dt)
         dicts.append(d)
     return dicts
 
@@ -383,6 +422,16 @@ def make_layout_clients(idx, layout):
 def split(K, rank, world):
     per = K // world
     return list(range(rank * per, (rank + 1) * per if rank < world - 1 else K))
+
+
+class _HostEvent:
+    """CPU rehearsal stand-in for a timing event (wall clock)."""
+
+    def record(self, _stream=None):
+        self.t = time.perf_counter()
+
+    def elapsed_time(self, other):
+        return (other.t - self.t) * 1e3
 
 
 class Timed:
@@ -396,14 +445,14 @@ class Timed:
 
     def __enter__(self):
         if self.on:
-            self.a = torch.cuda.Event(enable_timing=True)
-            self.a.record(torch.cuda.current_stream())
+            self.a = _HostEvent() if CPU_REHEARSAL else torch.cuda.Event(enable_timing=True)
+            self.a.record(None if CPU_REHEARSAL else torch.cuda.current_stream())
         return self
 
     def __exit__(self, *exc):
         if self.on:
-            b = torch.cuda.Event(enable_timing=True)
-            b.record(torch.cuda.current_stream())
+            b = _HostEvent() if CPU_REHEARSAL else torch.cuda.Event(enable_timing=True)
+            b.record(None if CPU_REHEARSAL else torch.cuda.current_stream())
             self.pairs.append((self.a, b))
 
     def start(self):
@@ -467,7 +516,7 @@ def sum_over_ranks(v, world):
     if world == 1:
         return v
     import torch.distributed as dist
-    t = torch.tensor([float(v)], dtype=torch.float64, device="cuda")
+    t = torch.tensor([float(v)], dtype=torch.float64, device=DEV)
     dist.all_reduce(t)
     return float(t.item())
 
@@ -498,7 +547,7 @@ def wl_metric(args, eng, rank, world, timer):
         xs = None
     else:
         xs = make_arena_rows(mine, P) if args.layout == "arena" else make_flat_clients(mine, P)
-    out = torch.empty(P, device="cuda")
+    out = torch.empty(P, device=DEV)
     res = {}
     if world > 1 or args.loopback:
         def timed_sum(xs_, mode, coef, div, o):
@@ -564,8 +613,8 @@ def wl_metric(args, eng, rank, world, timer):
                 ids = split(K, r, world)
                 cols = []
                 for i in ids:
-                    g = torch.Generator(device="cuda").manual_seed(1000 + i)
-                    cols.append(flat_pick(torch.randn(P, generator=g, device="cuda"), tiles, P))
+                    g = torch.Generator(device=DEV).manual_seed(1000 + i)
+                    cols.append(flat_pick(torch.randn(P, generator=g, device=DEV), tiles, P))
                 parts.append(orc.weighted_sum(cols, MUL_W, [counts[i] / N for i in ids]))
             exp = orc.weighted_sum(parts, 2)
             g_ = res["g"]
@@ -609,7 +658,7 @@ def wl_layout(args, eng, rank, world, timer):
         keep = ClientArena(ArenaLayout([(n, tuple(s), getattr(torch, dt)) for n, s, dt in layout]), capacity=len(mine))
         for j, d in enumerate(dicts):
             keep.adopt(j, d)
-        torch.cuda.synchronize()
+        sync()
         A = type("Args", (), {"federated_optimizer": "FedAvg"})()
         raw = [(counts[i], d) for i, d in zip(mine, dicts)]
         res_keep = keep  # the arena stays alive (its rows back the dicts; residency needs the object)
@@ -621,7 +670,7 @@ def wl_layout(args, eng, rank, world, timer):
             arena.write(j, d)
         if not arena.tiled:
             dicts = [arena.slot(j) for j in range(len(mine))]
-        torch.cuda.synchronize()
+        sync()
     P = sum(int(np.prod(s)) for _, s, _ in layout)
     size = {"int64": 8, "bfloat16": 2, "float32": 4}
     in_b = sum(int(np.prod(s)) * size[dt] for _, s, dt in layout)
@@ -639,7 +688,7 @@ def wl_layout(args, eng, rank, world, timer):
         red = reducer(args, eng, timer)
         te = TimedEngine()
         rows = list(range(len(mine)))
-        outs = {dt: torch.empty(n, dtype=torch.float32 if dt == torch.int64 else dt, device="cuda")
+        outs = {dt: torch.empty(n, dtype=torch.float32 if dt == torch.int64 else dt, device=DEV)
                 for dt, n in arena.layout.group_numel.items()}
 
     def step():
@@ -662,7 +711,7 @@ def wl_layout(args, eng, rank, world, timer):
             else:  # every client's dict regenerated from its seed, oracle partial per rank, rank-ordered sum
                 bad = cnt = 0
                 keys = layout[:: max(1, len(layout) // 24)]
-                idxs = {name: torch.arange(0, int(np.prod(shape)), max(1, int(np.prod(shape)) // 512), device="cuda")
+                idxs = {name: torch.arange(0, int(np.prod(shape)), max(1, int(np.prod(shape)) // 512), device=DEV)
                         for name, shape, _ in keys}
                 cols = {}  # (key, client) -> sampled elements
                 for i in range(K):
@@ -685,7 +734,7 @@ def wl_layout(args, eng, rank, world, timer):
         bad = 0
         for name, shape, dt in layout:
             n = int(np.prod(shape))
-            idx = torch.arange(0, n, max(1, n // 512), device="cuda")
+            idx = torch.arange(0, n, max(1, n // 512), device=DEV)
             exp = orc.weighted_sum([d[name].reshape(-1).index_select(0, idx).cpu() for d in dicts], MUL_W, w)
             got = res["out"][name].reshape(-1).index_select(0, idx).cpu()
             bad += count_bad(got, exp)
@@ -986,7 +1035,7 @@ def wl_fragmented(args, eng, rank, world, timer):
         bad = 0
         for name, shape, _ in layout[:: max(1, len(layout) // 16)]:
             n = int(np.prod(shape))
-            idx = torch.arange(0, n, max(1, n // 256), device="cuda")
+            idx = torch.arange(0, n, max(1, n // 256), device=DEV)
             exp = orc.weighted_sum([d[name].reshape(-1).index_select(0, idx).cpu() for d in dicts], MUL_W, w)
             got = res["out"][name].reshape(-1).index_select(0, idx).cpu()
             bad += int((got.view(torch.int32) != exp.view(torch.int32)).sum())
@@ -1020,7 +1069,7 @@ def wl_hier(args, eng, rank, world, timer):
     gn = [sum(c) for c in gcounts]
     w = [c / gn[j] for j, cs in enumerate(gcounts) for c in cs]
     gptr = [j * M for j in range(len(my_groups) + 1)]
-    out = torch.empty(P, device="cuda")
+    out = torch.empty(P, device=DEV)
     res = {}
 
     def timed_grouped(xs_, mode, coef, div, gp, gm, gc, gd, o):
@@ -1051,8 +1100,8 @@ def wl_hier(args, eng, rank, world, timer):
         for g in split(G, r, world):
             cols = []
             for i in range(g * M, (g + 1) * M):
-                gen = torch.Generator(device="cuda").manual_seed(1000 + i)
-                cols.append(flat_pick(torch.randn(P, generator=gen, device="cuda"), tiles, P))
+                gen = torch.Generator(device=DEV).manual_seed(1000 + i)
+                cols.append(flat_pick(torch.randn(P, generator=gen, device=DEV), tiles, P))
             cg = counts[g * M:(g + 1) * M]
             Gj = orc.weighted_sum(cols, 0, [c / sum(cg) for c in cg])
             terms.append(orc.weighted_sum([Gj], 1, [sum(cg)], float(N)))
@@ -1132,7 +1181,7 @@ def wl_gossip(args, eng, rank, world, timer):
                     eng.mix_tiled(buf, nodes, rp, cs, vs, obuf, nodes, n=P)
         else:
             xs = (make_arena_rows if args.layout == "arena" else make_flat_clients)(range(n), P)
-            outs = [torch.empty(P, device="cuda") for _ in range(n)]
+            outs = [torch.empty(P, device=DEV) for _ in range(n)]
 
             def step():
                 with timer:
@@ -1155,8 +1204,8 @@ def wl_gossip(args, eng, rank, world, timer):
             need = sorted({cs[j] for i in nodes for j in range(rp[i], rp[i + 1])})
             sin = {}
             for i in need:
-                gen = torch.Generator(device="cuda").manual_seed(1000 + i)
-                sin[i] = flat_pick(torch.randn(P, generator=gen, device="cuda"), tiles, P)
+                gen = torch.Generator(device=DEV).manual_seed(1000 + i)
+                sin[i] = flat_pick(torch.randn(P, generator=gen, device=DEV), tiles, P)
             hole = torch.zeros_like(next(iter(sin.values())))  # nodes no row of this rank reads
             sin = [sin.get(i, hole) for i in range(n)]
             sout = {i: flat_pick(o, tiles, P) for i, o in zip(nodes, res["outs"])}
@@ -1184,15 +1233,15 @@ def pcie_probe(nbytes=1 << 30, reps=5):
     """Pinned H2D and D2H copy rates (GB/s, best of ``reps``) of one ``nbytes`` buffer: the PCIe
     ceiling the host-path line is read against."""
     h = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
-    d = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    d = torch.empty(nbytes, dtype=torch.uint8, device=DEV)
     out = {}
     for name, (dst, src) in {"h2d": (d, h), "d2h": (h, d)}.items():
         best = float("inf")
         for _ in range(reps):
-            torch.cuda.synchronize()
+            sync()
             t0 = time.perf_counter()
             dst.copy_(src, non_blocking=True)
-            torch.cuda.synchronize()
+            sync()
             best = min(best, time.perf_counter() - t0)
         out[f"pinned_{name}_GBs"] = round(nbytes / best / 1e9, 2)
     return out
@@ -1272,9 +1321,9 @@ def wl_fedopt(args, eng, rank, world, timer):
         buf, rows, xs = arena.bufs[torch.float32], list(range(K)), None
     else:
         xs = make_arena_rows(range(K), P)
-    g = torch.Generator(device="cuda").manual_seed(5)
-    param = torch.randn(P, generator=g, device="cuda")
-    mbuf = torch.zeros(P, device="cuda")
+    g = torch.Generator(device=DEV).manual_seed(5)
+    param = torch.randn(P, generator=g, device=DEV)
+    mbuf = torch.zeros(P, device=DEV)
     state = {"first": True}
 
     def run(p_, b_, first, n=None):
@@ -1294,8 +1343,8 @@ def wl_fedopt(args, eng, rank, world, timer):
             return None
         from oracle import orc
         n = min(P, 1 << 20) // 1024 * 1024  # a fresh server state over the first n coordinates, two rounds
-        p_dev = torch.randn(n, generator=torch.Generator(device="cuda").manual_seed(6), device="cuda")
-        b_dev = torch.zeros(n, device="cuda")
+        p_dev = torch.randn(n, generator=torch.Generator(device=DEV).manual_seed(6), device=DEV)
+        b_dev = torch.zeros(n, device=DEV)
         p_cpu, b_cpu = p_dev.cpu(), b_dev.cpu()
         cols = list(buf[:n // buf.shape[2]].cpu().permute(1, 0, 2).reshape(buf.shape[1], -1)[rows]) if tiled \
             else [x[:n].cpu() for x in xs]
@@ -1303,7 +1352,7 @@ def wl_fedopt(args, eng, rank, world, timer):
         for first in (True, False):
             run(p_dev, b_dev, first, n)
             orc.sgd_apply(avg, p_cpu, b_cpu, lr, mom, first_step=first)
-        torch.cuda.synchronize()
+        sync()
         ok = torch.equal(p_dev.cpu().view(torch.int32), p_cpu.view(torch.int32)) and \
             torch.equal(b_dev.cpu().view(torch.int32), b_cpu.view(torch.int32))
         return f"{'bit-exact' if ok else 'MISMATCH'} vs oracle (FedAvg + SGD momentum, 2 rounds) on {n} coordinates"
@@ -1345,18 +1394,18 @@ def wl_secagg(args, eng, rank, world, timer):
     p, q = 2 ** 15 - 19, 10
     U, T = K, K // 2
     m = -(-P // (U - T))
-    g = torch.Generator(device="cuda").manual_seed(11)
+    g = torch.Generator(device=DEV).manual_seed(11)
     tiled = args.layout == "tiled"
     if tiled:  # tile-interleaved arena [tiles, K, 512] (fedml_amd/arena.py, fa_finite_sum_tiled)
         nt = -(-P // 512)
-        tbuf = torch.randint(0, p, (nt, K, 512), generator=g, dtype=torch.int64, device="cuda")
+        tbuf = torch.randint(0, p, (nt, K, 512), generator=g, dtype=torch.int64, device=DEV)
         rows = list(range(K))
         xs = None
     else:
         Ppad = -(-P // 64) * 64  # rows 512-byte aligned, as ClientArena lays them out (fedml_amd/arena.py)
-        arena = torch.randint(0, p, (K, Ppad), generator=g, dtype=torch.int64, device="cuda")
+        arena = torch.randint(0, p, (K, Ppad), generator=g, dtype=torch.int64, device=DEV)
         xs = [arena[i, :P] for i in range(K)]
-    F = torch.randint(0, p, (U, m), generator=g, dtype=torch.int64, device="cuda")
+    F = torch.randint(0, p, (U, m), generator=g, dtype=torch.int64, device=DEV)
     coef = gen_Lagrange_coeffs(np.arange(U) + K + 1, np.arange(K) + 1, p).tolist()
     state = {}
 
@@ -1375,15 +1424,15 @@ def wl_secagg(args, eng, rank, world, timer):
         if args.check_samples <= 0:
             return None
         from oracle import orc
-        gi = torch.Generator(device="cuda").manual_seed(99)
-        idx = torch.randint(0, P, (args.check_samples,), generator=gi, device="cuda")
+        gi = torch.Generator(device=DEV).manual_seed(99)
+        idx = torch.randint(0, P, (args.check_samples,), generator=gi, device=DEV)
         cols_in = ([tbuf[:, r, :].reshape(-1)[:P].index_select(0, idx).cpu() for r in rows] if tiled else
                    [x.index_select(0, idx).cpu() for x in xs])  # 1.5e9-element arena: one row at a time
         _, exp = orc.finite_sum(cols_in, p, MOD_END,
                                 mask=state["mask"].index_select(0, idx).cpu(), q_bits=q, scale=1 / K)
         ok = torch.equal(state["real"].index_select(0, idx).cpu().view(torch.int32), exp.view(torch.int32))
         # the decoded mask: every column of a row block is independent -> check a sampled slice
-        cols = torch.arange(0, min(m, 4096), device="cuda")
+        cols = torch.arange(0, min(m, 4096), device=DEV)
         dec = orc.lcc_decode(torch.tensor(coef, dtype=torch.int64)[: U - T], F[:, cols].cpu(), p, (U - T) * cols.numel())
         got = state["mask"].reshape(-1)
         rows_ok = all(torch.equal(got[j * m: j * m + cols.numel()].cpu(), dec[j * cols.numel():(j + 1) * cols.numel()])
@@ -1440,7 +1489,7 @@ def wl_samask(args, eng, rank, world, timer):
                 if j != i:
                     seeds.append(int(rng.randint(0, 2 ** 31 - 1)))
                     signs.append(-1 if j < i else 1)
-    out = torch.empty(P, dtype=torch.int64, device="cuda")
+    out = torch.empty(P, dtype=torch.int64, device=DEV)
     state = {}
 
     def step():
@@ -1485,8 +1534,8 @@ def wl_samask(args, eng, rank, world, timer):
 
 def _robust_inputs(K, P):
     Ppad = -(-P // 64) * 64  # ClientArena row alignment
-    g = torch.Generator(device="cuda").manual_seed(21)
-    arena = torch.randn((K, Ppad), generator=g, device="cuda")
+    g = torch.Generator(device=DEV).manual_seed(21)
+    arena = torch.randn((K, Ppad), generator=g, device=DEV)
     return [arena[i, :P] for i in range(K)]
 
 
@@ -1511,7 +1560,7 @@ def wl_median(args, eng, rank, world, timer):
     xs = _robust_inputs(K, P)
     if dt != torch.float32:
         Ppad = -(-P // 64) * 64
-        arena = torch.empty((K, Ppad), dtype=dt, device="cuda")
+        arena = torch.empty((K, Ppad), dtype=dt, device=DEV)
         for i, x in enumerate(xs):
             arena[i, :P].copy_(x)
         xs = [arena[i, :P] for i in range(K)]
@@ -1521,12 +1570,12 @@ def wl_median(args, eng, rank, world, timer):
         ta = ClientArena(ArenaLayout([("w", (P,), dt)]), capacity=K, zero=False, tiled=True)
         for i, x in enumerate(xs):
             ta.write(i, {"w": x})
-        torch.cuda.synchronize()
+        sync()
         ta._scratch.clear()
         buf, rows = ta.bufs[dt], list(range(K))
     es = xs[0].element_size()
     ibits = {4: torch.int32, 2: torch.int16}[es]
-    out = torch.empty(P, dtype=dt, device="cuda")
+    out = torch.empty(P, dtype=dt, device=DEV)
 
     def step():
         with timer:
@@ -1539,8 +1588,8 @@ def wl_median(args, eng, rank, world, timer):
         if args.check_samples <= 0:
             return None
         from oracle import orc
-        gi = torch.Generator(device="cuda").manual_seed(99)
-        idx = torch.randint(0, P, (args.check_samples,), generator=gi, device="cuda")
+        gi = torch.Generator(device=DEV).manual_seed(99)
+        idx = torch.randint(0, P, (args.check_samples,), generator=gi, device=DEV)
         exp = orc.coord_median([x.index_select(0, idx).cpu() for x in xs])
         ok = torch.equal(out.index_select(0, idx).cpu().view(ibits), exp.view(ibits))
         return f"{'bit-exact' if ok else 'MISMATCH'} vs oracle on {args.check_samples} sampled coordinates"
@@ -1772,9 +1821,9 @@ def main():
     args = parse()
     if (args.gpus > 1 or args.self_launch) and "WORLD_SIZE" not in os.environ:
         # no outer launcher: start the N ranks as child processes before anything touches the GPU
-        if os.environ.get("FEDML_AMD_BENCH_REHEARSAL") != "1" and not os.environ.get("FEDML_AMD_BENCH_CPU_PROBE"):
+        if os.environ.get("FEDML_AMD_BENCH_REHEARSAL") not in ("1", "cpu") and not os.environ.get("FEDML_AMD_BENCH_CPU_PROBE"):
             have = visible_gpu_count()  # sysfs / device nodes only: no HIP call in the parent
-            if 0 < have < args.gpus:  # 0: could not tell -- the ranks then report for themselves
+            if have is not None and have < args.gpus:  # None: could not tell -- the ranks then report
                 raise SystemExit(f"--gpus {args.gpus}: only {have} HIP device(s) visible "
                                  "(FEDML_AMD_BENCH_REHEARSAL=1 rehearses the N-rank path on one device over gloo)")
         sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.launch_timeout))
@@ -1783,8 +1832,17 @@ def main():
     rank, world, local = init_dist(args)
     stage = Stage(rank, args.stage_timeout)
     stage("setup")
-    from fedml_amd.engine import get_engine
-    eng = get_engine(local)
+    if CPU_REHEARSAL:
+        spec = os.environ.get("FEDML_AMD_BENCH_ENGINE")
+        if not spec:
+            raise SystemExit("FEDML_AMD_BENCH_REHEARSAL=cpu needs FEDML_AMD_BENCH_ENGINE=module:factory (a test's "
+                             "local-reduction stand-in); the product engine is HIP-only")
+        import importlib
+        mod, fn = spec.split(":")
+        eng = getattr(importlib.import_module(mod), fn)()
+    else:
+        from fedml_amd.engine import get_engine
+        eng = get_engine(local)
     if args.variant:
         eng.set_variant(args.variant)
     timer = Timed()
@@ -1796,31 +1854,31 @@ def main():
     for i in range(args.warmup):
         stage(f"warmup step {i}")
         wl["step"]()
-    torch.cuda.synchronize()
+    sync()
     stage("barrier before the timed steps")
     barrier(world)
-    torch.cuda.synchronize()
+    sync()
     timer.start()
     stage("timed steps")
     t0 = time.perf_counter()
     lat = []
     for _ in range(args.steps):
         lat.append(wl["step"]())
-    torch.cuda.synchronize()
+    sync()
     barrier(world)
-    torch.cuda.synchronize()
+    sync()
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
     timer.stop()
     sustained = None
     if args.soak_seconds > 0 and world == 1 and not wl.get("latency") and wl.get("bytes_total"):
         stage("soak")
         n_soak = 0
-        torch.cuda.synchronize()
+        sync()
         t_s = time.perf_counter()
         while time.perf_counter() - t_s < args.soak_seconds:
             for _ in range(max(1, args.steps)):
                 wl["step"]()
-            torch.cuda.synchronize()
+            sync()
             n_soak += max(1, args.steps)
         dt_s = time.perf_counter() - t_s
         sustained = {"seconds": round(dt_s, 2), "steps": n_soak,
@@ -1869,10 +1927,10 @@ def main():
             "config": {"workload": wl["name"], "clients": wl["clients"], "params_per_client": wl["params"],
                        "parallelism": f"client-groups x{world}" +
                                       (f", {args.collective} over "
-                                       f"{'gloo (one-GPU rehearsal)' if os.environ.get('FEDML_AMD_BENCH_REHEARSAL') else 'RCCL'}"
+                                       f"{'gloo (CPU rehearsal, injected local reductions)' if CPU_REHEARSAL else 'gloo (one-GPU rehearsal)' if os.environ.get('FEDML_AMD_BENCH_REHEARSAL') else 'RCCL'}"
                                        + (" (native fa_group_reduce)" if timer.natives else " (torch.distributed)")
                                        + f" in {args.chunks} chunks"
-                                       + (f", local partials on {args.cu_mask} CUs" if args.cu_mask else "")
+                                       + (f", local partials on {args.cu_mask} CUs" if args.cu_mask and not CPU_REHEARSAL else "")
                                        + (", loopback (own pieces through RCCL self send/recv)" if args.loopback
                                           else "")
                                        if world > 1 or args.loopback else ""),
@@ -1884,6 +1942,10 @@ def main():
         if wl.get("roofline_note"):
             line["roofline"]["note"] = wl["roofline_note"]
         line.update(wl.get("extra_line", {}))
+        if CPU_REHEARSAL:
+            line["rehearsal"] = ("CPU: bench.py's N-rank code path over gloo with a test's injected local reductions "
+                                 "(tests/rehearsal_engine.py) -- checks the exchange, not a measurement")
+            line["data"] = "synthetic N(0,1) client updates (CPU generator, seeds 1000+i), host memory"
         if sustained is not None:
             line["sustained"] = sustained
         if wl.get("latency"):
@@ -1897,6 +1959,9 @@ def main():
     stage("teardown")
     if world > 1 or args.loopback:
         import torch.distributed as dist
+        barrier(world)  # nobody closes its connections while a peer still finishes its last operation
+        from fedml_amd.distributed import group_reduce
+        group_reduce.release_groups()  # our extra communicators go before the default group, not at exit
         dist.destroy_process_group()
     stage.done()
 

@@ -594,6 +594,12 @@ int fa_group_reduce_scratch_bytes(const fa_comm* c, int exchange, const fa_local
   if (rc) return rc;
   const bool loop = (exchange & FA_XCHG_LOOPBACK) != 0;
   exchange &= ~FA_XCHG_LOOPBACK;
+  // the same validity rules as fa_group_reduce: the two entry points accept the same exchanges
+  if (exchange < FA_XCHG_ORDERED || exchange > FA_XCHG_REDUCE_SCATTER)
+    return fail(FA_ERR_INVALID, "fa_group_reduce_scratch_bytes: unknown exchange %d", exchange);
+  if (loop && exchange != FA_XCHG_ORDERED && exchange != FA_XCHG_ORDERED_ALL)
+    return fail(FA_ERR_INVALID,
+                "fa_group_reduce_scratch_bytes: FA_XCHG_LOOPBACK applies to the ordered exchanges only");
   if (n < 0 || chunks < 1 || align < 1 || root < 0 || root >= c->world)
     return fail(FA_ERR_INVALID, "fa_group_reduce_scratch_bytes: invalid n/chunks/align/root");
   Scratch s;

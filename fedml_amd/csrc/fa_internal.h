@@ -90,6 +90,7 @@ struct fa_ctx {
     bool pending = false;
     std::vector<char> shadow;     // the bytes `dev` holds, for stage(..., reuse) (valid if shadow_ok)
     bool shadow_ok = false;
+    bool acquired = false;        // acquire_slot'ed and not yet release()d
   } slots[fa_detail::kSlots];
   int next = 0;
   // fa_weighted_sum_host: one mapped pinned buffer the kernel reads and writes in place over PCIe

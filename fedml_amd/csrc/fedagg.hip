@@ -1018,6 +1018,10 @@ const char* last_error() { return g_last_error; }
 int acquire_slot(fa_ctx* ctx, size_t bytes, fa_ctx::Slot** out) {
   fa_ctx::Slot& s = ctx->slots[ctx->next];
   ctx->next = (ctx->next + 1) % kSlots;
+  // a use that never reached release() (its caller failed after stage()) leaves no event to wait
+  // on, so the slot's device table is not known to match its shadow: copy again next time
+  if (s.acquired) s.shadow_ok = false;
+  s.acquired = true;
   if (s.pending) {
     FA_HIP(hipEventSynchronize(s.ev));
     s.pending = false;
@@ -1096,12 +1100,9 @@ int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st, bool reuse) {
   reuse = reuse && stage_reuse_enabled();
   if (reuse && s->shadow_ok && s->shadow.size() == bytes && memcmp(s->host, s->shadow.data(), bytes) == 0)
     return FA_OK;  // acquire_slot waited for the slot's last reader, which waited for that copy
-  if (reuse) {
-    s->shadow.assign((const char*)s->host, (const char*)s->host + bytes);
-    s->shadow_ok = true;
-  } else {
-    s->shadow_ok = false;
-  }
+  // `dev` is about to be rewritten: the shadow is valid again only once the copy (and the caller
+  // stream's wait for it) has been enqueued -- every failure below returns with it invalid
+  s->shadow_ok = false;
   if (s->hmap && bytes <= (256u << 10) && stage_kernel_enabled()) {
     const int n16 = (int)((bytes + 15) / 16);  // slots are >= 16 KB and 16-byte multiples
     const int blocks = std::max(1, std::min(64, (n16 + kBlock - 1) / kBlock));
@@ -1116,15 +1117,20 @@ int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st, bool reuse) {
       FA_HIP(hipEventRecord(s->staged, cs));
       FA_HIP(hipStreamWaitEvent(st, s->staged, 0));
     }
-    return FA_OK;
+  } else {
+    FA_HIP(hipMemcpyAsync(s->dev, s->host, bytes, hipMemcpyHostToDevice, st));
   }
-  FA_HIP(hipMemcpyAsync(s->dev, s->host, bytes, hipMemcpyHostToDevice, st));
+  if (reuse) {
+    s->shadow.assign((const char*)s->host, (const char*)s->host + bytes);
+    s->shadow_ok = true;
+  }
   return FA_OK;
 }
 
 int release(fa_ctx::Slot* s, hipStream_t st) {
   FA_HIP(hipEventRecord(s->ev, st));
   s->pending = true;
+  s->acquired = false;
   return FA_OK;
 }
 

@@ -401,6 +401,22 @@ class GroupReducer:
         return out
 
 
+def release_groups():
+    """Destroy this process's extra torch.distributed groups (the "ordered" second groups) -- call
+    before dist.destroy_process_group(), so none is left for interpreter teardown to destroy (gloo
+    aborts with "terminate called without an active exception" when one is finalised at exit)."""
+    import gc
+    for key in list(_SECOND_GROUP):
+        if isinstance(key, tuple) and key[0] == "native":
+            continue  # libfedagg's RCCL communicators: owned by their reducers (fa_comm_destroy)
+        g = _SECOND_GROUP.pop(key)
+        try:
+            dist.destroy_process_group(g)
+        except Exception:  # noqa: BLE001 -- already gone with the default group
+            pass
+    gc.collect()
+
+
 def _native_comm(group):
     """This process's NativeComm over ``group`` (created collectively, once per group)."""
     from .native_exchange import NativeComm

@@ -197,10 +197,14 @@ class NativeExchange:
         return out
 
     def owned(self, n: int, align: int) -> List[tuple]:
-        """The pieces this rank summed in the ordered exchanges (its d_out holds them)."""
+        """The pieces this rank summed in the ordered exchanges AND holds in its d_out.  Under
+        FA_XCHG_LOOPBACK with "ordered" a non-root owner sums into the library's scratch and sends the
+        sum to the root only, so its d_out holds none of it: []."""
         if self.collective not in ("ordered", "ordered_all") or (self.comm.world == 1 and not self.loopback):
             return []
         me = self.comm.rank
+        if self.loopback and self.collective == "ordered" and me != self.root:
+            return []
         return [(pc[me][0], pc[me][0] + pc[me][1])
                 for _, _, pc in group_plan(n, self.chunks, align, self.comm.world, self.root, self.loopback)
                 if pc[me][1]]

@@ -129,11 +129,33 @@ class ArrivalIngest:
         return OrderedDict((k, views[k]) for k in averaged.keys())
 
 
+def _use_count_probe_ok() -> bool:
+    """torch._C._storage_Use_Count is private: check once that it exists and that its baseline is
+    the 2 references _storage_held assumes (the buffer's own tensor + the probe's storage object),
+    and that a derived view adds one."""
+    try:
+        t = torch.empty(4)
+        base = torch._C._storage_Use_Count(t.untyped_storage()._cdata)
+        v = t[1:]
+        held = torch._C._storage_Use_Count(t.untyped_storage()._cdata)
+        del v
+        return base == 2 and held == 3
+    except Exception:  # noqa: BLE001 -- the private API moved: take the conservative path
+        return False
+
+
+_USE_COUNT_OK = _use_count_probe_ok()
+
+
 def _storage_held(bufs) -> bool:
     """Is the storage of any of these (the ingest's own pinned buffers) still referenced from outside --
     by a tensor handed out from it or by ANY view derived from one (reshape, slice, ``.T``)?  Counted
     on the storage itself, not on the handed-out tensor objects: the buffer's own tensor and this
-    probe's storage object account for 2 references."""
+    probe's storage object account for 2 references.  If this torch's storage reference count does
+    not behave that way (checked once at import), every buffer counts as held: fresh pinned buffers
+    each round, never an overwritten result."""
+    if not _USE_COUNT_OK:
+        return any(b is not None for b in bufs)
     return any(torch._C._storage_Use_Count(b.untyped_storage()._cdata) > 2 for b in bufs if b is not None)
 
 

@@ -95,7 +95,7 @@ def test_prelaunch_device_count_never_touches_hip(monkeypatch):
     monkeypatch.setattr(torch._C, "_cuda_getDeviceCount", boom, raising=False)
     monkeypatch.setattr(torch.cuda, "is_available", boom)
     monkeypatch.setattr(torch.cuda, "init", boom)
-    assert isinstance(bench.visible_gpu_count(), int)
+    assert bench.visible_gpu_count() is None or isinstance(bench.visible_gpu_count(), int)
     calls = []
     monkeypatch.setattr(bench, "visible_gpu_count", lambda: 8)
     monkeypatch.setattr(bench, "launch_ranks", lambda n, argv, t, script=None: calls.append((n, list(argv))) or 0)
@@ -140,12 +140,33 @@ def test_visible_gpu_count_honours_visible_devices(monkeypatch, tmp_path):
     assert bench.visible_gpu_count() == 2
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "1")
     assert bench.visible_gpu_count() == 1
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")  # explicitly empty: no device
+    assert bench.visible_gpu_count() == 0
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    monkeypatch.setattr(_glob, "glob", lambda pat: [])  # nothing readable: unknown
+    assert bench.visible_gpu_count() is None
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", " , ")
+    assert bench.visible_gpu_count() == 0
+
+
+def test_prelaunch_refuses_with_empty_visible_mask(monkeypatch):
+    """An explicitly empty *_VISIBLE_DEVICES is 0 devices, not "unknown": the launcher refuses early."""
+    import bench
+    monkeypatch.setenv("ROCR_VISIBLE_DEVICES", "")
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.delenv("FEDML_AMD_BENCH_CPU_PROBE", raising=False)
+    monkeypatch.delenv("FEDML_AMD_BENCH_REHEARSAL", raising=False)
+    monkeypatch.setattr(bench, "launch_ranks", lambda *a, **k: pytest.fail("launched with no visible GPU"))
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2"])
+    with pytest.raises(SystemExit) as e:
+        bench.main()
+    assert "only 0" in str(e.value.code)
 
 
 def test_unknown_gpu_count_does_not_refuse(monkeypatch):
-    """0 = the parent could not tell (no readable topology): it launches and lets the ranks report."""
+    """None = the parent could not tell (no readable topology): it launches and lets the ranks report."""
     import bench
-    monkeypatch.setattr(bench, "visible_gpu_count", lambda: 0)
+    monkeypatch.setattr(bench, "visible_gpu_count", lambda: None)
     calls = []
     monkeypatch.setattr(bench, "launch_ranks", lambda n, argv, t, script=None: calls.append(n) or 0)
     monkeypatch.delenv("WORLD_SIZE", raising=False)

@@ -58,6 +58,9 @@ def _worker(rank, world, port, fn, errq):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         fn(rank, world)
+        dist.barrier()  # teardown only once every rank is done
+        from fedml_amd.distributed.group_reduce import release_groups
+        release_groups()  # no gloo group left for interpreter teardown (it can abort there)
     except Exception:  # noqa: BLE001
         errq.put(f"rank {rank}: {traceback.format_exc()}")
     finally:
@@ -72,7 +75,7 @@ def _spawn(fn, world=2):
     for p in procs:
         p.start()
     for p in procs:
-        p.join(120)
+        p.join(300)
     errs = []
     while not errq.empty():
         errs.append(errq.get())
@@ -400,3 +403,123 @@ def test_oracle_pushsum_restatement_matches_reference():
         assert om.tolist() == meta["omegas_out"]
         for i in range(n):
             assert _bits(oz[i], exp[i][key].reshape(-1).float()), (key, i)
+
+
+# ------------------------------------------------------------------------------ world 8 (the 8-GPU node's shape)
+def test_ordered_gloo_world8():
+    """ordered (dst 0 and dst 7) / ordered_all, flat and tiled, and the hierarchical cloud pre-scale
+    over 8 groups, with 8 real gloo ranks: 7 owners, every delivery, bit-exact
+    (simulation/nccl/base_framework/common.py:196-228)."""
+    _spawn(_case_ordered_multi, world=8)
+
+
+def _case_reduce_scatter_world(rank, world):
+    """reduce_scatter at the node's world size: ragged P (shards padded), several chunks, flat and
+    tiled; every rank's shard within 1e-6 normwise of the rank-ordered sum (the backend sums in its
+    own order) and equal to gloo's own reduce of the same partials."""
+    import torch.distributed as dist
+    from oracle import orc
+    from fedml_amd.distributed.group_reduce import GroupReducer
+    per = 2
+    K = per * world
+    for P in (8 * 1024 * 3 + 517, 1000):
+        xs, counts = _clients(K, P, seed=31 + P)
+        N = sum(counts)
+        ids = [list(range(r * per, (r + 1) * per)) for r in range(world)]
+        parts = [orc.weighted_sum([xs[i] for i in ids[r]], 0, [counts[i] / N for i in ids[r]]) for r in range(world)]
+        exp = orc.weighted_sum(parts, 2)
+        ref = parts[rank].clone()
+        dist.all_reduce(ref)  # gloo's own summation of the same partials
+        mine = ids[rank]
+        for chunks in (1, 5):
+            red = GroupReducer(collective="reduce_scatter", chunks=chunks, local_sum=_oracle_sum)
+            shard = red.fedavg([xs[i] for i in mine], [counts[i] / N for i in mine])
+            S = -(-P // world)
+            lo, hi = rank * S, min((rank + 1) * S, P)
+            assert shard.numel() == max(0, hi - lo), (P, chunks)
+            if hi > lo:
+                e = exp[lo:hi].double()
+                assert float((shard.double() - e).norm() / e.norm()) <= 1e-6, (P, chunks)
+                assert torch.allclose(shard, ref[lo:hi], rtol=0, atol=1e-6)
+        if P > 8 * 1024:  # tiled: shards of whole 1024-element tiles
+            red = GroupReducer(collective="reduce_scatter", chunks=3, local_sum=_oracle_sum)
+            shard = red.fedavg_tiled(_OracleTiledEngine(), _tiled_buf([xs[i] for i in mine]), list(range(per)),
+                                     [counts[i] / N for i in mine], P)
+            S = -(-P // (world * 1024)) * 1024
+            lo, hi = rank * S, min((rank + 1) * S, P)
+            assert shard.numel() == max(0, hi - lo)
+            if hi > lo:  # the last ranks own nothing when whole-tile shards cover P early
+                e = exp[lo:hi].double()
+                assert float((shard.double() - e).norm() / e.norm()) <= 1e-6
+
+
+def test_reduce_scatter_gloo_world8():
+    _spawn(_case_reduce_scatter_world, world=8)
+
+
+def _case_gossip_ring256(rank, world):
+    """DistributedGossip on a 256-node ring split 8 ways (32 nodes per rank, a 2-model halo), plain
+    DSGD rows and PushSum with the weights on the device: every node bit-identical to the whole-ring
+    step (client_dsgd.py:104-122, client_pushsum.py:127-156)."""
+    from oracle import orc
+    from fedml_amd.core.distributed.topology.topology_manager import SymmetricTopologyManager, gossip_rows
+    from fedml_amd.distributed.gossip import DistributedGossip
+    n, P = 256, 257
+    m = SymmetricTopologyManager(n, 2)
+    m.generate_topology()
+    W = m.topology
+    xs, _ = _clients(n, P, seed=17)
+    rp, cs, vs = gossip_rows(W)
+    exp_rows, _ = orc.mix(xs, rp, cs, vs)
+    dg = DistributedGossip(W, local_mix=_oracle_mix, local_pushsum=_oracle_pushsum)
+    mine = dg.mine
+    assert mine == list(range(rank * 32, rank * 32 + 32))
+    assert sorted(dg.halo_in) == sorted({(rank * 32 - 1) % n, (rank * 32 + 32) % n})
+    outs, _ = dg.step([xs[i] for i in mine])
+    for k, i in enumerate(mine):
+        assert _bits(outs[k], exp_rows[i]), i
+    om = np.array([1.0 + (i % 7) / 8 for i in range(n)], dtype=np.float32)
+    full_om = torch.empty(n, dtype=torch.float32)
+    exp_x = [torch.empty(P) for _ in range(n)]
+    exp_z = [torch.empty(P) for _ in range(n)]
+    _oracle_pushsum(xs, rp, cs, vs, torch.from_numpy(om), exp_x, exp_z, full_om)
+    x, z, om_out = dg.step([xs[i] for i in mine], omega=torch.from_numpy(om[mine].copy()))
+    for k, i in enumerate(mine):
+        assert _bits(x[k], exp_x[i]) and _bits(z[k], exp_z[i]), i
+        assert float(om_out[k]) == float(full_om[i]), i
+
+
+def test_gossip_ring256_gloo_world8():
+    _spawn(_case_gossip_ring256, world=8)
+
+
+def _case_hier_groups_world(rank, world):
+    """cfg4's shape at 8 ranks: 8 groups, one per rank, and 16 groups, two per rank
+    (hierarchical_groups): group FedAvg, cloud term (G N_g)/N, ordered sums -> bit-exact on every
+    rank (ordered_all) and on dst 7 (ordered)."""
+    from oracle import orc
+    from fedml_amd.distributed.group_reduce import GroupReducer
+    M, P = 3, 3001
+    for gpr in (1, 2):
+        G = world * gpr
+        xs, counts = _clients(G * M, P, seed=40 + gpr)
+        N = sum(counts)
+        terms = []
+        for g in range(G):
+            cg = counts[g * M:(g + 1) * M]
+            Gj = orc.weighted_sum(xs[g * M:(g + 1) * M], 0, [c / sum(cg) for c in cg])
+            terms.append(orc.weighted_sum([Gj], 1, [sum(cg)], float(N)))
+        rank_terms = [orc.weighted_sum(terms[r * gpr:(r + 1) * gpr], 2) if gpr > 1 else terms[r] for r in range(world)]
+        exp = orc.weighted_sum(rank_terms, 2)
+        my_groups = list(range(rank * gpr, (rank + 1) * gpr))
+        my_x = [xs[i] for g in my_groups for i in range(g * M, (g + 1) * M)]
+        gcounts = [counts[g * M:(g + 1) * M] for g in my_groups]
+        for coll, dst in (("ordered_all", 0), ("ordered", world - 1)):
+            red = GroupReducer(collective=coll, dst=dst, chunks=3, local_sum=_oracle_sum)
+            got = red.hierarchical_groups(my_x, gcounts, N)
+            if coll == "ordered_all" or rank == dst:
+                assert _bits(got, exp), (gpr, coll)
+
+
+def test_hier_groups_gloo_world8():
+    _spawn(_case_hier_groups_world, world=8)

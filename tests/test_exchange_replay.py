@@ -123,3 +123,27 @@ def test_ops_are_deterministic_and_pure():
     assert a == b and len(a) == 6 + 7  # its pieces to the 6 other owners; their 7 senders (root included) in
     root_ops = ops(125_000_000, 8, 1024, 8, 0, 0, False, 0, 5)
     assert all(o[1] for o in root_ops) and len(root_ops) == 7  # the root only sends in phase 0
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("loop", [False, True])
+@pytest.mark.parametrize("to_all", [False, True])
+def test_owned_pieces_are_in_d_out(world, loop, to_all):
+    """NativeExchange.owned(rank) names only pieces that rank's d_out really holds after the exchange
+    (replayed): under loopback + "ordered" a non-root owner sums into scratch, so it owns nothing
+    there; without loopback the owner's sum lands in its d_out at the piece's place."""
+    import types
+    from fedml_amd.distributed.native_exchange import NativeExchange
+    n, chunks, align, root = 1024 * 100 + 17, 4, 1024, 0
+    out, exp = replay(n, chunks, align, world, root, to_all, seed=world * 7 + 3, loop=loop)
+    for r in range(world):
+        x = object.__new__(NativeExchange)
+        x.collective, x.chunks, x.root, x.loopback = ("ordered_all" if to_all else "ordered"), chunks, root, loop
+        x.comm = types.SimpleNamespace(world=world, rank=r)
+        owned = x.owned(n, align)
+        if loop and not to_all and r != root:
+            assert owned == []
+        elif not loop and r == root:
+            assert owned == []  # the root owns no piece without loopback
+        for lo, hi in owned:
+            assert np.array_equal(out[r][lo:hi].view(np.int32), exp[lo:hi].view(np.int32)), (r, lo, hi)

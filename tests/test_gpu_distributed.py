@@ -268,3 +268,26 @@ def test_native_loopback_partial_and_repeat(pg, chunks):
         got = red.native.run(NativeExchange.partial(part), part.numel(), 256)
         torch.cuda.synchronize()
         assert _same_bits(got, orc.weighted_sum([x], 2))
+
+
+def test_scratch_bytes_and_reduce_agree_on_loopback(pg):
+    """fa_group_reduce_scratch_bytes rejects FA_XCHG_LOOPBACK on the non-ordered exchanges exactly as
+    fa_group_reduce does (both FA_ERR_INVALID), and accepts it on the ordered ones."""
+    import ctypes
+    from fedml_amd import _native as N
+    from fedml_amd.distributed.group_reduce import _native_comm
+    from fedml_amd.distributed.native_exchange import NativeExchange
+    comm = _native_comm(None)
+    part = torch.zeros(4096, device="cuda")
+    st, _, _ = NativeExchange.partial(part)
+    need = ctypes.c_int64()
+    L = N.lib()
+    for x in (N.XCHG_REDUCE, N.XCHG_ALL_REDUCE, N.XCHG_REDUCE_SCATTER):
+        assert L.fa_group_reduce_scratch_bytes(comm.handle, x | N.XCHG_LOOPBACK, ctypes.byref(st), 4096, 2, 256, 0,
+                                               ctypes.byref(need)) == N.FA_ERR_INVALID
+        assert "LOOPBACK" in L.fa_last_error().decode()
+    for x in (N.XCHG_ORDERED, N.XCHG_ORDERED_ALL):
+        assert L.fa_group_reduce_scratch_bytes(comm.handle, x | N.XCHG_LOOPBACK, ctypes.byref(st), 4096, 2, 256, 0,
+                                               ctypes.byref(need)) == N.FA_OK
+    assert L.fa_group_reduce_scratch_bytes(comm.handle, 9, ctypes.byref(st), 4096, 2, 256, 0,
+                                           ctypes.byref(need)) == N.FA_ERR_INVALID
