@@ -980,8 +980,57 @@ def wl_lr(args, eng, rank, world, timer):
                 "sample": f"median of 2000 calls of oracle/torch_port.agg('FedAvg') (agg_operator.py:35-44) on the "
                           f"same K={K} CPU state_dicts"}
 
+    extra = {}
+
+    def host_breakeven():
+        """Host-resident rounds: agg() latency with the round summed on the host (host_sum.h) vs sent
+        to the device (FEDML_AMD_HOST_CPU_BYTES=0: the zero-copy kernel), over round sizes -- the
+        measurement behind state_dict_agg._HOST_CPU_BYTES.  Both results compared bit for bit."""
+        from fedml_amd.ml.aggregator import state_dict_agg as sda
+        rows = []
+        old = os.environ.get("FEDML_AMD_HOST_CPU_BYTES")
+        try:
+            for kk, pp in ((2, 7850), (2, 32768), (8, 16384), (8, 32768), (8, 65536), (8, 131072), (16, 131072)):
+                gg = torch.Generator().manual_seed(kk * 7 + pp)
+                ds = [OrderedDict([("w", torch.randn(pp - 10, generator=gg)), ("b", torch.randn(10, generator=gg))])
+                      for _ in range(kk)]
+                rr = list(zip(client_counts(kk), ds))
+                lat, outs = {}, {}
+                for path, thr in (("host", str(1 << 40)), ("device", "0")):
+                    os.environ["FEDML_AMD_HOST_CPU_BYTES"] = thr
+                    ts = []
+                    for it in range(400):
+                        t0 = time.perf_counter()
+                        o = FedMLAggOperator.agg(A, rr)
+                        ts.append(time.perf_counter() - t0)
+                    lat[path] = float(np.median(ts[50:])) * 1e6
+                    outs[path] = o
+                bad = sum(count_bad(outs["host"][k].reshape(-1), outs["device"][k].reshape(-1)) for k in outs["host"])
+                rows.append({"K": kk, "params": pp, "bytes": kk * pp * 4, "host_us": round(lat["host"], 2),
+                             "device_us": round(lat["device"], 2), "host_vs_device_mismatches": bad})
+        finally:
+            if old is None:
+                os.environ.pop("FEDML_AMD_HOST_CPU_BYTES", None)
+            else:
+                os.environ["FEDML_AMD_HOST_CPU_BYTES"] = old
+        extra["host_breakeven"] = {"threshold_bytes": sda._host_cpu_bytes(), "rows": rows,
+                                   "note": "median agg() latency (us) of CPU dicts -> CPU result; host = "
+                                           "summed where the data is (fedml_amd/csrc/host_sum.h), device = "
+                                           "the zero-copy kernel k_wsum_host1"}
+
+    def parity_and_sweep():
+        p = parity()
+        if mode == "host":
+            from fedml_amd.ml.aggregator import state_dict_agg as sda
+            extra["host_path"] = ("host sum (fedml_amd/csrc/host_sum.h)" if K * P * 4 <= sda._host_cpu_bytes()
+                                  else "device (k_wsum_host1, zero-copy)")
+            if os.environ.get("FEDML_AMD_BENCH_LR_SWEEP", "1") == "1":
+                host_breakeven()
+        return p
+
     P = sum(int(np.prod(s)) for _, s, _ in layout)
-    return dict(name=f"fedavg_lr_mnist_K{K}_P{P}_{mode}", dtype="fp32", step=step, parity=parity, cpu=cpu,
+    return dict(name=f"fedavg_lr_mnist_K{K}_P{P}_{mode}", dtype="fp32", step=step, parity=parity_and_sweep, cpu=cpu,
+                extra_line=extra,
                 latency=True, stat="median", clients=K, params=P, cpu_K=K, bytes_total=None, launch_bytes=None,
                 data=f"synthetic LR-MNIST updates (784x10 + 10 fp32), {'CPU' if mode == 'host' else 'device'} "
                      f"state_dicts{' adopted into arena rows' if mode == 'adopted' else ''}",

@@ -388,6 +388,14 @@ __device__ __forceinline__ void wsum_tile(const Seg* __restrict__ segs, int nseg
 // translation caches see a few segments' allocations instead of all of them)
 __device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t tiles) { return xcd_tile_map(bid, tiles); }
 
+bool xcd_map_single() {  // FA_XCD_MAP=2: XCD-contiguous tiles for single-segment staged launches too (A/B)
+  static const int on = [] {
+    const char* e = getenv("FA_XCD_MAP");
+    return e && e[0] == '2' ? 1 : 0;
+  }();
+  return on != 0;
+}
+
 bool xcd_map_enabled() {  // FA_XCD_MAP=0: round-robin workgroup -> tile order everywhere (A/B)
   static const int on = [] {
     const char* e = getenv("FA_XCD_MAP");
@@ -927,7 +935,7 @@ void launch_wsum(int64_t tiles, hipStream_t st, const Seg* segs, int nseg, const
   // interleaved A/B: fragmented metric (26,112 tensors) 10.76-10.83 -> 10.64 ms.  One flat segment
   // keeps the hardware's round-robin (tools/layout_probe.py: an XCD-contiguous split read 6.38-6.45
   // vs 6.62-6.72 TB/s there).
-  const int xcd = xcd_map_enabled() && nseg > 1 ? 1 : 0;
+  const int xcd = xcd_map_enabled() && (nseg > 1 || xcd_map_single()) ? 1 : 0;
   hipLaunchKernelGGL((k_wsum<DT, MODE, U, S, NT, PF>), dim3((unsigned)tiles), dim3(kBlock), 0, st, segs,
                      nseg, coef, ptrs, k, divisor, sstr, xcd);
 }

@@ -3,9 +3,14 @@
 // A state_dict round hands the engine K client dicts x T keys = K*T tensors (ViT-B/16 at K=128:
 // 19,456).  Walking them in Python to validate and collect data pointers costs ~1 us per tensor,
 // i.e. longer than the GPU takes to aggregate them.  This helper does the walk in C++ (tens of ns
-// per tensor) and also carves the outputs out of one device allocation.  It never touches tensor
-// DATA: all arithmetic stays in the HIP kernels behind the C ABI (include/fedagg.h).
+// per tensor) and also carves the outputs out of one device allocation.  It touches tensor DATA in
+// one place only: small_host_round's host-resident rounds below the measured break-even size
+// (host_sum.h: the kernels' per-element contract on the CPU that already holds the data, where a
+// PCIe round trip alone costs more than the reference's whole CPU loop); every other round's
+// arithmetic is in the HIP kernels behind the C ABI (include/fedagg.h).
 #include <torch/extension.h>
+
+#include "host_sum.h"
 
 #include <algorithm>
 #include <cstring>
@@ -329,7 +334,7 @@ bool match_rows(py::list dicts, py::list keys, torch::Tensor base, torch::Tensor
   return true;
 }
 
-// small_host_round(dicts, keys, mode, coef, divisor, fn, err_fn, ctx, stream, max_bytes) ->
+// small_host_round(dicts, keys, mode, coef, divisor, fn, err_fn, ctx, stream, max_bytes, cpu_max_bytes) ->
 // OrderedDict | None: a whole small host-resident round (cfg1, the reference's quick_start: K = 2
 // LR-MNIST dicts, 63 KB a client) in one call -- the walk of gather(), the CPU outputs of
 // alloc_outputs() and one call of the C ABI's fa_weighted_sum_host per dtype group, through the
@@ -339,12 +344,15 @@ bool match_rows(py::list dicts, py::list keys, torch::Tensor base, torch::Tensor
 // None -- the general path then runs and raises the reference's errors -- unless every value is a
 // contiguous CPU tensor of a C-ABI dtype, the clients agree on every key's dtype and shape, and the
 // round's input bytes are <= max_bytes with K, T <= 4096 (fa_weighted_sum_host's table limits).
+// Rounds of at most cpu_max_bytes input bytes are summed right here on the host instead
+// (fa_host::sum_key_any, host_sum.h: the same ordered per-element arithmetic, bit for bit) -- the
+// engine's measured break-even below which a PCIe round trip costs more than the sum itself.
 using wsum_host_fn = int (*)(void*, int, int, int32_t, const int64_t*, int32_t, const void* const*, const double*,
                              double, void* const*, void*);
 using last_error_fn = const char* (*)();
 
 py::object small_host_round(py::list dicts, py::list keys, int mode, py::object coef, double divisor, int64_t fn,
-                            int64_t err_fn, int64_t ctx, int64_t stream, int64_t max_bytes) {
+                            int64_t err_fn, int64_t ctx, int64_t stream, int64_t max_bytes, int64_t cpu_max_bytes) {
   const int64_t K = (int64_t)py::len(dicts);
   const int64_t T = (int64_t)py::len(keys);
   if (K == 0 || T == 0 || K > 4096 || T > 4096) return py::none();
@@ -409,7 +417,16 @@ py::object small_host_round(py::list dicts, py::list keys, int mode, py::object 
   char* base = (char*)arena.data_ptr();
   // one C-ABI call per dtype group (key-major tables, keys in their dict order within a group)
   int rc = 0;
-  {
+  if (in_bytes <= cpu_max_bytes) {  // small host-resident round: summed where the data already is
+    py::gil_scoped_release nogil;
+    std::vector<const void*> in((size_t)K);
+    for (int64_t t = 0; t < T && rc == 0; ++t) {
+      for (int64_t i = 0; i < K; ++i) in[i] = (const void*)ptr[t * K + i];
+      rc = fa_host::sum_key_any(code[t], mode, numel[t], (int)K, in.data(), mode == 2 ? nullptr : w.data(), divisor,
+                                base + off[t]);
+    }
+    if (rc != 0) throw std::runtime_error("small_host_round: host sum rejected a dtype / mode");
+  } else {
     py::gil_scoped_release nogil;
     std::vector<int64_t> gn, gin, gout;
     for (int c = 0; c <= 4 && rc == 0; ++c) {
@@ -456,7 +473,10 @@ py::object small_host_round(py::list dicts, py::list keys, int mode, py::object 
 }
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
-  m.def("small_host_round", &small_host_round, "a whole small host-resident round through fa_weighted_sum_host");
+  m.def("small_host_round", &small_host_round,
+        "a whole small host-resident round: summed on the host below cpu_max_bytes, else through fa_weighted_sum_host",
+        py::arg("dicts"), py::arg("keys"), py::arg("mode"), py::arg("coef"), py::arg("divisor"), py::arg("fn"),
+        py::arg("err_fn"), py::arg("ctx"), py::arg("stream"), py::arg("max_bytes"), py::arg("cpu_max_bytes") = 0);
   m.def("match_rows", &match_rows, "are these state_dicts the row views of one arena?");
   m.def("pack_range", &pack_range, "multi-threaded packing of host tensors into a pinned staging range");
   m.doc() = "host-side table builder of the fedml_amd aggregation engine (no tensor data access)";

@@ -63,7 +63,7 @@ def aggregate(dicts: Sequence[Dict[str, torch.Tensor]], mode: int, coef: Optiona
         fn, err, ctx = eng.host_round_abi()
         with eng.lock:
             out = _host.small_host_round(dicts if isinstance(dicts, list) else list(dicts), keys, mode, coef,
-                                         divisor, fn, err, ctx, 0, _SMALL_HOST_BYTES)
+                                         divisor, fn, err, ctx, 0, _SMALL_HOST_BYTES, _host_cpu_bytes())
         if out is not None:
             return out
     hit = resident_rows(dicts)
@@ -112,6 +112,19 @@ def _host_small() -> bool:
 
 
 _SMALL_HOST_BYTES = 4 << 20             # CPU rounds up to this size: zero-copy kernel (fa_weighted_sum_host)
+
+
+def _host_cpu_bytes() -> int:
+    """Host-resident rounds of at most this many input bytes are summed on the host that holds them
+    (_host.small_host_round's host branch, fedml_amd/csrc/host_sum.h), larger ones go to the device:
+    the break-even measured on the GPU box -- a device round trip costs at
+    least the 13.7 us PCIe doorbell floor, more than the reference's whole 10.9 us CPU loop for
+    cfg1.  FEDML_AMD_HOST_CPU_BYTES overrides it (0: every host round on the device)."""
+    v = os.environ.get("FEDML_AMD_HOST_CPU_BYTES")
+    return int(v) if v not in (None, "") else _HOST_CPU_BYTES
+
+
+_HOST_CPU_BYTES = 1 << 20  # profiles/r05c/lr.json: host 2.6-2.8x faster than the device path up to 1 MiB
 _HOST_MAX_TABLE = 4096                  # fa_weighted_sum_host's limit on num_segments and on k
 
 

@@ -11,6 +11,8 @@ setup(
     version="0.1.0",
     packages=["fedml_amd"],
     ext_modules=[CppExtension("fedml_amd._host", ["fedml_amd/csrc/host_tables.cpp"],
-                              extra_compile_args=["-O2", "-std=c++17"])],
+                              extra_compile_args=["-O3", "-std=c++17",
+                                                  # host_sum.h: IEEE per-op rounding, never FMA
+                                                  "-ffp-contract=off", "-fno-fast-math"])],
     cmdclass={"build_ext": BuildExtension},
 )

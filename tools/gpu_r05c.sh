@@ -21,6 +21,9 @@ for rep in 1 2; do
   timeout -k 10 300 python bench.py $B --check-samples 0 > $O/$n.json 2> $O/$n.err || { tail -5 $O/$n.err; exit 1; }
   line $O/$n.json
 done
+# cfg1 with the host-resident sum (host_sum.h) and the host/device break-even sweep
+timeout -k 10 300 python bench.py --config lr > $O/lr.json 2> $O/lr.err || { tail -5 $O/lr.err; exit 1; }
+python -c "import json;d=json.loads(open('$O/lr.json').read().strip().splitlines()[-1]);print('lr',d['value'],d['unit'],d.get('latency_ms'),d['cpu_baseline']['value'],d['parity'],d.get('host_path'));[print(r) for r in d['host_breakeven']['rows']]"
 C1="TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum TCP_UTCL1_TRANSLATION_MISS_UNDER_MISS_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE"
 for v in 5 6; do
   timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $C1 --kernel-include-regex 'k_wsum' -d $O/pmc_tensors_v$v -o pmc --output-format csv -- python3 bench.py --layout tensors --variant $v --steps 3 --warmup 1 --no-cpu-baseline --check-samples 0 --soak-seconds 0 > $O/pmc_tensors_v$v.log 2>&1 \
