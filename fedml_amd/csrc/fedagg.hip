@@ -388,6 +388,8 @@ __device__ __forceinline__ void wsum_tile(const Seg* __restrict__ segs, int nseg
 // translation caches see a few segments' allocations instead of all of them)
 __device__ __forceinline__ int64_t xcd_tile(int64_t bid, int64_t tiles) { return xcd_tile_map(bid, tiles); }
 
+constexpr int kXcdMinClients = 32;  // single flat segments with at least this many client vectors: XCD map
+
 bool xcd_map_single() {  // FA_XCD_MAP=2: XCD-contiguous tiles for single-segment staged launches too (A/B)
   static const int on = [] {
     const char* e = getenv("FA_XCD_MAP");
@@ -404,6 +406,14 @@ bool xcd_map_enabled() {  // FA_XCD_MAP=0: round-robin workgroup -> tile order e
   return on != 0;
 }
 
+// XCD-contiguous tiles (xcd_tile) with workgroup 0 and the workgroup the map gives the last tile
+// swapped: the ragged last tile still starts first (a bijection of [0, tiles))
+__device__ __forceinline__ int64_t xcd_tail_first(int64_t bid, int64_t tiles) {
+  const int64_t m = xcd_tile(bid, tiles);
+  if (bid == 0) return tiles - 1;
+  return m == tiles - 1 ? xcd_tile(0, tiles) : m;
+}
+
 // one segment: workgroup 0 takes the last tile (ragged: the scalar path, one pass over every client
 // per element) so that it overlaps the stream instead of running alone after it (r04aa / r04ab)
 __device__ __forceinline__ int64_t tail_first(int nseg) {
@@ -414,7 +424,8 @@ template <int DT, int MODE, int U, int S, bool NT, bool PF>
 __global__ void __launch_bounds__(kBlock)
 k_wsum(const Seg* __restrict__ segs, int nseg, const double* __restrict__ coef,
        const void* const* __restrict__ ptrs, int k, double divisor, int64_t sstr, int xcd) {
-  const int64_t t = xcd ? xcd_tile(blockIdx.x, gridDim.x) : tail_first(nseg);
+  const int64_t t = xcd ? (nseg == 1 ? xcd_tail_first(blockIdx.x, gridDim.x) : xcd_tile(blockIdx.x, gridDim.x))
+                        : tail_first(nseg);
   wsum_tile<DT, MODE, U, S, NT, PF>(segs, nseg, coef, ptrs, k, divisor, sstr, t);
 }
 
@@ -430,9 +441,9 @@ struct InlineDesc {
 
 template <int DT, int MODE, int U, int S, bool NT, bool PF>
 __global__ void __launch_bounds__(kBlock)
-k_wsum_inl(const InlineDesc dsc, int nseg, int coef_off, int ptr_off, int k, double divisor, int64_t sstr) {
+k_wsum_inl(const InlineDesc dsc, int nseg, int coef_off, int ptr_off, int k, double divisor, int64_t sstr, int xcd) {
   const char* b = dsc.raw;
-  const int64_t t = tail_first(nseg);
+  const int64_t t = xcd ? xcd_tail_first((int64_t)blockIdx.x, (int64_t)gridDim.x) : tail_first(nseg);
   wsum_tile<DT, MODE, U, S, NT, PF>((const Seg*)b, nseg, (const double*)(b + coef_off),
                                     (const void* const*)(b + ptr_off), k, divisor, sstr, t);
 }
@@ -935,7 +946,7 @@ void launch_wsum(int64_t tiles, hipStream_t st, const Seg* segs, int nseg, const
   // interleaved A/B: fragmented metric (26,112 tensors) 10.76-10.83 -> 10.64 ms.  One flat segment
   // keeps the hardware's round-robin (tools/layout_probe.py: an XCD-contiguous split read 6.38-6.45
   // vs 6.62-6.72 TB/s there).
-  const int xcd = xcd_map_enabled() && (nseg > 1 || xcd_map_single()) ? 1 : 0;
+  const int xcd = xcd_map_enabled() && (nseg > 1 || xcd_map_single() || (sstr == 0 && k >= kXcdMinClients)) ? 1 : 0;
   hipLaunchKernelGGL((k_wsum<DT, MODE, U, S, NT, PF>), dim3((unsigned)tiles), dim3(kBlock), 0, st, segs,
                      nseg, coef, ptrs, k, divisor, sstr, xcd);
 }
@@ -944,12 +955,17 @@ void launch_wsum(int64_t tiles, hipStream_t st, const Seg* segs, int nseg, const
 template <int DT, int MODE>
 void launch_wsum_inl(int variant, int64_t tiles, hipStream_t st, const InlineDesc& dsc, int nseg, int coef_off,
                      int ptr_off, int k, double divisor, int64_t sstr) {
+  // one flat segment over many separately placed client vectors (not a tiled arena): XCD-contiguous
+  // tiles, so the workgroups sharing a CU / XCD read neighbouring tiles and reuse their address
+  // translations (r05e, 128 separate fp32[125 M] buffers, 2 interleaved reps: 10.43-10.58 ->
+  // 10.26-10.30 ms; UTCL1 misses -27 %, profiles/r05b/translation_summary.json)
+  const int xcd = nseg == 1 && sstr == 0 && k >= kXcdMinClients && xcd_map_enabled() ? 1 : 0;
   if (variant == 5)
     hipLaunchKernelGGL((k_wsum_inl<DT, MODE, 8, 2, true, false>), dim3((unsigned)tiles), dim3(kBlock), 0, st, dsc,
-                       nseg, coef_off, ptr_off, k, divisor, sstr);
+                       nseg, coef_off, ptr_off, k, divisor, sstr, xcd);
   else
     hipLaunchKernelGGL((k_wsum_inl<DT, MODE, 8, 1, true, false>), dim3((unsigned)tiles), dim3(kBlock), 0, st, dsc,
-                       nseg, coef_off, ptr_off, k, divisor, sstr);
+                       nseg, coef_off, ptr_off, k, divisor, sstr, xcd);
 }
 
 template <int DT>
@@ -1661,9 +1677,10 @@ void launch_pair(int64_t tiles, hipStream_t st, const char* dev, const InlineDes
 }
 
 template <int DT>
-void pair_modes(int mode, bool k16, int64_t tiles, hipStream_t st, const char* dev, const InlineDesc* dsc,
+void pair_modes(int mode, bool k16, bool s4, int64_t tiles, hipStream_t st, const char* dev, const InlineDesc* dsc,
                 const PairTables& L, const PairArgs& a) {
-#define FA_PM(MODE) (k16 ? launch_pair<DT, MODE, 2>(tiles, st, dev, dsc, L, a) : launch_pair<DT, MODE, 1>(tiles, st, dev, dsc, L, a))
+#define FA_PM(MODE) (s4 ? launch_pair<DT, MODE, 4>(tiles, st, dev, dsc, L, a) : k16 ? launch_pair<DT, MODE, 2>(tiles, st, dev, dsc, L, a) \
+                         : launch_pair<DT, MODE, 1>(tiles, st, dev, dsc, L, a))
   switch (mode) {
     case FA_MODE_MUL_W: FA_PM(FA_MODE_MUL_W); break;
     case FA_MODE_MUL_N_DIV_N: FA_PM(FA_MODE_MUL_N_DIV_N); break;
@@ -1697,12 +1714,22 @@ int pair_impl(fa_ctx* ctx, int dtype, int mode, int32_t nseg0, const int64_t* nu
     const char* e = getenv("FA_PAIR_S");
     return e && e[0] == '2';
   }();
-  const bool k16 = k <= 16 || s2;
+  // FA_PAIR_S=4: four slots per client and workgroup (A/B: fewer address-translation misses per byte
+  // on separately allocated tensors, profiles/r05c)
+  // Default: four slots when the float group is flat (separate tensors / client-major rows, sstr0 = 0)
+  // and K >= 32 -- r05f, cfg2 on 3,904 separate tensors, 3 interleaved pairs: 0.2776-0.2813 ->
+  // 0.2727-0.2777 ms/step; the tiled arena keeps one slot (FA_PAIR_S=1 forces one slot everywhere)
+  static const int s_env = [] {
+    const char* e = getenv("FA_PAIR_S");
+    return e ? atoi(e) : 0;
+  }();
+  const bool s4 = s_env == 4 || (s_env == 0 && sstr0 == 0 && k >= 32);
+  const bool k16 = !s4 && (k <= 16 || s2);
   const int nsg[2] = {nseg0, nseg1};
   const int64_t* numel[2] = {numel0, numel1};
   const void* const* din[2] = {d_in0, d_in1};
   void* const* dout[2] = {d_out0, d_out1};
-  const int64_t te[2] = {(int64_t)kBlock * elems_per_vec(dtype) * (k16 ? 2 : 1),
+  const int64_t te[2] = {(int64_t)kBlock * elems_per_vec(dtype) * (s4 ? 4 : k16 ? 2 : 1),
                          (int64_t)kBlock * elems_per_vec(FA_DTYPE_I64)};
   int live[2] = {0, 0};
   int64_t tiles[2] = {0, 0};
@@ -1772,10 +1799,10 @@ int pair_impl(fa_ctx* ctx, int dtype, int mode, int32_t nseg0, const int64_t* nu
   const int64_t total = tiles[0] + tiles[1];
   const InlineDesc* dp = inl ? &dsc : nullptr;
   switch (dtype) {
-    case FA_DTYPE_F32: pair_modes<FA_DTYPE_F32>(mode, k16, total, st, dev, dp, L, a); break;
-    case FA_DTYPE_BF16: pair_modes<FA_DTYPE_BF16>(mode, k16, total, st, dev, dp, L, a); break;
-    case FA_DTYPE_F16: pair_modes<FA_DTYPE_F16>(mode, k16, total, st, dev, dp, L, a); break;
-    case FA_DTYPE_F64: pair_modes<FA_DTYPE_F64>(mode, k16, total, st, dev, dp, L, a); break;
+    case FA_DTYPE_F32: pair_modes<FA_DTYPE_F32>(mode, k16, s4, total, st, dev, dp, L, a); break;
+    case FA_DTYPE_BF16: pair_modes<FA_DTYPE_BF16>(mode, k16, s4, total, st, dev, dp, L, a); break;
+    case FA_DTYPE_F16: pair_modes<FA_DTYPE_F16>(mode, k16, s4, total, st, dev, dp, L, a); break;
+    case FA_DTYPE_F64: pair_modes<FA_DTYPE_F64>(mode, k16, s4, total, st, dev, dp, L, a); break;
   }
   FA_HIP(hipGetLastError());
   return inl ? FA_OK : release(slot, st);

@@ -100,12 +100,22 @@ def test_cfg1_lr_mnist_K2():
     dicts = _dicts(2, layout)
     counts = _counts(2)
     w = [c / sum(counts) for c in counts]
-    for where in ("cuda", "cpu"):
-        raw = [(n, OrderedDict((k, v.to(where)) for k, v in d.items())) for n, d in zip(counts, dicts)]
-        got = FedMLAggOperator.agg(types.SimpleNamespace(federated_optimizer="FedAvg"), raw)
+    for where, thr in (("cuda", None), ("cpu", None), ("cpu", "0")):
+        # CPU dicts: summed on the host below the break-even (host_sum.h, the default for cfg1's
+        # 63 KB), or through the device's zero-copy kernel (FEDML_AMD_HOST_CPU_BYTES=0)
+        old = os.environ.pop("FEDML_AMD_HOST_CPU_BYTES", None)
+        if thr is not None:
+            os.environ["FEDML_AMD_HOST_CPU_BYTES"] = thr
+        try:
+            raw = [(n, OrderedDict((k, v.to(where)) for k, v in d.items())) for n, d in zip(counts, dicts)]
+            got = FedMLAggOperator.agg(types.SimpleNamespace(federated_optimizer="FedAvg"), raw)
+        finally:
+            os.environ.pop("FEDML_AMD_HOST_CPU_BYTES", None)
+            if old is not None:
+                os.environ["FEDML_AMD_HOST_CPU_BYTES"] = old
         for name, _, _ in layout:
             exp = orc.weighted_sum([d[name].cpu() for d in dicts], MUL_W, w)
-            assert got[name].device.type == where and _bad(got[name].cpu(), exp) == 0, (where, name)
+            assert got[name].device.type == where and _bad(got[name].cpu(), exp) == 0, (where, thr, name)
 
 
 # ------------------------------------------------------------------------------------ cfg2 / cfg3

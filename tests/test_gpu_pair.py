@@ -45,7 +45,7 @@ def _data(dt, cap, n, n64, seed):
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
 @pytest.mark.parametrize("mode", [MUL_W, MUL_N_DIV_N, SUM])
-@pytest.mark.parametrize("k", [5, 20])
+@pytest.mark.parametrize("k", [5, 20, 33])
 @pytest.mark.parametrize("layout", ["rows", "tiled"])
 def test_pair_matches_separate_launches(eng, dt, mode, k, layout):
     cap = k + 3
@@ -150,7 +150,7 @@ def test_inline_descriptors_match_staged(tmp_path):
 
 @pytest.mark.parametrize("fdt", [torch.float32, torch.bfloat16, torch.float16, torch.float64])
 @pytest.mark.parametrize("mode", [MUL_W, MUL_N_DIV_N, SUM])
-@pytest.mark.parametrize("k", [3, 17])
+@pytest.mark.parametrize("k", [3, 17, 40])
 def test_state_dict_pair_multi_vs_oracle(fdt, mode, k):
     """Device state_dicts with BatchNorm counters (the drop-in agg() path): the float keys and the
     int64 keys aggregate in one fa_weighted_sum_pair_multi launch; every key equals the oracle."""

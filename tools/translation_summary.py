@@ -46,4 +46,5 @@ for lay in ("tiled", "arena", "tensors"):
     res[f"{lay} (r05b, default kernel U8 S1)"] = load(sorted(glob.glob(os.path.join(ROOT, "profiles/r05b/pmc", f"{lay}_pass*_counters.csv"))))
 for v, what in ((5, "U8 S2"), (6, "U4 S4")):
     res[f"tensors (r05c, variant {v}: {what})"] = load([os.path.join(ROOT, "profiles/r05c/pmc", f"tensors_v{v}_counters.csv")])
+res["tensors (r05e, XCD-contiguous tiles, U8 S1)"] = load([os.path.join(ROOT, "profiles/r05e/pmc", "tensors_xcd_counters.csv")])
 print(json.dumps(res, indent=1))
