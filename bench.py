@@ -1690,7 +1690,17 @@ def wl_krum(args, eng, rank, world, timer):
                            "krum_defense.py:52-66)", digits=3)
 
     pairs = K * (K - 1) // 2
-    return dict(name=f"krum_pairdist_K{K}_P{P}_fp32", dtype="fp32", step=step, parity=parity,
+    extra = {}
+
+    def parity_and_form():
+        p = parity()
+        extra["pair_form"] = getattr(eng, "last_pair_form", None)
+        extra["kappa_max"] = getattr(eng, "last_kappa_max", None)
+        extra["pair_form_note"] = ("gram: D = A_i + A_j - 2 G_ij on the matrix cores (fa_pairwise_sqdist_gram), kept "
+                                   "when kappa_max <= 16; direct: the VALU difference kernel")
+        return p
+    return dict(name=f"krum_pairdist_K{K}_P{P}_fp32", dtype="fp32", step=step, parity=parity_and_form,
+                extra_line=extra,
                 bytes_total=K * P * 4, launch_bytes=K * P * 4, clients=K, params=P, cpu_K=K, cpu=cpu,
                 data="synthetic N(0,1) client weight vectors, resident in HBM (rows 256-byte aligned)",
                 roofline_note=f"VALU work {pairs} pairs x 3 flop per coordinate = {3 * pairs * P / 1e9:.1f} GFLOP/step; "

@@ -37,6 +37,7 @@ EXPORTED_SYMBOLS = (
     "fa_mt_randint_sum_scratch_bytes",
     # include/fedagg_robust.h
     "fa_coord_median", "fa_coord_median_tiled", "fa_pairwise_sqdist", "fa_pairwise_sqdist_rt", "fa_pairwise_sqdist_scratch_bytes",
+    "fa_pairwise_sqdist_gram", "fa_pairwise_sqdist_gram_scratch_bytes",
     # include/fedagg_comm.h
     "fa_comm_unique_id", "fa_comm_init", "fa_comm_wrap", "fa_comm_destroy", "fa_comm_size", "fa_local_out_dtype",
     "fa_group_plan", "fa_group_ops", "fa_group_reduce_scratch_bytes", "fa_group_reduce", "fa_comm_set_timing", "fa_comm_local_time",
@@ -167,6 +168,11 @@ def _declare(L):
                                         ctypes.c_size_t, _vp]
     L.fa_pairwise_sqdist_scratch_bytes.restype = ctypes.c_size_t
     L.fa_pairwise_sqdist_scratch_bytes.argtypes = [ctypes.c_int32, _P_i64, ctypes.c_int32]
+    L.fa_pairwise_sqdist_gram.restype = ctypes.c_int
+    L.fa_pairwise_sqdist_gram.argtypes = [_vp, ctypes.c_int32, _P_i64, ctypes.c_int32, _P_vp, _vp, _vp,
+                                          ctypes.c_double, _vp, ctypes.c_size_t, _vp]
+    L.fa_pairwise_sqdist_gram_scratch_bytes.restype = ctypes.c_size_t
+    L.fa_pairwise_sqdist_gram_scratch_bytes.argtypes = [ctypes.c_int32, _P_i64, ctypes.c_int32]
     L.fa_weighted_sum_host.restype = ctypes.c_int
     L.fa_weighted_sum_host.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int32, _P_i64, ctypes.c_int32,
                                        _P_vp, _P_d, ctypes.c_double, _P_vp, _vp]

@@ -874,7 +874,9 @@ __device__ __forceinline__ void pair_epilogue(float* lds, const double (&accd)[1
 template <bool VEC, int RT, bool PF, int NPL>
 __global__ void __launch_bounds__(kMaxPairThreads) __attribute__((amdgpu_waves_per_eu(4)))
 k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int kp,
-           int64_t nchunks, int ntiles, int esplit, int pe, double* __restrict__ partial) {
+           int64_t nchunks, int ntiles, int esplit, int pe, double* __restrict__ partial,
+           const double* __restrict__ guard, double limit) {
+  if (guard && *guard <= limit) return;  // the Gram form's result stands (fa_pairwise_sqdist_gram)
   extern __shared__ float lds[];              // [2][pe][kp + 4]
   const int stride = kp + 4;
   const int nb = kp / 4;
@@ -1017,7 +1019,9 @@ k_pairdist_lane(const PSeg* __restrict__ segs, int nseg, const void* const* __re
 template <int KPAD, int RT, bool PF>
 __global__ void __launch_bounds__(kMaxPairThreads) __attribute__((amdgpu_waves_per_eu(4)))
 k_pairdist(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k, int kp,
-           int64_t nchunks, int ntiles, int esplit, int ce, int rows, double* __restrict__ partial) {
+           int64_t nchunks, int ntiles, int esplit, int ce, int rows, double* __restrict__ partial,
+           const double* __restrict__ guard, double limit) {
+  if (guard && *guard <= limit) return;  // the Gram form's result stands (fa_pairwise_sqdist_gram)
   constexpr int S = KPAD + 4;                    // LDS row stride (floats), 16-byte rows
   constexpr int NP = kNPS;
   extern __shared__ float lds[];                 // [2][pe][S]
@@ -1205,7 +1209,9 @@ k_pairdist_f64(const PSeg* __restrict__ segs, int nseg, const void* const* __res
 }
 
 __global__ void __launch_bounds__(kBlock)
-k_pairdist_reduce(const double* __restrict__ partial, int nblocks, int k, double* __restrict__ d) {
+k_pairdist_reduce(const double* __restrict__ partial, int nblocks, int k, double* __restrict__ d,
+                  const double* __restrict__ guard, double limit) {
+  if (guard && *guard <= limit) return;
   // kRP pairs per workgroup, kBlock / kRP lanes per pair: lane l sums blocks l, l + L, ... (each
   // load row = kRP consecutive pairs), then the L lane sums are added in lane order -- a fixed
   // order, so the result is deterministic.  (A single thread per pair made this a serial chain of
@@ -1234,6 +1240,289 @@ k_pairdist_reduce(const double* __restrict__ partial, int nblocks, int k, double
     for (int i = threadIdx.x; i < k; i += kBlock) d[(int64_t)i * k + i] = 0.0;
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Gram form of the pairwise distances on the matrix cores (r05, float32 models):
+//   D_ij = A_i + A_j - 2 G_ij,  G = Y Y^T,  A_i = G_ii,  y_i[e] = x_i[e] - c[e]
+// with c a robust per-coordinate centre (the median of clients 0..4: with at most two of them
+// Byzantine it lies inside the honest clients' range, so the honest pairs' cancellation stays small).
+// One multiply-add per pair-coordinate on v_mfma_f32_32x32x2_f32 (f32 in / f32 accumulate, the FP32
+// vector rate), instead of the direct form's sub + fma on the VALU; operands read once per 32x32 tile.
+// The form cancels: relative error ~ eps * kappa_ij, kappa_ij = (A_i + A_j) / D_ij -- the distance
+// kernel reports max kappa (k_gram_dist) and the binding reruns the direct kernel when it is large
+// or not finite (fedml_amd/engine.py pairwise_sqdist).
+//
+// Layout: a workgroup owns a contiguous run of chunks (kGE coordinates of one segment, all clients);
+// a chunk is staged x -> LDS [client][kGS] (coalesced 16-byte loads of each client row, the next chunk
+// in registers while this one is computed), the centre row is computed once per chunk, and every wave
+// runs the MFMAs of its tile(s) (32x32 client blocks bi <= bj, upper triangle incl. the diagonal) over
+// its share of the chunk's coordinate groups: lane l takes client 32*b + (l & 31) and coordinates
+// 8g + 4*(l >> 5) + 0..3 (one ds_read_b128 feeds four MFMAs; A and B are the same fragment layout,
+// so k runs over (8g + u, 8g + 4 + u)).  float32 runs of one chunk, float64 across chunks.
+constexpr int kGE = 128;       // coordinates per chunk
+constexpr int kGS = kGE + 4;   // LDS row stride (floats): 16-byte rows, b128 reads conflict-free
+typedef float gf16 __attribute__((ext_vector_type(16)));
+typedef float gf4 __attribute__((ext_vector_type(4)));
+
+template <int KB> struct GramCfg {
+  static constexpr int T = KB * (KB + 1) / 2;             // 32x32 tiles, upper triangle
+  static constexpr int R = KB == 1 ? 4 : KB == 2 ? 4 : KB == 3 ? 2 : 1;  // coordinate-group splits per tile
+  static constexpr int W = T * R;                         // waves per workgroup, one (tile, split) each:
+                                                          // 4 / 12 / 12 / 10 -- a multiple of the CU's 4
+                                                          // SIMDs except K > 96 (3, 3, 2, 2 tiles per SIMD)
+  static constexpr int NT = W * 64;
+  static constexpr int KP = 32 * KB;
+  static constexpr int NLD = (KP * (kGE / 4) + NT - 1) / NT;  // staged 16-byte vectors per thread
+  static constexpr int LDS_FLOATS = 2 * KP * kGS + W * kGE;   // two chunk buffers + a centre row per wave
+};
+
+template <int KB>
+__device__ __forceinline__ void gram_tile_kb(int t, int& bi, int& bj) {
+  int i = 0, rem = t;
+  while (rem >= KB - i) { rem -= KB - i; ++i; }
+  bi = i;
+  bj = i + rem;
+}
+
+template <int KB, bool VEC>
+__global__ void __launch_bounds__(GramCfg<KB>::NT) __attribute__((amdgpu_waves_per_eu(4)))
+k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k,
+            int64_t nchunks, double* __restrict__ partial) {
+  using C = GramCfg<KB>;
+  extern __shared__ __attribute__((aligned(16))) float gl[];
+  float* const lds0 = gl;                       // [2][KP][kGS]
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  float* const cen = gl + 2 * C::KP * kGS + w * kGE;  // this wave's centre row (wave-private: no barrier)
+  const int ti = w / C::R, r = w % C::R;  // this wave's tile and coordinate-group split
+  int bi, bj;
+  gram_tile_kb<KB>(ti, bi, bj);
+  const bool diag = bi == bj;
+  const int half = lane >> 5, lrow = lane & 31;
+  const int ra = 32 * bi + lrow, rb = 32 * bj + lrow;
+  const float ma = ra < k ? 1.0f : 0.0f, mb = rb < k ? 1.0f : 0.0f;  // padding clients: y = 0
+  gf16 acc;
+  double accd[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) { acc[q] = 0.0f; accd[q] = 0.0; }
+  // staging: 16-byte vector q of client (idx / (kGE/4)) = coordinates 4 q .. 4 q + 3 of the chunk
+  constexpr int QV = kGE / 4;
+  gf4 v[C::NLD];
+  // this thread's client pointers for the current segment (one pointer load per segment, not per
+  // chunk: a per-chunk pointer load put a full memory round trip before every data load)
+  const float* src[C::NLD];
+  int cseg = -1;
+  auto load = [&](int64_t ch) {
+    const int si = nseg > 1 ? find_seg(segs, nseg, ch) : 0;
+    const PSeg sg = segs[si];
+    if (si != cseg) {
+      cseg = si;
+#pragma unroll
+      for (int u = 0; u < C::NLD; ++u) {
+        const int idx = t + u * C::NT;
+        const int cl = idx / QV;
+        src[u] = (C::NLD * C::NT == C::KP * QV || idx < C::KP * QV) && cl < k
+                     ? (const float*)ptrs[sg.ptr_base + cl] + 4 * (idx % QV) : nullptr;
+      }
+    }
+    const int64_t b0 = (ch - sg.tile_start) * kGE;
+    const bool full = VEC && b0 + kGE <= sg.numel;  // uniform: the segment's last chunk takes the slow path
+    if (full) {  // every load issued before any is consumed
+#pragma unroll
+      for (int u = 0; u < C::NLD; ++u) {
+        const gf4 z = {0.f, 0.f, 0.f, 0.f};
+        v[u] = src[u] ? *(const __attribute__((address_space(1))) gf4*)(src[u] + b0) : z;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < C::NLD; ++u) {
+        const int idx = t + u * C::NT;
+        gf4 x = {0.f, 0.f, 0.f, 0.f};
+        if (src[u]) {
+          const int64_t left = sg.numel - (b0 + 4 * (idx % QV));
+#pragma unroll
+          for (int z = 0; z < 4; ++z) if (z < left) x[z] = gld<float>(src[u] + b0, z);
+        }
+        v[u] = x;
+      }
+    }
+  };
+  auto put = [&](int buf) {
+    float* L = lds0 + buf * C::KP * kGS;
+#pragma unroll
+    for (int u = 0; u < C::NLD; ++u) {
+      const int idx = t + u * C::NT;
+      if (C::NLD * C::NT == C::KP * QV || idx < C::KP * QV) *(gf4*)&L[(idx / QV) * kGS + 4 * (idx % QV)] = v[u];
+    }
+  };
+  const int64_t c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
+  if (c0 < c1) {
+    load(c0);
+    put(0);
+    if (c0 + 1 < c1) load(c0 + 1);
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int64_t ch = c0; ch < c1; ++ch, cur ^= 1) {
+    const float* L = lds0 + cur * C::KP * kGS;
+    // the centre of the chunk's coordinates, by every wave for itself: the median of clients 0..4
+    // (fewer clients: of 0..2, or client 0); padding coordinates are 0 everywhere, so y = 0 there
+#pragma unroll
+    for (int e = lane; e < kGE; e += 64) {
+      float c;
+      if (k >= 5) {
+        const float a = L[e], b = L[kGS + e], cc = L[2 * kGS + e], d = L[3 * kGS + e], f = L[4 * kGS + e];
+        c = __builtin_amdgcn_fmed3f(f, fmaxf(fminf(a, b), fminf(cc, d)), fminf(fmaxf(a, b), fmaxf(cc, d)));
+      } else if (k >= 3) {
+        c = __builtin_amdgcn_fmed3f(L[e], L[kGS + e], L[2 * kGS + e]);
+      } else {
+        c = L[e];
+      }
+      cen[e] = c;
+    }
+    __builtin_amdgcn_wave_barrier();  // the wave's own LDS writes are seen by its later reads (in order)
+    const float* La = L + ra * kGS + 4 * half;
+    const float* Lb = L + rb * kGS + 4 * half;
+    const float* cr = cen + 4 * half;
+#pragma unroll
+    for (int g = r; g < kGE / 8; g += C::R) {
+      const gf4 cc = *(const gf4*)&cr[8 * g];
+      const gf4 ya = (*(const gf4*)&La[8 * g] - cc) * ma;
+      const gf4 yb = diag ? ya : (*(const gf4*)&Lb[8 * g] - cc) * mb;
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.x, yb.x, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.y, yb.y, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.z, yb.z, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.w, yb.w, acc, 0, 0, 0);
+    }
+    // float32 run of one chunk (kGE / R coordinates of this split) -> float64
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      accd[q] += (double)acc[q];
+      acc[q] = 0.0f;
+    }
+    if (ch + 1 < c1) {
+      put(cur ^ 1);  // chunk ch + 1 (in registers); buffer cur ^ 1 was last read before the last barrier
+      if (ch + 2 < c1) load(ch + 2);
+    }
+    __syncthreads();  // one barrier per chunk
+  }
+  // the R splits of a tile summed in split order through LDS (the chunk buffers are free now), then
+  // partial[(block * T + tile) * 1024 + row * 32 + col]; C/D layout of the 32x32 f32 MFMA: register q
+  // of lane l holds row (q & 3) + 8 (q >> 2) + 4 (l >> 5), column l & 31
+  double* red = (double*)gl;  // [W][1024]
+  if (C::R > 1) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) red[(int64_t)w * 1024 + q * 64 + lane] = accd[q];
+    __syncthreads();
+  }
+  if (r == 0) {
+    double* o = partial + ((int64_t)blockIdx.x * C::T + ti) * 1024;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      double s = accd[q];
+      for (int rr = 1; rr < C::R; ++rr) s += red[(int64_t)(w + rr) * 1024 + q * 64 + lane];
+      const int row = (q & 3) + 8 * (q >> 2) + 4 * half;
+      o[row * 32 + lrow] = s;
+    }
+  }
+}
+
+// G entries of the T tiles summed over the per-block partials in a fixed order (lanes over block
+// ranges, then lane order), written to g (KP x KP, upper tiles only).
+template <int KB>
+__global__ void __launch_bounds__(kBlock)
+k_gram_reduce(const double* __restrict__ partial, int nparts, double* __restrict__ g) {
+  using C = GramCfg<KB>;
+  constexpr int kRP = 8, L = kBlock / kRP;
+  __shared__ double red[L][kRP + 1];
+  const int pl = threadIdx.x % kRP, ln = threadIdx.x / kRP;
+  const int64_t e = (int64_t)blockIdx.x * kRP + pl;  // entry = tile * 1024 + row * 32 + col
+  const int64_t nent = (int64_t)C::T * 1024;
+  double s = 0.0;
+  if (e < nent)
+    for (int b = ln; b < nparts; b += L) s += partial[(int64_t)b * nent + e];
+  red[ln][pl] = s;
+  __syncthreads();
+  if (ln == 0 && e < nent) {
+    double tsum = 0.0;
+    for (int l = 0; l < L; ++l) tsum += red[l][pl];
+    int bi, bj;
+    gram_tile_kb<KB>((int)(e / 1024), bi, bj);
+    const int row = (int)(e % 1024) / 32, col = (int)(e % 32);
+    g[(int64_t)(32 * bi + row) * C::KP + 32 * bj + col] = tsum;
+  }
+}
+
+// D_ij = A_i + A_j - 2 G_ij (G from the upper tiles) for row i = blockIdx.x, j > i, into the k x k
+// matrix; the row's largest kappa_ij = (A_i + A_j) / D_ij (+inf for D_ij <= 0 or a NaN) to rowmax[i].
+__global__ void __launch_bounds__(128)
+k_gram_dist(const double* __restrict__ g, int kp, int k, double* __restrict__ d, double* __restrict__ rowmax) {
+  __shared__ double red[128];
+  const int i = blockIdx.x, j = threadIdx.x;
+  double m = 0.0;
+  if (j < k) {
+    if (j > i) {
+      const double ai = g[(int64_t)i * kp + i], aj = g[(int64_t)j * kp + j], gij = g[(int64_t)i * kp + j];
+      const double dd = ai + aj - 2.0 * gij;
+      d[(int64_t)i * k + j] = dd;
+      d[(int64_t)j * k + i] = dd;
+      const double kap = (ai + aj) / dd;
+      m = dd > 0.0 && kap == kap ? kap : __builtin_inf();
+    } else if (j == i) {
+      d[(int64_t)i * k + i] = 0.0;
+    }
+  }
+  red[j] = m;
+  __syncthreads();
+  for (int s = 64; s > 0; s >>= 1) {
+    if (j < s) red[j] = fmax(red[j], red[j + s]);
+    __syncthreads();
+  }
+  if (j == 0) rowmax[i] = red[0];
+}
+
+__global__ void __launch_bounds__(128) k_gram_kmax(const double* __restrict__ rowmax, int k, double* __restrict__ kmax) {
+  __shared__ double red[128];
+  const int j = threadIdx.x;
+  red[j] = j < k ? rowmax[j] : 0.0;
+  __syncthreads();
+  for (int s = 64; s > 0; s >>= 1) {
+    if (j < s) red[j] = fmax(red[j], red[j + s]);
+    __syncthreads();
+  }
+  if (j == 0) *kmax = red[0];
+}
+
+// workgroups: one per CU for K > 32 (12 / 12 / 10 waves, <= 128 VGPRs: 16 waves per CU), four per CU
+// for K <= 32 (4 waves; the read, not the MFMAs, bounds it)
+int gram_nblocks(int64_t nchunks, int kb) {
+  static const int ov = [] {  // FA_GRAM_BLOCKS: measurement override (A/B)
+    const char* e = getenv("FA_GRAM_BLOCKS");
+    return e ? atoi(e) : 0;
+  }();
+  const int64_t cap = ov >= 64 && ov <= 8192 ? ov : kb >= 2 ? 256 : 1024;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, cap));
+}
+
+int gram_T(int kb) { return kb * (kb + 1) / 2; }
+size_t gram_scratch(int32_t num_segments, const int64_t* seg_numel, int32_t k) {
+  int64_t nchunks = 0;
+  for (int s = 0; s < num_segments; ++s)
+    if (seg_numel[s] > 0) nchunks += (seg_numel[s] + kGE - 1) / kGE;
+  const int kb = (k + 31) / 32;
+  const size_t parts = (size_t)gram_nblocks(nchunks, kb);
+  return align16(sizeof(double) * (parts * gram_T(kb) * 1024 + (size_t)(32 * kb) * (32 * kb) + 128));
+}
+
+size_t gram_lds(int kb) {
+  const int T = gram_T(kb), R = kb == 1 ? 4 : kb == 2 ? 4 : kb == 3 ? 2 : 1, W = T * R;
+  const size_t stage = sizeof(float) * (2 * (size_t)(32 * kb) * kGS + (size_t)W * kGE);
+  return std::max(stage, sizeof(double) * 1024 * (size_t)W);  // the epilogue's split reduction
+}
+
+int pairdist_direct(fa_ctx* ctx, int diff_dtype, int32_t num_segments, const int64_t* seg_numel, int32_t k,
+                    const void* const* d_in, void* d_dist, void* d_scratch, size_t scratch_bytes, void* hip_stream,
+                    const double* guard, double limit);
+
 }  // namespace
 
 extern "C" {
@@ -1248,6 +1537,18 @@ int fa_pairwise_sqdist(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_num
 int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, const int64_t* seg_numel, int32_t k,
                           const void* const* d_in, void* d_dist, void* d_scratch, size_t scratch_bytes,
                           void* hip_stream) {
+  return pairdist_direct(ctx, diff_dtype, num_segments, seg_numel, k, d_in, d_dist, d_scratch, scratch_bytes,
+                         hip_stream, nullptr, 0.0);
+}
+
+}  // extern "C"
+
+namespace {
+// The direct (difference) kernels.  guard != nullptr: every launch returns at once unless *guard >
+// limit -- the Gram form's fallback, decided on the device (no host round trip).
+int pairdist_direct(fa_ctx* ctx, int diff_dtype, int32_t num_segments, const int64_t* seg_numel, int32_t k,
+                    const void* const* d_in, void* d_dist, void* d_scratch, size_t scratch_bytes, void* hip_stream,
+                    const double* guard, double limit) {
   if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
   if (diff_dtype != FA_DTYPE_F32 && diff_dtype != FA_DTYPE_BF16 && diff_dtype != FA_DTYPE_F16 &&
       diff_dtype != FA_DTYPE_F64)
@@ -1326,7 +1627,7 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
 #define FA_PDL1(V, R, P) if (q.npl == 16) FA_PDL2(V, R, P, 16); else FA_PDL2(V, R, P, kNPL)
 #define FA_PDL2(V, R, P, NP) hipLaunchKernelGGL((k_pairdist_lane<V, R, P, NP>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), \
       lds, st, (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit, pe,      \
-      (double*)d_scratch)
+      (double*)d_scratch, guard, limit)
     if (vec) {
       if (rt == 1) FA_PDL(true, 1); else if (rt == 2) FA_PDL(true, 2); else FA_PDL(true, 0);
     } else {
@@ -1340,7 +1641,7 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
 #define FA_PD(KPAD, R) if (pf) FA_PD2(KPAD, R, true); else FA_PD2(KPAD, R, false)
 #define FA_PD2(KPAD, R, P) hipLaunchKernelGGL((k_pairdist<KPAD, R, P>), dim3((unsigned)nblocks), dim3((unsigned)q.nthreads), \
       lds, st, (const PSeg*)dv, nseg, (const void* const*)(dv + seg_bytes), k, kp, nchunks, ntiles, esplit, q.ce,   \
-      q.rows, (double*)d_scratch)
+      q.rows, (double*)d_scratch, guard, limit)
 #define FA_PDR(KPAD) if (rt == 1) FA_PD(KPAD, 1); else if (rt == 2) FA_PD(KPAD, 2); else FA_PD(KPAD, 0)
     switch (q.kpad) {
       case 64: FA_PDR(64); break;
@@ -1353,10 +1654,13 @@ int fa_pairwise_sqdist_rt(fa_ctx* ctx, int diff_dtype, int32_t num_segments, con
   }
   const dim3 blk(kBlock);
   hipLaunchKernelGGL(k_pairdist_reduce, dim3((unsigned)((npairs + 7) / 8)), blk, 0,
-                     st, (const double*)d_scratch, nblocks, k, (double*)d_dist);
+                     st, (const double*)d_scratch, nblocks, k, (double*)d_dist, guard, limit);
   FA_HIP(hipGetLastError());
   return release(slot, st);
 }
+}  // namespace
+
+extern "C" {
 
 size_t fa_pairwise_sqdist_scratch_bytes(int32_t num_segments, const int64_t* seg_numel, int32_t k) {
   if (k < 2 || num_segments <= 0 || !seg_numel) return 0;
@@ -1366,6 +1670,103 @@ size_t fa_pairwise_sqdist_scratch_bytes(int32_t num_segments, const int64_t* seg
     if (seg_numel[s] > 0) nchunks += (seg_numel[s] + q.pe - 1) / q.pe;
   const int64_t nblocks = std::max<int64_t>(1, std::min<int64_t>(nchunks, q.nblocks));
   return sizeof(double) * (size_t)((int64_t)k * (k - 1) / 2) * (size_t)nblocks;
+}
+
+
+size_t fa_pairwise_sqdist_gram_scratch_bytes(int32_t num_segments, const int64_t* seg_numel, int32_t k) {
+  if (k < 2 || k > kMaxPairK || num_segments <= 0 || !seg_numel) return 0;
+  // the Gram form's partials + G + row maxima, then the guarded direct kernels' partials
+  return gram_scratch(num_segments, seg_numel, k) + fa_pairwise_sqdist_scratch_bytes(num_segments, seg_numel, k);
+}
+
+int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* seg_numel, int32_t k,
+                            const void* const* d_in, void* d_dist, void* d_kappa_max, double kappa_limit,
+                            void* d_scratch, size_t scratch_bytes, void* hip_stream) {
+  if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (k < 2 || k > kMaxPairK || num_segments <= 0 || !seg_numel || !d_in || !d_dist || !d_kappa_max)
+    return fail(FA_ERR_INVALID, "fa_pairwise_sqdist_gram: invalid arguments (2 <= k <= %d)", kMaxPairK);
+  int nseg = 0;
+  int64_t nchunks = 0;
+  for (int s = 0; s < num_segments; ++s) {
+    if (seg_numel[s] < 0) return fail(FA_ERR_INVALID, "segment %d has negative numel", s);
+    if (seg_numel[s] == 0) continue;
+    for (int i = 0; i < k; ++i)
+      if (!d_in[(int64_t)s * k + i]) return fail(FA_ERR_INVALID, "segment %d client %d: input NULL", s, i);
+    ++nseg;
+    nchunks += (seg_numel[s] + kGE - 1) / kGE;
+  }
+  const size_t need = fa_pairwise_sqdist_gram_scratch_bytes(num_segments, seg_numel, k);
+  if (scratch_bytes < need || !d_scratch)
+    return fail(FA_ERR_INVALID, "fa_pairwise_sqdist_gram: scratch must hold %zu bytes", need);
+  const size_t gram_bytes = gram_scratch(num_segments, seg_numel, k);
+  DeviceGuard g(ctx->device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
+  hipStream_t st = (hipStream_t)hip_stream;
+  if (nseg == 0) {
+    FA_HIP(hipMemsetAsync(d_dist, 0, sizeof(double) * (size_t)k * k, st));
+    FA_HIP(hipMemsetAsync(d_kappa_max, 0, sizeof(double), st));
+    return FA_OK;
+  }
+  const size_t seg_bytes = align16(sizeof(PSeg) * nseg);
+  const size_t ptr_bytes = sizeof(void*) * (size_t)nseg * k;
+  fa_ctx::Slot* slot = nullptr;
+  int rc = acquire_slot(ctx, seg_bytes + ptr_bytes, &slot);
+  if (rc) return rc;
+  PSeg* hs = (PSeg*)slot->host;
+  const void** hp = (const void**)((char*)slot->host + seg_bytes);
+  bool vec = true;
+  int j = 0;
+  int64_t c0 = 0;
+  for (int s = 0; s < num_segments; ++s) {
+    const int64_t n = seg_numel[s];
+    if (n == 0) continue;
+    for (int i = 0; i < k; ++i) {
+      hp[(int64_t)j * k + i] = d_in[(int64_t)s * k + i];
+      vec = vec && ((uintptr_t)d_in[(int64_t)s * k + i] % 16 == 0);
+    }
+    hs[j] = PSeg{n, c0, j * k, 0, 0};
+    c0 += (n + kGE - 1) / kGE;
+    ++j;
+  }
+  rc = stage(slot, seg_bytes + ptr_bytes, st);
+  if (rc) return rc;
+  const char* dv = (const char*)slot->dev;
+  const int kb = (k + 31) / 32;
+  const int nblocks = gram_nblocks(nchunks, kb);
+  double* part = (double*)d_scratch;
+  double* gm = part + (size_t)nblocks * gram_T(kb) * 1024;
+  double* rowmax = gm + (size_t)(32 * kb) * (32 * kb);
+  const PSeg* sg = (const PSeg*)dv;
+  const void* const* pp = (const void* const*)(dv + seg_bytes);
+  const int ntr = (gram_T(kb) * 1024 + 7) / 8;
+  const size_t lds = gram_lds(kb);
+#define FA_GR(KB)                                                                                              \
+  do {                                                                                                         \
+    if (vec)                                                                                                   \
+      hipLaunchKernelGGL((k_pair_gram<KB, true>), dim3((unsigned)nblocks), dim3(GramCfg<KB>::NT), lds, st, sg, \
+                         nseg, pp, k, nchunks, part);                                                          \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_pair_gram<KB, false>), dim3((unsigned)nblocks), dim3(GramCfg<KB>::NT), lds, st,    \
+                         sg, nseg, pp, k, nchunks, part);                                                      \
+    hipLaunchKernelGGL((k_gram_reduce<KB>), dim3((unsigned)ntr), dim3(kBlock), 0, st, (const double*)part,    \
+                       nblocks, gm);                                                                           \
+  } while (0)
+  switch (kb) {
+    case 1: FA_GR(1); break;
+    case 2: FA_GR(2); break;
+    case 3: FA_GR(3); break;
+    default: FA_GR(4); break;
+  }
+#undef FA_GR
+  hipLaunchKernelGGL(k_gram_dist, dim3((unsigned)k), dim3(128), 0, st, (const double*)gm, 32 * kb, k, (double*)d_dist,
+                     rowmax);
+  hipLaunchKernelGGL(k_gram_kmax, dim3(1), dim3(128), 0, st, (const double*)rowmax, k, (double*)d_kappa_max);
+  FA_HIP(hipGetLastError());
+  rc = release(slot, st);
+  if (rc || kappa_limit <= 0.0) return rc;
+  // the guarded direct kernels: they run (and overwrite d_dist) only if kappa_max > kappa_limit
+  return pairdist_direct(ctx, FA_DTYPE_F32, num_segments, seg_numel, k, d_in, d_dist, (char*)d_scratch + gram_bytes,
+                         scratch_bytes - gram_bytes, hip_stream, (const double*)d_kappa_max, kappa_limit);
 }
 
 }  // extern "C"

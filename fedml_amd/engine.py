@@ -6,6 +6,7 @@ and launches on the current torch stream.  All arithmetic happens in the HIP ker
 """
 from __future__ import annotations
 
+import os
 import threading
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -926,10 +927,44 @@ class AggEngine:
                 d.index_put_((idx.view(-1, 1), idx.view(1, -1)), sub)  # diagonal blocks rewritten, same values
         return d
 
-    def _pairwise_launch(self, segments, stream=None, diff_dtype=torch.float32) -> torch.Tensor:
+    # Gram form (fa_pairwise_sqdist_gram) for float32 models: its result stands when the largest
+    # cancellation factor kappa = (A_i + A_j) / D_ij is at most this (relative error ~1e-7 kappa,
+    # tests/test_gpu_robust.py); otherwise -- and for non-finite inputs -- the direct kernels queued
+    # behind it recompute the matrix, decided on the device (no host round trip)
+    KAPPA_MAX = 16.0
+
+    @property
+    def last_kappa_max(self) -> Optional[float]:
+        """kappa_max of the last Gram-form call (reads the device value: synchronises)."""
+        km = getattr(self, "_last_km", None)
+        return None if km is None else float(km.item())
+
+    @property
+    def last_pair_form(self) -> str:
+        """"gram" or "direct": which form's result the last float32 pairwise call returned."""
+        if getattr(self, "_last_form", None) != "auto":
+            return self._last_form
+        return "gram" if self.last_kappa_max <= self.KAPPA_MAX else "direct"
+
+    def _pairwise_launch(self, segments, stream=None, diff_dtype=torch.float32, form=None) -> torch.Tensor:
         k = len(segments[0])
         in_ptrs = [t.data_ptr() for seg in segments for t in seg]
         nl = N.i64_array([seg[0].numel() for seg in segments])
+        form = form or os.environ.get("FEDML_AMD_KRUM_FORM", "auto")
+        if diff_dtype == torch.float32 and form in ("auto", "gram"):
+            with self.lock:
+                need = self._lib.fa_pairwise_sqdist_gram_scratch_bytes(len(segments), nl, k)
+                scratch = self._scratch("pdg", need, stream)
+                d = torch.empty((k, k), dtype=torch.float64, device=self.device)
+                km = torch.empty(1, dtype=torch.float64, device=self.device)
+                rc = self._lib.fa_pairwise_sqdist_gram(self._ctx, len(segments), nl, k, N.ptr_array(in_ptrs),
+                                                       d.data_ptr(), km.data_ptr(),
+                                                       self.KAPPA_MAX if form == "auto" else 0.0,
+                                                       scratch.data_ptr(), scratch.numel(), self._stream(stream))
+            N.check(rc, "fa_pairwise_sqdist_gram")
+            self._last_km, self._last_form = km, form if form == "gram" else "auto"
+            return d
+        self._last_km, self._last_form = None, "direct"
         with self.lock:
             need = self._lib.fa_pairwise_sqdist_scratch_bytes(len(segments), nl, k)
             scratch = self._scratch("pd", need, stream)

@@ -9,6 +9,7 @@
  *   fa_pairwise_sqdist  core/security/defense/krum_defense.py:52-66 (_compute_krum_score's
  *                       compute_euclidean_distance(v_i, v_j) ** 2 for every pair)
  *   fa_pairwise_sqdist_rt  the same for bfloat16 / float16 models (differences in the model dtype)
+ *   fa_pairwise_sqdist_gram  the same for float32 models in the Gram form (matrix cores, kappa-guarded)
  *
  * Contract (bit-exact; pinned by tests/golden/g16_*): for every element e, out[e] is the input
  * element (bit pattern) that ATen's median selects: the first NaN in client order if any client
@@ -73,6 +74,22 @@ int fa_pairwise_sqdist_rt(fa_ctx *ctx, int diff_dtype, int32_t num_segments, con
                           const void *const *d_in, void *d_dist, void *d_scratch, size_t scratch_bytes,
                           void *hip_stream);
 size_t fa_pairwise_sqdist_scratch_bytes(int32_t num_segments, const int64_t *seg_numel, int32_t k);
+/*
+ * fa_pairwise_sqdist for float32 vectors in the Gram form on the matrix cores (r05):
+ * D_ij = A_i + A_j - 2 G_ij over y_i = x_i - c (c: the per-coordinate median of clients 0..4), G = Y Y^T
+ * on v_mfma_f32_32x32x2_f32, float32 runs of 64 coordinates summed in float64.  Same d_dist layout
+ * (k x k float64, symmetric, zero diagonal).  The form cancels -- relative error ~ 1e-7 * kappa_ij,
+ * kappa_ij = (A_i + A_j) / D_ij -- so it also writes kappa_max = max over pairs (one float64 at
+ * d_kappa_max; +inf when some D_ij <= 0 or an input is not finite).  kappa_limit > 0: the direct
+ * kernels of fa_pairwise_sqdist are queued behind it, guarded on the device by that value -- they
+ * return at once when kappa_max <= kappa_limit and otherwise recompute d_dist, so the call stays
+ * asynchronous (fedml_amd/engine.py uses 16); kappa_limit <= 0: the Gram result only.
+ * d_scratch: fa_pairwise_sqdist_gram_scratch_bytes(...) bytes.
+ */
+int fa_pairwise_sqdist_gram(fa_ctx *ctx, int32_t num_segments, const int64_t *seg_numel, int32_t k,
+                            const void *const *d_in, void *d_dist, void *d_kappa_max, double kappa_limit,
+                            void *d_scratch, size_t scratch_bytes, void *hip_stream);
+size_t fa_pairwise_sqdist_gram_scratch_bytes(int32_t num_segments, const int64_t *seg_numel, int32_t k);
 
 #ifdef __cplusplus
 }

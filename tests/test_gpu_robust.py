@@ -257,6 +257,59 @@ def test_pairwise_sqdist_unaligned_views(eng, k, off):
     np.testing.assert_allclose(D.numpy(), ref.numpy(), rtol=1e-6)
 
 
+@pytest.mark.parametrize("k", [2, 3, 4, 5, 8, 31, 32, 33, 63, 64, 65, 96, 97, 128])
+@pytest.mark.parametrize("form", ["gram", "direct"])
+def test_pairwise_forms_vs_oracle(eng, k, form):
+    """Both forms of fa_pairwise_sqdist for float32 models, forced: the Gram form on the matrix cores
+    (fa_pairwise_sqdist_gram: every 32-client tile count, padding clients, ragged segments, a
+    multi-chunk segment) and the direct kernel, each within 1e-6 relative of the float64 oracle on
+    clients spread around a common model (kappa small), with the Gram form's kappa reported."""
+    from oracle import orc
+    g = torch.Generator().manual_seed(1000 + k)
+    sizes = [9001, 3, 64, 130]
+    base = [torch.randn(s, generator=g) for s in sizes]
+    xs = [[b + 0.3 * torch.randn(s, generator=g) * (1 + (i % 3)) for b, s in zip(base, sizes)] for i in range(k)]
+    D = eng._pairwise_launch([[xs[i][s].to(DEV) for i in range(k)] for s in range(len(sizes))], form=form).cpu()
+    assert eng.last_pair_form == form
+    if form == "gram":
+        assert 0.5 <= eng.last_kappa_max <= eng.KAPPA_MAX, eng.last_kappa_max
+    ref = orc.pairwise_sqdist([torch.cat(x) for x in xs])
+    assert torch.equal(D, D.T) and torch.all(D.diag() == 0)
+    np.testing.assert_allclose(D.numpy(), ref.numpy(), rtol=1e-6)
+
+
+@pytest.mark.parametrize("k", [8, 40, 128])
+def test_pairwise_gram_falls_back_when_ill_conditioned(eng, k):
+    """Clients 0..4 (the Gram form's centre) far from a tight honest cluster: the honest pairs cancel
+    (kappa >> 16), so the default path reruns the direct kernel -- same bits as the direct form; and
+    a non-finite input or two identical clients (D = 0) also report kappa = inf and fall back."""
+    g = torch.Generator().manual_seed(7 * k)
+    P = 20000
+    honest = torch.randn(P, generator=g)
+    xs = [honest + 1e-3 * torch.randn(P, generator=g) for _ in range(k)]
+    for i in range(5):
+        xs[i] = xs[i] + 50.0 + torch.randn(P, generator=g)
+    segs = [[x.to(DEV) for x in xs]]
+    direct = eng._pairwise_launch(segs, form="direct").cpu()
+    auto = eng.pairwise_sqdist(segs).cpu()
+    assert eng.last_pair_form == "direct" and eng.last_kappa_max > eng.KAPPA_MAX
+    assert torch.equal(auto, direct)
+    for bad in ("nan", "dup"):
+        ys = [x.clone() for x in xs[5:]] + [torch.randn(P, generator=g) for _ in range(5)]
+        if bad == "nan":
+            ys[3][17] = float("nan")
+        else:
+            ys[2] = ys[1].clone()
+        segs = [[y.to(DEV) for y in ys]]
+        auto = eng.pairwise_sqdist(segs).cpu()
+        assert eng.last_pair_form == "direct", bad
+        direct = eng._pairwise_launch(segs, form="direct").cpu()
+        if bad == "dup":
+            assert torch.equal(auto, direct) and float(auto[1, 2]) == 0.0
+        else:  # the NaN client's row and column are NaN, the rest as the direct kernel
+            assert torch.isnan(auto[3]).sum() == k - 1 and torch.equal(auto[:3, :3], direct[:3, :3])
+
+
 @pytest.mark.parametrize("path", ROB["g18_"], ids=ids)
 @pytest.mark.parametrize("where", ["cpu", "cuda"])
 def test_krum_defense_golden(path, where):
