@@ -86,8 +86,14 @@ struct fa_ctx {
     void* dev = nullptr;
     size_t cap = 0;
     hipEvent_t ev = nullptr;
-    hipEvent_t staged = nullptr;  // the table copy on the side stream has landed (stage())
-    bool pending = false;
+    hipEvent_t staged = nullptr;  // the slot's last table copy has landed (stage())
+    bool pending = false;         // FA_SLOT_EVENT=1 only: `ev` recorded at release(), host-waited
+    bool ev_live = false;         // `ev` marks the end of the slot's last use (recorded at release())
+    bool hit = false;             // the current use found its table already staged (stage(), reuse)
+    bool copy_live = false;       // `staged` recorded and the host buffer may still be read by that copy
+    hipStream_t last = nullptr;   // the stream of the slot's last use (its readers of `dev`)
+    bool used = false;            // `last` is set
+    hipStream_t synced = nullptr; // a stream already ordered after the last copy
     std::vector<char> shadow;     // the bytes `dev` holds, for stage(..., reuse) (valid if shadow_ok)
     bool shadow_ok = false;
     bool acquired = false;        // acquire_slot'ed and not yet release()d
@@ -113,15 +119,16 @@ struct fa_ctx {
 
 namespace fa_detail {
 
-// Take the next staging slot with >= bytes of room; waits only if that slot's previous call is
-// still in flight (kSlots calls ago).
+// Take the next staging slot with >= bytes of room.  The host waits only for a table copy still
+// reading the slot's host buffer (a copy kSlots calls ago); the slot's earlier kernels are ordered
+// before a later copy into its device buffer on the device (stage()), with no per-call event.
 int acquire_slot(fa_ctx* ctx, size_t bytes, fa_ctx::Slot** out);
 // Copy the slot's first `bytes` host bytes to its device buffer (async on `st`).
 // reuse: the caller's kernels only READ the table; if the slot's device buffer already holds exactly
 // these bytes (the same table staged through this slot before), the copy -- and the caller stream's
 // wait for it -- is skipped.
 int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st, bool reuse = false);
-// Mark the slot busy until the work queued on `st` so far has finished.
+// End of the slot's use by the work queued on `st` (stage() orders a later copy after it).
 int release(fa_ctx::Slot* s, hipStream_t st);
 
 }  // namespace fa_detail

@@ -1039,25 +1039,49 @@ int fail(int code, const char* fmt, ...) {
 
 const char* last_error() { return g_last_error; }
 
+// r05: a per-call event record at release() put a marker between a call's kernels and the next
+// launch on the device (profiles/r05j: 5.6 us between k_gram_dist and the guarded direct kernels,
+// 14 us between calls).  Only a table COPY needs ordering after the slot's previous readers: a use
+// that found its table already staged (the steady state of repeated rounds) records no event -- the
+// slot's next use is predicted to hit too, and if it copies instead, it records the event then, at
+// the end of the readers' stream -- while a use that copied records one at release(), so the next
+// copy can overlap the calls in between.  The host waits only for a copy still reading the host
+// buffer before rewriting it.  FA_SLOT_EVENT=1: an event per call and a host wait (A/B).
+bool slot_event_mode() {
+  static const int on = [] {
+    const char* e = getenv("FA_SLOT_EVENT");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return on != 0;
+}
+
 int acquire_slot(fa_ctx* ctx, size_t bytes, fa_ctx::Slot** out) {
   fa_ctx::Slot& s = ctx->slots[ctx->next];
   ctx->next = (ctx->next + 1) % kSlots;
-  // a use that never reached release() (its caller failed after stage()) leaves no event to wait
-  // on, so the slot's device table is not known to match its shadow: copy again next time
+  // a use that never reached release() (its caller failed after stage()) leaves the device buffer's
+  // contents unknown: copy again next time
   if (s.acquired) s.shadow_ok = false;
   s.acquired = true;
   if (s.pending) {
     FA_HIP(hipEventSynchronize(s.ev));
     s.pending = false;
   }
+  if (s.copy_live) {  // the host buffer is rewritten next: the last copy from it must have read it
+    FA_HIP(hipEventSynchronize(s.staged));
+    s.copy_live = false;
+  }
   if (s.cap < bytes) {
+    // the buffers are freed: every earlier reader of `dev` (any stream) must be done
+    if (s.used) FA_HIP(hipDeviceSynchronize());
     size_t cap = align16(std::max(bytes, std::max<size_t>(2 * s.cap, 16384)));
     if (s.host) FA_HIP(hipHostFree(s.host));
     if (s.dev) FA_HIP(hipFree(s.dev));
     s.host = s.dev = nullptr;
     s.cap = 0;
     s.shadow_ok = false;
-    // mapped: the staging copy is a kernel on the caller's stream reading it over PCIe (stage())
+    s.used = false;
+    s.synced = nullptr;
+    // mapped: the staging copy is a kernel reading it over PCIe (stage())
     if (hipHostMalloc(&s.host, cap, hipHostMallocMapped) != hipSuccess)
       return fail(FA_ERR_NOMEM, "hipHostMalloc(%zu) failed", cap);
     if (hipHostGetDevicePointer(&s.hmap, s.host, 0) != hipSuccess) s.hmap = nullptr;
@@ -1122,28 +1146,50 @@ bool stage_reuse_enabled() {
 
 int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st, bool reuse) {
   reuse = reuse && stage_reuse_enabled();
-  if (reuse && s->shadow_ok && s->shadow.size() == bytes && memcmp(s->host, s->shadow.data(), bytes) == 0)
-    return FA_OK;  // acquire_slot waited for the slot's last reader, which waited for that copy
+  if (!s->staged && hipEventCreateWithFlags(&s->staged, hipEventDisableTiming) != hipSuccess)
+    return fail(FA_ERR_HIP, "hipEventCreate failed");
+  if (reuse && s->shadow_ok && s->shadow.size() == bytes && memcmp(s->host, s->shadow.data(), bytes) == 0) {
+    // the device buffer holds these bytes; a stream not yet ordered after that copy waits for it
+    if (s->synced != st) {
+      FA_HIP(hipStreamWaitEvent(st, s->staged, 0));
+      s->synced = st;
+    }
+    s->hit = true;
+    return FA_OK;
+  }
+  s->hit = false;
   // `dev` is about to be rewritten: the shadow is valid again only once the copy (and the caller
   // stream's wait for it) has been enqueued -- every failure below returns with it invalid
   s->shadow_ok = false;
+  const bool evmode = slot_event_mode();
   if (s->hmap && bytes <= (256u << 10) && stage_kernel_enabled()) {
     const int n16 = (int)((bytes + 15) / 16);  // slots are >= 16 KB and 16-byte multiples
     const int blocks = std::max(1, std::min(64, (n16 + kBlock - 1) / kBlock));
     hipStream_t cs = st;
     if (stage_side_enabled()) {
       hipStream_t ss = side_stream();
-      if (ss && (s->staged || hipEventCreateWithFlags(&s->staged, hipEventDisableTiming) == hipSuccess)) cs = ss;
+      if (ss) cs = ss;
+    }
+    // the copy overwrites `dev`: after the slot's previous readers (stream order when they ran on
+    // the copy's own stream; otherwise an event at their stream's current end)
+    if (!evmode && s->used && s->last != cs) {
+      if (!s->ev_live) FA_HIP(hipEventRecord(s->ev, s->last));
+      FA_HIP(hipStreamWaitEvent(cs, s->ev, 0));
     }
     hipLaunchKernelGGL(k_stage_copy, dim3(blocks), dim3(kBlock), 0, cs, (const u32x4*)s->hmap, (u32x4*)s->dev, n16);
     FA_HIP(hipGetLastError());
-    if (cs != st) {
-      FA_HIP(hipEventRecord(s->staged, cs));
-      FA_HIP(hipStreamWaitEvent(st, s->staged, 0));
-    }
+    FA_HIP(hipEventRecord(s->staged, cs));
+    if (cs != st) FA_HIP(hipStreamWaitEvent(st, s->staged, 0));
   } else {
+    if (!evmode && s->used && s->last != st) {
+      if (!s->ev_live) FA_HIP(hipEventRecord(s->ev, s->last));
+      FA_HIP(hipStreamWaitEvent(st, s->ev, 0));
+    }
     FA_HIP(hipMemcpyAsync(s->dev, s->host, bytes, hipMemcpyHostToDevice, st));
+    FA_HIP(hipEventRecord(s->staged, st));
   }
+  s->copy_live = true;
+  s->synced = st;
   if (reuse) {
     s->shadow.assign((const char*)s->host, (const char*)s->host + bytes);
     s->shadow_ok = true;
@@ -1152,8 +1198,16 @@ int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st, bool reuse) {
 }
 
 int release(fa_ctx::Slot* s, hipStream_t st) {
-  FA_HIP(hipEventRecord(s->ev, st));
-  s->pending = true;
+  const bool evmode = slot_event_mode();
+  s->ev_live = false;
+  if (evmode || !s->hit) {
+    FA_HIP(hipEventRecord(s->ev, st));
+    s->pending = evmode;
+    s->ev_live = !evmode;
+  }
+  s->hit = false;
+  s->last = st;
+  s->used = true;
   s->acquired = false;
   return FA_OK;
 }
@@ -1204,6 +1258,9 @@ int fa_ctx_create(int hip_device, fa_ctx** out) {
 int fa_ctx_destroy(fa_ctx* c) {
   if (!c) return FA_OK;
   DeviceGuard g(c->device);
+  bool used = false;
+  for (auto& s : c->slots) used = used || s.used || s.copy_live;
+  if (used) (void)hipDeviceSynchronize();  // the slots' last readers and copies, on any stream
   for (auto& s : c->slots) {
     if (s.pending && s.ev) (void)hipEventSynchronize(s.ev);
     if (s.ev) (void)hipEventDestroy(s.ev);

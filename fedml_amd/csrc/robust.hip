@@ -579,7 +579,7 @@ int median_impl(fa_ctx* ctx, int dtype, int32_t num_segments, const int64_t* seg
     t0 += (n + tile_elems - 1) / tile_elems;
     ++j;
   }
-  rc = stage(slot, seg_bytes + ptr_bytes, st);
+  rc = stage(slot, seg_bytes + ptr_bytes, st, true);
   if (rc) return rc;
   const char* dv = (const char*)slot->dev;
   const MSeg* ds = (const MSeg*)dv;
@@ -1276,6 +1276,9 @@ template <int KB> struct GramCfg {
   static constexpr int LDS_FLOATS = 2 * KP * kGS + W * kGE;   // two chunk buffers + a centre row per wave
 };
 
+// register staging depth: K <= 32 has the VGPRs (64 at depth 1) and the read, not the MFMAs, bounds it
+template <int KB> struct GramPD { static constexpr int v = KB == 1 ? 3 : 1; };
+
 template <int KB>
 __device__ __forceinline__ void gram_tile_kb(int t, int& bi, int& bj) {
   int i = 0, rem = t;
@@ -1284,8 +1287,8 @@ __device__ __forceinline__ void gram_tile_kb(int t, int& bi, int& bj) {
   bj = i + rem;
 }
 
-template <int KB, bool VEC>
-__global__ void __launch_bounds__(GramCfg<KB>::NT) __attribute__((amdgpu_waves_per_eu(4)))
+template <int KB, bool VEC, int PD>  // PD: chunks staged in registers ahead of the one computed
+__global__ void __launch_bounds__(GramCfg<KB>::NT) __attribute__((amdgpu_waves_per_eu(PD > 2 ? 2 : PD > 1 ? 3 : 4)))
 k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k,
             int64_t nchunks, double* __restrict__ partial) {
   using C = GramCfg<KB>;
@@ -1306,12 +1309,12 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
   for (int q = 0; q < 16; ++q) { acc[q] = 0.0f; accd[q] = 0.0; }
   // staging: 16-byte vector q of client (idx / (kGE/4)) = coordinates 4 q .. 4 q + 3 of the chunk
   constexpr int QV = kGE / 4;
-  gf4 v[C::NLD];
+  gf4 v[PD][C::NLD];  // a ring of PD chunks in flight (slot s: chunk c0 + 1 + s, + PD, ...)
   // this thread's client pointers for the current segment (one pointer load per segment, not per
   // chunk: a per-chunk pointer load put a full memory round trip before every data load)
   const float* src[C::NLD];
   int cseg = -1;
-  auto load = [&](int64_t ch) {
+  auto load = [&](int64_t ch, gf4 (&v)[C::NLD]) {
     const int si = nseg > 1 ? find_seg(segs, nseg, ch) : 0;
     const PSeg sg = segs[si];
     if (si != cseg) {
@@ -1346,7 +1349,7 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
       }
     }
   };
-  auto put = [&](int buf) {
+  auto put = [&](int buf, const gf4 (&v)[C::NLD]) {
     float* L = lds0 + buf * C::KP * kGS;
 #pragma unroll
     for (int u = 0; u < C::NLD; ++u) {
@@ -1356,54 +1359,63 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
   };
   const int64_t c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
   if (c0 < c1) {
-    load(c0);
-    put(0);
-    if (c0 + 1 < c1) load(c0 + 1);
+    load(c0, v[0]);
+    put(0, v[0]);
+#pragma unroll
+    for (int s = 0; s < PD; ++s)
+      if (c0 + 1 + s < c1) load(c0 + 1 + s, v[s]);
   }
   __syncthreads();
   int cur = 0;
-  for (int64_t ch = c0; ch < c1; ++ch, cur ^= 1) {
-    const float* L = lds0 + cur * C::KP * kGS;
-    // the centre of the chunk's coordinates, by every wave for itself: the median of clients 0..4
-    // (fewer clients: of 0..2, or client 0); padding coordinates are 0 everywhere, so y = 0 there
+  // unrolled by PD so that every ring slot is a fixed register set (no moves of in-flight loads)
+  for (int64_t base = c0; base < c1; base += PD) {
 #pragma unroll
-    for (int e = lane; e < kGE; e += 64) {
-      float c;
-      if (k >= 5) {
-        const float a = L[e], b = L[kGS + e], cc = L[2 * kGS + e], d = L[3 * kGS + e], f = L[4 * kGS + e];
-        c = __builtin_amdgcn_fmed3f(f, fmaxf(fminf(a, b), fminf(cc, d)), fminf(fmaxf(a, b), fmaxf(cc, d)));
-      } else if (k >= 3) {
-        c = __builtin_amdgcn_fmed3f(L[e], L[kGS + e], L[2 * kGS + e]);
-      } else {
-        c = L[e];
+    for (int s = 0; s < PD; ++s) {
+      const int64_t ch = base + s;
+      if (ch >= c1) break;
+      const float* L = lds0 + cur * C::KP * kGS;
+      // the centre of the chunk's coordinates, by every wave for itself: the median of clients 0..4
+      // (fewer clients: of 0..2, or client 0); padding coordinates are 0 everywhere, so y = 0 there
+#pragma unroll
+      for (int e = lane; e < kGE; e += 64) {
+        float c;
+        if (k >= 5) {
+          const float a = L[e], b = L[kGS + e], cc = L[2 * kGS + e], d = L[3 * kGS + e], f = L[4 * kGS + e];
+          c = __builtin_amdgcn_fmed3f(f, fmaxf(fminf(a, b), fminf(cc, d)), fminf(fmaxf(a, b), fmaxf(cc, d)));
+        } else if (k >= 3) {
+          c = __builtin_amdgcn_fmed3f(L[e], L[kGS + e], L[2 * kGS + e]);
+        } else {
+          c = L[e];
+        }
+        cen[e] = c;
       }
-      cen[e] = c;
-    }
-    __builtin_amdgcn_wave_barrier();  // the wave's own LDS writes are seen by its later reads (in order)
-    const float* La = L + ra * kGS + 4 * half;
-    const float* Lb = L + rb * kGS + 4 * half;
-    const float* cr = cen + 4 * half;
+      __builtin_amdgcn_wave_barrier();  // the wave's own LDS writes are seen by its later reads (in order)
+      const float* La = L + ra * kGS + 4 * half;
+      const float* Lb = L + rb * kGS + 4 * half;
+      const float* cr = cen + 4 * half;
 #pragma unroll
-    for (int g = r; g < kGE / 8; g += C::R) {
-      const gf4 cc = *(const gf4*)&cr[8 * g];
-      const gf4 ya = (*(const gf4*)&La[8 * g] - cc) * ma;
-      const gf4 yb = diag ? ya : (*(const gf4*)&Lb[8 * g] - cc) * mb;
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.x, yb.x, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.y, yb.y, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.z, yb.z, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.w, yb.w, acc, 0, 0, 0);
-    }
-    // float32 run of one chunk (kGE / R coordinates of this split) -> float64
+      for (int g = r; g < kGE / 8; g += C::R) {
+        const gf4 cc = *(const gf4*)&cr[8 * g];
+        const gf4 ya = (*(const gf4*)&La[8 * g] - cc) * ma;
+        const gf4 yb = diag ? ya : (*(const gf4*)&Lb[8 * g] - cc) * mb;
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.x, yb.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.y, yb.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.z, yb.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.w, yb.w, acc, 0, 0, 0);
+      }
+      // float32 run of one chunk (kGE / R coordinates of this split) -> float64
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      accd[q] += (double)acc[q];
-      acc[q] = 0.0f;
+      for (int q = 0; q < 16; ++q) {
+        accd[q] += (double)acc[q];
+        acc[q] = 0.0f;
+      }
+      if (ch + 1 < c1) {
+        put(cur ^ 1, v[s]);  // chunk ch + 1; buffer cur ^ 1 was last read before the last barrier
+        if (ch + 1 + PD < c1) load(ch + 1 + PD, v[s]);
+      }
+      __syncthreads();  // one barrier per chunk
+      cur ^= 1;
     }
-    if (ch + 1 < c1) {
-      put(cur ^ 1);  // chunk ch + 1 (in registers); buffer cur ^ 1 was last read before the last barrier
-      if (ch + 2 < c1) load(ch + 2);
-    }
-    __syncthreads();  // one barrier per chunk
   }
   // the R splits of a tile summed in split order through LDS (the chunk buffers are free now), then
   // partial[(block * T + tile) * 1024 + row * 32 + col]; C/D layout of the 32x32 f32 MFMA: register q
@@ -1430,8 +1442,9 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
 // ranges, then lane order), written to g (KP x KP, upper tiles only).
 template <int KB>
 __global__ void __launch_bounds__(kBlock)
-k_gram_reduce(const double* __restrict__ partial, int nparts, double* __restrict__ g) {
+k_gram_reduce(const double* __restrict__ partial, int nparts, double* __restrict__ g, double* __restrict__ kmax) {
   using C = GramCfg<KB>;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *kmax = 0.0;  // k_gram_dist's atomic maximum starts here
   constexpr int kRP = 8, L = kBlock / kRP;
   __shared__ double red[L][kRP + 1];
   const int pl = threadIdx.x % kRP, ln = threadIdx.x / kRP;
@@ -1453,9 +1466,12 @@ k_gram_reduce(const double* __restrict__ partial, int nparts, double* __restrict
 }
 
 // D_ij = A_i + A_j - 2 G_ij (G from the upper tiles) for row i = blockIdx.x, j > i, into the k x k
-// matrix; the row's largest kappa_ij = (A_i + A_j) / D_ij (+inf for D_ij <= 0 or a NaN) to rowmax[i].
+// matrix; the row's largest kappa_ij = (A_i + A_j) / D_ij (+inf for D_ij <= 0 or a NaN) into *kmax
+// by an unsigned 64-bit atomic max of its bits: every kappa is >= 0 (or +inf), where the bit order is
+// the value order, so the maximum is exact and independent of the blocks' order (k_gram_reduce
+// zeroed *kmax before this kernel).
 __global__ void __launch_bounds__(128)
-k_gram_dist(const double* __restrict__ g, int kp, int k, double* __restrict__ d, double* __restrict__ rowmax) {
+k_gram_dist(const double* __restrict__ g, int kp, int k, double* __restrict__ d, double* __restrict__ kmax) {
   __shared__ double red[128];
   const int i = blockIdx.x, j = threadIdx.x;
   double m = 0.0;
@@ -1466,7 +1482,7 @@ k_gram_dist(const double* __restrict__ g, int kp, int k, double* __restrict__ d,
       d[(int64_t)i * k + j] = dd;
       d[(int64_t)j * k + i] = dd;
       const double kap = (ai + aj) / dd;
-      m = dd > 0.0 && kap == kap ? kap : __builtin_inf();
+      m = dd > 0.0 && kap >= 0.0 ? kap : __builtin_inf();  // NaN, negative or D <= 0: +inf
     } else if (j == i) {
       d[(int64_t)i * k + i] = 0.0;
     }
@@ -1477,38 +1493,38 @@ k_gram_dist(const double* __restrict__ g, int kp, int k, double* __restrict__ d,
     if (j < s) red[j] = fmax(red[j], red[j + s]);
     __syncthreads();
   }
-  if (j == 0) rowmax[i] = red[0];
+  if (j == 0) atomicMax((unsigned long long*)kmax, (unsigned long long)__double_as_longlong(red[0]));
 }
 
-__global__ void __launch_bounds__(128) k_gram_kmax(const double* __restrict__ rowmax, int k, double* __restrict__ kmax) {
-  __shared__ double red[128];
-  const int j = threadIdx.x;
-  red[j] = j < k ? rowmax[j] : 0.0;
-  __syncthreads();
-  for (int s = 64; s > 0; s >>= 1) {
-    if (j < s) red[j] = fmax(red[j], red[j + s]);
-    __syncthreads();
-  }
-  if (j == 0) *kmax = red[0];
+int gram_pd1() {  // FA_GRAM_PD: K <= 32's register staging depth (measurement A/B; default GramPD<1>)
+  static const int d = [] {
+    const char* e = getenv("FA_GRAM_PD");
+    return e ? atoi(e) : 0;
+  }();
+  return d;
 }
 
-// workgroups: one per CU for K > 32 (12 / 12 / 10 waves, <= 128 VGPRs: 16 waves per CU), four per CU
-// for K <= 32 (4 waves; the read, not the MFMAs, bounds it)
+// workgroups: one per CU for K > 32 (12 / 12 / 10 waves, <= 128 VGPRs: 16 waves per CU); K <= 32 below
 int gram_nblocks(int64_t nchunks, int kb) {
   static const int ov = [] {  // FA_GRAM_BLOCKS: measurement override (A/B)
     const char* e = getenv("FA_GRAM_BLOCKS");
     return e ? atoi(e) : 0;
   }();
-  const int64_t cap = ov >= 64 && ov <= 8192 ? ov : kb >= 2 ? 256 : 1024;
+  // K <= 32: as many workgroups as are resident -- 4 per CU at staging depth 1 (<= 128 VGPRs), 3 at
+  // depth 2 / 3 (145 / 163 VGPRs), 2 at depth 4 -- each takes one contiguous run of chunks
+  const int pd = gram_pd1() >= 1 && gram_pd1() <= 4 && gram_pd1() != 3 ? gram_pd1() : GramPD<1>::v;
+  const int64_t cap = ov >= 64 && ov <= 8192 ? ov : kb >= 2 ? 256 : 256 * (pd == 1 ? 4 : pd == 4 ? 2 : 3);
   return (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, cap));
 }
 
 int gram_T(int kb) { return kb * (kb + 1) / 2; }
+int gram_chunk(int) { return kGE; }
+
 size_t gram_scratch(int32_t num_segments, const int64_t* seg_numel, int32_t k) {
+  const int kb = (k + 31) / 32;
   int64_t nchunks = 0;
   for (int s = 0; s < num_segments; ++s)
-    if (seg_numel[s] > 0) nchunks += (seg_numel[s] + kGE - 1) / kGE;
-  const int kb = (k + 31) / 32;
+    if (seg_numel[s] > 0) nchunks += (seg_numel[s] + gram_chunk(kb) - 1) / gram_chunk(kb);
   const size_t parts = (size_t)gram_nblocks(nchunks, kb);
   return align16(sizeof(double) * (parts * gram_T(kb) * 1024 + (size_t)(32 * kb) * (32 * kb) + 128));
 }
@@ -1605,7 +1621,7 @@ int pairdist_direct(fa_ctx* ctx, int diff_dtype, int32_t num_segments, const int
     c0 += (n + cpe - 1) / cpe;
     ++j;
   }
-  rc = stage(slot, seg_bytes + ptr_bytes, st);
+  rc = stage(slot, seg_bytes + ptr_bytes, st, true);
   if (rc) return rc;
   const char* dv = (const char*)slot->dev;
   // FA_PAIR_PF=1: the next coordinate's LDS reads issued before this one's arithmetic.  Off by default:
@@ -1685,6 +1701,7 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
   if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
   if (k < 2 || k > kMaxPairK || num_segments <= 0 || !seg_numel || !d_in || !d_dist || !d_kappa_max)
     return fail(FA_ERR_INVALID, "fa_pairwise_sqdist_gram: invalid arguments (2 <= k <= %d)", kMaxPairK);
+  const int kbc = (k + 31) / 32, cs = gram_chunk(kbc);
   int nseg = 0;
   int64_t nchunks = 0;
   for (int s = 0; s < num_segments; ++s) {
@@ -1693,7 +1710,7 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
     for (int i = 0; i < k; ++i)
       if (!d_in[(int64_t)s * k + i]) return fail(FA_ERR_INVALID, "segment %d client %d: input NULL", s, i);
     ++nseg;
-    nchunks += (seg_numel[s] + kGE - 1) / kGE;
+    nchunks += (seg_numel[s] + cs - 1) / cs;
   }
   const size_t need = fa_pairwise_sqdist_gram_scratch_bytes(num_segments, seg_numel, k);
   if (scratch_bytes < need || !d_scratch)
@@ -1725,42 +1742,59 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
       vec = vec && ((uintptr_t)d_in[(int64_t)s * k + i] % 16 == 0);
     }
     hs[j] = PSeg{n, c0, j * k, 0, 0};
-    c0 += (n + kGE - 1) / kGE;
+    c0 += (n + cs - 1) / cs;
     ++j;
   }
-  rc = stage(slot, seg_bytes + ptr_bytes, st);
+  rc = stage(slot, seg_bytes + ptr_bytes, st, true);
   if (rc) return rc;
   const char* dv = (const char*)slot->dev;
-  const int kb = (k + 31) / 32;
+  const int kb = kbc;
   const int nblocks = gram_nblocks(nchunks, kb);
   double* part = (double*)d_scratch;
   double* gm = part + (size_t)nblocks * gram_T(kb) * 1024;
-  double* rowmax = gm + (size_t)(32 * kb) * (32 * kb);
   const PSeg* sg = (const PSeg*)dv;
   const void* const* pp = (const void* const*)(dv + seg_bytes);
   const int ntr = (gram_T(kb) * 1024 + 7) / 8;
   const size_t lds = gram_lds(kb);
+#define FA_GR1(PD)                                                                                             \
+  do {                                                                                                         \
+    if (vec)                                                                                                   \
+      hipLaunchKernelGGL((k_pair_gram<1, true, PD>), dim3((unsigned)nblocks), dim3(GramCfg<1>::NT), lds, st,   \
+                         sg, nseg, pp, k, nchunks, part);                                                      \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_pair_gram<1, false, PD>), dim3((unsigned)nblocks), dim3(GramCfg<1>::NT), lds, st,  \
+                         sg, nseg, pp, k, nchunks, part);                                                      \
+    hipLaunchKernelGGL((k_gram_reduce<1>), dim3((unsigned)ntr), dim3(kBlock), 0, st, (const double*)part,     \
+                       nblocks, gm, (double*)d_kappa_max);                                                     \
+  } while (0)
 #define FA_GR(KB)                                                                                              \
   do {                                                                                                         \
     if (vec)                                                                                                   \
-      hipLaunchKernelGGL((k_pair_gram<KB, true>), dim3((unsigned)nblocks), dim3(GramCfg<KB>::NT), lds, st, sg, \
+      hipLaunchKernelGGL((k_pair_gram<KB, true, GramPD<KB>::v>), dim3((unsigned)nblocks), dim3(GramCfg<KB>::NT), lds, st, sg, \
                          nseg, pp, k, nchunks, part);                                                          \
     else                                                                                                       \
-      hipLaunchKernelGGL((k_pair_gram<KB, false>), dim3((unsigned)nblocks), dim3(GramCfg<KB>::NT), lds, st,    \
+      hipLaunchKernelGGL((k_pair_gram<KB, false, GramPD<KB>::v>), dim3((unsigned)nblocks), dim3(GramCfg<KB>::NT), lds, st,    \
                          sg, nseg, pp, k, nchunks, part);                                                      \
     hipLaunchKernelGGL((k_gram_reduce<KB>), dim3((unsigned)ntr), dim3(kBlock), 0, st, (const double*)part,    \
-                       nblocks, gm);                                                                           \
+                       nblocks, gm, (double*)d_kappa_max);                                                     \
   } while (0)
   switch (kb) {
-    case 1: FA_GR(1); break;
+    case 1:  // FA_GRAM_PD = 1 / 2 / 4: another register staging depth for K <= 32 (A/B)
+      switch (gram_pd1()) {
+        case 1: FA_GR1(1); break;
+        case 2: FA_GR1(2); break;
+        case 4: FA_GR1(4); break;
+        default: FA_GR(1); break;
+      }
+      break;
     case 2: FA_GR(2); break;
     case 3: FA_GR(3); break;
     default: FA_GR(4); break;
   }
 #undef FA_GR
+#undef FA_GR1
   hipLaunchKernelGGL(k_gram_dist, dim3((unsigned)k), dim3(128), 0, st, (const double*)gm, 32 * kb, k, (double*)d_dist,
-                     rowmax);
-  hipLaunchKernelGGL(k_gram_kmax, dim3(1), dim3(128), 0, st, (const double*)rowmax, k, (double*)d_kappa_max);
+                     (double*)d_kappa_max);
   FA_HIP(hipGetLastError());
   rc = release(slot, st);
   if (rc || kappa_limit <= 0.0) return rc;
