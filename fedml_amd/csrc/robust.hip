@@ -1249,7 +1249,7 @@ k_pairdist_reduce(const double* __restrict__ partial, int nblocks, int k, double
 // One multiply-add per pair-coordinate on v_mfma_f32_32x32x2_f32 (f32 in / f32 accumulate, the FP32
 // vector rate), instead of the direct form's sub + fma on the VALU; operands read once per 32x32 tile.
 // The form cancels: relative error ~ eps * kappa_ij, kappa_ij = (A_i + A_j) / D_ij -- the distance
-// kernel reports max kappa (k_gram_dist) and the binding reruns the direct kernel when it is large
+// kernel reports max kappa (k_gram_reduce's tail) and the binding reruns the direct kernel when it is large
 // or not finite (fedml_amd/engine.py pairwise_sqdist).
 //
 // Layout: a workgroup owns a contiguous run of chunks (kGE coordinates of one segment, all clients);
@@ -1276,8 +1276,9 @@ template <int KB> struct GramCfg {
   static constexpr int LDS_FLOATS = 2 * KP * kGS + W * kGE;   // two chunk buffers + a centre row per wave
 };
 
-// register staging depth: K <= 32 has the VGPRs (64 at depth 1) and the read, not the MFMAs, bounds it
-template <int KB> struct GramPD { static constexpr int v = KB == 1 ? 3 : 1; };
+// register staging depth (PD > 1 instantiated for K <= 32 as an A/B; r05k interleaved 3 x: depth 1
+// 0.413-0.437 ms, 2: 0.430-0.450, 3: 0.439-0.449, 4: 0.463-0.469 -- fewer resident waves cost more)
+template <int KB> struct GramPD { static constexpr int v = 1; };  // r05k: depth 2 / 3 / 4 not faster at K = 32
 
 template <int KB>
 __device__ __forceinline__ void gram_tile_kb(int t, int& bi, int& bj) {
@@ -1290,8 +1291,9 @@ __device__ __forceinline__ void gram_tile_kb(int t, int& bi, int& bj) {
 template <int KB, bool VEC, int PD>  // PD: chunks staged in registers ahead of the one computed
 __global__ void __launch_bounds__(GramCfg<KB>::NT) __attribute__((amdgpu_waves_per_eu(PD > 2 ? 2 : PD > 1 ? 3 : 4)))
 k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k,
-            int64_t nchunks, double* __restrict__ partial) {
+            int64_t nchunks, double* __restrict__ partial, int ilv, unsigned* __restrict__ ctr) {
   using C = GramCfg<KB>;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;  // k_gram_reduce's arrival counter
   extern __shared__ __attribute__((aligned(16))) float gl[];
   float* const lds0 = gl;                       // [2][KP][kGS]
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -1357,13 +1359,18 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
       if (C::NLD * C::NT == C::KP * QV || idx < C::KP * QV) *(gf4*)&L[(idx / QV) * kGS + 4 * (idx % QV)] = v[u];
     }
   };
-  const int64_t c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
+  // this block's chunks: one contiguous run (ilv = 0), or every gridDim.x-th chunk (ilv = 1: at any
+  // moment the blocks read one compact window of every client -- few pages, few DRAM rows)
+  const int64_t G = gridDim.x, B = blockIdx.x;
+  const int64_t c0 = ilv ? 0 : nchunks * B / G;
+  const int64_t c1 = ilv ? (nchunks - B + G - 1) / G : nchunks * (B + 1) / G;  // ilv: the count
+  auto at = [&](int64_t i) { return ilv ? B + i * G : i; };
   if (c0 < c1) {
-    load(c0, v[0]);
+    load(at(c0), v[0]);
     put(0, v[0]);
 #pragma unroll
     for (int s = 0; s < PD; ++s)
-      if (c0 + 1 + s < c1) load(c0 + 1 + s, v[s]);
+      if (c0 + 1 + s < c1) load(at(c0 + 1 + s), v[s]);
   }
   __syncthreads();
   int cur = 0;
@@ -1411,7 +1418,7 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
       }
       if (ch + 1 < c1) {
         put(cur ^ 1, v[s]);  // chunk ch + 1; buffer cur ^ 1 was last read before the last barrier
-        if (ch + 1 + PD < c1) load(ch + 1 + PD, v[s]);
+        if (ch + 1 + PD < c1) load(at(ch + 1 + PD), v[s]);
       }
       __syncthreads();  // one barrier per chunk
       cur ^= 1;
@@ -1438,62 +1445,276 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
   }
 }
 
-// G entries of the T tiles summed over the per-block partials in a fixed order (lanes over block
-// ranges, then lane order), written to g (KP x KP, upper tiles only).
-template <int KB>
-__global__ void __launch_bounds__(kBlock)
-k_gram_reduce(const double* __restrict__ partial, int nparts, double* __restrict__ g, double* __restrict__ kmax) {
-  using C = GramCfg<KB>;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *kmax = 0.0;  // k_gram_dist's atomic maximum starts here
-  constexpr int kRP = 8, L = kBlock / kRP;
-  __shared__ double red[L][kRP + 1];
-  const int pl = threadIdx.x % kRP, ln = threadIdx.x / kRP;
-  const int64_t e = (int64_t)blockIdx.x * kRP + pl;  // entry = tile * 1024 + row * 32 + col
-  const int64_t nent = (int64_t)C::T * 1024;
-  double s = 0.0;
-  if (e < nent)
-    for (int b = ln; b < nparts; b += L) s += partial[(int64_t)b * nent + e];
-  red[ln][pl] = s;
+// K <= 32 with an LDS-DMA ring (r05).  The register-staged kernel above waits vmcnt(0) for its one
+// chunk in flight at every put (the compiler cannot count a ring of register loads across the loop:
+// r05k, depths 2-4 all slower), and its time splits (r05o, measurement knobs on a first 4-wave ring
+// kernel): the read alone 251 us, + MFMA 104, + the centre 42 (every wave computed all 128), + the
+// float64 flush 29 -- the compute was not hidden under the read.  So: ONE workgroup of 16 waves per
+// CU (4 per SIMD), a ring of NB 32-KB chunk buffers filled by global_load_lds_dwordx4 (no staging
+// registers, no ds_write pass), NB - 1 chunks in flight across the one raw s_barrier per chunk with a
+// counted vmcnt (2 DMA instructions per thread and chunk: vmcnt(2 (NB - 2)) retires exactly chunk
+// i); each wave computes the centre of only ITS 16 coordinates, and flushes float32 into float64
+// every second chunk (64 products per run).  One wave-instruction of DMA writes one client row
+// (64 lanes x 16 bytes = 256 coordinates), lane-linear, so the bank swizzle goes on the SOURCE
+// address: physical unit p of row r holds coordinates 4 (p ^ (r & 15)) .. + 3 (16 rows read at one
+// unit offset hit 16 distinct units: conflict-free ds_read_b128).  Rows k..31 load client 0's
+// coordinates and are zeroed by the mask, as the register kernel's zero rows are (a non-finite input
+// makes D non-finite either way, and the kappa guard hands the call to the direct kernels).  Only
+// full 256-coordinate chunks go through the ring (tile_start = the segment's first full chunk, pad =
+// 1 when a partial chunk follows); partial chunks are taken after the ring has drained, segment s by
+// workgroup s % gridDim.x, through bounds-checked register loads.
+// CW coordinates per chunk, WV waves per workgroup (each wave: CW / (8 WV) = 2 groups of every chunk)
+template <int NB, int CW, int WV>
+__global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(4)))
+k_pair_gram_ring(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k,
+                 int64_t nfull, double* __restrict__ partial, int dbg, unsigned* __restrict__ ctr) {
+  constexpr int RS = CW, BUF = 32 * RS;        // floats per client row / per ring buffer
+  constexpr int U = CW / 4, RPI = 64 / U;      // 16-byte units per row, rows per DMA wave-instruction
+  constexpr int IPW = 32 / RPI / WV;           // DMA instructions per wave and chunk
+  constexpr int NT = 64 * WV;
+  static_assert(CW == 16 * WV && IPW >= 1 && U >= 16, "16 coordinates per wave and chunk");
+  static_assert(NB * BUF * 4 >= WV * 768 * 8, "the epilogue's float64 wave sums reuse the ring");
+  extern __shared__ __attribute__((aligned(16))) float gl[];  // [NB][32][CW] swizzled, then [WV][16] centres
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;  // k_gram_reduce's arrival counter
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // coordinates 16 w .. 16 w + 15 of every chunk
+  float* const cen = gl + NB * BUF + w * 16;
+  // 16x16x4 MFMA lanes: i = lane & 15 (client i of block 0, 16 + i of block 1), kk = lane >> 4
+  const int li = lane & 15, kk = lane >> 4;
+  gf4 t00 = {0.f, 0.f, 0.f, 0.f}, t01 = t00, t11 = t00;  // tiles (0,0), (0,1), (1,1) of the 32x32 G
+  double a00[4] = {0, 0, 0, 0}, a01[4] = {0, 0, 0, 0}, a11[4] = {0, 0, 0, 0};
+  const float* cp[IPW];  // DMA j of this wave: client rows RPI (IPW w + j) + lane / U
+  int cseg = -1;
+  int64_t cbase = 0;
+  auto seg_ptrs = [&](int si) {
+    const PSeg sg = segs[si];
+    cseg = si;
+    cbase = sg.tile_start;
+#pragma unroll
+    for (int j = 0; j < IPW; ++j) {
+      const int r0 = RPI * (IPW * w + j);  // wave-uniform: the row pointers are scalar loads
+      const void* p0 = ptrs[sg.ptr_base + (r0 < k ? r0 : 0)];
+      const void* p1 = RPI > 1 ? ptrs[sg.ptr_base + (r0 + 1 < k ? r0 + 1 : 0)] : p0;
+      const int row = r0 + lane / U;
+      cp[j] = (const float*)(lane / U ? p1 : p0) + 4 * ((lane % U) ^ (row & 15));
+    }
+  };
+  auto issue = [&](int64_t ch, int buf) {  // full chunk ch -> ring buffer buf
+    const int si = nseg > 1 ? find_seg(segs, nseg, ch) : 0;
+    if (si != cseg) seg_ptrs(si);
+    const int64_t off = (ch - cbase) * CW;
+#pragma unroll
+    for (int j = 0; j < IPW; ++j)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(cp[j] + off),
+                                       (__attribute__((address_space(3))) void*)(gl + buf * BUF + RPI * (IPW * w + j) * RS),
+                                       16, 0, 0);
+  };
+  // G on v_mfma_f32_16x16x4_f32 over the three tiles of the upper triangle (the 32x32 form's (1,0)
+  // quadrant is the (0,1) tile transposed: 3 x 32 instead of 2 x 64 MFMA cycles per 4 coordinates;
+  // K <= 16 needs tile (0,0) alone).  This wave takes coordinates 16 w .. 16 w + 15 of the chunk: lane
+  // (li, kk) reads 16-byte unit 4 w + kk of client rows li and 16 + li (one ds_read_b128 each; the k
+  // index of MFMA m is coordinate 4 kk + m -- any assignment works when A and B agree).  Rows >= k hold
+  // client 0's coordinates (DMA) or zeros (partial chunks): their G entries are never read.
+  auto compute = [&](const float* L, bool flush) {
+    if (!(dbg & 1) && lane < 16) {  // the centre of this wave's 16 coordinates (median of clients 0..4)
+      const int u = 4 * w + (lane >> 2), z = lane & 3;
+      float c;
+      if (k >= 5) {
+        const float a0 = L[4 * u + z], b0 = L[RS + 4 * (u ^ 1) + z], c0 = L[2 * RS + 4 * (u ^ 2) + z],
+                    d0 = L[3 * RS + 4 * (u ^ 3) + z], f0 = L[4 * RS + 4 * (u ^ 4) + z];
+        c = __builtin_amdgcn_fmed3f(f0, fmaxf(fminf(a0, b0), fminf(c0, d0)), fminf(fmaxf(a0, b0), fmaxf(c0, d0)));
+      } else if (k >= 3) {
+        c = __builtin_amdgcn_fmed3f(L[4 * u + z], L[RS + 4 * (u ^ 1) + z], L[2 * RS + 4 * (u ^ 2) + z]);
+      } else {
+        c = L[4 * u + z];
+      }
+      cen[lane] = c;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int pu = 4 * ((4 * w + kk) ^ li);  // physical unit of logical unit 4 w + kk in rows li and 16 + li
+    const gf4 cc = *(const gf4*)&cen[4 * kk];
+    const gf4 y0 = *(const gf4*)&L[li * RS + pu] - cc;
+    if (dbg & 4) {  // measurement only (FA_GRAM_DBG): no MFMA
+      t00[0] += y0.x + y0.y + y0.z + y0.w;
+    } else if (k > 16) {
+      const gf4 y1 = *(const gf4*)&L[(16 + li) * RS + pu] - cc;
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        t00 = __builtin_amdgcn_mfma_f32_16x16x4f32(y0[m], y0[m], t00, 0, 0, 0);
+        t01 = __builtin_amdgcn_mfma_f32_16x16x4f32(y0[m], y1[m], t01, 0, 0, 0);
+        t11 = __builtin_amdgcn_mfma_f32_16x16x4f32(y1[m], y1[m], t11, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int m = 0; m < 4; ++m) t00 = __builtin_amdgcn_mfma_f32_16x16x4f32(y0[m], y0[m], t00, 0, 0, 0);
+    }
+    if (flush && !(dbg & 2)) {  // float32 runs of 4 chunks (64 products per entry) -> float64
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a00[q] += (double)t00[q];
+        a01[q] += (double)t01[q];
+        a11[q] += (double)t11[q];
+        t00[q] = t01[q] = t11[q] = 0.0f;
+      }
+    }
+  };
+  // this workgroup's run of full chunks; ring fill past its end re-loads chunk 0 (L2-resident after
+  // the first) into a buffer nobody reads, so every iteration has NB - 1 chunks in flight
+  const int64_t G = gridDim.x, B = blockIdx.x;
+  const int64_t c0 = nfull * B / G, n = nfull * (B + 1) / G - c0;
+  if (n > 0) {
+#pragma unroll
+    for (int s = 0; s < NB - 1; ++s) issue(s < n ? c0 + s : 0, s);
+    for (int64_t i = 0; i < n; ++i) {
+      // s_waitcnt vmcnt(IPW (NB - 2)) lgkmcnt(0) (gfx9 encoding: vmcnt [3:0] + [15:14], expcnt [6:4] = 7: no wait)
+      __builtin_amdgcn_s_waitcnt(0x0070 | ((IPW * (NB - 2)) & 0xF) | (((IPW * (NB - 2)) >> 4) << 14));
+      __builtin_amdgcn_s_barrier();  // chunk i landed for every wave; every wave is done with buffer (i - 1) % NB
+      const int64_t nx = i + NB - 1;
+      issue(nx < n ? c0 + nx : 0, (int)(nx % NB));
+      if (!(dbg & 8)) compute(gl + (int)(i % NB) * BUF, (i & 3) == 3 || i + 1 == n);  // dbg 8: the read alone
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): the fill loads landed
   __syncthreads();
-  if (ln == 0 && e < nent) {
+  // the partial chunks: segment s's last (numel % CW coordinates) by workgroup s % G, register loads
+  // with bounds into buffer 0 (the same swizzle), then the same compute
+  for (int64_t si = B; si < nseg; si += G) {
+    const PSeg sg = segs[si];
+    if (!sg.pad) continue;
+    const int64_t b0 = (sg.numel / CW) * CW, left = sg.numel - b0;
+    for (int idx = t; idx < 32 * U; idx += NT) {
+      const int row = idx / U, u = idx % U;
+      gf4 x = {0.f, 0.f, 0.f, 0.f};
+      if (row < k) {
+        const float* p = (const float*)ptrs[sg.ptr_base + row] + b0;
+#pragma unroll
+        for (int z = 0; z < 4; ++z) if (4 * u + z < left) x[z] = gld<float>(p, 4 * u + z);
+      }
+      *(gf4*)&gl[row * RS + 4 * (u ^ (row & 15))] = x;
+    }
+    __syncthreads();
+    compute(gl, true);
+    __syncthreads();
+  }
+  // the WV waves' sums added in wave order through LDS, then partial[block * 1024 + row * 32 + col]
+  // (16x16 C/D layout: register q of lane l is row 4 (l >> 4) + q, column l & 15 of its tile; the
+  // lower-left quadrant, never read, is written as zeros)
+  double* red = (double*)gl;  // [WV][12][64]
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    red[(int64_t)w * 768 + q * 64 + lane] = a00[q];
+    red[(int64_t)w * 768 + (4 + q) * 64 + lane] = a01[q];
+    red[(int64_t)w * 768 + (8 + q) * 64 + lane] = a11[q];
+  }
+  __syncthreads();
+  if (w == 0) {
+    double* o = partial + (int64_t)blockIdx.x * 1024;
+#pragma unroll
+    for (int q = 0; q < 12; ++q) {
+      double sum = red[q * 64 + lane];
+      for (int v = 1; v < WV; ++v) sum += red[(int64_t)v * 768 + q * 64 + lane];
+      const int tile = q >> 2, row = 4 * kk + (q & 3), col = li;
+      const int R = tile == 2 ? 16 + row : row, C = tile == 0 ? col : 16 + col;
+      o[R * 32 + C] = sum;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[(16 + 4 * kk + q) * 32 + li] = 0.0;
+  }
+}
+
+// G entries of the T tiles summed over the per-block partials in a fixed order: a workgroup of 16
+// waves takes 64 consecutive entries (entry = tile * 1024 + row * 32 + col, lane = entry), wave v sums
+// partial rows v, v + 16, ... (512-byte row reads), then the 16 wave sums are added in wave order
+// through LDS; written to g (KP x KP, upper tiles only).  (r05: the r04 form -- 8 entries per 256-
+// thread group, 64-byte row reads -- took 11 us over K = 32's 768 partials.)
+// The LAST workgroup to finish (an arrival counter the Gram kernel zeroed; release / acquire at agent
+// scope around it) then forms D_ij = A_i + A_j - 2 G_ij for every pair into the k x k matrix and the
+// largest kappa_ij = (A_i + A_j) / D_ij (+inf for D_ij <= 0 or a NaN) into *kmax -- the former
+// k_gram_dist / k_gram_kmax launches, in this kernel's tail.
+constexpr int kGRW = 16;  // waves per k_gram_reduce workgroup
+template <int KB>
+__global__ void __launch_bounds__(64 * kGRW)
+k_gram_reduce(const double* __restrict__ partial, int nparts, double* __restrict__ g, int k, double* __restrict__ d,
+              double* __restrict__ kmax, unsigned* __restrict__ ctr) {
+  using C = GramCfg<KB>;
+  __shared__ double red[kGRW * 64];
+  __shared__ int last;
+  const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
+  const int64_t nent = (int64_t)C::T * 1024;
+  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  double s = 0.0;
+  int b = v;
+  for (; b + 7 * kGRW < nparts; b += 8 * kGRW) {  // 8 loads in flight, added in row order
+    double x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = partial[(int64_t)(b + u * kGRW) * nent + e];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += x[u];
+  }
+  for (; b < nparts; b += kGRW) s += partial[(int64_t)b * nent + e];
+  red[v * 64 + lane] = s;
+  __syncthreads();
+  if (v == 0) {
     double tsum = 0.0;
-    for (int l = 0; l < L; ++l) tsum += red[l][pl];
+#pragma unroll
+    for (int u = 0; u < kGRW; ++u) tsum += red[u * 64 + lane];
     int bi, bj;
     gram_tile_kb<KB>((int)(e / 1024), bi, bj);
     const int row = (int)(e % 1024) / 32, col = (int)(e % 32);
     g[(int64_t)(32 * bi + row) * C::KP + 32 * bj + col] = tsum;
   }
-}
-
-// D_ij = A_i + A_j - 2 G_ij (G from the upper tiles) for row i = blockIdx.x, j > i, into the k x k
-// matrix; the row's largest kappa_ij = (A_i + A_j) / D_ij (+inf for D_ij <= 0 or a NaN) into *kmax
-// by an unsigned 64-bit atomic max of its bits: every kappa is >= 0 (or +inf), where the bit order is
-// the value order, so the maximum is exact and independent of the blocks' order (k_gram_reduce
-// zeroed *kmax before this kernel).
-__global__ void __launch_bounds__(128)
-k_gram_dist(const double* __restrict__ g, int kp, int k, double* __restrict__ d, double* __restrict__ kmax) {
-  __shared__ double red[128];
-  const int i = blockIdx.x, j = threadIdx.x;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == gridDim.x - 1;
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (!last) return;
   double m = 0.0;
-  if (j < k) {
+  for (int idx = threadIdx.x; idx < k * k; idx += 64 * kGRW) {
+    const int i = idx / k, j = idx % k;
     if (j > i) {
-      const double ai = g[(int64_t)i * kp + i], aj = g[(int64_t)j * kp + j], gij = g[(int64_t)i * kp + j];
+      const double ai = g[(int64_t)i * C::KP + i], aj = g[(int64_t)j * C::KP + j], gij = g[(int64_t)i * C::KP + j];
       const double dd = ai + aj - 2.0 * gij;
       d[(int64_t)i * k + j] = dd;
       d[(int64_t)j * k + i] = dd;
       const double kap = (ai + aj) / dd;
-      m = dd > 0.0 && kap >= 0.0 ? kap : __builtin_inf();  // NaN, negative or D <= 0: +inf
+      m = fmax(m, dd > 0.0 && kap >= 0.0 ? kap : __builtin_inf());  // NaN, negative or D <= 0: +inf
     } else if (j == i) {
       d[(int64_t)i * k + i] = 0.0;
     }
   }
-  red[j] = m;
+  red[threadIdx.x] = m;
   __syncthreads();
-  for (int s = 64; s > 0; s >>= 1) {
-    if (j < s) red[j] = fmax(red[j], red[j + s]);
+  for (int w2 = 32 * kGRW; w2 > 0; w2 >>= 1) {
+    if ((int)threadIdx.x < w2) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + w2]);
     __syncthreads();
   }
-  if (j == 0) atomicMax((unsigned long long*)kmax, (unsigned long long)__double_as_longlong(red[0]));
+  if (threadIdx.x == 0) *kmax = red[0];
+}
+
+int gram_glds() {  // K <= 32: FA_GRAM_GLDS = 8 (default): two 8-wave ring workgroups per CU; 16: one of 16 waves;
+                  // 0: the register-staged k_pair_gram<1> (A/B)
+  static const int d = [] {
+    const char* e = getenv("FA_GRAM_GLDS");
+    if (!e) return 8;
+    const int v = atoi(e);
+    return v == 0 || v == 16 ? v : 8;
+  }();
+  return d;
+}
+
+int gram_ilv() {  // FA_GRAM_ILV=1: chunks dealt round-robin over the workgroups (A/B)
+  static const int d = [] {
+    const char* e = getenv("FA_GRAM_ILV");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return d;
 }
 
 int gram_pd1() {  // FA_GRAM_PD: K <= 32's register staging depth (measurement A/B; default GramPD<1>)
@@ -1512,7 +1733,7 @@ int gram_nblocks(int64_t nchunks, int kb) {
   }();
   // K <= 32: as many workgroups as are resident -- 4 per CU at staging depth 1 (<= 128 VGPRs), 3 at
   // depth 2 / 3 (145 / 163 VGPRs), 2 at depth 4 -- each takes one contiguous run of chunks
-  const int pd = gram_pd1() >= 1 && gram_pd1() <= 4 && gram_pd1() != 3 ? gram_pd1() : GramPD<1>::v;
+  const int pd = gram_pd1() >= 1 && gram_pd1() <= 4 ? gram_pd1() : GramPD<1>::v;
   const int64_t cap = ov >= 64 && ov <= 8192 ? ov : kb >= 2 ? 256 : 256 * (pd == 1 ? 4 : pd == 4 ? 2 : 3);
   return (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, cap));
 }
@@ -1701,7 +1922,16 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
   if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
   if (k < 2 || k > kMaxPairK || num_segments <= 0 || !seg_numel || !d_in || !d_dist || !d_kappa_max)
     return fail(FA_ERR_INVALID, "fa_pairwise_sqdist_gram: invalid arguments (2 <= k <= %d)", kMaxPairK);
-  const int kbc = (k + 31) / 32, cs = gram_chunk(kbc);
+  const int kbc = (k + 31) / 32;
+  bool vec = true;
+  for (int s = 0; s < num_segments; ++s)
+    if (seg_numel[s] > 0)
+      for (int i = 0; i < k; ++i) vec = vec && d_in[(int64_t)s * k + i] && ((uintptr_t)d_in[(int64_t)s * k + i] % 16 == 0);
+  // K <= 32 on 16-byte aligned clients: the LDS-DMA ring kernel (256-coordinate chunks), whose chunk
+  // index runs over FULL chunks only (tile_start = the segment's first full chunk, pad = 1: a partial
+  // chunk follows)
+  const int glds = kbc == 1 && vec ? gram_glds() : 0;
+  const int cs = glds == 16 ? 256 : glds == 8 ? 128 : gram_chunk(kbc);
   int nseg = 0;
   int64_t nchunks = 0;
   for (int s = 0; s < num_segments; ++s) {
@@ -1731,18 +1961,14 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
   if (rc) return rc;
   PSeg* hs = (PSeg*)slot->host;
   const void** hp = (const void**)((char*)slot->host + seg_bytes);
-  bool vec = true;
   int j = 0;
   int64_t c0 = 0;
   for (int s = 0; s < num_segments; ++s) {
     const int64_t n = seg_numel[s];
     if (n == 0) continue;
-    for (int i = 0; i < k; ++i) {
-      hp[(int64_t)j * k + i] = d_in[(int64_t)s * k + i];
-      vec = vec && ((uintptr_t)d_in[(int64_t)s * k + i] % 16 == 0);
-    }
-    hs[j] = PSeg{n, c0, j * k, 0, 0};
-    c0 += (n + cs - 1) / cs;
+    for (int i = 0; i < k; ++i) hp[(int64_t)j * k + i] = d_in[(int64_t)s * k + i];
+    hs[j] = PSeg{n, c0, j * k, glds && n % cs ? 1 : 0, 0};
+    c0 += glds ? n / cs : (n + cs - 1) / cs;
     ++j;
   }
   rc = stage(slot, seg_bytes + ptr_bytes, st, true);
@@ -1752,37 +1978,54 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
   const int nblocks = gram_nblocks(nchunks, kb);
   double* part = (double*)d_scratch;
   double* gm = part + (size_t)nblocks * gram_T(kb) * 1024;
+  unsigned* ctr = (unsigned*)(gm + (size_t)(32 * kb) * (32 * kb));  // k_gram_reduce's arrival counter
   const PSeg* sg = (const PSeg*)dv;
   const void* const* pp = (const void* const*)(dv + seg_bytes);
-  const int ntr = (gram_T(kb) * 1024 + 7) / 8;
+  const int ntr = gram_T(kb) * 1024 / 64;  // k_gram_reduce workgroups
   const size_t lds = gram_lds(kb);
+  const int ilv = gram_ilv();
 #define FA_GR1(PD)                                                                                             \
   do {                                                                                                         \
     if (vec)                                                                                                   \
       hipLaunchKernelGGL((k_pair_gram<1, true, PD>), dim3((unsigned)nblocks), dim3(GramCfg<1>::NT), lds, st,   \
-                         sg, nseg, pp, k, nchunks, part);                                                      \
+                         sg, nseg, pp, k, nchunks, part, ilv, ctr);                                                 \
     else                                                                                                       \
       hipLaunchKernelGGL((k_pair_gram<1, false, PD>), dim3((unsigned)nblocks), dim3(GramCfg<1>::NT), lds, st,  \
-                         sg, nseg, pp, k, nchunks, part);                                                      \
-    hipLaunchKernelGGL((k_gram_reduce<1>), dim3((unsigned)ntr), dim3(kBlock), 0, st, (const double*)part,     \
-                       nblocks, gm, (double*)d_kappa_max);                                                     \
+                         sg, nseg, pp, k, nchunks, part, ilv, ctr);                                                      \
+    hipLaunchKernelGGL((k_gram_reduce<1>), dim3((unsigned)ntr), dim3(64 * kGRW), 0, st, (const double*)part,     \
+                       nblocks, gm, k, (double*)d_dist, (double*)d_kappa_max, ctr);                           \
   } while (0)
 #define FA_GR(KB)                                                                                              \
   do {                                                                                                         \
     if (vec)                                                                                                   \
       hipLaunchKernelGGL((k_pair_gram<KB, true, GramPD<KB>::v>), dim3((unsigned)nblocks), dim3(GramCfg<KB>::NT), lds, st, sg, \
-                         nseg, pp, k, nchunks, part);                                                          \
+                         nseg, pp, k, nchunks, part, ilv, ctr);                                                          \
     else                                                                                                       \
       hipLaunchKernelGGL((k_pair_gram<KB, false, GramPD<KB>::v>), dim3((unsigned)nblocks), dim3(GramCfg<KB>::NT), lds, st,    \
-                         sg, nseg, pp, k, nchunks, part);                                                      \
-    hipLaunchKernelGGL((k_gram_reduce<KB>), dim3((unsigned)ntr), dim3(kBlock), 0, st, (const double*)part,    \
-                       nblocks, gm, (double*)d_kappa_max);                                                     \
+                         sg, nseg, pp, k, nchunks, part, ilv, ctr);                                                      \
+    hipLaunchKernelGGL((k_gram_reduce<KB>), dim3((unsigned)ntr), dim3(64 * kGRW), 0, st, (const double*)part,    \
+                       nblocks, gm, k, (double*)d_dist, (double*)d_kappa_max, ctr);                           \
   } while (0)
-  switch (kb) {
-    case 1:  // FA_GRAM_PD = 1 / 2 / 4: another register staging depth for K <= 32 (A/B)
+  if (glds) {  // c0 = the full-chunk count; one 16-wave workgroup per CU, or two of 8 waves
+    const int nbg = (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, glds == 16 ? 256 : 512));
+    const size_t lg = (size_t)4 * 32 * cs * sizeof(float) + (size_t)glds * 16 * sizeof(float);
+    static const int dbg = [] {  // FA_GRAM_DBG: measurement only -- parts of the compute skipped (wrong results)
+      const char* e = getenv("FA_GRAM_DBG");
+      return e ? atoi(e) : 0;
+    }();
+    if (glds == 16)
+      hipLaunchKernelGGL((k_pair_gram_ring<4, 256, 16>), dim3((unsigned)nbg), dim3(1024), lg, st, sg, nseg, pp, k, c0,
+                         part, dbg, ctr);
+    else
+      hipLaunchKernelGGL((k_pair_gram_ring<4, 128, 8>), dim3((unsigned)nbg), dim3(512), lg, st, sg, nseg, pp, k, c0,
+                         part, dbg, ctr);
+    hipLaunchKernelGGL((k_gram_reduce<1>), dim3((unsigned)ntr), dim3(64 * kGRW), 0, st, (const double*)part, nbg, gm,
+                       k, (double*)d_dist, (double*)d_kappa_max, ctr);
+  } else switch (kb) {
+    case 1:  // FA_GRAM_PD = 2 / 3 / 4: another register staging depth for K <= 32 (A/B)
       switch (gram_pd1()) {
-        case 1: FA_GR1(1); break;
         case 2: FA_GR1(2); break;
+        case 3: FA_GR1(3); break;
         case 4: FA_GR1(4); break;
         default: FA_GR(1); break;
       }
@@ -1793,8 +2036,6 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
   }
 #undef FA_GR
 #undef FA_GR1
-  hipLaunchKernelGGL(k_gram_dist, dim3((unsigned)k), dim3(128), 0, st, (const double*)gm, 32 * kb, k, (double*)d_dist,
-                     (double*)d_kappa_max);
   FA_HIP(hipGetLastError());
   rc = release(slot, st);
   if (rc || kappa_limit <= 0.0) return rc;
