@@ -77,7 +77,9 @@ size_t fa_pairwise_sqdist_scratch_bytes(int32_t num_segments, const int64_t *seg
 /*
  * fa_pairwise_sqdist for float32 vectors in the Gram form on the matrix cores (r05):
  * D_ij = A_i + A_j - 2 G_ij over y_i = x_i - c (c: the per-coordinate median of clients 0..4), G = Y Y^T
- * on v_mfma_f32_32x32x2_f32, float32 runs of 64 coordinates summed in float64.  Same d_dist layout
+ * on the f32-input MFMA (k <= 32 with 16-byte aligned clients: v_mfma_f32_16x16x4_f32 over the three
+ * upper 16x16 tiles, chunks streamed by LDS-DMA; otherwise v_mfma_f32_32x32x2_f32 over the upper
+ * 32x32 tiles), float32 runs of 32-64 products summed in float64.  Same d_dist layout
  * (k x k float64, symmetric, zero diagonal).  The form cancels -- relative error ~ 1e-7 * kappa_ij,
  * kappa_ij = (A_i + A_j) / D_ij -- so it also writes kappa_max = max over pairs (one float64 at
  * d_kappa_max; +inf when some D_ij <= 0 or an input is not finite).  kappa_limit > 0: the direct
