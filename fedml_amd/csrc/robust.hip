@@ -1264,21 +1264,29 @@ constexpr int kGS = kGE + 4;   // LDS row stride (floats): 16-byte rows, b128 re
 typedef float gf16 __attribute__((ext_vector_type(16)));
 typedef float gf4 __attribute__((ext_vector_type(4)));
 
-template <int KB> struct GramCfg {
+template <int KB, bool S16 = false> struct GramCfg {
   static constexpr int T = KB * (KB + 1) / 2;             // 32x32 tiles, upper triangle
-  static constexpr int R = KB == 1 ? 4 : KB == 2 ? 4 : KB == 3 ? 2 : 1;  // coordinate-group splits per tile
-  static constexpr int W = T * R;                         // waves per workgroup, one (tile, split) each:
+  static constexpr int R = S16 ? 1 : KB == 1 ? 4 : KB == 2 ? 4 : KB == 3 ? 2 : 1;  // coordinate-group splits per tile
+  static constexpr int W = S16 ? 12 : T * R;              // waves per workgroup, one (tile, split) each:
                                                           // 4 / 12 / 12 / 10 -- a multiple of the CU's 4
-                                                          // SIMDs except K > 96 (3, 3, 2, 2 tiles per SIMD)
+                                                          // SIMDs except K > 96 (3, 3, 2, 2 tiles per SIMD),
+                                                          // whose S16 form runs 12 waves of three 16x16 tiles
   static constexpr int NT = W * 64;
   static constexpr int KP = 32 * KB;
   static constexpr int NLD = (KP * (kGE / 4) + NT - 1) / NT;  // staged 16-byte vectors per thread
   static constexpr int LDS_FLOATS = 2 * KP * kGS + W * kGE;   // two chunk buffers + a centre row per wave
 };
 
-// register staging depth (PD > 1 instantiated for K <= 32 as an A/B; r05k interleaved 3 x: depth 1
-// 0.413-0.437 ms, 2: 0.430-0.450, 3: 0.439-0.449, 4: 0.463-0.469 -- fewer resident waves cost more)
-template <int KB> struct GramPD { static constexpr int v = 1; };  // r05k: depth 2 / 3 / 4 not faster at K = 32
+// (r05k: a register ring of 2-4 staged chunks measured slower at K = 32 -- the compiler waits vmcnt(0)
+// at every put whatever the depth; r05m: chunks dealt round-robin over the workgroups, within noise.
+// Both knobs were removed)
+
+// K in (96, 128], S16 form: 12 waves, each three 16x16 tiles of the 8 client blocks of 16 that share at
+// most 3 blocks -- waves 0-3 the diagonal pairs {2a, 2a + 1} (tiles (2a,2a), (2a,2a+1), (2a+1,2a+1)),
+// waves 4-11 the triangles of a decomposition of the remaining 24 block pairs (K_{2,2,2,2} into 8
+// triangles, found by search): every one of the 36 upper 16x16 tiles once, 3 per wave, 3 waves per SIMD
+__constant__ const int8_t kG16Blocks[12][3] = {{0, 1, 1}, {2, 3, 3}, {4, 5, 5}, {6, 7, 7}, {0, 2, 4}, {0, 3, 6},
+                                               {0, 5, 7}, {1, 2, 7}, {1, 3, 5}, {1, 4, 6}, {2, 5, 6}, {3, 4, 7}};
 
 template <int KB>
 __device__ __forceinline__ void gram_tile_kb(int t, int& bi, int& bj) {
@@ -1288,35 +1296,51 @@ __device__ __forceinline__ void gram_tile_kb(int t, int& bi, int& bj) {
   bj = i + rem;
 }
 
-template <int KB, bool VEC, int PD>  // PD: chunks staged in registers ahead of the one computed
-__global__ void __launch_bounds__(GramCfg<KB>::NT) __attribute__((amdgpu_waves_per_eu(PD > 2 ? 2 : PD > 1 ? 3 : 4)))
+template <int KB, bool VEC, bool S16>
+__global__ void __launch_bounds__((GramCfg<KB, S16>::NT)) __attribute__((amdgpu_waves_per_eu(S16 ? 3 : 4)))
 k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k,
-            int64_t nchunks, double* __restrict__ partial, int ilv, unsigned* __restrict__ ctr) {
-  using C = GramCfg<KB>;
+            int64_t nchunks, double* __restrict__ partial, unsigned* __restrict__ ctr) {
+  static_assert(!S16 || KB == 4, "the 16x16 wave table is for 8 client blocks");
+  using C = GramCfg<KB, S16>;
   if (blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;  // k_gram_reduce's arrival counter
   extern __shared__ __attribute__((aligned(16))) float gl[];
   float* const lds0 = gl;                       // [2][KP][kGS]
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   float* const cen = gl + 2 * C::KP * kGS + w * kGE;  // this wave's centre row (wave-private: no barrier)
-  const int ti = w / C::R, r = w % C::R;  // this wave's tile and coordinate-group split
-  int bi, bj;
-  gram_tile_kb<KB>(ti, bi, bj);
+  // 32x32 form: this wave's tile (bi, bj) and coordinate-group split r
+  const int ti = w / C::R, r = w % C::R;
+  int bi = 0, bj = 0;
+  if constexpr (!S16) gram_tile_kb<KB>(ti, bi, bj);
   const bool diag = bi == bj;
   const int half = lane >> 5, lrow = lane & 31;
   const int ra = 32 * bi + lrow, rb = 32 * bj + lrow;
-  const float ma = ra < k ? 1.0f : 0.0f, mb = rb < k ? 1.0f : 0.0f;  // padding clients: y = 0
-  gf16 acc;
-  double accd[16];
+  // 16x16 form: lane (li, kk); this wave's three blocks (waves 0-3: a diagonal pair, 4-11: a triangle)
+  const int li = lane & 15, kk = lane >> 4;
+  const bool dg = w < 4;
+  int ro[3] = {0, 0, 0};  // row offsets of client 16 b + li of the wave's blocks
+  if constexpr (S16) {
 #pragma unroll
-  for (int q = 0; q < 16; ++q) { acc[q] = 0.0f; accd[q] = 0.0; }
+    for (int x = 0; x < 3; ++x) ro[x] = (16 * kG16Blocks[w][x] + li) * kGS;
+  }
+  constexpr int NACC = S16 ? 12 : 16;
+  gf16 acc;
+  gf4 a16[3];
+  double accd[NACC];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.0f;
+#pragma unroll
+  for (int x = 0; x < 3; ++x) a16[x] = gf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < NACC; ++q) accd[q] = 0.0;
   // staging: 16-byte vector q of client (idx / (kGE/4)) = coordinates 4 q .. 4 q + 3 of the chunk
   constexpr int QV = kGE / 4;
-  gf4 v[PD][C::NLD];  // a ring of PD chunks in flight (slot s: chunk c0 + 1 + s, + PD, ...)
+  gf4 v[C::NLD];
   // this thread's client pointers for the current segment (one pointer load per segment, not per
   // chunk: a per-chunk pointer load put a full memory round trip before every data load)
   const float* src[C::NLD];
   int cseg = -1;
-  auto load = [&](int64_t ch, gf4 (&v)[C::NLD]) {
+  auto load = [&](int64_t ch) {
     const int si = nseg > 1 ? find_seg(segs, nseg, ch) : 0;
     const PSeg sg = segs[si];
     if (si != cseg) {
@@ -1351,7 +1375,7 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
       }
     }
   };
-  auto put = [&](int buf, const gf4 (&v)[C::NLD]) {
+  auto put = [&](int buf) {
     float* L = lds0 + buf * C::KP * kGS;
 #pragma unroll
     for (int u = 0; u < C::NLD; ++u) {
@@ -1359,88 +1383,141 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
       if (C::NLD * C::NT == C::KP * QV || idx < C::KP * QV) *(gf4*)&L[(idx / QV) * kGS + 4 * (idx % QV)] = v[u];
     }
   };
-  // this block's chunks: one contiguous run (ilv = 0), or every gridDim.x-th chunk (ilv = 1: at any
-  // moment the blocks read one compact window of every client -- few pages, few DRAM rows)
-  const int64_t G = gridDim.x, B = blockIdx.x;
-  const int64_t c0 = ilv ? 0 : nchunks * B / G;
-  const int64_t c1 = ilv ? (nchunks - B + G - 1) / G : nchunks * (B + 1) / G;  // ilv: the count
-  auto at = [&](int64_t i) { return ilv ? B + i * G : i; };
+  const int64_t c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
   if (c0 < c1) {
-    load(at(c0), v[0]);
-    put(0, v[0]);
-#pragma unroll
-    for (int s = 0; s < PD; ++s)
-      if (c0 + 1 + s < c1) load(at(c0 + 1 + s), v[s]);
+    load(c0);
+    put(0);
+    if (c0 + 1 < c1) load(c0 + 1);
   }
   __syncthreads();
   int cur = 0;
-  // unrolled by PD so that every ring slot is a fixed register set (no moves of in-flight loads)
-  for (int64_t base = c0; base < c1; base += PD) {
+  for (int64_t ch = c0; ch < c1; ++ch, cur ^= 1) {
+    const float* L = lds0 + cur * C::KP * kGS;
+    // the centre of the chunk's coordinates, by every wave for itself: the median of clients 0..4
+    // (fewer clients: of 0..2, or client 0); padding coordinates are 0 everywhere, so y = 0 there
 #pragma unroll
-    for (int s = 0; s < PD; ++s) {
-      const int64_t ch = base + s;
-      if (ch >= c1) break;
-      const float* L = lds0 + cur * C::KP * kGS;
-      // the centre of the chunk's coordinates, by every wave for itself: the median of clients 0..4
-      // (fewer clients: of 0..2, or client 0); padding coordinates are 0 everywhere, so y = 0 there
-#pragma unroll
-      for (int e = lane; e < kGE; e += 64) {
-        float c;
-        if (k >= 5) {
-          const float a = L[e], b = L[kGS + e], cc = L[2 * kGS + e], d = L[3 * kGS + e], f = L[4 * kGS + e];
-          c = __builtin_amdgcn_fmed3f(f, fmaxf(fminf(a, b), fminf(cc, d)), fminf(fmaxf(a, b), fmaxf(cc, d)));
-        } else if (k >= 3) {
-          c = __builtin_amdgcn_fmed3f(L[e], L[kGS + e], L[2 * kGS + e]);
-        } else {
-          c = L[e];
-        }
-        cen[e] = c;
+    for (int e = lane; e < kGE; e += 64) {
+      float c;
+      if (k >= 5) {
+        const float a = L[e], b = L[kGS + e], cc = L[2 * kGS + e], d = L[3 * kGS + e], f = L[4 * kGS + e];
+        c = __builtin_amdgcn_fmed3f(f, fmaxf(fminf(a, b), fminf(cc, d)), fminf(fmaxf(a, b), fmaxf(cc, d)));
+      } else if (k >= 3) {
+        c = __builtin_amdgcn_fmed3f(L[e], L[kGS + e], L[2 * kGS + e]);
+      } else {
+        c = L[e];
       }
-      __builtin_amdgcn_wave_barrier();  // the wave's own LDS writes are seen by its later reads (in order)
+      cen[e] = c;
+    }
+    __builtin_amdgcn_wave_barrier();  // the wave's own LDS writes are seen by its later reads (in order)
+    // no padding mask: rows >= k are staged as zeros and their G entries are never read
+    if constexpr (S16) {
+      // lane (li, kk) reads unit 4 G + kk (coordinates 16 G + 4 kk .. + 3) of its blocks' rows: the k
+      // index of MFMA m is coordinate 16 G + 4 kk + m (any assignment works when A and B agree);
+      // rows 528 bytes apart, so the 16 rows of one b128 read hit distinct banks
+#pragma unroll
+      for (int G = 0; G < kGE / 16; ++G) {
+        const int u4 = 4 * (4 * G + kk);
+        const gf4 cc = *(const gf4*)&cen[u4];
+        const gf4 y0 = *(const gf4*)&L[ro[0] + u4] - cc;
+        const gf4 y1 = *(const gf4*)&L[ro[1] + u4] - cc;
+        if (dg) {  // (a,a), (a,b), (b,b)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            a16[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(y0[m], y0[m], a16[0], 0, 0, 0);
+            a16[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(y0[m], y1[m], a16[1], 0, 0, 0);
+            a16[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(y1[m], y1[m], a16[2], 0, 0, 0);
+          }
+        } else {  // (p,q), (p,r), (q,r)
+          const gf4 y2 = *(const gf4*)&L[ro[2] + u4] - cc;
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            a16[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(y0[m], y1[m], a16[0], 0, 0, 0);
+            a16[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(y0[m], y2[m], a16[1], 0, 0, 0);
+            a16[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(y1[m], y2[m], a16[2], 0, 0, 0);
+          }
+        }
+      }
+    } else {
       const float* La = L + ra * kGS + 4 * half;
       const float* Lb = L + rb * kGS + 4 * half;
       const float* cr = cen + 4 * half;
 #pragma unroll
       for (int g = r; g < kGE / 8; g += C::R) {
         const gf4 cc = *(const gf4*)&cr[8 * g];
-        const gf4 ya = (*(const gf4*)&La[8 * g] - cc) * ma;
-        const gf4 yb = diag ? ya : (*(const gf4*)&Lb[8 * g] - cc) * mb;
+        const gf4 ya = *(const gf4*)&La[8 * g] - cc;
+        const gf4 yb = diag ? ya : *(const gf4*)&Lb[8 * g] - cc;
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.x, yb.x, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.y, yb.y, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.z, yb.z, acc, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ya.w, yb.w, acc, 0, 0, 0);
       }
-      // float32 run of one chunk (kGE / R coordinates of this split) -> float64
+    }
+    // float32 runs of FL chunks (FL kGE / R coordinates of this split: 128 / 256) -> float64
+    constexpr int FL = KB == 1 ? 4 : 2;
+    if ((ch - c0) % FL == FL - 1 || ch + 1 == c1) {
+      if constexpr (S16) {
+#pragma unroll
+        for (int x = 0; x < 3; ++x)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            accd[4 * x + q] += (double)a16[x][q];
+            a16[x][q] = 0.0f;
+          }
+      } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          accd[q] += (double)acc[q];
+          acc[q] = 0.0f;
+        }
+      }
+    }
+    if (ch + 1 < c1) {
+      put(cur ^ 1);  // chunk ch + 1 (in registers); buffer cur ^ 1 was last read before the last barrier
+      if (ch + 2 < c1) load(ch + 2);
+    }
+    __syncthreads();  // one barrier per chunk
+  }
+  if constexpr (S16) {
+    // 16x16 C/D layout: register q of lane l is row 4 (l >> 4) + q, column l & 15 of its tile; tile
+    // (A, B) of the 16-blocks lands in 32x32 tile (A / 2, B / 2), quadrant (A % 2, B % 2), of this
+    // block's partial (the k_gram_reduce layout); a diagonal 32x32 tile's lower-left quadrant, never
+    // read, is written as zeros by its diagonal-pair wave
+    double* o = partial + (int64_t)blockIdx.x * C::T * 1024;
+#pragma unroll
+    for (int x = 0; x < 3; ++x) {
+      const int pa = dg ? (x == 2 ? 1 : 0) : (x == 2 ? 1 : 0), pb = dg ? (x == 0 ? 0 : 1) : (x == 0 ? 1 : 2);
+      const int A = kG16Blocks[w][pa], Bk = kG16Blocks[w][pb];
+      const int I = A >> 1, J = Bk >> 1;
+      const int t32 = I * KB - I * (I - 1) / 2 + (J - I);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        o[(int64_t)t32 * 1024 + (16 * (A & 1) + 4 * kk + q) * 32 + 16 * (Bk & 1) + li] = accd[4 * x + q];
+    }
+    if (dg) {
+      const int I = kG16Blocks[w][0] >> 1, t32 = I * KB - I * (I - 1) / 2;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[(int64_t)t32 * 1024 + (16 + 4 * kk + q) * 32 + li] = 0.0;
+    }
+    return;
+  } else {
+    // the R splits of a tile summed in split order through LDS (the chunk buffers are free now), then
+    // partial[(block * T + tile) * 1024 + row * 32 + col]; C/D layout of the 32x32 f32 MFMA: register q
+    // of lane l holds row (q & 3) + 8 (q >> 2) + 4 (l >> 5), column l & 31
+    double* red = (double*)gl;  // [W][1024]
+    if (C::R > 1) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) red[(int64_t)w * 1024 + q * 64 + lane] = accd[q];
+      __syncthreads();
+    }
+    if (r == 0) {
+      double* o = partial + ((int64_t)blockIdx.x * C::T + ti) * 1024;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
-        accd[q] += (double)acc[q];
-        acc[q] = 0.0f;
+        double sm = accd[q];
+        for (int rr = 1; rr < C::R; ++rr) sm += red[(int64_t)(w + rr) * 1024 + q * 64 + lane];
+        const int row = (q & 3) + 8 * (q >> 2) + 4 * half;
+        o[row * 32 + lrow] = sm;
       }
-      if (ch + 1 < c1) {
-        put(cur ^ 1, v[s]);  // chunk ch + 1; buffer cur ^ 1 was last read before the last barrier
-        if (ch + 1 + PD < c1) load(at(ch + 1 + PD), v[s]);
-      }
-      __syncthreads();  // one barrier per chunk
-      cur ^= 1;
-    }
-  }
-  // the R splits of a tile summed in split order through LDS (the chunk buffers are free now), then
-  // partial[(block * T + tile) * 1024 + row * 32 + col]; C/D layout of the 32x32 f32 MFMA: register q
-  // of lane l holds row (q & 3) + 8 (q >> 2) + 4 (l >> 5), column l & 31
-  double* red = (double*)gl;  // [W][1024]
-  if (C::R > 1) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) red[(int64_t)w * 1024 + q * 64 + lane] = accd[q];
-    __syncthreads();
-  }
-  if (r == 0) {
-    double* o = partial + ((int64_t)blockIdx.x * C::T + ti) * 1024;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      double s = accd[q];
-      for (int rr = 1; rr < C::R; ++rr) s += red[(int64_t)(w + rr) * 1024 + q * 64 + lane];
-      const int row = (q & 3) + 8 * (q >> 2) + 4 * half;
-      o[row * 32 + lrow] = s;
     }
   }
 }
@@ -1698,6 +1775,14 @@ k_gram_reduce(const double* __restrict__ partial, int nparts, double* __restrict
   if (threadIdx.x == 0) *kmax = red[0];
 }
 
+bool gram_s16() {  // K in (96, 128]: the 12-wave 16x16 form (FA_GRAM16=0: the 10-wave 32x32 form, A/B)
+  static const bool on = [] {
+    const char* e = getenv("FA_GRAM16");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int gram_glds() {  // K <= 32: FA_GRAM_GLDS = 8 (default): two 8-wave ring workgroups per CU; 16: one of 16 waves;
                   // 0: the register-staged k_pair_gram<1> (A/B)
   static const int d = [] {
@@ -1709,32 +1794,13 @@ int gram_glds() {  // K <= 32: FA_GRAM_GLDS = 8 (default): two 8-wave ring workg
   return d;
 }
 
-int gram_ilv() {  // FA_GRAM_ILV=1: chunks dealt round-robin over the workgroups (A/B)
-  static const int d = [] {
-    const char* e = getenv("FA_GRAM_ILV");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
-  return d;
-}
-
-int gram_pd1() {  // FA_GRAM_PD: K <= 32's register staging depth (measurement A/B; default GramPD<1>)
-  static const int d = [] {
-    const char* e = getenv("FA_GRAM_PD");
-    return e ? atoi(e) : 0;
-  }();
-  return d;
-}
-
 // workgroups: one per CU for K > 32 (12 / 12 / 10 waves, <= 128 VGPRs: 16 waves per CU); K <= 32 below
 int gram_nblocks(int64_t nchunks, int kb) {
   static const int ov = [] {  // FA_GRAM_BLOCKS: measurement override (A/B)
     const char* e = getenv("FA_GRAM_BLOCKS");
     return e ? atoi(e) : 0;
   }();
-  // K <= 32: as many workgroups as are resident -- 4 per CU at staging depth 1 (<= 128 VGPRs), 3 at
-  // depth 2 / 3 (145 / 163 VGPRs), 2 at depth 4 -- each takes one contiguous run of chunks
-  const int pd = gram_pd1() >= 1 && gram_pd1() <= 4 ? gram_pd1() : GramPD<1>::v;
-  const int64_t cap = ov >= 64 && ov <= 8192 ? ov : kb >= 2 ? 256 : 256 * (pd == 1 ? 4 : pd == 4 ? 2 : 3);
+  const int64_t cap = ov >= 64 && ov <= 8192 ? ov : kb >= 2 ? 256 : 1024;
   return (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, cap));
 }
 
@@ -1751,7 +1817,8 @@ size_t gram_scratch(int32_t num_segments, const int64_t* seg_numel, int32_t k) {
 }
 
 size_t gram_lds(int kb) {
-  const int T = gram_T(kb), R = kb == 1 ? 4 : kb == 2 ? 4 : kb == 3 ? 2 : 1, W = T * R;
+  const int T = gram_T(kb), R = kb == 1 ? 4 : kb == 2 ? 4 : kb == 3 ? 2 : 1;
+  const int W = kb == 4 && gram_s16() ? 12 : T * R;
   const size_t stage = sizeof(float) * (2 * (size_t)(32 * kb) * kGS + (size_t)W * kGE);
   return std::max(stage, sizeof(double) * 1024 * (size_t)W);  // the epilogue's split reduction
 }
@@ -1983,26 +2050,14 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
   const void* const* pp = (const void* const*)(dv + seg_bytes);
   const int ntr = gram_T(kb) * 1024 / 64;  // k_gram_reduce workgroups
   const size_t lds = gram_lds(kb);
-  const int ilv = gram_ilv();
-#define FA_GR1(PD)                                                                                             \
+#define FA_GR(KB, S)                                                                                           \
   do {                                                                                                         \
     if (vec)                                                                                                   \
-      hipLaunchKernelGGL((k_pair_gram<1, true, PD>), dim3((unsigned)nblocks), dim3(GramCfg<1>::NT), lds, st,   \
-                         sg, nseg, pp, k, nchunks, part, ilv, ctr);                                                 \
+      hipLaunchKernelGGL((k_pair_gram<KB, true, S>), dim3((unsigned)nblocks), dim3(GramCfg<KB, S>::NT), lds,    \
+                         st, sg, nseg, pp, k, nchunks, part, ctr);                                             \
     else                                                                                                       \
-      hipLaunchKernelGGL((k_pair_gram<1, false, PD>), dim3((unsigned)nblocks), dim3(GramCfg<1>::NT), lds, st,  \
-                         sg, nseg, pp, k, nchunks, part, ilv, ctr);                                                      \
-    hipLaunchKernelGGL((k_gram_reduce<1>), dim3((unsigned)ntr), dim3(64 * kGRW), 0, st, (const double*)part,     \
-                       nblocks, gm, k, (double*)d_dist, (double*)d_kappa_max, ctr);                           \
-  } while (0)
-#define FA_GR(KB)                                                                                              \
-  do {                                                                                                         \
-    if (vec)                                                                                                   \
-      hipLaunchKernelGGL((k_pair_gram<KB, true, GramPD<KB>::v>), dim3((unsigned)nblocks), dim3(GramCfg<KB>::NT), lds, st, sg, \
-                         nseg, pp, k, nchunks, part, ilv, ctr);                                                          \
-    else                                                                                                       \
-      hipLaunchKernelGGL((k_pair_gram<KB, false, GramPD<KB>::v>), dim3((unsigned)nblocks), dim3(GramCfg<KB>::NT), lds, st,    \
-                         sg, nseg, pp, k, nchunks, part, ilv, ctr);                                                      \
+      hipLaunchKernelGGL((k_pair_gram<KB, false, S>), dim3((unsigned)nblocks), dim3(GramCfg<KB, S>::NT), lds,   \
+                         st, sg, nseg, pp, k, nchunks, part, ctr);                                             \
     hipLaunchKernelGGL((k_gram_reduce<KB>), dim3((unsigned)ntr), dim3(64 * kGRW), 0, st, (const double*)part,    \
                        nblocks, gm, k, (double*)d_dist, (double*)d_kappa_max, ctr);                           \
   } while (0)
@@ -2022,20 +2077,15 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
     hipLaunchKernelGGL((k_gram_reduce<1>), dim3((unsigned)ntr), dim3(64 * kGRW), 0, st, (const double*)part, nbg, gm,
                        k, (double*)d_dist, (double*)d_kappa_max, ctr);
   } else switch (kb) {
-    case 1:  // FA_GRAM_PD = 2 / 3 / 4: another register staging depth for K <= 32 (A/B)
-      switch (gram_pd1()) {
-        case 2: FA_GR1(2); break;
-        case 3: FA_GR1(3); break;
-        case 4: FA_GR1(4); break;
-        default: FA_GR(1); break;
-      }
+    case 1: FA_GR(1, false); break;
+    case 2: FA_GR(2, false); break;
+    case 3: FA_GR(3, false); break;
+    default:
+      if (gram_s16()) FA_GR(4, true);
+      else FA_GR(4, false);
       break;
-    case 2: FA_GR(2); break;
-    case 3: FA_GR(3); break;
-    default: FA_GR(4); break;
   }
 #undef FA_GR
-#undef FA_GR1
   FA_HIP(hipGetLastError());
   rc = release(slot, st);
   if (rc || kappa_limit <= 0.0) return rc;
