@@ -1267,13 +1267,10 @@ typedef float gf4 __attribute__((ext_vector_type(4)));
 template <int KB, bool S16 = false> struct GramCfg {
   static constexpr int T = KB * (KB + 1) / 2;             // 32x32 tiles, upper triangle
   static constexpr int R = S16 ? 1 : KB == 1 ? 4 : KB == 2 ? 4 : KB == 3 ? 2 : 1;  // coordinate-group splits per tile
-  static constexpr int TPW = KB == 4 ? 3 : 1;             // S16: 16x16 tiles per wave (K > 96: 3; K <= 64: 1)
-  static constexpr int W = S16 ? (KB == 4 ? 12 : 10) : T * R;  // waves per workgroup, one (tile, split) each:
+  static constexpr int W = S16 ? 12 : T * R;              // waves per workgroup, one (tile, split) each:
                                                           // 4 / 12 / 12 / 10 -- a multiple of the CU's 4
                                                           // SIMDs except K > 96 (3, 3, 2, 2 tiles per SIMD),
-                                                          // whose S16 form runs 12 waves of three 16x16 tiles;
-                                                          // K in (32, 64] S16: 10 waves of one 16x16 tile,
-                                                          // two workgroups per CU (5 waves per SIMD)
+                                                          // whose S16 form runs 12 waves of three 16x16 tiles
   static constexpr int NT = W * 64;
   static constexpr int KP = 32 * KB;
   static constexpr int NLD = (KP * (kGE / 4) + NT - 1) / NT;  // staged 16-byte vectors per thread
@@ -1288,8 +1285,6 @@ template <int KB, bool S16 = false> struct GramCfg {
 // most 3 blocks -- waves 0-3 the diagonal pairs {2a, 2a + 1} (tiles (2a,2a), (2a,2a+1), (2a+1,2a+1)),
 // waves 4-11 the triangles of a decomposition of the remaining 24 block pairs (K_{2,2,2,2} into 8
 // triangles, found by search): every one of the 36 upper 16x16 tiles once, 3 per wave, 3 waves per SIMD
-// K in (32, 64], S16 form: the 10 upper 16x16 tiles of 4 client blocks, one per wave
-__constant__ const int8_t kG16Tiles2[10][2] = {{0, 0}, {0, 1}, {0, 2}, {0, 3}, {1, 1}, {1, 2}, {1, 3}, {2, 2}, {2, 3}, {3, 3}};
 __constant__ const int8_t kG16Blocks[12][3] = {{0, 1, 1}, {2, 3, 3}, {4, 5, 5}, {6, 7, 7}, {0, 2, 4}, {0, 3, 6},
                                                {0, 5, 7}, {1, 2, 7}, {1, 3, 5}, {1, 4, 6}, {2, 5, 6}, {3, 4, 7}};
 
@@ -1302,11 +1297,10 @@ __device__ __forceinline__ void gram_tile_kb(int t, int& bi, int& bj) {
 }
 
 template <int KB, bool VEC, bool S16>
-__global__ void __launch_bounds__((GramCfg<KB, S16>::NT)) __attribute__((amdgpu_waves_per_eu(S16 ? (KB == 4 ? 3 : 5) : 4)))
+__global__ void __launch_bounds__((GramCfg<KB, S16>::NT)) __attribute__((amdgpu_waves_per_eu(S16 ? 3 : 4)))
 k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k,
             int64_t nchunks, double* __restrict__ partial, unsigned* __restrict__ ctr) {
-  static_assert(!S16 || KB == 4 || KB == 2, "16x16 wave tables for 8 (K > 96) or 4 (K <= 64) client blocks");
-  constexpr int TPW = GramCfg<KB, S16>::TPW;
+  static_assert(!S16 || KB == 4, "the 16x16 wave table is for 8 client blocks");
   using C = GramCfg<KB, S16>;
   if (blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;  // k_gram_reduce's arrival counter
   extern __shared__ __attribute__((aligned(16))) float gl[];
@@ -1327,9 +1321,9 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
   int ro[3] = {0, 0, 0};  // row offsets of client 16 b + li of the wave's blocks
   if constexpr (S16) {
 #pragma unroll
-    for (int x = 0; x < 3; ++x) ro[x] = (16 * (KB == 4 ? kG16Blocks[w][x] : kG16Tiles2[w][x < 2 ? x : 1]) + li) * kGS;
+    for (int x = 0; x < 3; ++x) ro[x] = (16 * kG16Blocks[w][x] + li) * kGS;
   }
-  constexpr int NACC = S16 ? 4 * TPW : 16;
+  constexpr int NACC = S16 ? 12 : 16;
   gf16 acc;
   gf4 a16[3];
   double accd[NACC];
@@ -1426,10 +1420,7 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
         const gf4 cc = *(const gf4*)&cen[u4];
         const gf4 y0 = *(const gf4*)&L[ro[0] + u4] - cc;
         const gf4 y1 = *(const gf4*)&L[ro[1] + u4] - cc;
-        if (KB == 2) {  // the wave's one tile (A, B)
-#pragma unroll
-          for (int m = 0; m < 4; ++m) a16[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(y0[m], y1[m], a16[0], 0, 0, 0);
-        } else if (dg) {  // (a,a), (a,b), (b,b)
+        if (dg) {  // (a,a), (a,b), (b,b)
 #pragma unroll
           for (int m = 0; m < 4; ++m) {
             a16[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(y0[m], y0[m], a16[0], 0, 0, 0);
@@ -1466,7 +1457,7 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
     if ((ch - c0) % FL == FL - 1 || ch + 1 == c1) {
       if constexpr (S16) {
 #pragma unroll
-        for (int x = 0; x < TPW; ++x)
+        for (int x = 0; x < 3; ++x)
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             accd[4 * x + q] += (double)a16[x][q];
@@ -1493,18 +1484,17 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
     // read, is written as zeros by its diagonal-pair wave
     double* o = partial + (int64_t)blockIdx.x * C::T * 1024;
 #pragma unroll
-    for (int x = 0; x < TPW; ++x) {
+    for (int x = 0; x < 3; ++x) {
       const int pa = dg ? (x == 2 ? 1 : 0) : (x == 2 ? 1 : 0), pb = dg ? (x == 0 ? 0 : 1) : (x == 0 ? 1 : 2);
-      const int A = KB == 4 ? kG16Blocks[w][pa] : kG16Tiles2[w][0], Bk = KB == 4 ? kG16Blocks[w][pb] : kG16Tiles2[w][1];
+      const int A = kG16Blocks[w][pa], Bk = kG16Blocks[w][pb];
       const int I = A >> 1, J = Bk >> 1;
       const int t32 = I * KB - I * (I - 1) / 2 + (J - I);
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         o[(int64_t)t32 * 1024 + (16 * (A & 1) + 4 * kk + q) * 32 + 16 * (Bk & 1) + li] = accd[4 * x + q];
     }
-    const bool zq = KB == 4 ? dg : (kG16Tiles2[w][0] & 1) == 0 && kG16Tiles2[w][1] == kG16Tiles2[w][0] + 1;
-    if (zq) {  // the (2I, 2I + 1) tile's wave zeroes 32x32 tile (I, I)'s lower-left quadrant
-      const int I = (KB == 4 ? kG16Blocks[w][0] : kG16Tiles2[w][0]) >> 1, t32 = I * KB - I * (I - 1) / 2;
+    if (dg) {
+      const int I = kG16Blocks[w][0] >> 1, t32 = I * KB - I * (I - 1) / 2;
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[(int64_t)t32 * 1024 + (16 + 4 * kk + q) * 32 + li] = 0.0;
     }
@@ -1785,7 +1775,7 @@ k_gram_reduce(const double* __restrict__ partial, int nparts, double* __restrict
   if (threadIdx.x == 0) *kmax = red[0];
 }
 
-bool gram_s16() {  // K in (32, 64] and (96, 128]: the 16x16 forms (FA_GRAM16=0: the 32x32 forms, A/B)
+bool gram_s16() {  // K in (96, 128]: the 12-wave 16x16 form (FA_GRAM16=0: the 10-wave 32x32 form, A/B)
   static const bool on = [] {
     const char* e = getenv("FA_GRAM16");
     return !(e && e[0] == '0');
@@ -1810,8 +1800,7 @@ int gram_nblocks(int64_t nchunks, int kb) {
     const char* e = getenv("FA_GRAM_BLOCKS");
     return e ? atoi(e) : 0;
   }();
-  // (K in (32, 64] in the S16 form: two 10-wave workgroups per CU)
-  const int64_t cap = ov >= 64 && ov <= 8192 ? ov : kb == 2 && gram_s16() ? 512 : kb >= 2 ? 256 : 1024;
+  const int64_t cap = ov >= 64 && ov <= 8192 ? ov : kb >= 2 ? 256 : 1024;
   return (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, cap));
 }
 
@@ -1829,7 +1818,7 @@ size_t gram_scratch(int32_t num_segments, const int64_t* seg_numel, int32_t k) {
 
 size_t gram_lds(int kb) {
   const int T = gram_T(kb), R = kb == 1 ? 4 : kb == 2 ? 4 : kb == 3 ? 2 : 1;
-  const int W = kb == 4 && gram_s16() ? 12 : kb == 2 && gram_s16() ? 10 : T * R;
+  const int W = kb == 4 && gram_s16() ? 12 : T * R;
   const size_t stage = sizeof(float) * (2 * (size_t)(32 * kb) * kGS + (size_t)W * kGE);
   return std::max(stage, sizeof(double) * 1024 * (size_t)W);  // the epilogue's split reduction
 }
@@ -2089,10 +2078,7 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
                        k, (double*)d_dist, (double*)d_kappa_max, ctr);
   } else switch (kb) {
     case 1: FA_GR(1, false); break;
-    case 2:
-      if (gram_s16()) FA_GR(2, true);
-      else FA_GR(2, false);
-      break;
+    case 2: FA_GR(2, false); break;
     case 3: FA_GR(3, false); break;
     default:
       if (gram_s16()) FA_GR(4, true);
