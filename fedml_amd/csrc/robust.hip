@@ -1544,7 +1544,7 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
 template <int NB, int CW, int WV>
 __global__ void __launch_bounds__(64 * WV) __attribute__((amdgpu_waves_per_eu(4)))
 k_pair_gram_ring(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k,
-                 int64_t nfull, double* __restrict__ partial, int dbg, unsigned* __restrict__ ctr) {
+                 int64_t nfull, double* __restrict__ partial, unsigned* __restrict__ ctr) {
   constexpr int RS = CW, BUF = 32 * RS;        // floats per client row / per ring buffer
   constexpr int U = CW / 4, RPI = 64 / U;      // 16-byte units per row, rows per DMA wave-instruction
   constexpr int IPW = 32 / RPI / WV;           // DMA instructions per wave and chunk
@@ -1593,7 +1593,7 @@ k_pair_gram_ring(const PSeg* __restrict__ segs, int nseg, const void* const* __r
   // index of MFMA m is coordinate 4 kk + m -- any assignment works when A and B agree).  Rows >= k hold
   // client 0's coordinates (DMA) or zeros (partial chunks): their G entries are never read.
   auto compute = [&](const float* L, bool flush) {
-    if (!(dbg & 1) && lane < 16) {  // the centre of this wave's 16 coordinates (median of clients 0..4)
+    if (lane < 16) {  // the centre of this wave's 16 coordinates (median of clients 0..4)
       const int u = 4 * w + (lane >> 2), z = lane & 3;
       float c;
       if (k >= 5) {
@@ -1611,9 +1611,7 @@ k_pair_gram_ring(const PSeg* __restrict__ segs, int nseg, const void* const* __r
     const int pu = 4 * ((4 * w + kk) ^ li);  // physical unit of logical unit 4 w + kk in rows li and 16 + li
     const gf4 cc = *(const gf4*)&cen[4 * kk];
     const gf4 y0 = *(const gf4*)&L[li * RS + pu] - cc;
-    if (dbg & 4) {  // measurement only (FA_GRAM_DBG): no MFMA
-      t00[0] += y0.x + y0.y + y0.z + y0.w;
-    } else if (k > 16) {
+    if (k > 16) {
       const gf4 y1 = *(const gf4*)&L[(16 + li) * RS + pu] - cc;
 #pragma unroll
       for (int m = 0; m < 4; ++m) {
@@ -1625,7 +1623,7 @@ k_pair_gram_ring(const PSeg* __restrict__ segs, int nseg, const void* const* __r
 #pragma unroll
       for (int m = 0; m < 4; ++m) t00 = __builtin_amdgcn_mfma_f32_16x16x4f32(y0[m], y0[m], t00, 0, 0, 0);
     }
-    if (flush && !(dbg & 2)) {  // float32 runs of 4 chunks (64 products per entry) -> float64
+    if (flush) {  // float32 runs of 4 chunks (64 products per entry) -> float64
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         a00[q] += (double)t00[q];
@@ -1648,7 +1646,7 @@ k_pair_gram_ring(const PSeg* __restrict__ segs, int nseg, const void* const* __r
       __builtin_amdgcn_s_barrier();  // chunk i landed for every wave; every wave is done with buffer (i - 1) % NB
       const int64_t nx = i + NB - 1;
       issue(nx < n ? c0 + nx : 0, (int)(nx % NB));
-      if (!(dbg & 8)) compute(gl + (int)(i % NB) * BUF, (i & 3) == 3 || i + 1 == n);  // dbg 8: the read alone
+      compute(gl + (int)(i % NB) * BUF, (i & 3) == 3 || i + 1 == n);
     }
   }
   __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): the fill loads landed
@@ -1783,13 +1781,10 @@ bool gram_s16() {  // K in (96, 128]: the 12-wave 16x16 form (FA_GRAM16=0: the 1
   return on;
 }
 
-int gram_glds() {  // K <= 32: FA_GRAM_GLDS = 8 (default): two 8-wave ring workgroups per CU; 16: one of 16 waves;
-                  // 0: the register-staged k_pair_gram<1> (A/B)
+int gram_glds() {  // K <= 32: the LDS-DMA ring kernel (FA_GRAM_GLDS=0: the register-staged k_pair_gram<1>, A/B)
   static const int d = [] {
     const char* e = getenv("FA_GRAM_GLDS");
-    if (!e) return 8;
-    const int v = atoi(e);
-    return v == 0 || v == 16 ? v : 8;
+    return e && e[0] == '0' ? 0 : 8;
   }();
   return d;
 }
@@ -1998,7 +1993,7 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
   // index runs over FULL chunks only (tile_start = the segment's first full chunk, pad = 1: a partial
   // chunk follows)
   const int glds = kbc == 1 && vec ? gram_glds() : 0;
-  const int cs = glds == 16 ? 256 : glds == 8 ? 128 : gram_chunk(kbc);
+  const int cs = glds ? 128 : gram_chunk(kbc);
   int nseg = 0;
   int64_t nchunks = 0;
   for (int s = 0; s < num_segments; ++s) {
@@ -2061,19 +2056,11 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
     hipLaunchKernelGGL((k_gram_reduce<KB>), dim3((unsigned)ntr), dim3(64 * kGRW), 0, st, (const double*)part,    \
                        nblocks, gm, k, (double*)d_dist, (double*)d_kappa_max, ctr);                           \
   } while (0)
-  if (glds) {  // c0 = the full-chunk count; one 16-wave workgroup per CU, or two of 8 waves
-    const int nbg = (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, glds == 16 ? 256 : 512));
+  if (glds) {  // c0 = the full-chunk count; two 8-wave workgroups per CU
+    const int nbg = (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, 512));
     const size_t lg = (size_t)4 * 32 * cs * sizeof(float) + (size_t)glds * 16 * sizeof(float);
-    static const int dbg = [] {  // FA_GRAM_DBG: measurement only -- parts of the compute skipped (wrong results)
-      const char* e = getenv("FA_GRAM_DBG");
-      return e ? atoi(e) : 0;
-    }();
-    if (glds == 16)
-      hipLaunchKernelGGL((k_pair_gram_ring<4, 256, 16>), dim3((unsigned)nbg), dim3(1024), lg, st, sg, nseg, pp, k, c0,
-                         part, dbg, ctr);
-    else
-      hipLaunchKernelGGL((k_pair_gram_ring<4, 128, 8>), dim3((unsigned)nbg), dim3(512), lg, st, sg, nseg, pp, k, c0,
-                         part, dbg, ctr);
+    hipLaunchKernelGGL((k_pair_gram_ring<4, 128, 8>), dim3((unsigned)nbg), dim3(512), lg, st, sg, nseg, pp, k, c0,
+                       part, ctr);
     hipLaunchKernelGGL((k_gram_reduce<1>), dim3((unsigned)ntr), dim3(64 * kGRW), 0, st, (const double*)part, nbg, gm,
                        k, (double*)d_dist, (double*)d_kappa_max, ctr);
   } else switch (kb) {
