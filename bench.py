@@ -43,6 +43,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+MFMA_F32_PEAK_TFS = 157.3  # dense f32-input MFMA (v_mfma_f32_{32x32x2,16x16x4}_f32), MI355X_MICROARCH.md
 # FEDML_AMD_BENCH_REHEARSAL=cpu (tests only): the N-rank metric / hier / gossip code paths -- launcher,
 # gloo process group, GroupReducer / DistributedGossip, per-rank parity -- on the CPU, with the local
 # reductions of an engine the TEST injects (FEDML_AMD_BENCH_ENGINE=module:factory, e.g.
@@ -1703,8 +1704,11 @@ def wl_krum(args, eng, rank, world, timer):
                 extra_line=extra,
                 bytes_total=K * P * 4, launch_bytes=K * P * 4, clients=K, params=P, cpu_K=K, cpu=cpu,
                 data="synthetic N(0,1) client weight vectors, resident in HBM (rows 256-byte aligned)",
-                roofline_note=f"VALU work {pairs} pairs x 3 flop per coordinate = {3 * pairs * P / 1e9:.1f} GFLOP/step; "
-                              "achieved here is the HBM rate (each client read once)")
+                mfma_flops_per_launch=K * (K + 1) * P, mfma_bound=K > 32,
+                roofline_note=(f"Gram form (float32 default): G = Y Y^T on the f32 MFMA, K (K + 1) P = "
+                               f"{K * (K + 1) * P / 1e9:.1f} GFLOP per launch (the upper triangle incl. the "
+                               "diagonal); K <= 32 the read bounds it (each client read once), K > 32 the "
+                               f"matrix cores; the direct form: {pairs} pairs x 3 flop per coordinate"))
 
 
 # ----------------------------------------------------------------------------- CPU baseline
@@ -2001,6 +2005,16 @@ def main():
         if wl.get("roofline_note"):
             line["roofline"]["note"] = wl["roofline_note"]
         line.update(wl.get("extra_line", {}))
+        mf = wl.get("mfma_flops_per_launch")
+        if mf and world == 1 and kernel_ms and line.get("pair_form") == "gram" and wl.get("mfma_bound"):
+            # Krum's Gram form past K = 32 is matrix-core work: the bound is the f32 MFMA peak, the HBM
+            # figures stay beside it
+            rl = line["roofline"]
+            hbm = {k: rl.get(k) for k in ("achieved", "peak", "unit", "frac")}
+            tfs = mf / (kernel_ms * 1e-3) / 1e12
+            rl.update({"bound": "mfma", "achieved": round(tfs, 2), "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
+                       "frac": round(tfs / MFMA_F32_PEAK_TFS, 4), "algorithmic_flops_per_launch": int(mf),
+                       "hbm": hbm})
         if CPU_REHEARSAL:
             line["rehearsal"] = ("CPU: bench.py's N-rank code path over gloo with a test's injected local reductions "
                                  "(tests/rehearsal_engine.py) -- checks the exchange, not a measurement")
