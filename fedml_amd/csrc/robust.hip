@@ -1266,11 +1266,12 @@ typedef float gf4 __attribute__((ext_vector_type(4)));
 
 template <int KB, bool S16 = false> struct GramCfg {
   static constexpr int T = KB * (KB + 1) / 2;             // 32x32 tiles, upper triangle
-  static constexpr int R = S16 ? 1 : KB == 1 ? 4 : KB == 2 ? 4 : KB == 3 ? 2 : 1;  // coordinate-group splits per tile
-  static constexpr int W = S16 ? 12 : T * R;              // waves per workgroup, one (tile, split) each:
+  static constexpr int R = S16 ? (KB == 4 ? 1 : 4) : KB == 1 ? 4 : KB == 2 ? 4 : KB == 3 ? 2 : 1;  // coordinate splits
+  static constexpr int W = S16 ? (KB == 4 ? 12 : 16) : T * R;  // waves per workgroup, one (tile, split) each:
                                                           // 4 / 12 / 12 / 10 -- a multiple of the CU's 4
                                                           // SIMDs except K > 96 (3, 3, 2, 2 tiles per SIMD),
-                                                          // whose S16 form runs 12 waves of three 16x16 tiles
+                                                          // whose S16 form runs 12 waves of three 16x16 tiles;
+                                                          // K in (32, 64] S16: 16 waves, 4 tile sets x 4 splits
   static constexpr int NT = W * 64;
   static constexpr int KP = 32 * KB;
   static constexpr int NLD = (KP * (kGE / 4) + NT - 1) / NT;  // staged 16-byte vectors per thread
@@ -1287,6 +1288,11 @@ template <int KB, bool S16 = false> struct GramCfg {
 // triangles, found by search): every one of the 36 upper 16x16 tiles once, 3 per wave, 3 waves per SIMD
 __constant__ const int8_t kG16Blocks[12][3] = {{0, 1, 1}, {2, 3, 3}, {4, 5, 5}, {6, 7, 7}, {0, 2, 4}, {0, 3, 6},
                                                {0, 5, 7}, {1, 2, 7}, {1, 3, 5}, {1, 4, 6}, {2, 5, 6}, {3, 4, 7}};
+// K in (32, 64], S16 form: 4 tile sets of the 4 client blocks -- the diagonal pairs {0, 1} and {2, 3}
+// (3 tiles each) and the cross pairs (0, {2, 3}) and (1, {2, 3}) (2 tiles each) -- each over 4
+// coordinate splits; wave w runs set (w % 4 + w / 4) % 4, split w / 4, so every SIMD (w % 4) holds
+// two 3-tile and two 2-tile waves.  Row: {type (0 diagonal pair, 2 cross pair), block 0, 1, 2}.
+__constant__ const int8_t kG16Sets2[4][4] = {{0, 0, 1, 1}, {0, 2, 3, 3}, {2, 0, 2, 3}, {2, 1, 2, 3}};
 
 template <int KB>
 __device__ __forceinline__ void gram_tile_kb(int t, int& bi, int& bj) {
@@ -1297,10 +1303,10 @@ __device__ __forceinline__ void gram_tile_kb(int t, int& bi, int& bj) {
 }
 
 template <int KB, bool VEC, bool S16>
-__global__ void __launch_bounds__((GramCfg<KB, S16>::NT)) __attribute__((amdgpu_waves_per_eu(S16 ? 3 : 4)))
+__global__ void __launch_bounds__((GramCfg<KB, S16>::NT)) __attribute__((amdgpu_waves_per_eu(S16 && KB == 4 ? 3 : 4)))
 k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k,
             int64_t nchunks, double* __restrict__ partial, unsigned* __restrict__ ctr) {
-  static_assert(!S16 || KB == 4, "the 16x16 wave table is for 8 client blocks");
+  static_assert(!S16 || KB == 4 || KB == 2, "16x16 wave tables for 8 (K > 96) or 4 (K in (32, 64]) client blocks");
   using C = GramCfg<KB, S16>;
   if (blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;  // k_gram_reduce's arrival counter
   extern __shared__ __attribute__((aligned(16))) float gl[];
@@ -1315,13 +1321,20 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
   const bool diag = bi == bj;
   const int half = lane >> 5, lrow = lane & 31;
   const int ra = 32 * bi + lrow, rb = 32 * bj + lrow;
-  // 16x16 form: lane (li, kk); this wave's three blocks (waves 0-3: a diagonal pair, 4-11: a triangle)
+  // 16x16 form: lane (li, kk); this wave's tile set -- type 0: a diagonal pair (b0,b0), (b0,b1),
+  // (b1,b1); 1: a triangle (b0,b1), (b0,b2), (b1,b2); 2: a cross pair (b0,b1), (b0,b2) -- and split
   const int li = lane & 15, kk = lane >> 4;
-  const bool dg = w < 4;
+  const int r16 = KB == 4 ? 0 : w / 4, set16 = KB == 4 ? w : (w % 4 + w / 4) % 4;
+  const int typ = KB == 4 ? (w < 4 ? 0 : 1) : kG16Sets2[set16][0];
+  const bool dg = typ == 0;
+  int blk[3] = {0, 0, 0};
   int ro[3] = {0, 0, 0};  // row offsets of client 16 b + li of the wave's blocks
   if constexpr (S16) {
 #pragma unroll
-    for (int x = 0; x < 3; ++x) ro[x] = (16 * kG16Blocks[w][x] + li) * kGS;
+    for (int x = 0; x < 3; ++x) {
+      blk[x] = KB == 4 ? kG16Blocks[w][x] : kG16Sets2[set16][1 + x];
+      ro[x] = (16 * blk[x] + li) * kGS;
+    }
   }
   constexpr int NACC = S16 ? 12 : 16;
   gf16 acc;
@@ -1415,7 +1428,8 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
       // index of MFMA m is coordinate 16 G + 4 kk + m (any assignment works when A and B agree);
       // rows 528 bytes apart, so the 16 rows of one b128 read hit distinct banks
 #pragma unroll
-      for (int G = 0; G < kGE / 16; ++G) {
+      for (int gi = 0; gi < kGE / 16 / C::R; ++gi) {
+        const int G = r16 + gi * C::R;
         const int u4 = 4 * (4 * G + kk);
         const gf4 cc = *(const gf4*)&cen[u4];
         const gf4 y0 = *(const gf4*)&L[ro[0] + u4] - cc;
@@ -1427,13 +1441,20 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
             a16[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(y0[m], y1[m], a16[1], 0, 0, 0);
             a16[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(y1[m], y1[m], a16[2], 0, 0, 0);
           }
-        } else {  // (p,q), (p,r), (q,r)
+        } else if (typ == 1) {  // (p,q), (p,r), (q,r)
           const gf4 y2 = *(const gf4*)&L[ro[2] + u4] - cc;
 #pragma unroll
           for (int m = 0; m < 4; ++m) {
             a16[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(y0[m], y1[m], a16[0], 0, 0, 0);
             a16[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(y0[m], y2[m], a16[1], 0, 0, 0);
             a16[2] = __builtin_amdgcn_mfma_f32_16x16x4f32(y1[m], y2[m], a16[2], 0, 0, 0);
+          }
+        } else {  // (a,p), (a,q)
+          const gf4 y2 = *(const gf4*)&L[ro[2] + u4] - cc;
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            a16[0] = __builtin_amdgcn_mfma_f32_16x16x4f32(y0[m], y1[m], a16[0], 0, 0, 0);
+            a16[1] = __builtin_amdgcn_mfma_f32_16x16x4f32(y0[m], y2[m], a16[1], 0, 0, 0);
           }
         }
       }
@@ -1481,12 +1502,24 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
     // 16x16 C/D layout: register q of lane l is row 4 (l >> 4) + q, column l & 15 of its tile; tile
     // (A, B) of the 16-blocks lands in 32x32 tile (A / 2, B / 2), quadrant (A % 2, B % 2), of this
     // block's partial (the k_gram_reduce layout); a diagonal 32x32 tile's lower-left quadrant, never
-    // read, is written as zeros by its diagonal-pair wave
+    // read, is written as zeros by its diagonal-pair wave.  K in (32, 64]: the 4 splits of a set are
+    // summed in split order through LDS first (the chunk buffers are free now)
+    if constexpr (C::R > 1) {
+      double* red = (double*)gl;  // [W][12][64]
+#pragma unroll
+      for (int q = 0; q < 12; ++q) red[(int64_t)w * 768 + q * 64 + lane] = accd[q];
+      __syncthreads();
+      if (r16 != 0) return;
+#pragma unroll
+      for (int q = 0; q < 12; ++q)
+        for (int rr = 1; rr < C::R; ++rr) accd[q] += red[(int64_t)(4 * rr + ((set16 - rr + 4) % 4)) * 768 + q * 64 + lane];
+    }
     double* o = partial + (int64_t)blockIdx.x * C::T * 1024;
 #pragma unroll
     for (int x = 0; x < 3; ++x) {
-      const int pa = dg ? (x == 2 ? 1 : 0) : (x == 2 ? 1 : 0), pb = dg ? (x == 0 ? 0 : 1) : (x == 0 ? 1 : 2);
-      const int A = kG16Blocks[w][pa], Bk = kG16Blocks[w][pb];
+      if (typ == 2 && x == 2) break;  // a cross pair has two tiles
+      const int pa = x == 2 ? 1 : 0, pb = dg ? (x == 0 ? 0 : 1) : (x == 0 ? 1 : 2);
+      const int A = blk[pa], Bk = blk[pb];
       const int I = A >> 1, J = Bk >> 1;
       const int t32 = I * KB - I * (I - 1) / 2 + (J - I);
 #pragma unroll
@@ -1494,7 +1527,7 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
         o[(int64_t)t32 * 1024 + (16 * (A & 1) + 4 * kk + q) * 32 + 16 * (Bk & 1) + li] = accd[4 * x + q];
     }
     if (dg) {
-      const int I = kG16Blocks[w][0] >> 1, t32 = I * KB - I * (I - 1) / 2;
+      const int I = blk[0] >> 1, t32 = I * KB - I * (I - 1) / 2;
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[(int64_t)t32 * 1024 + (16 + 4 * kk + q) * 32 + li] = 0.0;
     }
@@ -1773,7 +1806,7 @@ k_gram_reduce(const double* __restrict__ partial, int nparts, double* __restrict
   if (threadIdx.x == 0) *kmax = red[0];
 }
 
-bool gram_s16() {  // K in (96, 128]: the 12-wave 16x16 form (FA_GRAM16=0: the 10-wave 32x32 form, A/B)
+bool gram_s16() {  // K in (32, 64] and (96, 128]: the 16x16 forms (FA_GRAM16=0: the 32x32 forms, A/B)
   static const bool on = [] {
     const char* e = getenv("FA_GRAM16");
     return !(e && e[0] == '0');
@@ -1813,9 +1846,10 @@ size_t gram_scratch(int32_t num_segments, const int64_t* seg_numel, int32_t k) {
 
 size_t gram_lds(int kb) {
   const int T = gram_T(kb), R = kb == 1 ? 4 : kb == 2 ? 4 : kb == 3 ? 2 : 1;
-  const int W = kb == 4 && gram_s16() ? 12 : T * R;
+  const bool s16 = (kb == 4 || kb == 2) && gram_s16();
+  const int W = s16 ? (kb == 4 ? 12 : 16) : T * R;
   const size_t stage = sizeof(float) * (2 * (size_t)(32 * kb) * kGS + (size_t)W * kGE);
-  return std::max(stage, sizeof(double) * 1024 * (size_t)W);  // the epilogue's split reduction
+  return std::max(stage, sizeof(double) * (s16 ? 768 : 1024) * (size_t)W);  // the epilogue's split reduction
 }
 
 int pairdist_direct(fa_ctx* ctx, int diff_dtype, int32_t num_segments, const int64_t* seg_numel, int32_t k,
@@ -2065,7 +2099,10 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
                        k, (double*)d_dist, (double*)d_kappa_max, ctr);
   } else switch (kb) {
     case 1: FA_GR(1, false); break;
-    case 2: FA_GR(2, false); break;
+    case 2:
+      if (gram_s16()) FA_GR(2, true);
+      else FA_GR(2, false);
+      break;
     case 3: FA_GR(3, false); break;
     default:
       if (gram_s16()) FA_GR(4, true);
