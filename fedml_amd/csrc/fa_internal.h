@@ -93,7 +93,6 @@ struct fa_ctx {
     bool copy_live = false;       // `staged` recorded and the host buffer may still be read by that copy
     hipStream_t last = nullptr;   // the stream of the slot's last use (its readers of `dev`)
     bool used = false;            // `last` is set
-    hipStream_t synced = nullptr; // a stream already ordered after the last copy
     std::vector<char> shadow;     // the bytes `dev` holds, for stage(..., reuse) (valid if shadow_ok)
     bool shadow_ok = false;
     bool acquired = false;        // acquire_slot'ed and not yet release()d

@@ -1080,7 +1080,6 @@ int acquire_slot(fa_ctx* ctx, size_t bytes, fa_ctx::Slot** out) {
     s.cap = 0;
     s.shadow_ok = false;
     s.used = false;
-    s.synced = nullptr;
     // mapped: the staging copy is a kernel reading it over PCIe (stage())
     if (hipHostMalloc(&s.host, cap, hipHostMallocMapped) != hipSuccess)
       return fail(FA_ERR_NOMEM, "hipHostMalloc(%zu) failed", cap);
@@ -1149,11 +1148,11 @@ int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st, bool reuse) {
   if (!s->staged && hipEventCreateWithFlags(&s->staged, hipEventDisableTiming) != hipSuccess)
     return fail(FA_ERR_HIP, "hipEventCreate failed");
   if (reuse && s->shadow_ok && s->shadow.size() == bytes && memcmp(s->host, s->shadow.data(), bytes) == 0) {
-    // the device buffer holds these bytes; a stream not yet ordered after that copy waits for it
-    if (s->synced != st) {
-      FA_HIP(hipStreamWaitEvent(st, s->staged, 0));
-      s->synced = st;
-    }
+    // the device buffer holds these bytes; while the copy that put them there may still be in
+    // flight, the caller's stream waits for it (any stream: no bookkeeping of which streams did)
+    const hipError_t q = hipEventQuery(s->staged);
+    if (q == hipErrorNotReady) FA_HIP(hipStreamWaitEvent(st, s->staged, 0));
+    else if (q != hipSuccess) FA_HIP(q);
     s->hit = true;
     return FA_OK;
   }
@@ -1189,7 +1188,6 @@ int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st, bool reuse) {
     FA_HIP(hipEventRecord(s->staged, st));
   }
   s->copy_live = true;
-  s->synced = st;
   if (reuse) {
     s->shadow.assign((const char*)s->host, (const char*)s->host + bytes);
     s->shadow_ok = true;
