@@ -278,6 +278,22 @@ def test_pairwise_forms_vs_oracle(eng, k, form):
     np.testing.assert_allclose(D.numpy(), ref.numpy(), rtol=1e-6)
 
 
+@pytest.mark.parametrize("k", [5, 16, 17, 32])
+@pytest.mark.parametrize("sizes", [(3, 9001, 64), (64, 3, 129, 128), (256,), (127,)])
+def test_pairwise_ring_segment_orders(eng, k, sizes):
+    """K <= 32's LDS-DMA ring kernel (k_pair_gram_ring): segments without a full 128-coordinate chunk
+    before, between and after full ones (the ring's full-chunk index and its fill loads of chunk 0),
+    exact multiples of the chunk, and a lone partial chunk; within 1e-6 of the float64 oracle."""
+    from oracle import orc
+    g = torch.Generator().manual_seed(31 * k + len(sizes))
+    base = [torch.randn(s, generator=g) for s in sizes]
+    xs = [[b + 0.3 * torch.randn(s, generator=g) for b, s in zip(base, sizes)] for _ in range(k)]
+    D = eng._pairwise_launch([[xs[i][s].to(DEV) for i in range(k)] for s in range(len(sizes))], form="gram").cpu()
+    ref = orc.pairwise_sqdist([torch.cat(x) for x in xs])
+    assert torch.equal(D, D.T) and torch.all(D.diag() == 0)
+    np.testing.assert_allclose(D.numpy(), ref.numpy(), rtol=1e-6)
+
+
 @pytest.mark.parametrize("k", [8, 40, 128])
 def test_pairwise_gram_falls_back_when_ill_conditioned(eng, k):
     """Clients 0..4 (the Gram form's centre) far from a tight honest cluster: the honest pairs cancel
