@@ -1153,6 +1153,12 @@ int stage(fa_ctx::Slot* s, size_t bytes, hipStream_t st, bool reuse) {
     const hipError_t q = hipEventQuery(s->staged);
     if (q == hipErrorNotReady) FA_HIP(hipStreamWaitEvent(st, s->staged, 0));
     else if (q != hipSuccess) FA_HIP(q);
+    // readers on another stream: this stream's use is ordered after the slot's previous one, so the
+    // readers of `dev` form one chain and a later copy, ordered after the last of them, is after all
+    if (!slot_event_mode() && s->used && s->last != st) {
+      if (!s->ev_live) FA_HIP(hipEventRecord(s->ev, s->last));
+      FA_HIP(hipStreamWaitEvent(st, s->ev, 0));
+    }
     s->hit = true;
     return FA_OK;
   }
