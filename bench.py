@@ -436,30 +436,52 @@ class _HostEvent:
 
 
 class Timed:
-    """HIP-event timing of the dominant kernel launches, on the stream they are issued on."""
+    """HIP-event timing of the dominant kernel launches, on the stream they are issued on.
+
+    Per-launch mode (default): an event pair around every timed launch.  Loop mode (``loop``, set
+    for one-GPU workloads whose step IS the timed call -- ``loop_timing`` in the workload): one event
+    pair around the whole timed region and a count of the timed launches inside it, so the average
+    launch duration includes the gaps between launches and the measured loop carries no per-step
+    event records (r05: they cost 6-8 us a step, tools/event_cost_probe.py)."""
 
     def __init__(self):
         self.pairs = []
         self.on = False
+        self.loop = False
+        self.launches = 0
+        self.loop_events = None
         self.natives = []  # native GroupReducers: their local-step kernels are timed inside libfedagg
         self.native_ms, self.native_launches = 0.0, 0
 
+    def _event(self):
+        e = _HostEvent() if CPU_REHEARSAL else torch.cuda.Event(enable_timing=True)
+        e.record(None if CPU_REHEARSAL else torch.cuda.current_stream())
+        return e
+
     def __enter__(self):
-        if self.on:
-            self.a = _HostEvent() if CPU_REHEARSAL else torch.cuda.Event(enable_timing=True)
-            self.a.record(None if CPU_REHEARSAL else torch.cuda.current_stream())
+        if self.on and not self.loop:
+            self.a = self._event()
         return self
 
     def __exit__(self, *exc):
         if self.on:
-            b = _HostEvent() if CPU_REHEARSAL else torch.cuda.Event(enable_timing=True)
-            b.record(None if CPU_REHEARSAL else torch.cuda.current_stream())
-            self.pairs.append((self.a, b))
+            if self.loop:
+                self.launches += 1
+            else:
+                self.pairs.append((self.a, self._event()))
 
     def start(self):
         for r in self.natives:  # drop the warmup steps' native local-step timings
             r.local_time(reset=True)
         self.on = True
+        if self.loop:
+            self.launches = 0
+            self.loop_events = [self._event(), None]
+
+    def end(self):
+        """After the last timed step is issued (before the synchronisation): loop mode's end event."""
+        if self.on and self.loop:
+            self.loop_events[1] = self._event()
 
     def stop(self):
         self.on = False
@@ -469,9 +491,16 @@ class Timed:
             self.native_ms += ms
             self.native_launches += cnt
 
+    def _loop_ms(self):
+        a, b = self.loop_events or (None, None)
+        return a.elapsed_time(b) if a is not None and b is not None else None
+
     def avg_ms(self):
         if self.native_launches:
             return self.native_ms / self.native_launches
+        if self.loop:
+            t = self._loop_ms()
+            return t / self.launches if t is not None and self.launches else None
         d = [a.elapsed_time(b) for a, b in self.pairs]
         return float(np.mean(d)) if d else None
 
@@ -479,6 +508,9 @@ class Timed:
         """Summed kernel time per step (several timed launches per step)."""
         if self.native_launches:
             return self.native_ms / steps
+        if self.loop:
+            t = self._loop_ms()
+            return t / steps if t is not None else None
         d = [a.elapsed_time(b) for a, b in self.pairs]
         return float(np.sum(d)) / steps if d else None
 
@@ -632,7 +664,7 @@ def wl_metric(args, eng, rank, world, timer):
                 f"elements differ in the last bits) on {int(cnt)} sampled elements of {where}")
 
     suffix = {"arena": "", "tiled": "_tiled", "tensors": "_tensors"}[args.layout]
-    return dict(name=f"fedavg_flat_K{K}_P{P}_fp32" + suffix,
+    return dict(loop_timing=True, name=f"fedavg_flat_K{K}_P{P}_fp32" + suffix,
                 dtype="fp32", step=step, parity=parity,
                 bytes_total=K * P * 4 + P * 4, launch_bytes=(len(mine) * P * 4 + P * 4) / launches,
                 clients=K, params=P, cpu_K=K)
@@ -743,7 +775,7 @@ def wl_layout(args, eng, rank, world, timer):
 
     tag = ("resnet18gn" if resnet else "vitb16_bf16") + {"arena": "", "tiled": "_tiled", "tensors": "_tensors",
                                                          "adopted": "_adopted_agg"}[args.layout]
-    return dict(name=f"fedavg_{tag}_K{K}_P{P}", dtype="fp32" if resnet else "bf16", step=step, parity=parity,
+    return dict(loop_timing=True, name=f"fedavg_{tag}_K{K}_P{P}", dtype="fp32" if resnet else "bf16", step=step, parity=parity,
                 bytes_total=K * in_b + out_b, launch_bytes=None, clients=K, params=P, cpu_K=None,
                 step_bytes=len(mine) * in_b + out_b if world > 1 else None)
 
@@ -1091,7 +1123,7 @@ def wl_fragmented(args, eng, rank, world, timer):
             bad += int((got.view(torch.int32) != exp.view(torch.int32)).sum())
         return f"{'bit-exact' if bad == 0 else f'{bad} MISMATCHES'} vs oracle on a strided sample of 16 keys"
 
-    return dict(name=f"fedavg_fragmented{len(layout)}_K{K}_P{P}_fp32", dtype="fp32", step=step, parity=parity,
+    return dict(loop_timing=True, name=f"fedavg_fragmented{len(layout)}_K{K}_P{P}_fp32", dtype="fp32", step=step, parity=parity,
                 bytes_total=K * P * 4 + P * 4, launch_bytes=None, clients=K, params=P, cpu_K=None,
                 roofline_note="kernel time = the whole aggregate() call (host pointer tables + launch + kernel)")
 
@@ -1185,7 +1217,7 @@ def wl_hier(args, eng, rank, world, timer):
                 f"term -> ordered sum{' per rank -> rank-ordered sum' if world > 1 else ''}) on {int(cnt)} sampled "
                 f"elements" + (f" of {collective_note(args, world)}" if world > 1 else ""))
 
-    return dict(name=f"hier_fedavg_G{G}x{M}_P{P}_fp32" + ("_tiled" if tiled else ""), dtype="fp32", step=step, parity=parity,
+    return dict(loop_timing=True, name=f"hier_fedavg_G{G}x{M}_P{P}_fp32" + ("_tiled" if tiled else ""), dtype="fp32", step=step, parity=parity,
                 bytes_total=G * M * P * 4 + P * 4, launch_bytes=(len(clients) * P * 4 + P * 4) / launches,
                 clients=G * M, params=P, cpu_K=None)
 
@@ -1650,7 +1682,7 @@ def wl_median(args, eng, rank, world, timer):
         return _robust_cpu(robust_port.median_port, K, Pc, budget_s, K * Pc * 4 + Pc * 4,
                            "oracle/robust_port.median_port (cat + torch.median, coordinate_wise_median_defense.py:26-31)")
 
-    return dict(name=f"coord_median_K{K}_P{P}_{args.dtype}" + ("_tiled" if tiled else ""), dtype=args.dtype,
+    return dict(loop_timing=True, name=f"coord_median_K{K}_P{P}_{args.dtype}" + ("_tiled" if tiled else ""), dtype=args.dtype,
                 step=step, parity=parity,
                 bytes_total=(K * P + P) * es, launch_bytes=(K * P + P) * es, clients=K, params=P, cpu_K=K, cpu=cpu,
                 data="synthetic N(0,1) client weight vectors, resident in HBM (" +
@@ -1700,7 +1732,7 @@ def wl_krum(args, eng, rank, world, timer):
         extra["pair_form_note"] = ("gram: D = A_i + A_j - 2 G_ij on the matrix cores (fa_pairwise_sqdist_gram), kept "
                                    "when kappa_max <= 16; direct: the VALU difference kernel")
         return p
-    return dict(name=f"krum_pairdist_K{K}_P{P}_fp32", dtype="fp32", step=step, parity=parity_and_form,
+    return dict(loop_timing=True, name=f"krum_pairdist_K{K}_P{P}_fp32", dtype="fp32", step=step, parity=parity_and_form,
                 extra_line=extra,
                 bytes_total=K * P * 4, launch_bytes=K * P * 4, clients=K, params=P, cpu_K=K, cpu=cpu,
                 data="synthetic N(0,1) client weight vectors, resident in HBM (rows 256-byte aligned)",
@@ -1914,6 +1946,7 @@ def main():
           "krum": wl_krum, "arrival": wl_arrival, "lr": wl_lr, "samask": wl_samask}[args.config](args, eng, rank, world,
                                                                                                timer)
 
+    timer.loop = bool(wl.get("loop_timing")) and world == 1 and not args.loopback
     for i in range(args.warmup):
         stage(f"warmup step {i}")
         wl["step"]()
@@ -1927,6 +1960,7 @@ def main():
     lat = []
     for _ in range(args.steps):
         lat.append(wl["step"]())
+    timer.end()
     sync()
     barrier(world)
     sync()
