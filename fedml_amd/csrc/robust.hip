@@ -1731,10 +1731,9 @@ k_pair_gram_ring(const PSeg* __restrict__ segs, int nseg, const void* const* __r
 }
 
 // G entries of the T tiles summed over the per-block partials in a fixed order: a workgroup of 16
-// waves takes 64 consecutive entries (entry = tile * 1024 + row * 32 + col, lane = entry), wave v sums
-// partial rows v, v + 16, ... (512-byte row reads), then the 16 wave sums are added in wave order
-// through LDS; written to g (KP x KP, upper tiles only).  (r05: the r04 form -- 8 entries per 256-
-// thread group, 64-byte row reads -- took 11 us over K = 32's 768 partials.)
+// waves takes 16 consecutive entries (entry = tile * 1024 + row * 32 + col) and splits the partial
+// rows 64 ways (128-byte row reads), then the 64 split sums are added in split order through LDS;
+// written to g (KP x KP, upper tiles only).
 // The LAST workgroup to finish (an arrival counter the Gram kernel zeroed; release / acquire at agent
 // scope around it) then forms D_ij = A_i + A_j - 2 G_ij for every pair into the k x k matrix and the
 // largest kappa_ij = (A_i + A_j) / D_ij (+inf for D_ij <= 0 or a NaN) into *kmax -- the former
@@ -1747,25 +1746,31 @@ k_gram_reduce(const double* __restrict__ partial, int nparts, double* __restrict
   using C = GramCfg<KB>;
   __shared__ double red[kGRW * 64];
   __shared__ int last;
+  // lane = (row lane rl, entry el): a workgroup takes kGRE consecutive entries and splits the rows
+  // 64 ways (16 waves x 4 row lanes), so every lane has at most nparts / 64 rows to add (r05: one
+  // entry per lane and 16 row splits left 32 dependent-latency rows per lane at K <= 32's 512
+  // partials); each row read is kGRE x 8 = 128 contiguous bytes
+  constexpr int kGRE = 16, RS = kGRW * 64 / kGRE;
   const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
+  const int el = lane % kGRE, rl = lane / kGRE;
+  const int rs = v * (64 / kGRE) + rl;  // this lane's row split, 0 .. RS - 1
   const int64_t nent = (int64_t)C::T * 1024;
-  const int64_t e = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t e = (int64_t)blockIdx.x * kGRE + el;
   double s = 0.0;
-  int b = v;
-  for (; b + 7 * kGRW < nparts; b += 8 * kGRW) {  // 8 loads in flight, added in row order
+  int b = rs;
+  for (; b + 7 * RS < nparts; b += 8 * RS) {  // 8 loads in flight, added in row order
     double x[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) x[u] = partial[(int64_t)(b + u * kGRW) * nent + e];
+    for (int u = 0; u < 8; ++u) x[u] = partial[(int64_t)(b + u * RS) * nent + e];
 #pragma unroll
     for (int u = 0; u < 8; ++u) s += x[u];
   }
-  for (; b < nparts; b += kGRW) s += partial[(int64_t)b * nent + e];
-  red[v * 64 + lane] = s;
+  for (; b < nparts; b += RS) s += partial[(int64_t)b * nent + e];
+  red[threadIdx.x] = s;
   __syncthreads();
-  if (v == 0) {
+  if (threadIdx.x < kGRE) {  // the RS split sums in split order
     double tsum = 0.0;
-#pragma unroll
-    for (int u = 0; u < kGRW; ++u) tsum += red[u * 64 + lane];
+    for (int u = 0; u < RS; ++u) tsum += red[(u / (64 / kGRE)) * 64 + (u % (64 / kGRE)) * kGRE + threadIdx.x];
     int bi, bj;
     gram_tile_kb<KB>((int)(e / 1024), bi, bj);
     const int row = (int)(e % 1024) / 32, col = (int)(e % 32);
@@ -2077,7 +2082,7 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
   unsigned* ctr = (unsigned*)(gm + (size_t)(32 * kb) * (32 * kb));  // k_gram_reduce's arrival counter
   const PSeg* sg = (const PSeg*)dv;
   const void* const* pp = (const void* const*)(dv + seg_bytes);
-  const int ntr = gram_T(kb) * 1024 / 64;  // k_gram_reduce workgroups
+  const int ntr = gram_T(kb) * 1024 / 16;  // k_gram_reduce workgroups (16 entries each)
   const size_t lds = gram_lds(kb);
 #define FA_GR(KB, S)                                                                                           \
   do {                                                                                                         \
