@@ -64,7 +64,9 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=None,
+                   help="untimed warmup steps (default: 3, and on one GPU as many more as make ~0.2 s of the "
+                        "workload's own steps -- short steps otherwise run on the clock ramp, DESIGN §0.2 3b)")
     p.add_argument("--config", default="metric",
                    choices=["metric", "fragmented", "resnet18", "vit_bf16", "hier", "gossip", "host", "secagg", "fedopt",
                             "dropin_cpu", "median",
@@ -1947,10 +1949,26 @@ def main():
                                                                                                timer)
 
     timer.loop = bool(wl.get("loop_timing")) and world == 1 and not args.loopback
+    auto_warmup = args.warmup is None
+    if auto_warmup:
+        args.warmup = 3
     for i in range(args.warmup):
         stage(f"warmup step {i}")
         wl["step"]()
     sync()
+    if auto_warmup and world == 1 and not wl.get("latency"):
+        # the chip raises its clock over the first ~10-50 ms of sustained work (r05t): keep warming up
+        # until ~0.2 s of this workload's own steps have run
+        t_w = time.perf_counter()
+        wl["step"]()
+        sync()
+        one = max(time.perf_counter() - t_w, 1e-6)
+        extra = min(2000, int(0.2 / one))
+        for i in range(extra):
+            stage(f"warmup step {args.warmup + 1 + i}")
+            wl["step"]()
+        sync()
+        args.warmup += 1 + extra
     stage("barrier before the timed steps")
     barrier(world)
     sync()
