@@ -105,6 +105,13 @@ def parse():
     p.add_argument("--soak-seconds", type=float, default=5.0,
                    help="one GPU: after the timed steps, keep stepping (untimed by the line's value) for this long and "
                         "report the sustained rate beside it (clock / thermal steadiness; 0 = off)")
+    p.add_argument("--cold-reps", type=int, default=5,
+                   help="one GPU: after the soak, this many single calls each after --cold-idle seconds of idle; "
+                        "their median wall time is the line's `cold.ms` (the reference's per-round AggregationTime "
+                        "pays one call after waiting for the clients; 0 = off)")
+    p.add_argument("--cold-idle", type=float, default=1.0, help="idle seconds before each cold call")
+    p.add_argument("--no-read-probe", action="store_true",
+                   help="skip the in-process read-stream probe (measured_read_ceiling)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     p.add_argument("--check-samples", type=int, default=65536)
@@ -669,7 +676,10 @@ def wl_metric(args, eng, rank, world, timer):
     return dict(loop_timing=True, name=f"fedavg_flat_K{K}_P{P}_fp32" + suffix,
                 dtype="fp32", step=step, parity=parity,
                 bytes_total=K * P * 4 + P * 4, launch_bytes=(len(mine) * P * 4 + P * 4) / launches,
-                clients=K, params=P, cpu_K=K)
+                clients=K, params=P, cpu_K=K,
+                probe=(buf, buf.shape[1], f"this workload's tiled arena group ({buf.shape[1]} consecutive 4-KiB rows "
+                       "per workgroup: the pages and the row runs the kernel reads)") if tiled and not CPU_REHEARSAL
+                else None)
 
 
 def wl_layout(args, eng, rank, world, timer):
@@ -1685,6 +1695,8 @@ def wl_median(args, eng, rank, world, timer):
                            "oracle/robust_port.median_port (cat + torch.median, coordinate_wise_median_defense.py:26-31)")
 
     return dict(loop_timing=True, name=f"coord_median_K{K}_P{P}_{args.dtype}" + ("_tiled" if tiled else ""), dtype=args.dtype,
+                probe=(buf, buf.shape[1], f"this workload's tiled arena group ({buf.shape[1]} consecutive 4-KiB rows "
+                       "per workgroup)") if tiled else None,
                 step=step, parity=parity,
                 bytes_total=(K * P + P) * es, launch_bytes=(K * P + P) * es, clients=K, params=P, cpu_K=K, cpu=cpu,
                 data="synthetic N(0,1) client weight vectors, resident in HBM (" +
@@ -1843,13 +1855,59 @@ def cpu_model():
     return None
 
 
-def measured_ceiling():
-    """Best read-stream rate measured on an MI355X box by tools/hbm_probe.py (profiles/)."""
-    try:
-        with open(os.path.join(ROOT, "profiles", "r01_hbm_probe.json")) as f:
-            return json.load(f).get("read_best_GBs")
-    except (OSError, ValueError):
-        return None
+def read_ceiling(eng, wl, reps=5):
+    """THIS box's read ceiling, measured in this process before the timed region (never inside it):
+    fa_read_probe streams the workload's own tiled arena group -- the same pages, in the same
+    per-workgroup row runs (K consecutive 4-KiB rows) as the aggregation kernel reads them, with no
+    arithmetic and no output stream -- or, for workloads without a tiled arena, a 8 GiB scratch
+    allocation in runs of 128 rows.  Best and median of ``reps`` HIP-event-timed passes (one untimed
+    pass first) on the stream the probe is launched on."""
+    spec = wl.get("probe")
+    scratch = None
+    if spec is None:
+        scratch = torch.empty(8 << 30, dtype=torch.uint8, device=DEV)
+        spec = (scratch, 128, "8 GiB scratch allocation, runs of 128 rows")
+    buf, rows, what = spec
+    nbytes = (buf.numel() * buf.element_size()) // 4096 * 4096
+    st = torch.cuda.current_stream()
+    eng.read_probe(buf, rows)
+    ms = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        eng.read_probe(buf, rows)
+        b.record(st)
+        b.synchronize()
+        ms.append(a.elapsed_time(b))
+    del scratch
+    best, med = min(ms), float(np.median(ms))
+    return {"value": round(nbytes / (best * 1e-3) / 1e9, 1), "median": round(nbytes / (med * 1e-3) / 1e9, 1),
+            "unit": "GB/s", "bytes": int(nbytes), "reps": reps, "buffer": what,
+            "probe": "fa_read_probe (include/fedagg.h): the weighted-sum kernel's tiled read pattern, no arithmetic, "
+                     "no output stream; run in this process after the warmup, before the timed steps"}
+
+
+def cold_calls(wl, reps, idle_s):
+    """The per-round latency the reference pays (python/fedml/cross_silo/server/
+    fedml_server_manager.py:184-195 times ONE aggregation after the server has waited for every
+    client): ``reps`` single calls, each after ``idle_s`` of idle, wall time from the call to its
+    completion (median reported), and the HIP-event time of the call's GPU work beside it."""
+    wall, ev = [], []
+    for _ in range(reps):
+        sync()
+        time.sleep(idle_s)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        a.record()
+        wl["step"]()
+        b.record()
+        sync()
+        wall.append((time.perf_counter() - t0) * 1e3)
+        ev.append(a.elapsed_time(b))
+    return {"ms": round(float(np.median(wall)), 4), "event_ms": round(float(np.median(ev)), 4),
+            "all_ms": [round(x, 4) for x in wall], "idle_s": idle_s, "reps": reps,
+            "note": "one call after idle (median of reps; wall time incl. launch and completion) -- the reference's "
+                    "per-round AggregationTime case; `ms_per_step` is the back-to-back rate at the sustained clock"}
 
 
 def pmc_traffic(workload):
@@ -1887,7 +1945,6 @@ def roofline_block(wl, world, value, unit, achieved, kernel_ms, launch_bytes):
     block["traffic"] = traffic
     block["traffic_source"] = ("profiles/pmc_traffic.json (rocprofv3 FETCH_SIZE/WRITE_SIZE of a separate "
                                "profiling run of this workload, not measured in this run)" if traffic else None)
-    block["measured_read_ceiling"] = measured_ceiling()
     return block
 
 
@@ -1969,6 +2026,10 @@ def main():
             wl["step"]()
         sync()
         args.warmup += 1 + extra
+    ceiling = None
+    if world == 1 and not CPU_REHEARSAL and not args.no_read_probe and not wl.get("latency"):
+        stage("read probe")
+        ceiling = read_ceiling(eng, wl)
     stage("barrier before the timed steps")
     barrier(world)
     sync()
@@ -2000,6 +2061,10 @@ def main():
                      "value": round(wl["bytes_total"] * n_soak / dt_s / 1e9, 2), "unit": "GB/s",
                      "ms_per_step": round(dt_s / n_soak * 1e3, 4),
                      "note": "the same step repeated after the timed region (not part of `value`)"}
+    cold = None
+    if args.cold_reps > 0 and world == 1 and not CPU_REHEARSAL and not wl.get("latency"):
+        stage("cold calls")
+        cold = cold_calls(wl, args.cold_reps, args.cold_idle)
     stage("parity check")
     ms_per_step = elapsed / args.steps * 1e3
     if wl.get("latency"):  # the step returns its own latency (s); value = mean (or median) latency in ms
@@ -2056,13 +2121,21 @@ def main():
         }
         if wl.get("roofline_note"):
             line["roofline"]["note"] = wl["roofline_note"]
+        if ceiling is not None:
+            rl = line["roofline"]
+            rl["measured_read_ceiling"] = ceiling
+            if rl.get("unit") == "GB/s" and rl.get("achieved"):
+                rl["frac_of_ceiling"] = round(rl["achieved"] / ceiling["value"], 4)
+        if cold is not None:
+            line["cold"] = cold
         line.update(wl.get("extra_line", {}))
         mf = wl.get("mfma_flops_per_launch")
         if mf and world == 1 and kernel_ms and line.get("pair_form") == "gram" and wl.get("mfma_bound"):
             # Krum's Gram form past K = 32 is matrix-core work: the bound is the f32 MFMA peak, the HBM
             # figures stay beside it
             rl = line["roofline"]
-            hbm = {k: rl.get(k) for k in ("achieved", "peak", "unit", "frac")}
+            hbm = {k: rl.get(k) for k in ("achieved", "peak", "unit", "frac", "frac_of_ceiling")}
+            rl.pop("frac_of_ceiling", None)
             tfs = mf / (kernel_ms * 1e-3) / 1e12
             rl.update({"bound": "mfma", "achieved": round(tfs, 2), "peak": MFMA_F32_PEAK_TFS, "unit": "TFLOP/s",
                        "frac": round(tfs / MFMA_F32_PEAK_TFS, 4), "algorithmic_flops_per_launch": int(mf),

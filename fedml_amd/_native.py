@@ -31,13 +31,13 @@ EXPORTED_SYMBOLS = (
     "fa_weighted_sum_multi", "fa_weighted_sum_tiled", "fa_weighted_sum_tiled_multi", "fa_weighted_sum_pair", "fa_weighted_sum_pair_multi", "fa_weighted_sum_grouped", "fa_weighted_sum_grouped_tiled",
     "fa_fedavg_sgd", "fa_fedavg_sgd_tiled", "fa_fedavg_rmsprop", "fa_mix", "fa_mix_tiled", "fa_ctx_set_variant",
     "fa_ctx_set_mix_band", "fa_stream_create_cu_masked", "fa_stream_destroy", "fa_strerror", "fa_last_error",
-    "fa_promote_add", "fa_weighted_sum_host", "fa_pushsum",
+    "fa_promote_add", "fa_weighted_sum_host", "fa_pushsum", "fa_read_probe",
     # include/fedagg_finite.h
     "fa_finite_sum", "fa_finite_sum_tiled", "fa_finite_quantize", "fa_lcc_decode", "fa_mt_randint_sum",
     "fa_mt_randint_sum_scratch_bytes",
     # include/fedagg_robust.h
     "fa_coord_median", "fa_coord_median_tiled", "fa_pairwise_sqdist", "fa_pairwise_sqdist_rt", "fa_pairwise_sqdist_scratch_bytes",
-    "fa_pairwise_sqdist_gram", "fa_pairwise_sqdist_gram_scratch_bytes",
+    "fa_pairwise_sqdist_gram", "fa_pairwise_sqdist_gram_scratch_bytes", "fa_pairwise_sqdist_gram_limit",
     # include/fedagg_comm.h
     "fa_comm_unique_id", "fa_comm_init", "fa_comm_wrap", "fa_comm_destroy", "fa_comm_size", "fa_local_out_dtype",
     "fa_group_plan", "fa_group_ops", "fa_group_reduce_scratch_bytes", "fa_group_reduce", "fa_comm_set_timing", "fa_comm_local_time",
@@ -173,12 +173,16 @@ def _declare(L):
                                           ctypes.c_double, _vp, ctypes.c_size_t, _vp]
     L.fa_pairwise_sqdist_gram_scratch_bytes.restype = ctypes.c_size_t
     L.fa_pairwise_sqdist_gram_scratch_bytes.argtypes = [ctypes.c_int32, _P_i64, ctypes.c_int32]
+    L.fa_pairwise_sqdist_gram_limit.restype = ctypes.c_double
+    L.fa_pairwise_sqdist_gram_limit.argtypes = [ctypes.c_int32, _P_i64, ctypes.c_int32, _P_vp, ctypes.c_double]
     L.fa_weighted_sum_host.restype = ctypes.c_int
     L.fa_weighted_sum_host.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int32, _P_i64, ctypes.c_int32,
                                        _P_vp, _P_d, ctypes.c_double, _P_vp, _vp]
     L.fa_pushsum.restype = ctypes.c_int
     L.fa_pushsum.argtypes = [_vp, ctypes.c_int, ctypes.c_int64, ctypes.c_int32, _P_i32, _P_i32, _P_d, ctypes.c_int32,
                              _P_vp, _vp, _P_vp, _P_vp, _vp, _vp]
+    L.fa_read_probe.restype = ctypes.c_int
+    L.fa_read_probe.argtypes = [_vp, _vp, ctypes.c_int64, ctypes.c_int32, _vp, _vp]
     L.fa_promote_add.restype = ctypes.c_int
     L.fa_promote_add.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _vp, _vp, _vp, _vp]
     _P_ls = ctypes.POINTER(LocalStep)

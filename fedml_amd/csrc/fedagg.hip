@@ -1058,9 +1058,14 @@ bool slot_event_mode() {
 int acquire_slot(fa_ctx* ctx, size_t bytes, fa_ctx::Slot** out) {
   fa_ctx::Slot& s = ctx->slots[ctx->next];
   ctx->next = (ctx->next + 1) % kSlots;
-  // a use that never reached release() (its caller failed after stage()) leaves the device buffer's
-  // contents unknown: copy again next time
-  if (s.acquired) s.shadow_ok = false;
+  // a use that never reached release() (its caller failed after stage(), possibly after queueing
+  // kernels that read `dev` on a stream the slot never recorded) leaves the device buffer's contents
+  // and readers unknown: copy again next time, and only after every queued reader is done (a device
+  // sync -- an error path, never taken by a call that succeeds)
+  if (s.acquired) {
+    s.shadow_ok = false;
+    FA_HIP(hipDeviceSynchronize());
+  }
   s.acquired = true;
   if (s.pending) {
     FA_HIP(hipEventSynchronize(s.ev));
@@ -1785,7 +1790,7 @@ int pair_impl(fa_ctx* ctx, int dtype, int mode, int32_t nseg0, const int64_t* nu
     return e ? atoi(e) : 0;
   }();
   const bool s4 = s_env == 4 || (s_env == 0 && sstr0 == 0 && k >= 32);
-  const bool k16 = !s4 && (k <= 16 || s2);
+  const bool k16 = !s4 && s_env != 1 && (k <= 16 || s2);  // FA_PAIR_S=1: one slot for every K
   const int nsg[2] = {nseg0, nseg1};
   const int64_t* numel[2] = {numel0, numel1};
   const void* const* din[2] = {d_in0, d_in1};
@@ -2282,3 +2287,51 @@ int fa_mix_tiled(fa_ctx* ctx, int dtype, int64_t n, int32_t rows, const int32_t*
 }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------------------------------------
+// Read-stream probe (measurement only; no arithmetic contract): the weighted-sum kernel's access
+// pattern with the arithmetic and the output stream removed.  The buffer is a run of FA_TILE_BYTES
+// rows; workgroup b reads rows [b R, (b + 1) R) -- lane l the 16 bytes at l * 16 of every row, U = 8
+// rows per load group (non-temporal, as k_wsum) -- and XORs them together.  With R = K on a tiled
+// arena group this is exactly the address sequence k_wsum_inl issues on it, so its rate is the
+// box's ceiling for that kernel on those very pages (bench.py: measured_read_ceiling).  The XOR is
+// stored only if it equals a constant (never, in practice): the loads stay live without a write.
+namespace {
+template <int U>
+__global__ void __launch_bounds__(kBlock)
+k_read_probe(const char* __restrict__ buf, int64_t nrows, int rows_per_wg, unsigned* __restrict__ word) {
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_wg;
+  const int64_t r1 = r0 + rows_per_wg < nrows ? r0 + rows_per_wg : nrows;
+  const char* p = buf + (int64_t)threadIdx.x * 16;
+  u32x4 acc = {0u, 0u, 0u, 0u};
+  int64_t r = r0;
+  for (; r + U <= r1; r += U) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = ld16<true>(p + (r + u) * FA_TILE_BYTES);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u];
+  }
+  for (; r < r1; ++r) acc ^= ld16<true>(p + r * FA_TILE_BYTES);
+  const unsigned x = acc[0] ^ acc[1] ^ acc[2] ^ acc[3];
+  if (x == 0x9E3779B9u) word[0] = x;
+}
+}  // namespace
+
+extern "C" int fa_read_probe(fa_ctx* ctx, const void* d_buf, int64_t bytes, int32_t rows_per_workgroup,
+                             void* d_word, void* hip_stream) {
+  if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (!d_buf || !d_word || !al16(d_buf) || bytes < FA_TILE_BYTES || rows_per_workgroup < 1 ||
+      rows_per_workgroup > 65536)
+    return fail(FA_ERR_INVALID, "fa_read_probe: 16-byte aligned buffer of >= %d bytes, 1 <= rows_per_workgroup "
+                "<= 65536, and a device word are required", FA_TILE_BYTES);
+  const int64_t nrows = bytes / FA_TILE_BYTES;
+  const int64_t grid = (nrows + rows_per_workgroup - 1) / rows_per_workgroup;
+  if (grid > 0x7FFFFFFF) return fail(FA_ERR_INVALID, "fa_read_probe: too many workgroups (%lld)", (long long)grid);
+  DeviceGuard g(ctx->device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
+  hipLaunchKernelGGL(k_read_probe<8>, dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)hip_stream,
+                     (const char*)d_buf, nrows, (int)rows_per_workgroup, (unsigned*)d_word);
+  FA_HIP(hipGetLastError());
+  return FA_OK;
+}

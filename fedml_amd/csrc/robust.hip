@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cmath>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -708,7 +709,7 @@ PairSplit pair_split(int k) {
   }
   q.dgroups = q.nthreads / q.nb;  // threads per block in the within-block phase
   q.nblocks = 1024;  // workgroups (each writes all pair partials once)
-  static const char* ob = getenv("FA_PAIR_BLOCKS");  // measurement override (tools/gpu_r02v.sh)
+  static const char* ob = getenv("FA_PAIR_BLOCKS");  // measurement override (A/B runs, r02v)
   if (ob && atoi(ob) >= 64 && atoi(ob) <= 16384) q.nblocks = atoi(ob);
   return q;
 }
@@ -1295,6 +1296,9 @@ __constant__ const int8_t kG16Blocks[12][3] = {{0, 1, 1}, {2, 3, 3}, {4, 5, 5}, 
 __constant__ const int8_t kG16Sets2[4][4] = {{0, 0, 1, 1}, {0, 2, 3, 3}, {2, 0, 2, 3}, {2, 1, 2, 3}};
 
 template <int KB>
+__host__ __device__ constexpr int gram_T_c() { return KB * (KB + 1) / 2; }
+
+template <int KB>
 __device__ __forceinline__ void gram_tile_kb(int t, int& bi, int& bj) {
   int i = 0, rem = t;
   while (rem >= KB - i) { rem -= KB - i; ++i; }
@@ -1552,6 +1556,196 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
         o[row * 32 + lrow] = sm;
       }
     }
+  }
+}
+
+// K in (96, 128], bf16x3 split form (r06).  The f32-input MFMA issues at the FP32 vector rate (32
+// cycles per v_mfma_f32_16x16x4_f32 on a SIMD); the bf16 MFMA is 16x faster per product
+// (v_mfma_f32_16x16x32_bf16: 32 products per lane pair in 16 cycles).  So y = x - c (float32, as the
+// forms above) is split EXACTLY into three bf16 values, y = h + m + l (8 + 8 + 8 significant bits of
+// y's 24; each remainder is exact in float32), once per element and chunk into three LDS planes, and
+//   G_ab = H_a H_b^T + H_a M_b^T + M_a H_b^T + H_a L_b^T + L_a H_b^T + M_a M_b^T
+// on the bf16 matrix cores, accumulated in float32 (the dropped M L^T + L M^T + L L^T are <= 2^-25 of
+// a product: below the float32 rounding of the sum).  Per chunk and tile that is 4 groups x 6 MFMAs
+// x 16 cycles = 384 instead of 32 x 32 = 1,024 MFMA cycles; the split costs ~5 VALU per element,
+// once per workgroup instead of once per wave and operand read.
+// Per chunk (128 coordinates, the same 12-wave tile map as the S16 form, kG16Blocks): A) the staged
+// rows 0..4 go to LDS; barrier; B) every wave computes the chunk's centre (median of clients 0..4)
+// into its own row; C) every thread splits its staged elements into the planes, then issues the
+// next chunk's loads (in flight during the MFMAs); barrier; D) MFMAs.  The planes are single-buffered:
+// the barrier of the next chunk's step A separates its step C from this chunk's reads.
+constexpr int kG3S = kGE + 8;  // bf16 per plane row: 272-byte rows, 16-lane b128 reads conflict-free
+typedef __bf16 gbf8 __attribute__((ext_vector_type(8)));
+typedef __bf16 gbf4 __attribute__((ext_vector_type(4)));
+struct Gram3Cfg {
+  static constexpr int KP = 128, W = 12, NT = W * 64, QV = kGE / 4;
+  static constexpr int NLD = (KP * QV + NT - 1) / NT;         // staged 16-byte vectors per thread (6)
+  static constexpr int PLANE = KP * kG3S;                      // bf16 per plane
+  static constexpr size_t PLANE_BYTES = (size_t)3 * PLANE * 2;  // h, m, l
+  static constexpr size_t LDS = PLANE_BYTES + sizeof(float) * (5 * kGE + W * kGE);  // + rows 0..4 + centres
+};
+static_assert(Gram3Cfg::PLANE_BYTES >= sizeof(double) * 12 * 768, "the epilogue's wave sums reuse the planes");
+
+__device__ __forceinline__ float bf_f(__bf16 b) { return (float)b; }
+
+template <bool VEC>
+__global__ void __launch_bounds__(Gram3Cfg::NT) __attribute__((amdgpu_waves_per_eu(3)))
+k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k,
+             int64_t nchunks, double* __restrict__ partial, unsigned* __restrict__ ctr) {
+  using C = Gram3Cfg;
+  constexpr int KB = 4, QV = C::QV;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;  // k_gram_reduce's arrival counter
+  extern __shared__ __attribute__((aligned(16))) char g3[];
+  __bf16* const planes = (__bf16*)g3;
+  float* const c5 = (float*)(g3 + C::PLANE_BYTES);  // [5][kGE] raw rows 0..4
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  float* const crow = c5 + 5 * kGE + w * kGE;  // this wave's centre row (wave-private)
+  const int li = lane & 15, kk = lane >> 4;
+  const bool dg = w < 4;  // waves 0-3: a diagonal pair (3 tiles of 2 blocks); 4-11: a triangle of 3 blocks
+  int blk[3], ro[3];
+#pragma unroll
+  for (int x = 0; x < 3; ++x) {
+    blk[x] = kG16Blocks[w][x];
+    ro[x] = (16 * blk[x] + li) * kG3S + 8 * kk;
+  }
+  gf4 a16[3];
+  double accd[12];
+#pragma unroll
+  for (int x = 0; x < 3; ++x) a16[x] = gf4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int q = 0; q < 12; ++q) accd[q] = 0.0;
+  gf4 v[C::NLD];
+  const float* src[C::NLD];
+  int cseg = -1;
+  auto load = [&](int64_t ch) {  // as k_pair_gram: client rows, coalesced 16-byte loads
+    const int si = nseg > 1 ? find_seg(segs, nseg, ch) : 0;
+    const PSeg sg = segs[si];
+    if (si != cseg) {
+      cseg = si;
+#pragma unroll
+      for (int u = 0; u < C::NLD; ++u) {
+        const int idx = t + u * C::NT;
+        const int cl = idx / QV;
+        src[u] = idx < C::KP * QV && cl < k ? (const float*)ptrs[sg.ptr_base + cl] + 4 * (idx % QV) : nullptr;
+      }
+    }
+    const int64_t b0 = (ch - sg.tile_start) * kGE;
+    if (VEC && b0 + kGE <= sg.numel) {
+#pragma unroll
+      for (int u = 0; u < C::NLD; ++u) {
+        const gf4 z = {0.f, 0.f, 0.f, 0.f};
+        v[u] = src[u] ? *(const __attribute__((address_space(1))) gf4*)(src[u] + b0) : z;
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < C::NLD; ++u) {
+        const int idx = t + u * C::NT;
+        gf4 x = {0.f, 0.f, 0.f, 0.f};
+        if (src[u]) {
+          const int64_t left = sg.numel - (b0 + 4 * (idx % QV));
+#pragma unroll
+          for (int z = 0; z < 4; ++z) if (z < left) x[z] = gld<float>(src[u] + b0, z);
+        }
+        v[u] = x;
+      }
+    }
+  };
+  const int64_t c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
+  if (c0 < c1) load(c0);
+  for (int64_t ch = c0; ch < c1; ++ch) {
+    // A) rows 0..4 (staged by threads 0..159 in their first vector) to LDS
+    if (t < 5 * QV) *(gf4*)&c5[(t / QV) * kGE + 4 * (t % QV)] = v[0];
+    __syncthreads();  // also: every wave is done reading the planes of chunk ch - 1
+    // B) this wave's copy of the chunk's centre: the median of clients 0..4 (k > 96 here)
+    if (lane < QV) {
+      const gf4 a = *(const gf4*)&c5[4 * lane], b = *(const gf4*)&c5[kGE + 4 * lane],
+                 c = *(const gf4*)&c5[2 * kGE + 4 * lane], d = *(const gf4*)&c5[3 * kGE + 4 * lane],
+                 f = *(const gf4*)&c5[4 * kGE + 4 * lane];
+      gf4 m;
+#pragma unroll
+      for (int z = 0; z < 4; ++z)
+        m[z] = __builtin_amdgcn_fmed3f(f[z], fmaxf(fminf(a[z], b[z]), fminf(c[z], d[z])),
+                                       fminf(fmaxf(a[z], b[z]), fmaxf(c[z], d[z])));
+      *(gf4*)&crow[4 * lane] = m;
+    }
+    __builtin_amdgcn_wave_barrier();
+    // C) y = x - c split into h + m + l, written to the three planes
+#pragma unroll
+    for (int u = 0; u < C::NLD; ++u) {
+      const int idx = t + u * C::NT;
+      if (C::NLD * C::NT == C::KP * QV || idx < C::KP * QV) {
+        const int cl = idx / QV, q = idx % QV;
+        const gf4 y = v[u] - *(const gf4*)&crow[4 * q];
+        gbf4 h, m, l;
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+          h[z] = (__bf16)y[z];
+          const float r = y[z] - bf_f(h[z]);
+          m[z] = (__bf16)r;
+          l[z] = (__bf16)(r - bf_f(m[z]));
+        }
+        __bf16* const row = planes + cl * kG3S + 4 * q;
+        *(gbf4*)row = h;
+        *(gbf4*)(row + C::PLANE) = m;
+        *(gbf4*)(row + 2 * C::PLANE) = l;
+      }
+    }
+    if (ch + 1 < c1) load(ch + 1);  // in flight during the MFMAs
+    __syncthreads();
+    // D) the wave's three 16x16 tiles over the chunk's 4 groups of 32 coordinates
+#pragma unroll
+    for (int G = 0; G < kGE / 32; ++G) {
+      gbf8 f[3][3];
+#pragma unroll
+      for (int x = 0; x < 3; ++x)
+        if (x < 2 || !dg)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) f[x][p] = *(const gbf8*)&planes[p * C::PLANE + ro[x] + 32 * G];
+#pragma unroll
+      for (int x = 0; x < 3; ++x) {
+        // tiles: diagonal pair (0,0), (0,1), (1,1); triangle (0,1), (0,2), (1,2)
+        const int pa = dg ? (x == 2 ? 1 : 0) : (x == 2 ? 1 : 0);
+        const int pb = dg ? (x == 0 ? 0 : 1) : (x == 0 ? 1 : 2);
+        gf4 acc = a16[x];
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][1], f[pb][1], acc, 0, 0, 0);  // M M
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][0], f[pb][2], acc, 0, 0, 0);  // H L
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][2], f[pb][0], acc, 0, 0, 0);  // L H
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][0], f[pb][1], acc, 0, 0, 0);  // H M
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][1], f[pb][0], acc, 0, 0, 0);  // M H
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][0], f[pb][0], acc, 0, 0, 0);  // H H
+        a16[x] = acc;
+      }
+    }
+    // float32 runs of 2 chunks (256 coordinates) -> float64
+    if ((ch - c0) % 2 == 1 || ch + 1 == c1) {
+#pragma unroll
+      for (int x = 0; x < 3; ++x)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          accd[4 * x + q] += (double)a16[x][q];
+          a16[x][q] = 0.0f;
+        }
+    }
+  }
+  // epilogue: as k_pair_gram<4, *, true> -- 16x16 tile (A, B) into 32x32 tile (A / 2, B / 2),
+  // quadrant (A % 2, B % 2); a diagonal 32x32 tile's lower-left quadrant written as zeros
+  __syncthreads();
+  double* o = partial + (int64_t)blockIdx.x * gram_T_c<KB>() * 1024;
+#pragma unroll
+  for (int x = 0; x < 3; ++x) {
+    const int pa = x == 2 ? 1 : 0, pb = dg ? (x == 0 ? 0 : 1) : (x == 0 ? 1 : 2);
+    const int A = blk[pa], Bk = blk[pb];
+    const int I = A >> 1, J = Bk >> 1;
+    const int t32 = I * KB - I * (I - 1) / 2 + (J - I);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      o[(int64_t)t32 * 1024 + (16 * (A & 1) + 4 * kk + q) * 32 + 16 * (Bk & 1) + li] = accd[4 * x + q];
+  }
+  if (dg) {
+    const int I = blk[0] >> 1, t32 = I * KB - I * (I - 1) / 2;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[(int64_t)t32 * 1024 + (16 + 4 * kk + q) * 32 + li] = 0.0;
   }
 }
 
@@ -1819,6 +2013,14 @@ bool gram_s16() {  // K in (32, 64] and (96, 128]: the 16x16 forms (FA_GRAM16=0:
   return on;
 }
 
+bool gram3() {  // K in (96, 128]: the bf16x3 split form (FA_GRAM3=1; default: the f32-input 16x16 form)
+  static const bool on = [] {
+    const char* e = getenv("FA_GRAM3");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 int gram_glds() {  // K <= 32: the LDS-DMA ring kernel (FA_GRAM_GLDS=0: the register-staged k_pair_gram<1>, A/B)
   static const int d = [] {
     const char* e = getenv("FA_GRAM_GLDS");
@@ -1860,6 +2062,41 @@ size_t gram_lds(int kb) {
 int pairdist_direct(fa_ctx* ctx, int diff_dtype, int32_t num_segments, const int64_t* seg_numel, int32_t k,
                     const void* const* d_in, void* d_dist, void* d_scratch, size_t scratch_bytes, void* hip_stream,
                     const double* guard, double limit);
+
+// The Gram form's error model and the guard it sets (Krum; calibrated by
+// tools/krum_kappa_sweep.py, profiles/r06b).  A G entry is accumulated in float32 runs of n products,
+// p products per MFMA instruction (one rounding per instruction), and the runs are added in float64.
+// With random rounding the run sums' error is ~0.25 u n sqrt(P / p) t for P coordinates of mean term
+// t, i.e. sigma(A) / A ~ 0.25 u n / sqrt(p P) (u = 2^-24); D = A_i + A_j - 2 G_ij collects three such
+// errors, so sigma(D) / D ~ 0.30 kappa u n / sqrt(p P).  The guard keeps the Gram result only while
+// MARGIN sigma(D) / D <= 1e-6 (MARGIN = 6: the largest of 8,128 pairs sits near 4 sigma):
+//   kappa <= kGramKappaC sqrt(p P) / n,  kGramKappaC = 1e-6 / (6 x 0.30 x 2^-24) = 9.3.
+// Large models are unaffected (P = 11.7 M, K = 128: 108 > 16); small ones with long runs are handed
+// to the direct kernel at lower kappa (P = 7,850, K = 128: 6.4).
+struct GramRun {
+  int n, p;  // float32 products per run of one G entry, products per MFMA instruction
+};
+GramRun gram_run(int kb, bool glds) {
+  if (glds) return {64, 4};  // k_pair_gram_ring: 16 products per chunk, flushed every 4 chunks
+  const bool s16 = (kb == 4 || kb == 2) && gram_s16();
+  switch (kb) {
+    case 1: return {128, 2};                            // R = 4, FL = 4
+    case 2: return s16 ? GramRun{64, 4} : GramRun{64, 2};  // R = 4, FL = 2
+    case 3: return {128, 2};                            // R = 2, FL = 2
+    default: return s16 ? GramRun{256, 4} : GramRun{256, 2};  // R = 1, FL = 2
+  }
+}
+constexpr double kGramKappaC = 9.3;
+double gram_kappa_bound(int64_t p_total, GramRun r) {
+  return kGramKappaC * std::sqrt((double)r.p * (double)p_total) / r.n;
+}
+bool gram_vec(int32_t num_segments, const int64_t* seg_numel, int32_t k, const void* const* d_in) {
+  bool vec = true;
+  for (int s = 0; s < num_segments; ++s)
+    if (seg_numel[s] > 0)
+      for (int i = 0; i < k; ++i) vec = vec && d_in[(int64_t)s * k + i] && ((uintptr_t)d_in[(int64_t)s * k + i] % 16 == 0);
+  return vec;
+}
 
 }  // namespace
 
@@ -2024,10 +2261,7 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
   if (k < 2 || k > kMaxPairK || num_segments <= 0 || !seg_numel || !d_in || !d_dist || !d_kappa_max)
     return fail(FA_ERR_INVALID, "fa_pairwise_sqdist_gram: invalid arguments (2 <= k <= %d)", kMaxPairK);
   const int kbc = (k + 31) / 32;
-  bool vec = true;
-  for (int s = 0; s < num_segments; ++s)
-    if (seg_numel[s] > 0)
-      for (int i = 0; i < k; ++i) vec = vec && d_in[(int64_t)s * k + i] && ((uintptr_t)d_in[(int64_t)s * k + i] % 16 == 0);
+  const bool vec = gram_vec(num_segments, seg_numel, k, d_in);
   // K <= 32 on 16-byte aligned clients: the LDS-DMA ring kernel (256-coordinate chunks), whose chunk
   // index runs over FULL chunks only (tile_start = the segment's first full chunk, pad = 1: a partial
   // chunk follows)
@@ -2096,7 +2330,8 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
                        nblocks, gm, k, (double*)d_dist, (double*)d_kappa_max, ctr);                           \
   } while (0)
   if (glds) {  // c0 = the full-chunk count; two 8-wave workgroups per CU
-    const int nbg = (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, 512));
+    // the workgroup count the scratch was sized for (gram_scratch -> gram_nblocks), at most 512
+    const int nbg = std::min(gram_nblocks(nchunks, 1), 512);
     const size_t lg = (size_t)4 * 32 * cs * sizeof(float) + (size_t)glds * 16 * sizeof(float);
     hipLaunchKernelGGL((k_pair_gram_ring<4, 128, 8>), dim3((unsigned)nbg), dim3(512), lg, st, sg, nseg, pp, k, c0,
                        part, ctr);
@@ -2110,17 +2345,43 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
       break;
     case 3: FA_GR(3, false); break;
     default:
-      if (gram_s16()) FA_GR(4, true);
-      else FA_GR(4, false);
+      if (gram3()) {  // the bf16x3 split form (K in (96, 128])
+        if (vec)
+          hipLaunchKernelGGL((k_pair_gram3<true>), dim3((unsigned)nblocks), dim3(Gram3Cfg::NT), Gram3Cfg::LDS, st, sg,
+                             nseg, pp, k, nchunks, part, ctr);
+        else
+          hipLaunchKernelGGL((k_pair_gram3<false>), dim3((unsigned)nblocks), dim3(Gram3Cfg::NT), Gram3Cfg::LDS, st, sg,
+                             nseg, pp, k, nchunks, part, ctr);
+        hipLaunchKernelGGL((k_gram_reduce<4>), dim3((unsigned)ntr), dim3(64 * kGRW), 0, st, (const double*)part,
+                           nblocks, gm, k, (double*)d_dist, (double*)d_kappa_max, ctr);
+      } else if (gram_s16()) {
+        FA_GR(4, true);
+      } else {
+        FA_GR(4, false);
+      }
       break;
   }
 #undef FA_GR
   FA_HIP(hipGetLastError());
   rc = release(slot, st);
   if (rc || kappa_limit <= 0.0) return rc;
-  // the guarded direct kernels: they run (and overwrite d_dist) only if kappa_max > kappa_limit
+  // the guarded direct kernels: they run (and overwrite d_dist) only if kappa_max exceeds the limit
+  // the error model allows at this size (fa_pairwise_sqdist_gram_limit)
+  int64_t ptot = 0;
+  for (int s = 0; s < num_segments; ++s) ptot += std::max<int64_t>(seg_numel[s], 0);
+  const double lim = std::min(kappa_limit, gram_kappa_bound(ptot, gram_run(kb, glds != 0)));
   return pairdist_direct(ctx, FA_DTYPE_F32, num_segments, seg_numel, k, d_in, d_dist, (char*)d_scratch + gram_bytes,
-                         scratch_bytes - gram_bytes, hip_stream, (const double*)d_kappa_max, kappa_limit);
+                         scratch_bytes - gram_bytes, hip_stream, (const double*)d_kappa_max, lim);
+}
+
+double fa_pairwise_sqdist_gram_limit(int32_t num_segments, const int64_t* seg_numel, int32_t k,
+                                     const void* const* d_in, double kappa_limit) {
+  if (k < 2 || k > kMaxPairK || num_segments <= 0 || !seg_numel || !d_in || kappa_limit <= 0.0) return 0.0;
+  const int kb = (k + 31) / 32;
+  const bool glds = kb == 1 && gram_vec(num_segments, seg_numel, k, d_in) && gram_glds();
+  int64_t ptot = 0;
+  for (int s = 0; s < num_segments; ++s) ptot += std::max<int64_t>(seg_numel[s], 0);
+  return std::min(kappa_limit, gram_kappa_bound(ptot, gram_run(kb, glds)));
 }
 
 }  // extern "C"

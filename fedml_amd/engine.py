@@ -122,6 +122,19 @@ class AggEngine:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         return N.ctypes.c_void_p(s.cuda_stream)
 
+    def read_probe(self, buf: torch.Tensor, rows_per_workgroup: int, stream=None) -> None:
+        """Measurement only (fa_read_probe): stream ``buf``'s bytes in the weighted-sum kernel's
+        tiled read pattern -- ``rows_per_workgroup`` consecutive 4-KiB rows per workgroup, no
+        arithmetic, no output stream.  Asynchronous; time it with events on ``stream``."""
+        if buf.device != self.device or not buf.is_contiguous():
+            raise ValueError("read_probe: a contiguous tensor on this engine's device is required")
+        word = self.__dict__.get("_probe_word")
+        if word is None:
+            word = self._probe_word = torch.zeros(1, dtype=torch.int32, device=self.device)
+        N.check(self._lib.fa_read_probe(self._ctx, N.ctypes.c_void_p(buf.data_ptr()),
+                                        buf.numel() * buf.element_size(), int(rows_per_workgroup),
+                                        N.ctypes.c_void_p(word.data_ptr()), self._stream(stream)), "fa_read_probe")
+
     def _scratch(self, name: str, need: int, stream=None) -> torch.Tensor:
         """Device scratch of >= need bytes, cached per (name, stream): calls queued on different
         streams never share one, and a buffer replaced while a kernel on ``stream`` may still read it
@@ -928,10 +941,16 @@ class AggEngine:
         return d
 
     # Gram form (fa_pairwise_sqdist_gram) for float32 models: its result stands when the largest
-    # cancellation factor kappa = (A_i + A_j) / D_ij is at most this (relative error ~1e-7 kappa,
-    # tests/test_gpu_robust.py); otherwise -- and for non-finite inputs -- the direct kernels queued
-    # behind it recompute the matrix, decided on the device (no host round trip)
+    # cancellation factor kappa = (A_i + A_j) / D_ij is at most min(KAPPA_MAX, the error model's
+    # bound at this size) -- fa_pairwise_sqdist_gram_limit: 6 sigma of the modelled float32 run error
+    # <= 1e-6 relative (tests/test_gpu_robust.py's kappa band); otherwise -- and for non-finite
+    # inputs or D_ij <= 0 -- the direct kernels queued behind it recompute the matrix, decided on the
+    # device (no host round trip)
     KAPPA_MAX = 16.0
+    # A shape whose last guarded call fell back (e.g. the reference's ByzantineAttack "zero" mode:
+    # identical attacker vectors, D = 0 every round) goes straight to the direct kernels, re-trying
+    # the Gram form every GRAM_RETRY-th call (FEDML_AMD_KRUM_STICKY=0: always the guarded Gram form)
+    GRAM_RETRY = 8
 
     @property
     def last_kappa_max(self) -> Optional[float]:
@@ -940,29 +959,62 @@ class AggEngine:
         return None if km is None else float(km.item())
 
     @property
+    def last_kappa_limit(self) -> Optional[float]:
+        """The kappa limit the last guarded Gram-form call applied (fa_pairwise_sqdist_gram_limit)."""
+        return getattr(self, "_last_limit", None)
+
+    @property
     def last_pair_form(self) -> str:
         """"gram" or "direct": which form's result the last float32 pairwise call returned."""
         if getattr(self, "_last_form", None) != "auto":
             return self._last_form
-        return "gram" if self.last_kappa_max <= self.KAPPA_MAX else "direct"
+        return "gram" if self.last_kappa_max <= self._last_limit else "direct"
+
+    def _gram_fell_back(self, key) -> bool:
+        """Whether the last guarded call of this shape fell back (without waiting: a call still
+        running counts as not fallen back)."""
+        memo = self.__dict__.setdefault("_gram_memo", {})
+        m = memo.get(key)
+        if m is None or not m["ev"].query():
+            return False
+        return not (float(m["km"][0]) <= m["limit"])
 
     def _pairwise_launch(self, segments, stream=None, diff_dtype=torch.float32, form=None) -> torch.Tensor:
         k = len(segments[0])
         in_ptrs = [t.data_ptr() for seg in segments for t in seg]
         nl = N.i64_array([seg[0].numel() for seg in segments])
         form = form or os.environ.get("FEDML_AMD_KRUM_FORM", "auto")
+        key = (k, tuple(seg[0].numel() for seg in segments))
+        if (diff_dtype == torch.float32 and form == "auto" and os.environ.get("FEDML_AMD_KRUM_STICKY", "1") != "0"
+                and self._gram_fell_back(key)):
+            m = self._gram_memo[key]
+            m["skips"] += 1
+            if m["skips"] % self.GRAM_RETRY:
+                form = "direct"
         if diff_dtype == torch.float32 and form in ("auto", "gram"):
+            ptrs = N.ptr_array(in_ptrs)
+            limit = self._lib.fa_pairwise_sqdist_gram_limit(len(segments), nl, k, ptrs, self.KAPPA_MAX) \
+                if form == "auto" else 0.0
             with self.lock:
                 need = self._lib.fa_pairwise_sqdist_gram_scratch_bytes(len(segments), nl, k)
                 scratch = self._scratch("pdg", need, stream)
                 d = torch.empty((k, k), dtype=torch.float64, device=self.device)
                 km = torch.empty(1, dtype=torch.float64, device=self.device)
-                rc = self._lib.fa_pairwise_sqdist_gram(self._ctx, len(segments), nl, k, N.ptr_array(in_ptrs),
+                rc = self._lib.fa_pairwise_sqdist_gram(self._ctx, len(segments), nl, k, ptrs,
                                                        d.data_ptr(), km.data_ptr(),
                                                        self.KAPPA_MAX if form == "auto" else 0.0,
                                                        scratch.data_ptr(), scratch.numel(), self._stream(stream))
             N.check(rc, "fa_pairwise_sqdist_gram")
-            self._last_km, self._last_form = km, form if form == "gram" else "auto"
+            self._last_km, self._last_form, self._last_limit = km, form if form == "gram" else "auto", limit
+            if form == "auto":  # kappa_max to pinned host memory, read by the next call of this shape
+                memo = self.__dict__.setdefault("_gram_memo", {})
+                m = memo.get(key) or {"km": torch.zeros(1, dtype=torch.float64, pin_memory=True), "skips": 0,
+                                      "ev": torch.cuda.Event()}
+                s = stream if stream is not None else torch.cuda.current_stream(self.device)
+                m["km"].copy_(km, non_blocking=True)
+                m["ev"].record(s)
+                m["limit"], m["skips"] = limit, 0
+                memo[key] = m
             return d
         self._last_km, self._last_form = None, "direct"
         with self.lock:

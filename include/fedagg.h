@@ -301,6 +301,17 @@ int fa_weighted_sum_host(fa_ctx *ctx, int dtype, int mode, int32_t num_segments,
 int fa_promote_add(fa_ctx *ctx, int acc_dtype, int t_dtype, int64_t n, const void *d_acc, const void *d_t,
                    void *d_out, void *hip_stream);
 
+/*
+ * Measurement only (no arithmetic contract, not an aggregation): streams `bytes` of d_buf (whole
+ * FA_TILE_BYTES rows; a remainder is ignored) the way the weighted-sum kernel reads a tiled arena
+ * group -- workgroup b reads rows [b R, (b + 1) R), R = rows_per_workgroup, each lane 16 bytes of every
+ * row -- with no arithmetic and no output stream (d_word: one device word, written only with
+ * vanishing probability).  Its duration gives the box's read ceiling for that pattern on those
+ * pages (bench.py measured_read_ceiling).  Asynchronous on hip_stream; 0 or a negative status.
+ */
+int fa_read_probe(fa_ctx *ctx, const void *d_buf, int64_t bytes, int32_t rows_per_workgroup, void *d_word,
+                  void *hip_stream);
+
 /* Static name of a status code. */
 const char *fa_strerror(int code);
 /* Detail of the calling thread's last error ("" if none). */

@@ -10,6 +10,7 @@
  *                       compute_euclidean_distance(v_i, v_j) ** 2 for every pair)
  *   fa_pairwise_sqdist_rt  the same for bfloat16 / float16 models (differences in the model dtype)
  *   fa_pairwise_sqdist_gram  the same for float32 models in the Gram form (matrix cores, kappa-guarded)
+ *   fa_pairwise_sqdist_gram_limit  the kappa limit that guard applies to an input (its error model)
  *
  * Contract (bit-exact; pinned by tests/golden/g16_*): for every element e, out[e] is the input
  * element (bit pattern) that ATen's median selects: the first NaN in client order if any client
@@ -79,19 +80,29 @@ size_t fa_pairwise_sqdist_scratch_bytes(int32_t num_segments, const int64_t *seg
  * D_ij = A_i + A_j - 2 G_ij over y_i = x_i - c (c: the per-coordinate median of clients 0..4), G = Y Y^T
  * on the f32-input MFMA (k <= 32 with 16-byte aligned clients: v_mfma_f32_16x16x4_f32 over the three
  * upper 16x16 tiles, chunks streamed by LDS-DMA; otherwise v_mfma_f32_32x32x2_f32 over the upper
- * 32x32 tiles), float32 runs of 32-64 products summed in float64.  Same d_dist layout
- * (k x k float64, symmetric, zero diagonal).  The form cancels -- relative error ~ 1e-7 * kappa_ij,
- * kappa_ij = (A_i + A_j) / D_ij -- so it also writes kappa_max = max over pairs (one float64 at
- * d_kappa_max; +inf when some D_ij <= 0 or an input is not finite).  kappa_limit > 0: the direct
- * kernels of fa_pairwise_sqdist are queued behind it, guarded on the device by that value -- they
- * return at once when kappa_max <= kappa_limit and otherwise recompute d_dist, so the call stays
- * asynchronous (fedml_amd/engine.py uses 16); kappa_limit <= 0: the Gram result only.
+ * 32x32 tiles), float32 runs of n = 64-256 products (p = 2 or 4 per instruction) summed in float64.
+ * Same d_dist layout (k x k float64, symmetric, zero diagonal).  The form cancels: its relative error
+ * is ~ 0.30 kappa_ij u n / sqrt(p P) (one sigma, u = 2^-24, P = total coordinates), kappa_ij =
+ * (A_i + A_j) / D_ij -- so it also writes kappa_max = max over pairs (one float64 at d_kappa_max; +inf
+ * when some D_ij <= 0 or an input is not finite).  kappa_limit > 0: the direct kernels of
+ * fa_pairwise_sqdist are queued behind it, guarded on the device -- they return at once when
+ * kappa_max <= fa_pairwise_sqdist_gram_limit(..., kappa_limit) and otherwise recompute d_dist, so the
+ * call stays asynchronous and every distance it returns is within 1e-6 relative of the exact value
+ * (fedml_amd/engine.py passes 16); kappa_limit <= 0: the Gram result only, no guard.
  * d_scratch: fa_pairwise_sqdist_gram_scratch_bytes(...) bytes.
  */
 int fa_pairwise_sqdist_gram(fa_ctx *ctx, int32_t num_segments, const int64_t *seg_numel, int32_t k,
                             const void *const *d_in, void *d_dist, void *d_kappa_max, double kappa_limit,
                             void *d_scratch, size_t scratch_bytes, void *hip_stream);
 size_t fa_pairwise_sqdist_gram_scratch_bytes(int32_t num_segments, const int64_t *seg_numel, int32_t k);
+/*
+ * The kappa limit fa_pairwise_sqdist_gram's guard applies to this input: min(kappa_limit,
+ * 9.3 sqrt(p P) / n) -- the largest kappa at which 6 sigma of the error model above stays <= 1e-6
+ * relative (n, p of the kernel the call would run; d_in only for its 16-byte alignment).  0 for
+ * invalid arguments or kappa_limit <= 0.  Host only, no device work.
+ */
+double fa_pairwise_sqdist_gram_limit(int32_t num_segments, const int64_t *seg_numel, int32_t k,
+                                     const void *const *d_in, double kappa_limit);
 
 #ifdef __cplusplus
 }

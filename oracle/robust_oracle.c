@@ -92,15 +92,20 @@ int orc_pairwise_sqdist_rt(int64_t n, int32_t k, const float *const *x, int rt, 
 
 int orc_pairwise_sqdist(int64_t n, int32_t k, const float *const *x, double *d) {
     if (k <= 0 || n < 0) return -1;
-    for (int32_t i = 0; i < k; ++i)
-        for (int32_t j = 0; j < k; ++j) {
-            double s = 0.0;
-            if (i != j)
-                for (int64_t e = 0; e < n; ++e) {
-                    const double t = (double)x[i][e] - (double)x[j][e];
-                    s += t * t;
-                }
-            d[(int64_t)i * k + j] = s;
+    /* one sequential float64 sum per unordered pair (the (j, i) entry is the same sum: the float32
+       differences are exact in float64 and square to the same terms); pairs spread over threads */
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t p = 0; p < (int64_t)k * k; ++p) {
+        const int32_t i = (int32_t)(p / k), j = (int32_t)(p % k);
+        if (j <= i) continue;
+        double s = 0.0;
+        for (int64_t e = 0; e < n; ++e) {
+            const double t = (double)x[i][e] - (double)x[j][e];
+            s += t * t;
         }
+        d[(int64_t)i * k + j] = s;
+        d[(int64_t)j * k + i] = s;
+    }
+    for (int32_t i = 0; i < k; ++i) d[(int64_t)i * k + i] = 0.0;
     return 0;
 }

@@ -1025,6 +1025,73 @@ def cases_krum_f64():
                    ref="core/security/defense/krum_defense.py:27-66, common/utils.py:8-27"))
 
 
+def _band_kappa_max(vec):
+    """max over pairs of kappa_ij = (A_i + A_j) / D_ij, A_i = |x_i - c|^2 with c the per-coordinate
+    median of clients 0..4 (the Gram form's centre, fedml_amd/csrc/robust.hip), exact in float64."""
+    X = torch.stack([v.double() for v in vec])
+    K = X.shape[0]
+    c = torch.stack(vec[:5]).median(0).values.double() if K >= 5 else X[0]
+    A = ((X - c) ** 2).sum(1)
+    best = 0.0
+    for i in range(K):
+        for j in range(i + 1, K):
+            D = float(((X[i] - X[j]) ** 2).sum())
+            best = max(best, float(A[i] + A[j]) / D)
+    return best
+
+
+def cases_krum_band():
+    """r06: Krum over float32 models whose pairs sit in the Gram form's cancellation band (kappa_max
+    2..16), so that the selection there is pinned by the REFERENCE: `offset` --
+    clients 0..2 (three of the five that define the Gram form's centre) shifted by delta, every honest
+    pair at kappa ~ (delta^2 + s^2) / s^2; `pair` -- the last client a near copy of the one before it.
+    Records the reference's selection, scores and every `compute_euclidean_distance(v_i, v_j).item()
+    ** 2` (krum_defense.py:27-66, common/utils.py:8-27) and the realised kappa_max."""
+    _, _, Krum = load_defenses()
+    import fedml.core.security.common.utils as su
+    lr = [("linear.weight", (10, 784), torch.float32), ("linear.bias", (10,), torch.float32)]
+    sm = [("fc.weight", (10, 196), torch.float32), ("fc.bias", (10,), torch.float32)]  # P = 1,970
+    for tag, lay, K, f, m, kind, kappa in (("lr_offset16", lr, 6, 1, 1, "offset", 15.9),
+                                           ("p1970_offset8", sm, 12, 2, 1, "offset", 8.0),
+                                           ("p1970_offset16m3", sm, 12, 2, 3, "offset", 15.9),
+                                           ("p1970_pair12", sm, 10, 2, 2, "pair", 12.0)):
+        g = torch.Generator().manual_seed(4040 + K + int(kappa * 10) + len(tag))
+        sgm = 1e-2
+        base = OrderedDict((k, 0.05 * torch.randn(sh, generator=g)) for k, sh, _ in lay)
+        clients = [OrderedDict((k, (v + sgm * torch.randn(v.shape, generator=g)).float()) for k, v in base.items())
+                   for _ in range(K)]
+        if kind == "offset":  # delta by bisection until the realised kappa_max is within 2 % of the target
+            honest = clients[:3]
+            lo, hi = 0.0, 20 * sgm
+            for _ in range(40):
+                delta = 0.5 * (lo + hi)
+                clients[:3] = [OrderedDict((k, (v + delta).float()) for k, v in c.items()) for c in honest]
+                km = _band_kappa_max([su.vectorize_weight(c) for c in clients])
+                if abs(km - kappa) <= 0.02 * kappa:
+                    break
+                lo, hi = (delta, hi) if km < kappa else (lo, delta)
+        else:
+            eps = sgm * (2 * 1.29 / kappa) ** 0.5
+            clients[K - 1] = OrderedDict((k, (v + eps * torch.randn(v.shape, generator=g)).float())
+                                         for k, v in clients[K - 2].items())
+        n = gen_counts(4040 + K, K)
+        raw = list(zip(n, clients))
+        d = Krum(Args(byzantine_client_num=f, krum_param_m=m))
+        sel = d.defend_before_aggregation(raw)
+        idx = [next(i for i, (_, c) in enumerate(raw) if c is sc) for _, sc in sel]
+        vec = [su.vectorize_weight(c) for c in clients]
+        assert vec[0].dtype == torch.float32
+        scores = d._compute_krum_score(vec)
+        dists = [[su.compute_euclidean_distance(vec[i], vec[j]).item() ** 2 if i != j else 0.0 for j in range(K)]
+                 for i in range(K)]
+        km = _band_kappa_max(vec)
+        assert abs(km - kappa) <= 0.02 * kappa or kind == "pair", (tag, km)
+        write(f"g18_krum_band_{tag}_K{K}_f{f}_m{m}", clients, [clients[0]],
+              dict(kind="krum", n=n, byzantine_client_num=f, krum_param_m=m, selected=idx, scores=scores,
+                   dists=dists, vector_dtype="float32", kappa_max=km, construction=kind,
+                   ref="core/security/defense/krum_defense.py:27-66, common/utils.py:8-27"))
+
+
 def out2_equal(a, b):
     return all(np.array_equal(np.asarray(a[k]), np.asarray(b[k])) for k in a)
 

@@ -39,7 +39,7 @@ def oracle_median_defense(meta, arrays):
 
 def test_inventory():
     assert len(ROB["g16_"]) >= 20 and len(ROB["g17_"]) >= 5 and len(ROB["g18_"]) >= 4
-    assert sum(os.path.getsize(p) for p in CASES) < 5e6
+    assert sum(os.path.getsize(p) for p in CASES) < 5.5e6  # r06: + the Krum kappa-band fixtures
 
 
 @pytest.mark.parametrize("path", ROB["g16_"], ids=ids)
