@@ -2063,7 +2063,7 @@ def main():
                      "ms_per_step": round(dt_s / n_soak * 1e3, 4),
                      "note": "the same step repeated after the timed region (not part of `value`)"}
     cold = None
-    if args.cold_reps > 0 and world == 1 and not CPU_REHEARSAL and not wl.get("latency"):
+    if args.cold_reps > 0 and world == 1 and not CPU_REHEARSAL:
         stage("cold calls")
         cold = cold_calls(wl, args.cold_reps, args.cold_idle)
     stage("parity check")

@@ -1577,23 +1577,28 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
 constexpr int kG3S = kGE + 8;  // bf16 per plane row: 272-byte rows, 16-lane b128 reads conflict-free
 typedef __bf16 gbf8 __attribute__((ext_vector_type(8)));
 typedef __bf16 gbf4 __attribute__((ext_vector_type(4)));
+template <int KB>
 struct Gram3Cfg {
-  static constexpr int KP = 128, W = 12, NT = W * 64, QV = kGE / 4;
-  static constexpr int NLD = (KP * QV + NT - 1) / NT;         // staged 16-byte vectors per thread (6)
-  static constexpr int PLANE = KP * kG3S;                      // bf16 per plane
+  static_assert(KB == 2 || KB == 4, "16x16 wave tables for 4 (K in (32, 64]) or 8 (K in (96, 128]) client blocks");
+  static constexpr int KP = 32 * KB, QV = kGE / 4;
+  static constexpr int W = KB == 4 ? 12 : 16, NT = W * 64;
+  static constexpr int R = KB == 4 ? 1 : 4;                     // coordinate splits (groups of 32 per chunk / R)
+  static constexpr int NLD = (KP * QV + NT - 1) / NT;           // staged 16-byte vectors per thread (6 / 2)
+  static constexpr int PLANE = KP * kG3S;                       // bf16 per plane
   static constexpr size_t PLANE_BYTES = (size_t)3 * PLANE * 2;  // h, m, l
-  static constexpr size_t LDS = PLANE_BYTES + sizeof(float) * (5 * kGE + W * kGE);  // + rows 0..4 + centres
+  static constexpr size_t STAGE = PLANE_BYTES + sizeof(float) * (5 * kGE + W * kGE);  // + rows 0..4 + centres
+  static constexpr size_t RED = R > 1 ? sizeof(double) * W * 768 : 0;               // the splits' sums
+  static constexpr size_t LDS = STAGE > RED ? STAGE : RED;
 };
-static_assert(Gram3Cfg::PLANE_BYTES >= sizeof(double) * 12 * 768, "the epilogue's wave sums reuse the planes");
 
 __device__ __forceinline__ float bf_f(__bf16 b) { return (float)b; }
 
-template <bool VEC>
-__global__ void __launch_bounds__(Gram3Cfg::NT) __attribute__((amdgpu_waves_per_eu(3)))
+template <int KB, bool VEC>
+__global__ void __launch_bounds__(Gram3Cfg<KB>::NT) __attribute__((amdgpu_waves_per_eu(KB == 4 ? 3 : 4)))
 k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k,
              int64_t nchunks, double* __restrict__ partial, unsigned* __restrict__ ctr) {
-  using C = Gram3Cfg;
-  constexpr int KB = 4, QV = C::QV;
+  using C = Gram3Cfg<KB>;
+  constexpr int QV = C::QV;
   if (blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;  // k_gram_reduce's arrival counter
   extern __shared__ __attribute__((aligned(16))) char g3[];
   __bf16* const planes = (__bf16*)g3;
@@ -1602,11 +1607,16 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   float* const crow = c5 + 5 * kGE + w * kGE;  // this wave's centre row (wave-private)
   const int li = lane & 15, kk = lane >> 4;
-  const bool dg = w < 4;  // waves 0-3: a diagonal pair (3 tiles of 2 blocks); 4-11: a triangle of 3 blocks
+  // the wave's tile set (the S16 forms' tables): type 0 a diagonal pair (b0,b0), (b0,b1), (b1,b1);
+  // 1 a triangle (b0,b1), (b0,b2), (b1,b2); 2 a cross pair (b0,b1), (b0,b2) -- and its coordinate split
+  const int set16 = KB == 4 ? w : (w % 4 + w / 4) % 4, r16 = KB == 4 ? 0 : w / 4;
+  const int typ = KB == 4 ? (w < 4 ? 0 : 1) : kG16Sets2[set16][0];
+  const bool dg = typ == 0;
+  const int ntile = typ == 2 ? 2 : 3;
   int blk[3], ro[3];
 #pragma unroll
   for (int x = 0; x < 3; ++x) {
-    blk[x] = kG16Blocks[w][x];
+    blk[x] = KB == 4 ? kG16Blocks[w][x] : kG16Sets2[set16][1 + x];
     ro[x] = (16 * blk[x] + li) * kG3S + 8 * kk;
   }
   gf4 a16[3];
@@ -1657,7 +1667,7 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
     // A) rows 0..4 (staged by threads 0..159 in their first vector) to LDS
     if (t < 5 * QV) *(gf4*)&c5[(t / QV) * kGE + 4 * (t % QV)] = v[0];
     __syncthreads();  // also: every wave is done reading the planes of chunk ch - 1
-    // B) this wave's copy of the chunk's centre: the median of clients 0..4 (k > 96 here)
+    // B) this wave's copy of the chunk's centre: the median of clients 0..4 (k > 32 here)
     if (lane < QV) {
       const gf4 a = *(const gf4*)&c5[4 * lane], b = *(const gf4*)&c5[kGE + 4 * lane],
                  c = *(const gf4*)&c5[2 * kGE + 4 * lane], d = *(const gf4*)&c5[3 * kGE + 4 * lane],
@@ -1693,9 +1703,10 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
     }
     if (ch + 1 < c1) load(ch + 1);  // in flight during the MFMAs
     __syncthreads();
-    // D) the wave's three 16x16 tiles over the chunk's 4 groups of 32 coordinates
+    // D) the wave's 16x16 tiles over its groups of 32 coordinates of the chunk
 #pragma unroll
-    for (int G = 0; G < kGE / 32; ++G) {
+    for (int gi = 0; gi < kGE / 32 / C::R; ++gi) {
+      const int G = r16 + gi * C::R;
       gbf8 f[3][3];
 #pragma unroll
       for (int x = 0; x < 3; ++x)
@@ -1704,9 +1715,8 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
           for (int p = 0; p < 3; ++p) f[x][p] = *(const gbf8*)&planes[p * C::PLANE + ro[x] + 32 * G];
 #pragma unroll
       for (int x = 0; x < 3; ++x) {
-        // tiles: diagonal pair (0,0), (0,1), (1,1); triangle (0,1), (0,2), (1,2)
-        const int pa = dg ? (x == 2 ? 1 : 0) : (x == 2 ? 1 : 0);
-        const int pb = dg ? (x == 0 ? 0 : 1) : (x == 0 ? 1 : 2);
+        if (x == 2 && typ == 2) break;
+        const int pa = x == 2 ? 1 : 0, pb = dg ? (x == 0 ? 0 : 1) : (x == 0 ? 1 : 2);
         gf4 acc = a16[x];
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][1], f[pb][1], acc, 0, 0, 0);  // M M
         acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][0], f[pb][2], acc, 0, 0, 0);  // H L
@@ -1717,7 +1727,7 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
         a16[x] = acc;
       }
     }
-    // float32 runs of 2 chunks (256 coordinates) -> float64
+    // float32 runs (256 coordinates of the chunks for K > 96, 64 per split for K <= 64) -> float64
     if ((ch - c0) % 2 == 1 || ch + 1 == c1) {
 #pragma unroll
       for (int x = 0; x < 3; ++x)
@@ -1728,12 +1738,24 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
         }
     }
   }
-  // epilogue: as k_pair_gram<4, *, true> -- 16x16 tile (A, B) into 32x32 tile (A / 2, B / 2),
-  // quadrant (A % 2, B % 2); a diagonal 32x32 tile's lower-left quadrant written as zeros
+  // epilogue: as k_pair_gram<KB, *, true> -- the splits summed in split order through LDS (the planes
+  // are free now), then 16x16 tile (A, B) into 32x32 tile (A / 2, B / 2), quadrant (A % 2, B % 2); a
+  // diagonal 32x32 tile's lower-left quadrant written as zeros
   __syncthreads();
+  if constexpr (C::R > 1) {
+    double* red = (double*)g3;  // [W][12][64]
+#pragma unroll
+    for (int q = 0; q < 12; ++q) red[(int64_t)w * 768 + q * 64 + lane] = accd[q];
+    __syncthreads();
+    if (r16 != 0) return;
+#pragma unroll
+    for (int q = 0; q < 12; ++q)
+      for (int rr = 1; rr < C::R; ++rr) accd[q] += red[(int64_t)(4 * rr + ((set16 - rr + 4) % 4)) * 768 + q * 64 + lane];
+  }
   double* o = partial + (int64_t)blockIdx.x * gram_T_c<KB>() * 1024;
 #pragma unroll
   for (int x = 0; x < 3; ++x) {
+    if (x == 2 && typ == 2) break;
     const int pa = x == 2 ? 1 : 0, pb = dg ? (x == 0 ? 0 : 1) : (x == 0 ? 1 : 2);
     const int A = blk[pa], Bk = blk[pb];
     const int I = A >> 1, J = Bk >> 1;
@@ -1747,6 +1769,7 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
 #pragma unroll
     for (int q = 0; q < 4; ++q) o[(int64_t)t32 * 1024 + (16 + 4 * kk + q) * 32 + li] = 0.0;
   }
+  (void)ntile;
 }
 
 // K <= 32 with an LDS-DMA ring (r05).  The register-staged kernel above waits vmcnt(0) for its one
@@ -2329,6 +2352,17 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
     hipLaunchKernelGGL((k_gram_reduce<KB>), dim3((unsigned)ntr), dim3(64 * kGRW), 0, st, (const double*)part,    \
                        nblocks, gm, k, (double*)d_dist, (double*)d_kappa_max, ctr);                           \
   } while (0)
+#define FA_GR3(KB)                                                                                             \
+  do {                                                                                                         \
+    if (vec)                                                                                                   \
+      hipLaunchKernelGGL((k_pair_gram3<KB, true>), dim3((unsigned)nblocks), dim3(Gram3Cfg<KB>::NT),             \
+                         Gram3Cfg<KB>::LDS, st, sg, nseg, pp, k, nchunks, part, ctr);                           \
+    else                                                                                                       \
+      hipLaunchKernelGGL((k_pair_gram3<KB, false>), dim3((unsigned)nblocks), dim3(Gram3Cfg<KB>::NT),            \
+                         Gram3Cfg<KB>::LDS, st, sg, nseg, pp, k, nchunks, part, ctr);                           \
+    hipLaunchKernelGGL((k_gram_reduce<KB>), dim3((unsigned)ntr), dim3(64 * kGRW), 0, st, (const double*)part,    \
+                       nblocks, gm, k, (double*)d_dist, (double*)d_kappa_max, ctr);                           \
+  } while (0)
   if (glds) {  // c0 = the full-chunk count; two 8-wave workgroups per CU
     // the workgroup count the scratch was sized for (gram_scratch -> gram_nblocks), at most 512
     const int nbg = std::min(gram_nblocks(nchunks, 1), 512);
@@ -2340,20 +2374,14 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
   } else switch (kb) {
     case 1: FA_GR(1, false); break;
     case 2:
-      if (gram_s16()) FA_GR(2, true);
+      if (gram3()) FA_GR3(2);  // the bf16x3 split form (K in (32, 64])
+      else if (gram_s16()) FA_GR(2, true);
       else FA_GR(2, false);
       break;
     case 3: FA_GR(3, false); break;
     default:
       if (gram3()) {  // the bf16x3 split form (K in (96, 128])
-        if (vec)
-          hipLaunchKernelGGL((k_pair_gram3<true>), dim3((unsigned)nblocks), dim3(Gram3Cfg::NT), Gram3Cfg::LDS, st, sg,
-                             nseg, pp, k, nchunks, part, ctr);
-        else
-          hipLaunchKernelGGL((k_pair_gram3<false>), dim3((unsigned)nblocks), dim3(Gram3Cfg::NT), Gram3Cfg::LDS, st, sg,
-                             nseg, pp, k, nchunks, part, ctr);
-        hipLaunchKernelGGL((k_gram_reduce<4>), dim3((unsigned)ntr), dim3(64 * kGRW), 0, st, (const double*)part,
-                           nblocks, gm, k, (double*)d_dist, (double*)d_kappa_max, ctr);
+        FA_GR3(4);
       } else if (gram_s16()) {
         FA_GR(4, true);
       } else {
@@ -2362,6 +2390,7 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
       break;
   }
 #undef FA_GR
+#undef FA_GR3
   FA_HIP(hipGetLastError());
   rc = release(slot, st);
   if (rc || kappa_limit <= 0.0) return rc;

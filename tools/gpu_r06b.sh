@@ -11,7 +11,7 @@ tail -3 $O/tests_default.log; [ $rc = 0 ] || exit $rc
 timeout -k 10 600 python tools/krum_kappa_sweep.py > $O/sweep_default.jsonl 2> $O/sweep_default.err || { tail -5 $O/sweep_default.err; exit 1; }
 echo sweep_default $(wc -l < $O/sweep_default.jsonl)
 export FA_GRAM3=1
-timeout -k 10 600 env KS=100,128 python tools/krum_kappa_sweep.py > $O/sweep_gram3.jsonl 2> $O/sweep_gram3.err || { tail -5 $O/sweep_gram3.err; exit 1; }
+timeout -k 10 600 env KS=40,64,100,128 python tools/krum_kappa_sweep.py > $O/sweep_gram3.jsonl 2> $O/sweep_gram3.err || { tail -5 $O/sweep_gram3.err; exit 1; }
 echo sweep_gram3 $(wc -l < $O/sweep_gram3.jsonl)
 timeout -k 10 900 $T tests/test_gpu_krum_band.py tests/test_gpu_robust.py -k "band or pairwise or krum or sticky" > $O/tests_gram3.log 2>&1; rc=$?
 tail -3 $O/tests_gram3.log; [ $rc = 0 ] || exit $rc
