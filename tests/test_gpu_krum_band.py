@@ -12,6 +12,7 @@ selections itself in the g18_krum_band_* fixtures (tests/golden/make_golden.py c
 selection, scores and every distance the reference measured."""
 from __future__ import annotations
 
+import math
 import os
 
 import numpy as np
@@ -41,20 +42,24 @@ def eng():
 
 def _clients(P, K, kind, kappa, seed):
     """[K, P] fp32 clients on the device, rows 256-byte aligned (arena rows), the construction's
-    parameter tuned so that the exact kappa_max is within 3 % of ``kappa`` (offset: bisection on
-    delta; pair: eps from the honest A)."""
+    parameter tuned by bisection so that the exact kappa_max is within 3 % of ``kappa`` (offset:
+    delta; pair: eps)."""
     g = torch.Generator(device=DEV).manual_seed(seed)
     s = 1e-2
     x = 0.05 * torch.randn(P, generator=g, device=DEV) + s * torch.randn((K, P), generator=g, device=DEV)
     Ppad = -(-P // 64) * 64
     buf = torch.zeros((K, Ppad), device=DEV)
     buf[:, :P] = x
-    if kind == "pair":
-        c = buf[:5, :P].median(0).values.double()
-        A = ((buf[K - 2, :P].double() - c) ** 2).sum()
+    if kind == "pair":  # eps by bisection (kappa_max falls as eps grows; at K = 5 the pair moves the centre too)
         z = torch.randn(P, generator=g, device=DEV)
-        eps = float((2 * A / (kappa * P)) ** 0.5)
-        buf[K - 1, :P] = buf[K - 2, :P] + eps * z
+        lo, hi = math.log(1e-4 * s), math.log(10 * s)  # on log(eps): kappa ~ 1 / eps^2
+        for _ in range(60):
+            eps = math.exp(0.5 * (lo + hi))
+            buf[K - 1, :P] = buf[K - 2, :P] + eps * z
+            km = _kappa_max(buf[:, :P])
+            if abs(km - kappa) <= 0.03 * kappa:
+                break
+            lo, hi = (lo, math.log(eps)) if km < kappa else (math.log(eps), hi)
         return buf[:, :P]
     honest = buf[:3, :P].clone()
     lo, hi = 0.0, 20 * s
