@@ -1703,30 +1703,48 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
     }
     if (ch + 1 < c1) load(ch + 1);  // in flight during the MFMAs
     __syncthreads();
-    // D) the wave's 16x16 tiles over its groups of 32 coordinates of the chunk
+    // D) the wave's 16x16 tiles over its groups of 32 coordinates of the chunk, one code path per
+    // tile-set type (the operand registers of every MFMA fixed at compile time: no fragment copies)
+    // with the next group's fragments read before this group's MFMAs
+    auto tiles = [&](auto typc) {
+      constexpr int TYP = decltype(typc)::value;
+      constexpr int NB = TYP == 0 ? 2 : 3, NT3 = TYP == 2 ? 2 : 3;
+      constexpr int NG = kGE / 32 / C::R;
+      gbf8 f[NB][3], fn[NB][3];
+      auto rd = [&](gbf8 (&d)[NB][3], int G) {
 #pragma unroll
-    for (int gi = 0; gi < kGE / 32 / C::R; ++gi) {
-      const int G = r16 + gi * C::R;
-      gbf8 f[3][3];
+        for (int x = 0; x < NB; ++x)
 #pragma unroll
-      for (int x = 0; x < 3; ++x)
-        if (x < 2 || !dg)
+          for (int p = 0; p < 3; ++p) d[x][p] = *(const gbf8*)&planes[p * C::PLANE + ro[x] + 32 * G];
+      };
+      rd(f, r16);
 #pragma unroll
-          for (int p = 0; p < 3; ++p) f[x][p] = *(const gbf8*)&planes[p * C::PLANE + ro[x] + 32 * G];
+      for (int gi = 0; gi < NG; ++gi) {
+        if (gi + 1 < NG) rd(fn, r16 + (gi + 1) * C::R);
 #pragma unroll
-      for (int x = 0; x < 3; ++x) {
-        if (x == 2 && typ == 2) break;
-        const int pa = x == 2 ? 1 : 0, pb = dg ? (x == 0 ? 0 : 1) : (x == 0 ? 1 : 2);
-        gf4 acc = a16[x];
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][1], f[pb][1], acc, 0, 0, 0);  // M M
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][0], f[pb][2], acc, 0, 0, 0);  // H L
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][2], f[pb][0], acc, 0, 0, 0);  // L H
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][0], f[pb][1], acc, 0, 0, 0);  // H M
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][1], f[pb][0], acc, 0, 0, 0);  // M H
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][0], f[pb][0], acc, 0, 0, 0);  // H H
-        a16[x] = acc;
+        for (int x = 0; x < NT3; ++x) {
+          // type 0: (0,0), (0,1), (1,1); type 1: (0,1), (0,2), (1,2); type 2: (0,1), (0,2)
+          const int pa = x == 2 ? 1 : 0, pb = TYP == 0 ? (x == 0 ? 0 : 1) : (x == 0 ? 1 : 2);
+          gf4 acc = a16[x];
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][1], f[pb][1], acc, 0, 0, 0);  // M M
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][0], f[pb][2], acc, 0, 0, 0);  // H L
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][2], f[pb][0], acc, 0, 0, 0);  // L H
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][0], f[pb][1], acc, 0, 0, 0);  // H M
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][1], f[pb][0], acc, 0, 0, 0);  // M H
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][0], f[pb][0], acc, 0, 0, 0);  // H H
+          a16[x] = acc;
+        }
+        if (gi + 1 < NG) {
+#pragma unroll
+          for (int x = 0; x < NB; ++x)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) f[x][p] = fn[x][p];
+        }
       }
-    }
+    };
+    if (typ == 0) tiles(std::integral_constant<int, 0>{});
+    else if (KB == 4 || typ == 1) tiles(std::integral_constant<int, 1>{});
+    else tiles(std::integral_constant<int, 2>{});
     // float32 runs (256 coordinates of the chunks for K > 96, 64 per split for K <= 64) -> float64
     if ((ch - c0) % 2 == 1 || ch + 1 == c1) {
 #pragma unroll
@@ -2086,33 +2104,32 @@ int pairdist_direct(fa_ctx* ctx, int diff_dtype, int32_t num_segments, const int
                     const void* const* d_in, void* d_dist, void* d_scratch, size_t scratch_bytes, void* hip_stream,
                     const double* guard, double limit);
 
-// The Gram form's error model and the guard it sets (Krum; calibrated by
-// tools/krum_kappa_sweep.py, profiles/r06b).  A G entry is accumulated in float32 runs of n products,
-// p products per MFMA instruction (one rounding per instruction), and the runs are added in float64.
-// With random rounding the run sums' error is ~0.25 u n sqrt(P / p) t for P coordinates of mean term
-// t, i.e. sigma(A) / A ~ 0.25 u n / sqrt(p P) (u = 2^-24); D = A_i + A_j - 2 G_ij collects three such
-// errors, so sigma(D) / D ~ 0.30 kappa u n / sqrt(p P).  The guard keeps the Gram result only while
-// MARGIN sigma(D) / D <= 1e-6 (MARGIN = 6: the largest of 8,128 pairs sits near 4 sigma):
-//   kappa <= kGramKappaC sqrt(p P) / n,  kGramKappaC = 1e-6 / (6 x 0.30 x 2^-24) = 9.3.
-// Large models are unaffected (P = 11.7 M, K = 128: 108 > 16); small ones with long runs are handed
-// to the direct kernel at lower kappa (P = 7,850, K = 128: 6.4).
+// The Gram form's error model and the guard it sets (Krum; calibrated on the box by
+// tools/krum_kappa_sweep.py and tests/test_gpu_krum_band.py, profiles/r06b).  A G entry is accumulated
+// in float32 runs of n products and the runs are added in float64.  With one random rounding per
+// product (the MFMA's accumulator; the measured errors fit this, not one rounding per instruction)
+// the run sums' error is ~0.25 u n sqrt(P) t for P coordinates of mean term t, i.e. sigma(A) / A ~
+// 0.25 u n / sqrt(P) (u = 2^-24); D = A_i + A_j - 2 G_ij collects three such errors, so
+// sigma(D) / D ~ 0.30 kappa u n / sqrt(P).  Measured (r06b, forced Gram form, max over every pair):
+// K = 128, P = 1 M, kappa 15.8: 2.7e-7 = 3.8 sigma; K = 128, P = 11.7 M, kappa 1.29: 7e-9 = 4 sigma.
+// The guard keeps the Gram result only while MARGIN sigma(D) / D <= 1e-6 (MARGIN = 6):
+//   kappa <= kGramKappaC sqrt(P) / n,  kGramKappaC = 1e-6 / (6 x 0.30 x 2^-24) = 9.3.
+// Large models are unaffected (P = 11.7 M, K = 128: 124 > 16); small ones with long runs hand over to
+// the direct kernel at lower kappa (P = 7,850, K = 128: 3.2).
 struct GramRun {
-  int n, p;  // float32 products per run of one G entry, products per MFMA instruction
+  int n;  // float32 products per run of one G entry
 };
 GramRun gram_run(int kb, bool glds) {
-  if (glds) return {64, 4};  // k_pair_gram_ring: 16 products per chunk, flushed every 4 chunks
-  const bool s16 = (kb == 4 || kb == 2) && gram_s16();
+  if (glds) return {64};  // k_pair_gram_ring: 16 products per chunk, flushed every 4 chunks
   switch (kb) {
-    case 1: return {128, 2};                            // R = 4, FL = 4
-    case 2: return s16 ? GramRun{64, 4} : GramRun{64, 2};  // R = 4, FL = 2
-    case 3: return {128, 2};                            // R = 2, FL = 2
-    default: return s16 ? GramRun{256, 4} : GramRun{256, 2};  // R = 1, FL = 2
+    case 1: return {128};  // R = 4, FL = 4
+    case 2: return {64};   // R = 4, FL = 2 (the bf16x3 form: one 32-coordinate group per split, 2 chunks)
+    case 3: return {128};  // R = 2, FL = 2
+    default: return {256};  // R = 1, FL = 2 (either form)
   }
 }
 constexpr double kGramKappaC = 9.3;
-double gram_kappa_bound(int64_t p_total, GramRun r) {
-  return kGramKappaC * std::sqrt((double)r.p * (double)p_total) / r.n;
-}
+double gram_kappa_bound(int64_t p_total, GramRun r) { return kGramKappaC * std::sqrt((double)p_total) / r.n; }
 bool gram_vec(int32_t num_segments, const int64_t* seg_numel, int32_t k, const void* const* d_in) {
   bool vec = true;
   for (int s = 0; s < num_segments; ++s)

@@ -80,9 +80,10 @@ size_t fa_pairwise_sqdist_scratch_bytes(int32_t num_segments, const int64_t *seg
  * D_ij = A_i + A_j - 2 G_ij over y_i = x_i - c (c: the per-coordinate median of clients 0..4), G = Y Y^T
  * on the f32-input MFMA (k <= 32 with 16-byte aligned clients: v_mfma_f32_16x16x4_f32 over the three
  * upper 16x16 tiles, chunks streamed by LDS-DMA; otherwise v_mfma_f32_32x32x2_f32 over the upper
- * 32x32 tiles), float32 runs of n = 64-256 products (p = 2 or 4 per instruction) summed in float64.
+ * 32x32 tiles; k in (32, 64] or (96, 128] with FA_GRAM3=1: y split exactly into three bf16 parts on the
+ * bf16 MFMA), float32 runs of n = 64-256 products summed in float64.
  * Same d_dist layout (k x k float64, symmetric, zero diagonal).  The form cancels: its relative error
- * is ~ 0.30 kappa_ij u n / sqrt(p P) (one sigma, u = 2^-24, P = total coordinates), kappa_ij =
+ * is ~ 0.30 kappa_ij u n / sqrt(P) (one sigma, u = 2^-24, P = total coordinates), kappa_ij =
  * (A_i + A_j) / D_ij -- so it also writes kappa_max = max over pairs (one float64 at d_kappa_max; +inf
  * when some D_ij <= 0 or an input is not finite).  kappa_limit > 0: the direct kernels of
  * fa_pairwise_sqdist are queued behind it, guarded on the device -- they return at once when
@@ -97,8 +98,8 @@ int fa_pairwise_sqdist_gram(fa_ctx *ctx, int32_t num_segments, const int64_t *se
 size_t fa_pairwise_sqdist_gram_scratch_bytes(int32_t num_segments, const int64_t *seg_numel, int32_t k);
 /*
  * The kappa limit fa_pairwise_sqdist_gram's guard applies to this input: min(kappa_limit,
- * 9.3 sqrt(p P) / n) -- the largest kappa at which 6 sigma of the error model above stays <= 1e-6
- * relative (n, p of the kernel the call would run; d_in only for its 16-byte alignment).  0 for
+ * 9.3 sqrt(P) / n) -- the largest kappa at which 6 sigma of the error model above stays <= 1e-6
+ * relative (n of the kernel the call would run; d_in only for its 16-byte alignment).  0 for
  * invalid arguments or kappa_limit <= 0.  Host only, no device work.
  */
 double fa_pairwise_sqdist_gram_limit(int32_t num_segments, const int64_t *seg_numel, int32_t k,
