@@ -1583,6 +1583,7 @@ struct Gram3Cfg {
   static constexpr int KP = 32 * KB, QV = kGE / 4;
   static constexpr int W = KB == 4 ? 12 : 16, NT = W * 64;
   static constexpr int R = KB == 4 ? 1 : 4;                     // coordinate splits (groups of 32 per chunk / R)
+  static constexpr int FL = KB == 4 ? 1 : 2;                    // chunks per float32 run
   static constexpr int NLD = (KP * QV + NT - 1) / NT;           // staged 16-byte vectors per thread (6 / 2)
   static constexpr int PLANE = KP * kG3S;                       // bf16 per plane
   static constexpr size_t PLANE_BYTES = (size_t)3 * PLANE * 2;  // h, m, l
@@ -1745,8 +1746,10 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
     if (typ == 0) tiles(std::integral_constant<int, 0>{});
     else if (KB == 4 || typ == 1) tiles(std::integral_constant<int, 1>{});
     else tiles(std::integral_constant<int, 2>{});
-    // float32 runs (256 coordinates of the chunks for K > 96, 64 per split for K <= 64) -> float64
-    if ((ch - c0) % 2 == 1 || ch + 1 == c1) {
+    // float32 runs -> float64: every chunk for K > 96 (128 coordinates, 24 MFMAs per tile: the bf16
+    // MFMA's accumulation carries a small bias that grows with the run, profiles/r06b), every second
+    // chunk for K <= 64 (64 coordinates of the split, 12 MFMAs)
+    if (C::FL == 1 || (ch - c0) % C::FL == C::FL - 1 || ch + 1 == c1) {
 #pragma unroll
       for (int x = 0; x < 3; ++x)
 #pragma unroll
@@ -2113,23 +2116,31 @@ int pairdist_direct(fa_ctx* ctx, int diff_dtype, int32_t num_segments, const int
 // sigma(D) / D ~ 0.30 kappa u n / sqrt(P).  Measured (r06b, forced Gram form, max over every pair):
 // K = 128, P = 1 M, kappa 15.8: 2.7e-7 = 3.8 sigma; K = 128, P = 11.7 M, kappa 1.29: 7e-9 = 4 sigma.
 // The guard keeps the Gram result only while MARGIN sigma(D) / D <= 1e-6 (MARGIN = 6):
-//   kappa <= kGramKappaC sqrt(P) / n,  kGramKappaC = 1e-6 / (6 x 0.30 x 2^-24) = 9.3.
+//   kappa <= 1e-6 / (6 x 0.30 x 2^-24 x n / sqrt(P)) = 9.3 sqrt(P) / n.
 // Large models are unaffected (P = 11.7 M, K = 128: 124 > 16); small ones with long runs hand over to
 // the direct kernel at lower kappa (P = 7,850, K = 128: 3.2).
+// The bf16x3 split forms (k_pair_gram3) add a size-independent part: their measured error per unit
+// kappa levels off with P (r06b sweep, max over every pair: K in (96, 128] 5.4e-8 with 2-chunk runs,
+// K in (32, 64] 7.4e-9) -- a bias of the bf16 MFMA's float32 accumulation that grows with the run --
+// so their bound is kappa (6 sigma(P) + b) <= 1e-6 with b about 1.5x the measured level.
 struct GramRun {
-  int n;  // float32 products per run of one G entry
+  int n;     // float32 products per run of one G entry
+  double b;  // size-independent relative error per unit kappa (0 for the f32-input forms)
 };
 GramRun gram_run(int kb, bool glds) {
-  if (glds) return {64};  // k_pair_gram_ring: 16 products per chunk, flushed every 4 chunks
+  if (glds) return {64, 0.0};  // k_pair_gram_ring: 16 products per chunk, flushed every 4 chunks
+  const bool g3 = (kb == 2 || kb == 4) && gram3();
   switch (kb) {
-    case 1: return {128};  // R = 4, FL = 4
-    case 2: return {64};   // R = 4, FL = 2 (the bf16x3 form: one 32-coordinate group per split, 2 chunks)
-    case 3: return {128};  // R = 2, FL = 2
-    default: return {256};  // R = 1, FL = 2 (either form)
+    case 1: return {128, 0.0};                        // R = 4, FL = 4
+    case 2: return {64, g3 ? 1.2e-8 : 0.0};           // R = 4, FL = 2 (bf16x3: one 32-coordinate group per split)
+    case 3: return {128, 0.0};                        // R = 2, FL = 2
+    default: return g3 ? GramRun{128, 6e-8} : GramRun{256, 0.0};  // bf16x3: FL = 1; f32: R = 1, FL = 2
   }
 }
-constexpr double kGramKappaC = 9.3;
-double gram_kappa_bound(int64_t p_total, GramRun r) { return kGramKappaC * std::sqrt((double)p_total) / r.n; }
+constexpr double kGramSigma = 0.30 * 5.9604644775390625e-8;  // sigma(D) / D per unit kappa x sqrt(P) / n
+double gram_kappa_bound(int64_t p_total, GramRun r) {
+  return 1e-6 / (6.0 * kGramSigma * r.n / std::sqrt((double)std::max<int64_t>(p_total, 1)) + r.b);
+}
 bool gram_vec(int32_t num_segments, const int64_t* seg_numel, int32_t k, const void* const* d_in) {
   bool vec = true;
   for (int s = 0; s < num_segments; ++s)

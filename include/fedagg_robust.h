@@ -98,8 +98,9 @@ int fa_pairwise_sqdist_gram(fa_ctx *ctx, int32_t num_segments, const int64_t *se
 size_t fa_pairwise_sqdist_gram_scratch_bytes(int32_t num_segments, const int64_t *seg_numel, int32_t k);
 /*
  * The kappa limit fa_pairwise_sqdist_gram's guard applies to this input: min(kappa_limit,
- * 9.3 sqrt(P) / n) -- the largest kappa at which 6 sigma of the error model above stays <= 1e-6
- * relative (n of the kernel the call would run; d_in only for its 16-byte alignment).  0 for
+ * 1e-6 / (6 x 0.30 u n / sqrt(P) + b)) -- the largest kappa at which 6 sigma of the error model above
+ * (plus, for the bf16x3 forms, a measured size-independent part b) stays <= 1e-6 relative (n, b of the
+ * kernel the call would run; d_in only for its 16-byte alignment).  0 for
  * invalid arguments or kappa_limit <= 0.  Host only, no device work.
  */
 double fa_pairwise_sqdist_gram_limit(int32_t num_segments, const int64_t *seg_numel, int32_t k,
