@@ -2057,10 +2057,10 @@ bool gram_s16() {  // K in (32, 64] and (96, 128]: the 16x16 forms (FA_GRAM16=0:
   return on;
 }
 
-bool gram3() {  // K in (96, 128]: the bf16x3 split form (FA_GRAM3=1; default: the f32-input 16x16 form)
+bool gram3() {  // K in (32, 64] and (96, 128]: the bf16x3 split form (FA_GRAM3=0: the f32-input 16x16 forms, A/B)
   static const bool on = [] {
     const char* e = getenv("FA_GRAM3");
-    return e && e[0] == '1';
+    return !(e && e[0] == '0');
   }();
   return on;
 }
@@ -2120,9 +2120,10 @@ int pairdist_direct(fa_ctx* ctx, int diff_dtype, int32_t num_segments, const int
 // Large models are unaffected (P = 11.7 M, K = 128: 124 > 16); small ones with long runs hand over to
 // the direct kernel at lower kappa (P = 7,850, K = 128: 3.2).
 // The bf16x3 split forms (k_pair_gram3) add a size-independent part: their measured error per unit
-// kappa levels off with P (r06b sweep, max over every pair: K in (96, 128] 5.4e-8 with 2-chunk runs,
-// K in (32, 64] 7.4e-9) -- a bias of the bf16 MFMA's float32 accumulation that grows with the run --
-// so their bound is kappa (6 sigma(P) + b) <= 1e-6 with b about 1.5x the measured level.
+// kappa levels off with P (max over every pair, P >= 1 M: K in (96, 128] 5.4e-8 with 2-chunk runs
+// (profiles/r06b), 2.1e-8 with 1-chunk runs (r06d); K in (32, 64] 7.4e-9) -- a bias of the bf16 MFMA's
+// float32 accumulation that grows with the run -- so their bound is kappa (6 sigma(P) + b) <= 1e-6
+// with b = 4e-8 / 1.2e-8, 1.9x / 1.6x the measured level.
 struct GramRun {
   int n;     // float32 products per run of one G entry
   double b;  // size-independent relative error per unit kappa (0 for the f32-input forms)
@@ -2134,7 +2135,7 @@ GramRun gram_run(int kb, bool glds) {
     case 1: return {128, 0.0};                        // R = 4, FL = 4
     case 2: return {64, g3 ? 1.2e-8 : 0.0};           // R = 4, FL = 2 (bf16x3: one 32-coordinate group per split)
     case 3: return {128, 0.0};                        // R = 2, FL = 2
-    default: return g3 ? GramRun{128, 6e-8} : GramRun{256, 0.0};  // bf16x3: FL = 1; f32: R = 1, FL = 2
+    default: return g3 ? GramRun{128, 4e-8} : GramRun{256, 0.0};  // bf16x3: FL = 1; f32: R = 1, FL = 2
   }
 }
 constexpr double kGramSigma = 0.30 * 5.9604644775390625e-8;  // sigma(D) / D per unit kappa x sqrt(P) / n
