@@ -6,6 +6,8 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r06c; mkdir -p $O
 export TMPDIR=/tmp
 line() { python -c "import json,sys;d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]);r=d.get('roofline') or {};c=d.get('cold') or {};print(sys.argv[1].split('/')[-1],d['value'],d['unit'],d['ms_per_step'],r.get('kernel_avg_ms'),r.get('frac'),r.get('frac_of_ceiling'),'cold',c.get('ms'),c.get('event_ms'),d.get('pair_form'),str(d.get('parity'))[:60])" $1; }
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_krum_band.py tests/test_gpu_robust.py -k "band or pairwise or krum or sticky" > $O/tests_krum.log 2>&1; rc=$?
+tail -2 $O/tests_krum.log; [ $rc = 0 ] || exit $rc
 run() {  # name, bench args
   n=$1; shift
   timeout -k 10 400 python bench.py "$@" --no-cpu-baseline --soak-seconds 0 > $O/$n.json 2> $O/$n.err || { tail -5 $O/$n.err; exit 1; }
