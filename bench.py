@@ -65,8 +65,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=None,
-                   help="untimed warmup steps (default: 3, and on one GPU as many more as make ~0.2 s of the "
-                        "workload's own steps -- short steps otherwise run on the clock ramp, DESIGN §0.2 3b)")
+                   help="untimed warmup steps (default: 3, and on one GPU as many more as make ~1 s of the "
+                        "workload's own steps -- short steps otherwise run on the clock ramp, DESIGN A.2 3b)")
     p.add_argument("--config", default="metric",
                    choices=["metric", "fragmented", "resnet18", "vit_bf16", "hier", "gossip", "host", "secagg", "fedopt",
                             "dropin_cpu", "median",
@@ -2015,13 +2015,14 @@ def main():
         wl["step"]()
     sync()
     if auto_warmup and world == 1 and not wl.get("latency"):
-        # the chip raises its clock over the first ~10-50 ms of sustained work (r05t): keep warming up
-        # until ~0.2 s of this workload's own steps have run
+        # the chip raises its clock over the first part of sustained work (r05t): keep warming up until
+        # ~1 s of this workload's own steps have run (r06c: median K = 128 still ran 1.18 ms per step
+        # after 0.2 s of them, 0.98 ms over a 3 s soak)
         t_w = time.perf_counter()
         wl["step"]()
         sync()
         one = max(time.perf_counter() - t_w, 1e-6)
-        extra = min(2000, int(0.2 / one))
+        extra = min(5000, int(1.0 / one))
         for i in range(extra):
             stage(f"warmup step {args.warmup + 1 + i}")
             wl["step"]()

@@ -1793,205 +1793,6 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
   (void)ntile;
 }
 
-// K in (96, 128], bf16x3 split form, pipelined (r06, FA_GRAM3=2): 64-coordinate chunks with the planes
-// double-buffered, so that the split of chunk ch + 1 and the MFMAs of chunk ch share ONE barrier
-// interval -- with 3 waves per SIMD one wave's split VALU issues beside another's MFMAs, where
-// k_pair_gram3 runs them in separate phases (barrier, split, barrier, MFMAs).  Per chunk: the staged
-// rows 0..4 of chunk ch + 1 to LDS; barrier; every wave the centre of ch + 1 (its own row) and its
-// share of the split of ch + 1 into the other plane buffer, then the loads of ch + 2; the MFMAs of ch.
-constexpr int kGP = 64;          // coordinates per chunk
-constexpr int kGPS = kGP + 8;    // bf16 per plane row: 144-byte rows (9 x 16 B), 16-lane b128 reads conflict-free
-struct Gram3PCfg {
-  static constexpr int KP = 128, QV = kGP / 4, W = 12, NT = W * 64;
-  static constexpr int NLD = (KP * QV + NT - 1) / NT;          // 3
-  static constexpr int PLANE = KP * kGPS;                       // bf16 per plane
-  static constexpr size_t BUF_BYTES = (size_t)3 * PLANE * 2;   // h, m, l of one chunk
-  static constexpr size_t LDS = 2 * BUF_BYTES + sizeof(float) * (2 * 5 * kGP + W * kGP);
-};
-
-template <bool VEC>
-__global__ void __launch_bounds__(Gram3PCfg::NT) __attribute__((amdgpu_waves_per_eu(3)))
-k_pair_gram3p(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k,
-              int64_t nchunks, double* __restrict__ partial, unsigned* __restrict__ ctr) {
-  using C = Gram3PCfg;
-  constexpr int QV = C::QV, KB = 4;
-  if (blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;  // k_gram_reduce's arrival counter
-  extern __shared__ __attribute__((aligned(16))) char g3[];
-  __bf16* const planes = (__bf16*)g3;                    // [2][3][PLANE]
-  float* const c5 = (float*)(g3 + 2 * C::BUF_BYTES);     // [2][5][kGP] raw rows 0..4
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  float* const crow = c5 + 2 * 5 * kGP + w * kGP;        // this wave's centre row
-  const int li = lane & 15, kk = lane >> 4;
-  const bool dg = w < 4;
-  int blk[3], ro[3];
-#pragma unroll
-  for (int x = 0; x < 3; ++x) {
-    blk[x] = kG16Blocks[w][x];
-    ro[x] = (16 * blk[x] + li) * kGPS + 8 * kk;
-  }
-  gf4 a16[3];
-  double accd[12];
-#pragma unroll
-  for (int x = 0; x < 3; ++x) a16[x] = gf4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int q = 0; q < 12; ++q) accd[q] = 0.0;
-  gf4 v[C::NLD];
-  const float* src[C::NLD];
-  int cseg = -1;
-  auto load = [&](int64_t ch) {
-    const int si = nseg > 1 ? find_seg(segs, nseg, ch) : 0;
-    const PSeg sg = segs[si];
-    if (si != cseg) {
-      cseg = si;
-#pragma unroll
-      for (int u = 0; u < C::NLD; ++u) {
-        const int idx = t + u * C::NT;
-        const int cl = idx / QV;
-        src[u] = idx < C::KP * QV && cl < k ? (const float*)ptrs[sg.ptr_base + cl] + 4 * (idx % QV) : nullptr;
-      }
-    }
-    const int64_t b0 = (ch - sg.tile_start) * kGP;
-    if (VEC && b0 + kGP <= sg.numel) {
-#pragma unroll
-      for (int u = 0; u < C::NLD; ++u) {
-        const gf4 z = {0.f, 0.f, 0.f, 0.f};
-        v[u] = src[u] ? *(const __attribute__((address_space(1))) gf4*)(src[u] + b0) : z;
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < C::NLD; ++u) {
-        const int idx = t + u * C::NT;
-        gf4 x = {0.f, 0.f, 0.f, 0.f};
-        if (src[u]) {
-          const int64_t left = sg.numel - (b0 + 4 * (idx % QV));
-#pragma unroll
-          for (int z = 0; z < 4; ++z) if (z < left) x[z] = gld<float>(src[u] + b0, z);
-        }
-        v[u] = x;
-      }
-    }
-  };
-  auto rows05 = [&](int b) {  // rows 0..4 of the staged chunk (threads 0..79, first vector) to c5[b]
-    if (t < 5 * QV) *(gf4*)&c5[b * 5 * kGP + (t / QV) * kGP + 4 * (t % QV)] = v[0];
-  };
-  auto split = [&](int b) {  // centre of the staged chunk (from c5[b]) and its split into plane buffer b
-    if (lane < QV) {
-      const float* r = c5 + b * 5 * kGP + 4 * lane;
-      const gf4 a = *(const gf4*)r, bb = *(const gf4*)(r + kGP), c = *(const gf4*)(r + 2 * kGP),
-                 d = *(const gf4*)(r + 3 * kGP), f = *(const gf4*)(r + 4 * kGP);
-      gf4 m;
-#pragma unroll
-      for (int z = 0; z < 4; ++z)
-        m[z] = __builtin_amdgcn_fmed3f(f[z], fmaxf(fminf(a[z], bb[z]), fminf(c[z], d[z])),
-                                       fminf(fmaxf(a[z], bb[z]), fmaxf(c[z], d[z])));
-      *(gf4*)&crow[4 * lane] = m;
-    }
-    __builtin_amdgcn_wave_barrier();
-    __bf16* const pb = planes + b * 3 * C::PLANE;
-#pragma unroll
-    for (int u = 0; u < C::NLD; ++u) {
-      const int idx = t + u * C::NT;
-      if (C::NLD * C::NT == C::KP * QV || idx < C::KP * QV) {
-        const int cl = idx / QV, q = idx % QV;
-        const gf4 y = v[u] - *(const gf4*)&crow[4 * q];
-        gbf4 h, m, l;
-#pragma unroll
-        for (int z = 0; z < 4; ++z) {
-          h[z] = (__bf16)y[z];
-          const float r = y[z] - bf_f(h[z]);
-          m[z] = (__bf16)r;
-          l[z] = (__bf16)(r - bf_f(m[z]));
-        }
-        __bf16* const row = pb + cl * kGPS + 4 * q;
-        *(gbf4*)row = h;
-        *(gbf4*)(row + C::PLANE) = m;
-        *(gbf4*)(row + 2 * C::PLANE) = l;
-      }
-    }
-  };
-  auto tiles = [&](auto typc, const __bf16* pb) {  // the wave's tiles over the chunk's 2 groups of 32
-    constexpr int TYP = decltype(typc)::value;
-    constexpr int NB = TYP == 0 ? 2 : 3;
-    gbf8 f[NB][3], fn[NB][3];
-    auto rd = [&](gbf8 (&d)[NB][3], int G) {
-#pragma unroll
-      for (int x = 0; x < NB; ++x)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) d[x][p] = *(const gbf8*)&pb[p * C::PLANE + ro[x] + 32 * G];
-    };
-    rd(f, 0);
-    rd(fn, 1);
-#pragma unroll
-    for (int G = 0; G < kGP / 32; ++G) {
-#pragma unroll
-      for (int x = 0; x < 3; ++x) {
-        const int pa = x == 2 ? 1 : 0, pbk = TYP == 0 ? (x == 0 ? 0 : 1) : (x == 0 ? 1 : 2);
-        gf4 acc = a16[x];
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][1], f[pbk][1], acc, 0, 0, 0);  // M M
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][0], f[pbk][2], acc, 0, 0, 0);  // H L
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][2], f[pbk][0], acc, 0, 0, 0);  // L H
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][0], f[pbk][1], acc, 0, 0, 0);  // H M
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][1], f[pbk][0], acc, 0, 0, 0);  // M H
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[pa][0], f[pbk][0], acc, 0, 0, 0);  // H H
-        a16[x] = acc;
-      }
-      if (G == 0) {
-#pragma unroll
-        for (int x = 0; x < NB; ++x)
-#pragma unroll
-          for (int p = 0; p < 3; ++p) f[x][p] = fn[x][p];
-      }
-    }
-  };
-  const int64_t c0 = nchunks * blockIdx.x / gridDim.x, c1 = nchunks * (blockIdx.x + 1) / gridDim.x;
-  if (c0 < c1) {
-    load(c0);
-    rows05(0);
-    __syncthreads();
-    split(0);
-    if (c0 + 1 < c1) load(c0 + 1);
-  }
-  for (int64_t ch = c0; ch < c1; ++ch) {
-    const int b = (int)((ch - c0) & 1);
-    if (ch + 1 < c1) rows05(b ^ 1);
-    __syncthreads();  // planes[b] complete; planes[b ^ 1] and c5[b ^ 1]'s last readers done; c5[b ^ 1] written
-    if (ch + 1 < c1) {
-      split(b ^ 1);
-      if (ch + 2 < c1) load(ch + 2);  // in flight during this chunk's MFMAs and the next split
-    }
-    const __bf16* pb = planes + b * 3 * C::PLANE;
-    if (dg) tiles(std::integral_constant<int, 0>{}, pb);
-    else tiles(std::integral_constant<int, 1>{}, pb);
-    // float32 runs of 2 chunks (128 coordinates, 24 MFMAs per tile, as k_pair_gram3's) -> float64
-    if ((ch - c0) % 2 == 1 || ch + 1 == c1) {
-#pragma unroll
-      for (int x = 0; x < 3; ++x)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          accd[4 * x + q] += (double)a16[x][q];
-          a16[x][q] = 0.0f;
-        }
-    }
-  }
-  double* o = partial + (int64_t)blockIdx.x * gram_T_c<KB>() * 1024;
-#pragma unroll
-  for (int x = 0; x < 3; ++x) {
-    const int pa = x == 2 ? 1 : 0, pbk = dg ? (x == 0 ? 0 : 1) : (x == 0 ? 1 : 2);
-    const int A = blk[pa], Bk = blk[pbk];
-    const int I = A >> 1, J = Bk >> 1;
-    const int t32 = I * KB - I * (I - 1) / 2 + (J - I);
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      o[(int64_t)t32 * 1024 + (16 * (A & 1) + 4 * kk + q) * 32 + 16 * (Bk & 1) + li] = accd[4 * x + q];
-  }
-  if (dg) {
-    const int I = blk[0] >> 1, t32 = I * KB - I * (I - 1) / 2;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) o[(int64_t)t32 * 1024 + (16 + 4 * kk + q) * 32 + li] = 0.0;
-  }
-}
-
 // K <= 32 with an LDS-DMA ring (r05).  The register-staged kernel above waits vmcnt(0) for its one
 // chunk in flight at every put (the compiler cannot count a ring of register loads across the loop:
 // r05k, depths 2-4 all slower), and its time splits (r05o, measurement knobs on a first 4-wave ring
@@ -2256,14 +2057,13 @@ bool gram_s16() {  // K in (32, 64] and (96, 128]: the 16x16 forms (FA_GRAM16=0:
   return on;
 }
 
-int gram3_mode() {  // FA_GRAM3: 0 the f32-input 16x16 forms, 1 (default) k_pair_gram3, 2 k_pair_gram3p for K > 96 (A/B)
-  static const int m = [] {
+bool gram3() {  // K in (32, 64] and (96, 128]: the bf16x3 split form (FA_GRAM3=0: the f32-input 16x16 forms, A/B)
+  static const bool on = [] {
     const char* e = getenv("FA_GRAM3");
-    return e && e[0] == '0' ? 0 : e && e[0] == '2' ? 2 : 1;
+    return !(e && e[0] == '0');
   }();
-  return m;
+  return on;
 }
-bool gram3() { return gram3_mode() != 0; }  // K in (32, 64] and (96, 128]: the bf16x3 split form
 
 int gram_glds() {  // K <= 32: the LDS-DMA ring kernel (FA_GRAM_GLDS=0: the register-staged k_pair_gram<1>, A/B)
   static const int d = [] {
@@ -2548,10 +2348,6 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
   if (rc) return rc;
   PSeg* hs = (PSeg*)slot->host;
   const void** hp = (const void**)((char*)slot->host + seg_bytes);
-  // k_pair_gram3p (K > 96, FA_GRAM3=2) walks 64-coordinate chunks; the workgroup count stays the
-  // 128-coordinate one the scratch was sized for
-  const bool g3p = kbc == 4 && gram3_mode() == 2;
-  const int csk = g3p ? kGP : cs;
   int j = 0;
   int64_t c0 = 0;
   for (int s = 0; s < num_segments; ++s) {
@@ -2559,7 +2355,7 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
     if (n == 0) continue;
     for (int i = 0; i < k; ++i) hp[(int64_t)j * k + i] = d_in[(int64_t)s * k + i];
     hs[j] = PSeg{n, c0, j * k, glds && n % cs ? 1 : 0, 0};
-    c0 += glds ? n / cs : (n + csk - 1) / csk;
+    c0 += glds ? n / cs : (n + cs - 1) / cs;
     ++j;
   }
   rc = stage(slot, seg_bytes + ptr_bytes, st, true);
@@ -2613,16 +2409,7 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
       break;
     case 3: FA_GR(3, false); break;
     default:
-      if (g3p) {  // the bf16x3 split form, pipelined (K in (96, 128], FA_GRAM3=2)
-        if (vec)
-          hipLaunchKernelGGL((k_pair_gram3p<true>), dim3((unsigned)nblocks), dim3(Gram3PCfg::NT), Gram3PCfg::LDS, st,
-                             sg, nseg, pp, k, c0, part, ctr);
-        else
-          hipLaunchKernelGGL((k_pair_gram3p<false>), dim3((unsigned)nblocks), dim3(Gram3PCfg::NT), Gram3PCfg::LDS, st,
-                             sg, nseg, pp, k, c0, part, ctr);
-        hipLaunchKernelGGL((k_gram_reduce<4>), dim3((unsigned)ntr), dim3(64 * kGRW), 0, st, (const double*)part,
-                           nblocks, gm, k, (double*)d_dist, (double*)d_kappa_max, ctr);
-      } else if (gram3()) {  // the bf16x3 split form (K in (96, 128])
+      if (gram3()) {  // the bf16x3 split form (K in (96, 128])
         FA_GR3(4);
       } else if (gram_s16()) {
         FA_GR(4, true);
