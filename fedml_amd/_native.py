@@ -17,7 +17,8 @@ import threading
 import torch  # noqa: F401  (load torch's HIP runtime before libfedagg.so)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libfedagg.so")
+# FEDML_AMD_LIB: another build of the same ABI (interleaved A/B measurements of a kernel change only)
+LIB_PATH = os.environ.get("FEDML_AMD_LIB") or os.path.join(HERE, "libfedagg.so")
 ABI_VERSION = 3
 TILE_BYTES = 4096  # FA_TILE_BYTES
 

@@ -359,7 +359,16 @@ __device__ __forceinline__ void wsum_tile(const Seg* __restrict__ segs, int nseg
         B::template consume<true>(acc, ra, coef, i0, k, d);
       }
     } else {
-      for (int i0 = 0; i0 < k; i0 += U) {
+      // whole groups unguarded: a guarded consume (a wave-uniform branch per client) let hipcc sink
+      // the group's second load into its branch, issued only after the first client's arithmetic and
+      // waited for with vmcnt(0) -- one serialized memory round trip per group of U clients (r06)
+      int i0 = 0;
+      for (; i0 + U <= k; i0 += U) {
+        u32x4 r[U][S];
+        B::load(r, in, i0, k, boff, sst);
+        B::template consume<false>(acc, r, coef, i0, k, d);
+      }
+      if (i0 < k) {
         u32x4 r[U][S];
         B::load(r, in, i0, k, boff, sst);
         B::template consume<true>(acc, r, coef, i0, k, d);
@@ -534,7 +543,13 @@ k_wsum_grouped(const Seg* __restrict__ segs, const double* __restrict__ coef,
       A acc[1][V];
 #pragma unroll
       for (int v = 0; v < V; ++v) acc[0][v] = T::zero();
-      for (int i0 = gd.begin; i0 < gd.end; i0 += U) {
+      int i0 = gd.begin;
+      for (; i0 + U <= gd.end; i0 += U) {  // whole groups unguarded (see wsum_tile)
+        u32x4 r[U][1];
+        B::load(r, in, i0, gd.end, boff, sst);
+        B::template consume<false>(acc, r, coef, i0, gd.end, d);
+      }
+      if (i0 < gd.end) {
         u32x4 r[U][1];
         B::load(r, in, i0, gd.end, boff, sst);
         B::template consume<true>(acc, r, coef, i0, gd.end, d);
