@@ -653,7 +653,13 @@ __device__ __forceinline__ void fedavg_sgd_tile(const Seg* __restrict__ segs, in
     float acc[1][V];
 #pragma unroll
     for (int v = 0; v < V; ++v) acc[0][v] = -0.0f;
-    for (int i0 = 0; i0 < k; i0 += U) {
+    int i0 = 0;
+    for (; i0 + U <= k; i0 += U) {  // whole groups unguarded (see wsum_tile)
+      u32x4 r[U][1];
+      B::load(r, in, i0, k, boff, sst);
+      B::template consume<false>(acc, r, coef, i0, k, d);
+    }
+    if (i0 < k) {
       u32x4 r[U][1];
       B::load(r, in, i0, k, boff, sst);
       B::template consume<true>(acc, r, coef, i0, k, d);

@@ -1,7 +1,8 @@
 # r06g: whole client groups unguarded in wsum_tile / k_wsum_grouped (r06: the guarded consume let hipcc
 # sink each group's second load behind the first client's arithmetic with a vmcnt(0)).  The -m gpu
 # parity tests of the weighted-sum family on the new build, then interleaved A/B against the previous
-# build (fedml_amd/ab/libfedagg_prev.so via FEDML_AMD_LIB): the metric line x3 pairs, cfg4 hier x3.
+# build (fedml_amd/ab/libfedagg_prev.so via FEDML_AMD_LIB): the metric line x3 pairs, cfg4 hier x3, FedOpt and
+# LightSecAgg (the same fix in k_fedavg_sgd and k_finite_sum) x2.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r06g; mkdir -p $O
 export TMPDIR=/tmp
@@ -15,6 +16,12 @@ for i in 1 2 3; do
     line $O/metric_${v}_$i.json
     timeout -k 10 300 python bench.py --config hier --no-cpu-baseline --soak-seconds 0 --cold-reps 0 > $O/hier_${v}_$i.json 2> $O/hier_${v}_$i.err || { tail -5 $O/hier_${v}_$i.err; exit 1; }
     line $O/hier_${v}_$i.json
+    if [ $i -le 2 ]; then
+      for c in fedopt secagg; do
+        timeout -k 10 300 python bench.py --config $c --no-cpu-baseline --soak-seconds 0 --cold-reps 0 > $O/${c}_${v}_$i.json 2> $O/${c}_${v}_$i.err || { tail -5 $O/${c}_${v}_$i.err; exit 1; }
+        line $O/${c}_${v}_$i.json
+      done
+    fi
   done
 done
 unset FEDML_AMD_LIB
