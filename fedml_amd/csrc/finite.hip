@@ -163,17 +163,7 @@ k_finite_sum(const FSeg* __restrict__ segs, int nseg, const void* const* __restr
     long long a0 = 0, a1 = 0;
     // the mask is needed only at the end: issue its load first, it lands while the clients stream
     const u32x4 mk = sg.mask ? __builtin_nontemporal_load((gp_u32x4)(sg.mask + e0)) : u32x4{0, 0, 0, 0};
-    // client 0 starts the sums; then whole groups of kU clients unguarded (a per-client wave-uniform
-    // branch let hipcc sink a group's loads behind its arithmetic, r06 -- see fedagg.hip wsum_tile),
-    // and a guarded last group.  Same per-element order: client 0, 1, ..., k - 1.
-    {
-      const u32x4 r0 = __builtin_nontemporal_load((gp_u32x4)((const char*)in[0] + boff));
-      const long long x0 = lo64(r0), x1 = hi64(r0);
-      a0 = first ? mod_any(x0, m) : x0;
-      a1 = first ? mod_any(x1, m) : x1;
-    }
-    auto group = [&](int i0, auto guardc) {
-      constexpr bool GUARD = decltype(guardc)::value;
+    for (int i0 = 0; i0 < k; i0 += kU) {
       u32x4 r[kU];
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
@@ -182,15 +172,19 @@ k_finite_sum(const FSeg* __restrict__ segs, int nseg, const void* const* __restr
       }
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
-        if (!GUARD || i0 + u < k) {  // wave-uniform
-          a0 = step<EACH>(a0, lo64(r[u]), m);
-          a1 = step<EACH>(a1, hi64(r[u]), m);
+        const int i = i0 + u;
+        if (i < k) {  // wave-uniform
+          const long long x0 = lo64(r[u]), x1 = hi64(r[u]);
+          if (i == 0) {
+            a0 = first ? mod_any(x0, m) : x0;
+            a1 = first ? mod_any(x1, m) : x1;
+          } else {
+            a0 = step<EACH>(a0, x0, m);
+            a1 = step<EACH>(a1, x1, m);
+          }
         }
       }
-    };
-    int i0 = 1;
-    for (; i0 + kU <= k; i0 += kU) group(i0, std::false_type{});
-    if (i0 < k) group(i0, std::true_type{});
+    }
     finish(a0, sg.mask != nullptr, lo64(mk), flags, m);
     finish(a1, sg.mask != nullptr, hi64(mk), flags, m);
     if (sg.out_fin) __builtin_nontemporal_store(pack64(a0, a1), (gpw_u32x4)(sg.out_fin + e0));
