@@ -847,15 +847,12 @@ k_mix_band(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict
     u32x4 win[RG + 2];  // win[s] = input (r0 + off - 1 + s) mod num_in
     win[0] = ld16<NT>((const char*)in[wrap(off - 1)] + boff);
     win[1] = ld16<NT>((const char*)in[wrap(off)] + boff);
-    // whole groups of RG rows unguarded, then a guarded last group (a per-row wave-uniform guard lets
-    // hipcc sink a group's window loads into the branches, r06 -- see wsum_tile)
-    auto group = [&](int r0, auto guardc) {
-      constexpr bool GUARD = decltype(guardc)::value;
+    for (int r0 = 0; r0 < nrows; r0 += RG) {
 #pragma unroll
       for (int g = 0; g < RG; ++g) win[2 + g] = ld16<NT>((const char*)in[wrap(r0 + off + 1 + g)] + boff);
 #pragma unroll
       for (int g = 0; g < RG; ++g) {
-        if (!GUARD || r0 + g < nrows) {  // wave-uniform
+        if (r0 + g < nrows) {  // wave-uniform
           const MixRow row = rows[r0 + g];
           float acc[V];
 #pragma unroll
@@ -882,10 +879,7 @@ k_mix_band(const MixRow* __restrict__ rows, int nrows, const int32_t* __restrict
       }
       win[0] = win[RG];
       win[1] = win[RG + 1];
-    };
-    int r0 = 0;
-    for (; r0 + RG <= nrows; r0 += RG) group(r0, std::false_type{});
-    if (r0 < nrows) group(r0, std::true_type{});
+    }
   } else {
     const int64_t end = min(base + TILE, n);
     for (int r = 0; r < nrows; ++r) {
