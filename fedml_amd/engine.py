@@ -1009,10 +1009,19 @@ class AggEngine:
             if form == "auto":  # kappa_max to pinned host memory, read by the next call of this shape
                 memo = self.__dict__.setdefault("_gram_memo", {})
                 m = memo.get(key) or {"km": torch.zeros(1, dtype=torch.float64, pin_memory=True), "skips": 0,
-                                      "ev": torch.cuda.Event()}
+                                      "ev": torch.cuda.Event(), "done": torch.cuda.Event()}
                 s = stream if stream is not None else torch.cuda.current_stream(self.device)
-                m["km"].copy_(km, non_blocking=True)
-                m["ev"].record(s)
+                # the 8-byte copy runs on a side stream behind this call, off the caller's stream (a
+                # blit kernel there put ~4 us between this call and the next one, r06c)
+                side = self.__dict__.get("_memo_stream")
+                if side is None:
+                    side = self._memo_stream = torch.cuda.Stream(self.device)
+                m["done"].record(s)
+                side.wait_event(m["done"])
+                with torch.cuda.stream(side):
+                    m["km"].copy_(km, non_blocking=True)
+                km.record_stream(side)
+                m["ev"].record(side)
                 m["limit"], m["skips"] = limit, 0
                 memo[key] = m
             return d
