@@ -1294,6 +1294,11 @@ __constant__ const int8_t kG16Blocks[12][3] = {{0, 1, 1}, {2, 3, 3}, {4, 5, 5}, 
 // coordinate splits; wave w runs set (w % 4 + w / 4) % 4, split w / 4, so every SIMD (w % 4) holds
 // two 3-tile and two 2-tile waves.  Row: {type (0 diagonal pair, 2 cross pair), block 0, 1, 2}.
 __constant__ const int8_t kG16Sets2[4][4] = {{0, 0, 1, 1}, {0, 2, 3, 3}, {2, 0, 2, 3}, {2, 1, 2, 3}};
+// K in (64, 96] (bf16x3 form, r06): the 6 client blocks of 16 as 7 sets of 3 tiles -- the diagonal pairs
+// {0, 1}, {2, 3}, {4, 5} and the 4 triangles of K_{2,2,2} (one block of each pair) that cover the 12
+// cross pairs once; wave w runs set w over the whole chunk.  Row: {type, block 0, 1, 2}.
+__constant__ const int8_t kG16Sets3[7][4] = {{0, 0, 1, 1}, {0, 2, 3, 3}, {0, 4, 5, 5}, {1, 0, 2, 4},
+                                             {1, 0, 3, 5}, {1, 1, 2, 5}, {1, 1, 3, 4}};
 
 template <int KB>
 __host__ __device__ constexpr int gram_T_c() { return KB * (KB + 1) / 2; }
@@ -1579,12 +1584,13 @@ typedef __bf16 gbf8 __attribute__((ext_vector_type(8)));
 typedef __bf16 gbf4 __attribute__((ext_vector_type(4)));
 template <int KB>
 struct Gram3Cfg {
-  static_assert(KB == 2 || KB == 4, "16x16 wave tables for 4 (K in (32, 64]) or 8 (K in (96, 128]) client blocks");
+  static_assert(KB >= 2 && KB <= 4, "16x16 wave tables for 4, 6 or 8 client blocks of 16");
   static constexpr int KP = 32 * KB, QV = kGE / 4;
-  static constexpr int W = KB == 4 ? 12 : 16, NT = W * 64;
-  static constexpr int R = KB == 4 ? 1 : 4;                     // coordinate splits (groups of 32 per chunk / R)
-  static constexpr int FL = KB == 4 ? 1 : 2;                    // chunks per float32 run
-  static constexpr int NLD = (KP * QV + NT - 1) / NT;           // staged 16-byte vectors per thread (6 / 2)
+  static constexpr int W = KB == 4 ? 12 : KB == 3 ? 7 : 16, NT = W * 64;
+  static constexpr int R = KB == 2 ? 4 : 1;                    // coordinate splits (groups of 32 per chunk / R)
+  static constexpr int FL = KB == 2 ? 2 : 1;                    // chunks per float32 run
+  static constexpr int NLD = (KP * QV + NT - 1) / NT;           // staged 16-byte vectors per thread (6 / 7 / 2)
+  static constexpr bool PRE = KB != 2;                          // next group's fragments read ahead (VGPRs)
   static constexpr int PLANE = KP * kG3S;                       // bf16 per plane
   static constexpr size_t PLANE_BYTES = (size_t)3 * PLANE * 2;  // h, m, l
   static constexpr size_t STAGE = PLANE_BYTES + sizeof(float) * (5 * kGE + W * kGE);  // + rows 0..4 + centres
@@ -1595,7 +1601,7 @@ struct Gram3Cfg {
 __device__ __forceinline__ float bf_f(__bf16 b) { return (float)b; }
 
 template <int KB, bool VEC>
-__global__ void __launch_bounds__(Gram3Cfg<KB>::NT) __attribute__((amdgpu_waves_per_eu(KB == 4 ? 3 : 4)))
+__global__ void __launch_bounds__(Gram3Cfg<KB>::NT) __attribute__((amdgpu_waves_per_eu(KB >= 3 ? 3 : 4)))
 k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k,
              int64_t nchunks, double* __restrict__ partial, unsigned* __restrict__ ctr) {
   using C = Gram3Cfg<KB>;
@@ -1610,14 +1616,15 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
   const int li = lane & 15, kk = lane >> 4;
   // the wave's tile set (the S16 forms' tables): type 0 a diagonal pair (b0,b0), (b0,b1), (b1,b1);
   // 1 a triangle (b0,b1), (b0,b2), (b1,b2); 2 a cross pair (b0,b1), (b0,b2) -- and its coordinate split
-  const int set16 = KB == 4 ? w : (w % 4 + w / 4) % 4, r16 = KB == 4 ? 0 : w / 4;
-  const int typ = KB == 4 ? (w < 4 ? 0 : 1) : kG16Sets2[set16][0];
+  const int set16 = KB >= 3 ? w : (w % 4 + w / 4) % 4;
+  const int r16 = KB >= 3 ? 0 : w / 4;
+  const int typ = KB == 4 ? (w < 4 ? 0 : 1) : KB == 3 ? kG16Sets3[set16][0] : kG16Sets2[set16][0];
   const bool dg = typ == 0;
   const int ntile = typ == 2 ? 2 : 3;
   int blk[3], ro[3];
 #pragma unroll
   for (int x = 0; x < 3; ++x) {
-    blk[x] = KB == 4 ? kG16Blocks[w][x] : kG16Sets2[set16][1 + x];
+    blk[x] = KB == 4 ? kG16Blocks[w][x] : KB == 3 ? kG16Sets3[set16][1 + x] : kG16Sets2[set16][1 + x];
     ro[x] = (16 * blk[x] + li) * kG3S + 8 * kk;
   }
   gf4 a16[3];
@@ -1721,7 +1728,7 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
       rd(f, r16);
 #pragma unroll
       for (int gi = 0; gi < NG; ++gi) {
-        if (gi + 1 < NG) rd(fn, r16 + (gi + 1) * C::R);
+        if (C::PRE && gi + 1 < NG) rd(fn, r16 + (gi + 1) * C::R);
 #pragma unroll
         for (int x = 0; x < NT3; ++x) {
           // type 0: (0,0), (0,1), (1,1); type 1: (0,1), (0,2), (1,2); type 2: (0,1), (0,2)
@@ -1736,10 +1743,14 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
           a16[x] = acc;
         }
         if (gi + 1 < NG) {
+          if constexpr (C::PRE) {
 #pragma unroll
-          for (int x = 0; x < NB; ++x)
+            for (int x = 0; x < NB; ++x)
 #pragma unroll
-            for (int p = 0; p < 3; ++p) f[x][p] = fn[x][p];
+              for (int p = 0; p < 3; ++p) f[x][p] = fn[x][p];
+          } else {
+            rd(f, r16 + (gi + 1) * C::R);
+          }
         }
       }
     };
@@ -2057,7 +2068,7 @@ bool gram_s16() {  // K in (32, 64] and (96, 128]: the 16x16 forms (FA_GRAM16=0:
   return on;
 }
 
-bool gram3() {  // K in (32, 64] and (96, 128]: the bf16x3 split form (FA_GRAM3=0: the f32-input 16x16 forms, A/B)
+bool gram3() {  // K in (32, 128]: the bf16x3 split form (FA_GRAM3=0: the f32-input forms, A/B)
   static const bool on = [] {
     const char* e = getenv("FA_GRAM3");
     return !(e && e[0] == '0');
@@ -2130,11 +2141,11 @@ struct GramRun {
 };
 GramRun gram_run(int kb, bool glds) {
   if (glds) return {64, 0.0};  // k_pair_gram_ring: 16 products per chunk, flushed every 4 chunks
-  const bool g3 = (kb == 2 || kb == 4) && gram3();
+  const bool g3 = kb >= 2 && gram3();
   switch (kb) {
     case 1: return {128, 0.0};                        // R = 4, FL = 4
     case 2: return {64, g3 ? 1.2e-8 : 0.0};           // R = 4, FL = 2 (bf16x3: one 32-coordinate group per split)
-    case 3: return {128, 0.0};                        // R = 2, FL = 2
+    case 3: return {128, g3 ? 4e-8 : 0.0};            // f32: R = 2, FL = 2; bf16x3: R = 1, FL = 1 (as K > 96)
     default: return g3 ? GramRun{128, 4e-8} : GramRun{256, 0.0};  // bf16x3: FL = 1; f32: R = 1, FL = 2
   }
 }
@@ -2407,7 +2418,10 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
       else if (gram_s16()) FA_GR(2, true);
       else FA_GR(2, false);
       break;
-    case 3: FA_GR(3, false); break;
+    case 3:
+      if (gram3()) FA_GR3(3);  // the bf16x3 split form (K in (64, 96])
+      else FA_GR(3, false);
+      break;
     default:
       if (gram3()) {  // the bf16x3 split form (K in (96, 128])
         FA_GR3(4);

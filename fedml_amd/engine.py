@@ -970,14 +970,19 @@ class AggEngine:
             return self._last_form
         return "gram" if self.last_kappa_max <= self._last_limit else "direct"
 
-    def _gram_fell_back(self, key) -> bool:
-        """Whether the last guarded call of this shape fell back (without waiting: a call still
-        running counts as not fallen back)."""
-        memo = self.__dict__.setdefault("_gram_memo", {})
-        m = memo.get(key)
-        if m is None or not m["ev"].query():
-            return False
-        return not (float(m["km"][0]) <= m["limit"])
+    def _gram_memo_form(self, key) -> Tuple[bool, bool]:
+        """(go straight to the direct kernels, copy this call's kappa_max) for a guarded call of this
+        shape.  kappa_max is copied to pinned memory on the first call and every GRAM_RETRY-th call
+        after it only, and read once that copy's event has completed (never waited on): in the
+        common case -- no fallback -- the memo costs one 8-byte copy per GRAM_RETRY calls."""
+        m = self.__dict__.setdefault("_gram_memo", {}).get(key)
+        if m is None:
+            return False, True
+        if m["pending"] and m["ev"].query():
+            m["fell"], m["pending"] = not (float(m["km"][0]) <= m["limit"]), False
+        m["calls"] += 1
+        check = m["calls"] % self.GRAM_RETRY == 0
+        return m["fell"] and not check, check
 
     def _pairwise_launch(self, segments, stream=None, diff_dtype=torch.float32, form=None) -> torch.Tensor:
         k = len(segments[0])
@@ -985,11 +990,10 @@ class AggEngine:
         nl = N.i64_array([seg[0].numel() for seg in segments])
         form = form or os.environ.get("FEDML_AMD_KRUM_FORM", "auto")
         key = (k, tuple(seg[0].numel() for seg in segments))
-        if (diff_dtype == torch.float32 and form == "auto" and os.environ.get("FEDML_AMD_KRUM_STICKY", "1") != "0"
-                and self._gram_fell_back(key)):
-            m = self._gram_memo[key]
-            m["skips"] += 1
-            if m["skips"] % self.GRAM_RETRY:
+        copy = False
+        if diff_dtype == torch.float32 and form == "auto" and os.environ.get("FEDML_AMD_KRUM_STICKY", "1") != "0":
+            skip, copy = self._gram_memo_form(key)
+            if skip:
                 form = "direct"
         if diff_dtype == torch.float32 and form in ("auto", "gram"):
             ptrs = N.ptr_array(in_ptrs)
@@ -1006,10 +1010,10 @@ class AggEngine:
                                                        scratch.data_ptr(), scratch.numel(), self._stream(stream))
             N.check(rc, "fa_pairwise_sqdist_gram")
             self._last_km, self._last_form, self._last_limit = km, form if form == "gram" else "auto", limit
-            if form == "auto":  # kappa_max to pinned host memory, read by the next call of this shape
-                memo = self.__dict__.setdefault("_gram_memo", {})
-                m = memo.get(key) or {"km": torch.zeros(1, dtype=torch.float64, pin_memory=True), "skips": 0,
-                                      "ev": torch.cuda.Event(), "done": torch.cuda.Event()}
+            if copy:  # kappa_max to pinned host memory, read by a later call of this shape
+                memo = self._gram_memo
+                m = memo.get(key) or {"km": torch.zeros(1, dtype=torch.float64, pin_memory=True), "calls": 0,
+                                      "fell": False, "ev": torch.cuda.Event(), "done": torch.cuda.Event()}
                 s = stream if stream is not None else torch.cuda.current_stream(self.device)
                 # the 8-byte copy runs on a side stream behind this call, off the caller's stream (a
                 # blit kernel there put ~4 us between this call and the next one, r06c)
@@ -1022,7 +1026,7 @@ class AggEngine:
                     m["km"].copy_(km, non_blocking=True)
                 km.record_stream(side)
                 m["ev"].record(side)
-                m["limit"], m["skips"] = limit, 0
+                m["limit"], m["pending"] = limit, True
                 memo[key] = m
             return d
         self._last_km, self._last_form = None, "direct"

@@ -27,9 +27,9 @@ TOL = 1e-6  # north_star: 1e-6 relative (fp32 work, float64 oracle)
 
 # (P, K, kind, kappa): the full grid at the small sizes, where the error model bites; at 11.7 M the
 # oracle's K^2 P work limits the count (K = 128: ~95 G float64 terms per case)
-SMALL = [(P, K, kind, kap) for P in (7850, 9001) for K in (5, 32, 64, 128) for kind in ("offset", "pair")
+SMALL = [(P, K, kind, kap) for P in (7850, 9001) for K in (5, 32, 64, 96, 128) for kind in ("offset", "pair")
          for kap in (2.0, 4.0, 8.0, 12.0, 15.9)]
-MID = [(1_000_000, K, kind, kap) for K in (5, 32, 64, 128) for kind in ("offset", "pair") for kap in (4.0, 12.0, 15.9)]
+MID = [(1_000_000, K, kind, kap) for K in (5, 32, 64, 80, 128) for kind in ("offset", "pair") for kap in (4.0, 12.0, 15.9)]
 LARGE = [(11_699_132, 5, "offset", 15.9), (11_699_132, 32, "offset", 8.0), (11_699_132, 32, "offset", 15.9),
          (11_699_132, 64, "offset", 15.9), (11_699_132, 64, "pair", 12.0), (11_699_132, 128, "offset", 15.9)]
 
@@ -122,7 +122,8 @@ def test_krum_band_default_path_vs_oracle(eng, P, K, kind, kappa, monkeypatch):
         assert sel == sel_ref
 
 
-@pytest.mark.parametrize("P,K,kappa", [(7850, 128, 15.9), (9001, 128, 12.0), (9001, 96, 15.9), (7850, 32, 15.9),
+@pytest.mark.parametrize("P,K,kappa", [(7850, 128, 15.9), (9001, 128, 12.0), (9001, 96, 15.9), (7850, 80, 15.9), (7850, 32, 15.9),
+                                       (1_000_000, 96, 15.9),
                                        (1_000_000, 128, 15.9), (11_699_132, 32, 15.9)])
 def test_krum_band_gram_error_within_model(eng, P, K, kappa):
     """The forced Gram form (no guard) against the oracle: its error stays below what the guard's
