@@ -112,6 +112,8 @@ def parse():
     p.add_argument("--cold-idle", type=float, default=1.0, help="idle seconds before each cold call")
     p.add_argument("--no-read-probe", action="store_true",
                    help="skip the in-process read-stream probe (measured_read_ceiling)")
+    p.add_argument("--no-clock", action="store_true",
+                   help="skip the amdsmi clock / power / temperature sampler (the line's `clock`)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline time budget")
     p.add_argument("--check-samples", type=int, default=65536)
@@ -362,6 +364,9 @@ def make_arena_rows(idx, P, dtype=torch.float32):
     return rows
 
 
+ARENA_ALLOC = set()  # how the tiled arenas of this run were allocated (ClientArena.alloc_kind)
+
+
 def make_tiled_arena(idx, P, dtype=torch.float32):
     """Client updates in a TILE-INTERLEAVED ClientArena (same values as make_flat_clients)."""
     if CPU_REHEARSAL:  # the same [tiles, capacity, E] group layout in host memory (E: 4 KiB of fp32)
@@ -377,6 +382,7 @@ def make_tiled_arena(idx, P, dtype=torch.float32):
         return types.SimpleNamespace(bufs={dtype: buf})
     from fedml_amd.arena import ArenaLayout, ClientArena
     arena = ClientArena(ArenaLayout([("w", (P,), dtype)]), capacity=len(idx), zero=False, tiled=True)
+    ARENA_ALLOC.add(arena.alloc_kind[dtype])
     for j, i in enumerate(idx):
         g = torch.Generator(device=DEV).manual_seed(1000 + i)
         arena.write(j, {"w": torch.randn(P, generator=g, device=DEV, dtype=torch.float32).to(dtype)})
@@ -1911,6 +1917,88 @@ def cold_calls(wl, reps, idle_s):
                     "per-round AggregationTime case; `ms_per_step` is the back-to-back rate at the sustained clock"}
 
 
+class ClockSampler:
+    """The clocks, power and temperature this process's GPU ran at, sampled by a thread every
+    ``period`` s from the SMU's gpu_metrics table through amdsmi (sysfs reads: no HIP call) while a
+    region runs -- so that a slow line can be told apart as a slower clock (DVFS, power or thermal
+    limits) or a slower memory path at the same clock.  Never raises: a box where amdsmi cannot read
+    the table gets {"error": ...} in the line."""
+
+    def __init__(self, device_index: int, period: float = 0.01):
+        self.period, self.h, self.err, self.amdsmi = period, None, None, None
+        try:
+            import amdsmi
+            amdsmi.amdsmi_init()
+            self.amdsmi = amdsmi
+            p = torch.cuda.get_device_properties(device_index)
+            want = (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+            for h in amdsmi.amdsmi_get_processor_handles():
+                dom, bus, rest = amdsmi.amdsmi_get_gpu_device_bdf(h).split(":")
+                if (int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16)) == want:
+                    self.h = h
+            if self.h is None:
+                self.err = f"no amdsmi handle with PCI {want}"
+        except Exception as e:  # no library, no permission, no table
+            self.err = f"{type(e).__name__}: {e}"[:200]
+
+    def _one(self):
+        m = self.amdsmi.amdsmi_get_gpu_metrics_info(self.h)
+
+        def num(v):
+            return float(v) if isinstance(v, (int, float)) else None
+        xcd = [float(v) for v in (m.get("current_gfxclks") or []) if isinstance(v, (int, float)) and v > 0] \
+            if isinstance(m.get("current_gfxclks"), list) else []
+        return {"gfx_mhz": sum(xcd) / len(xcd) if xcd else num(m.get("current_gfxclk")) or
+                num(m.get("average_gfxclk_frequency")),
+                "mem_mhz": num(m.get("current_uclk")), "power_w": num(m.get("current_socket_power")),
+                "hotspot_c": num(m.get("temperature_hotspot")), "hbm_c": num(m.get("temperature_mem")),
+                "throttle": m.get("indep_throttle_status") if m.get("indep_throttle_status") not in (None, "N/A")
+                else m.get("throttle_status")}
+
+    def __enter__(self):
+        import threading
+        self.samples, self.stop_ev = [], threading.Event()
+        if self.h is None:
+            return self
+
+        def run():
+            while not self.stop_ev.is_set():
+                try:
+                    self.samples.append(self._one())
+                except Exception as e:
+                    self.err = f"{type(e).__name__}: {e}"[:200]
+                    return
+                self.stop_ev.wait(self.period)
+        self.th = threading.Thread(target=run, daemon=True)
+        self.th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop_ev.set()
+        if self.h is not None:
+            self.th.join(1.0)
+        return False
+
+    @staticmethod
+    def maybe(s):
+        """``s`` as a context manager, or a no-op one yielding None."""
+        import contextlib
+        return s if s is not None else contextlib.nullcontext()
+
+    def summary(self):
+        if not self.samples:
+            return {"error": self.err or "no samples"}
+        out = {"samples": len(self.samples), "period_s": self.period, "source": "amdsmi gpu_metrics"}
+        for k in ("gfx_mhz", "mem_mhz", "power_w", "hotspot_c", "hbm_c"):
+            v = [s[k] for s in self.samples if s[k] is not None]
+            if v:
+                out[k] = {"median": round(float(np.median(v)), 1), "min": round(min(v), 1), "max": round(max(v), 1)}
+        th = [s["throttle"] for s in self.samples if s["throttle"] not in (None, "N/A")]
+        if th:
+            out["throttle_frac"] = round(sum(1 for t in th if t) / len(th), 3)
+        return out
+
+
 def pmc_traffic(workload):
     """HBM bytes per launch from the committed rocprofv3 PMC summary (tools/pmc_traffic.py), if any."""
     try:
@@ -2028,10 +2116,14 @@ def main():
             wl["step"]()
         sync()
         args.warmup += 1 + extra
+    clk = None if CPU_REHEARSAL or args.no_clock or rank != 0 or wl.get("latency") else ClockSampler(local)
     ceiling = None
     if world == 1 and not CPU_REHEARSAL and not args.no_read_probe and not wl.get("latency"):
         stage("read probe")
-        ceiling = read_ceiling(eng, wl)
+        with ClockSampler.maybe(clk) as cs:
+            ceiling = read_ceiling(eng, wl)
+        if cs is not None:
+            ceiling["clock"] = cs.summary()
     stage("barrier before the timed steps")
     barrier(world)
     sync()
@@ -2039,10 +2131,11 @@ def main():
     stage("timed steps")
     t0 = time.perf_counter()
     lat = []
-    for _ in range(args.steps):
-        lat.append(wl["step"]())
-    timer.end()
-    sync()
+    with ClockSampler.maybe(clk) as cs_timed:
+        for _ in range(args.steps):
+            lat.append(wl["step"]())
+        timer.end()
+        sync()
     barrier(world)
     sync()
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
@@ -2116,7 +2209,8 @@ def main():
                                        + (", loopback (own pieces through RCCL self send/recv)" if args.loopback
                                           else "")
                                        if world > 1 or args.loopback else ""),
-                       "kernel_variant": args.variant, "layout": args.layout},
+                       "kernel_variant": args.variant, "layout": args.layout,
+                       "arena_alloc": "/".join(sorted(ARENA_ALLOC)) or None},
             "roofline": roofline_block(wl, world, value, unit, achieved, kernel_ms, launch_bytes),
             "cpu_baseline": cpu,
             "parity": parity,
@@ -2130,6 +2224,8 @@ def main():
                 rl["frac_of_ceiling"] = round(rl["achieved"] / ceiling["value"], 4)
         if cold is not None:
             line["cold"] = cold
+        if cs_timed is not None:
+            line["clock"] = dict(cs_timed.summary(), region="the timed steps (rank 0's GPU)")
         line.update(wl.get("extra_line", {}))
         mf = wl.get("mfma_flops_per_launch")
         if mf and world == 1 and kernel_ms and line.get("pair_form") == "gram" and wl.get("mfma_bound"):

@@ -33,6 +33,7 @@ EXPORTED_SYMBOLS = (
     "fa_fedavg_sgd", "fa_fedavg_sgd_tiled", "fa_fedavg_rmsprop", "fa_mix", "fa_mix_tiled", "fa_ctx_set_variant",
     "fa_ctx_set_mix_band", "fa_stream_create_cu_masked", "fa_stream_destroy", "fa_strerror", "fa_last_error",
     "fa_promote_add", "fa_weighted_sum_host", "fa_pushsum", "fa_read_probe",
+    "fa_device_alloc_contiguous", "fa_device_free",
     # include/fedagg_finite.h
     "fa_finite_sum", "fa_finite_sum_tiled", "fa_finite_quantize", "fa_lcc_decode", "fa_mt_randint_sum",
     "fa_mt_randint_sum_scratch_bytes",
@@ -184,6 +185,10 @@ def _declare(L):
                              _P_vp, _vp, _P_vp, _P_vp, _vp, _vp]
     L.fa_read_probe.restype = ctypes.c_int
     L.fa_read_probe.argtypes = [_vp, _vp, ctypes.c_int64, ctypes.c_int32, _vp, _vp]
+    L.fa_device_alloc_contiguous.restype = ctypes.c_int
+    L.fa_device_alloc_contiguous.argtypes = [_vp, ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p)]
+    L.fa_device_free.restype = ctypes.c_int
+    L.fa_device_free.argtypes = [_vp, _vp]
     L.fa_promote_add.restype = ctypes.c_int
     L.fa_promote_add.argtypes = [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int64, _vp, _vp, _vp, _vp]
     _P_ls = ctypes.POINTER(LocalStep)

@@ -30,6 +30,7 @@ H2D per dtype group is issued on a copy stream, and the aggregation stream waits
 """
 from __future__ import annotations
 
+import os
 import weakref
 from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence, Tuple
@@ -119,14 +120,11 @@ class ClientArena:
         self.tiled = bool(tiled)
         self.engine = engine or get_engine(None if device is None else torch.device(device).index)
         self.device = self.engine.device
-        alloc = torch.zeros if zero else torch.empty  # zeroed padding keeps padded outputs finite
-        if self.tiled:
-            self.bufs: Dict[torch.dtype, torch.Tensor] = {
-                dt: alloc((-(-n // tile_elems(dt)), self.capacity, tile_elems(dt)), dtype=dt, device=self.device)
-                for dt, n in layout.group_numel.items()}
-        else:
-            self.bufs = {dt: alloc((self.capacity, n), dtype=dt, device=self.device)
-                         for dt, n in layout.group_numel.items()}
+        self.alloc_kind: Dict[torch.dtype, str] = {}
+        self.bufs: Dict[torch.dtype, torch.Tensor] = {}
+        for dt, n in layout.group_numel.items():
+            shape = (-(-n // tile_elems(dt)), self.capacity, tile_elems(dt)) if self.tiled else (self.capacity, n)
+            self.bufs[dt] = self._alloc(shape, dt, zero)
         self._scratch: Dict[torch.dtype, torch.Tensor] = {}
         self._stage_dev: Dict[torch.dtype, torch.Tensor] = {}  # copy-stream row staging (tiled host ingest)
         self._copy_stream = None
@@ -135,6 +133,29 @@ class ClientArena:
         self._pending: List[torch.cuda.Event] = []
         self._rows_adopted: Dict[int, int] = {}  # row -> id of the state_dict adopted into it
         self._handed: Dict[int, list] = {}        # row -> weakrefs of the row views adopt() handed out
+
+    # Groups of at least CONTIG_MIN_BYTES live in physically contiguous device memory
+    # (AggEngine.alloc_contiguous): the weighted-sum kernel's rate over a 64.5 GB arena depended on the
+    # allocation -- 9.28-10.0 ms per K = 128 x 125 M step on one box with identical translation, L2
+    # and request counters (profiles/r06n-r06q) -- and contiguous blocks ran at the fast end more
+    # often (DESIGN A.3 item 11).  FEDML_AMD_ARENA_ALLOC=torch: the caching allocator for every group.
+    CONTIG_MIN_BYTES = 1 << 30
+
+    def _alloc(self, shape, dt: torch.dtype, zero: bool) -> torch.Tensor:
+        n = 1
+        for d in shape:
+            n *= int(d)
+        nbytes = n * torch.empty((), dtype=dt).element_size()
+        if nbytes >= self.CONTIG_MIN_BYTES and os.environ.get("FEDML_AMD_ARENA_ALLOC", "contiguous") != "torch":
+            raw = self.engine.alloc_contiguous(nbytes)
+            if raw is not None:
+                t = raw.view(dt).view(shape)
+                if zero:  # zeroed padding keeps padded outputs finite
+                    t.zero_()
+                self.alloc_kind[dt] = "contiguous"
+                return t
+        self.alloc_kind[dt] = "torch"
+        return (torch.zeros if zero else torch.empty)(shape, dtype=dt, device=self.device)
 
     @classmethod
     def for_model(cls, template_state_dict, capacity: int, device=None, **kw) -> "ClientArena":

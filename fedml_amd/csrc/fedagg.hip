@@ -2339,6 +2339,31 @@ k_read_probe(const char* __restrict__ buf, int64_t nrows, int rows_per_wg, unsig
 }
 }  // namespace
 
+extern "C" int fa_device_alloc_contiguous(fa_ctx* ctx, int64_t bytes, void** d_out) {
+  if (!ctx || !d_out || bytes <= 0) return fail(FA_ERR_INVALID, "fa_device_alloc_contiguous: ctx, d_out, bytes > 0");
+  *d_out = nullptr;
+  DeviceGuard g(ctx->device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
+  void* p = nullptr;
+  const hipError_t e = hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocContiguous);
+  if (e != hipSuccess || !p) {
+    (void)hipGetLastError();  // not sticky: the caller falls back to an ordinary allocation
+    return fail(FA_ERR_HIP, "hipExtMallocWithFlags(%lld bytes, contiguous): %s", (long long)bytes,
+                hipGetErrorString(e));
+  }
+  *d_out = p;
+  return FA_OK;
+}
+
+extern "C" int fa_device_free(fa_ctx* ctx, void* d_ptr) {
+  if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");
+  if (!d_ptr) return FA_OK;
+  DeviceGuard g(ctx->device);
+  if (!g.ok) return fail(FA_ERR_HIP, "hipSetDevice(%d) failed", ctx->device);
+  FA_HIP(hipFree(d_ptr));
+  return FA_OK;
+}
+
 extern "C" int fa_read_probe(fa_ctx* ctx, const void* d_buf, int64_t bytes, int32_t rows_per_workgroup,
                              void* d_word, void* hip_stream) {
   if (!ctx) return fail(FA_ERR_INVALID, "ctx is NULL");

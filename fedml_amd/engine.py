@@ -135,6 +135,15 @@ class AggEngine:
                                         buf.numel() * buf.element_size(), int(rows_per_workgroup),
                                         N.ctypes.c_void_p(word.data_ptr()), self._stream(stream)), "fa_read_probe")
 
+    def alloc_contiguous(self, nbytes: int) -> Optional[torch.Tensor]:
+        """``nbytes`` of physically contiguous device memory (fa_device_alloc_contiguous) as a uint8
+        tensor (view it as the arena's dtype), freed when its storage is; None when the device has
+        no contiguous range that large.  Arena storage: see ClientArena."""
+        p = N.ctypes.c_void_p()
+        if self._lib.fa_device_alloc_contiguous(self._ctx, int(nbytes), N.ctypes.byref(p)) != N.FA_OK or not p.value:
+            return None
+        return torch.as_tensor(_DeviceBlock(self, p.value, int(nbytes)), device=self.device)
+
     def _scratch(self, name: str, need: int, stream=None) -> torch.Tensor:
         """Device scratch of >= need bytes, cached per (name, stream): calls queued on different
         streams never share one, and a buffer replaced while a kernel on ``stream`` may still read it
@@ -1040,6 +1049,33 @@ class AggEngine:
         N.check(rc, "fa_pairwise_sqdist")
         return d
 
+
+class _DeviceBlock:
+    """Owner of one fa_device_alloc_contiguous block, exposed through __cuda_array_interface__ (the
+    tensor torch builds from it holds this object until its storage dies, then fa_device_free)."""
+    _exiting = False  # interpreter teardown: the process's exit returns the memory
+
+    def __init__(self, eng: "AggEngine", ptr: int, nbytes: int):
+        self.eng, self.ptr = eng, ptr
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
+                                         "version": 3, "strides": None}
+
+    def __del__(self):
+        if self.ptr and not _DeviceBlock._exiting:
+            try:
+                self.eng._lib.fa_device_free(self.eng._ctx, N.ctypes.c_void_p(self.ptr))
+            except Exception:
+                pass
+        self.ptr = 0
+
+
+def _mark_exiting():
+    _DeviceBlock._exiting = True
+
+
+import atexit  # noqa: E402
+
+atexit.register(_mark_exiting)
 
 _DIFF_DT = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2, torch.float64: 3}  # FA_DTYPE_*
 

@@ -312,6 +312,18 @@ int fa_promote_add(fa_ctx *ctx, int acc_dtype, int t_dtype, int64_t n, const voi
 int fa_read_probe(fa_ctx *ctx, const void *d_buf, int64_t bytes, int32_t rows_per_workgroup, void *d_word,
                   void *hip_stream);
 
+/*
+ * Arena storage (r06): `bytes` of physically contiguous device memory on ctx's device
+ * (hipExtMallocWithFlags(hipDeviceMallocContiguous)), for the client arenas.  The weighted-sum
+ * kernel's rate over a 64.5 GB arena depended on the allocation (9.28-10.0 ms per K = 128 x 125 M
+ * step on one box, identical translation / L2 / request counters; profiles/r06n-r06q); contiguous
+ * allocations ran at the fast end more often.  *d_out = NULL and FA_ERR_HIP when the device has no
+ * contiguous range that large (the caller then allocates normally).  Synchronous.
+ */
+int fa_device_alloc_contiguous(fa_ctx *ctx, int64_t bytes, void **d_out);
+/* Frees what fa_device_alloc_contiguous returned (synchronises the device, as hipFree does). */
+int fa_device_free(fa_ctx *ctx, void *d_ptr);
+
 /* Static name of a status code. */
 const char *fa_strerror(int code);
 /* Detail of the calling thread's last error ("" if none). */

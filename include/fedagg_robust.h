@@ -80,7 +80,7 @@ size_t fa_pairwise_sqdist_scratch_bytes(int32_t num_segments, const int64_t *seg
  * D_ij = A_i + A_j - 2 G_ij over y_i = x_i - c (c: the per-coordinate median of clients 0..4), G = Y Y^T
  * on the f32-input MFMA (k <= 32 with 16-byte aligned clients: v_mfma_f32_16x16x4_f32 over the three
  * upper 16x16 tiles, chunks streamed by LDS-DMA; otherwise v_mfma_f32_32x32x2_f32 over the upper
- * 32x32 tiles; k in (32, 64] or (96, 128] with FA_GRAM3=1: y split exactly into three bf16 parts on the
+ * 32x32 tiles; k in (32, 128] with 16-byte aligned clients (FA_GRAM3=0: off): y split exactly into three bf16 parts on the
  * bf16 MFMA), float32 runs of n = 64-256 products summed in float64.
  * Same d_dist layout (k x k float64, symmetric, zero diagonal).  The form cancels: its relative error
  * is ~ 0.30 kappa_ij u n / sqrt(P) (one sigma, u = 2^-24, P = total coordinates), kappa_ij =
