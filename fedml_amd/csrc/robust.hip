@@ -1575,36 +1575,40 @@ k_pair_gram(const PSeg* __restrict__ segs, int nseg, const void* const* __restri
 // x 16 cycles = 384 instead of 32 x 32 = 1,024 MFMA cycles; the split costs ~5 VALU per element,
 // once per workgroup instead of once per wave and operand read.
 // Per chunk (128 coordinates, the same 12-wave tile map as the S16 form, kG16Blocks): A) the staged
-// rows 0..4 go to LDS; barrier; B) every wave computes the chunk's centre (median of clients 0..4)
-// into its own row; C) every thread splits its staged elements into the planes, then issues the
+// rows 0..4 go to LDS; barrier; B) every thread computes the chunk's centre (median of clients 0..4)
+// at its one coordinate quad (r06: no centre rows); C) every thread splits its staged elements into the planes, then issues the
 // next chunk's loads (in flight during the MFMAs); barrier; D) MFMAs.  The planes are single-buffered:
 // the barrier of the next chunk's step A separates its step C from this chunk's reads.
 constexpr int kG3S = kGE + 8;  // bf16 per plane row: 272-byte rows, 16-lane b128 reads conflict-free
 typedef __bf16 gbf8 __attribute__((ext_vector_type(8)));
 typedef __bf16 gbf4 __attribute__((ext_vector_type(4)));
-template <int KB>
+// L = 1 (K in (32, 64] only, the default there): 8 waves in 2 splits, two workgroups per CU -- two
+// chunks of loads in flight per CU instead of one: K = 64 1.01-1.03 -> 0.84-0.86 ms (profiles/r06s)
+template <int KB, int L = 0>
 struct Gram3Cfg {
   static_assert(KB >= 2 && KB <= 4, "16x16 wave tables for 4, 6 or 8 client blocks of 16");
+  static_assert(L == 0 || KB == 2, "the two-workgroup layout is for 4 client blocks of 16");
   static constexpr int KP = 32 * KB, QV = kGE / 4;
-  static constexpr int W = KB == 4 ? 12 : KB == 3 ? 7 : 16, NT = W * 64;
-  static constexpr int R = KB == 2 ? 4 : 1;                    // coordinate splits (groups of 32 per chunk / R)
-  static constexpr int FL = KB == 2 ? 2 : 1;                    // chunks per float32 run
+  static constexpr int W = KB == 4 ? 12 : KB == 3 ? 7 : L ? 8 : 16, NT = W * 64;
+  static constexpr int R = KB == 2 ? (L ? 2 : 4) : 1;          // coordinate splits (groups of 32 per chunk / R)
+  static constexpr int FL = KB == 2 && !L ? 2 : 1;              // chunks per float32 run (64 products at K <= 64)
   static constexpr int NLD = (KP * QV + NT - 1) / NT;           // staged 16-byte vectors per thread (6 / 7 / 2)
-  static constexpr bool PRE = KB != 2;                          // next group's fragments read ahead (VGPRs)
+  static constexpr bool PRE = KB != 2 && !L;                    // next group's fragments read ahead (VGPRs)
   static constexpr int PLANE = KP * kG3S;                       // bf16 per plane
   static constexpr size_t PLANE_BYTES = (size_t)3 * PLANE * 2;  // h, m, l
-  static constexpr size_t STAGE = PLANE_BYTES + sizeof(float) * (5 * kGE + W * kGE);  // + rows 0..4 + centres
+  static constexpr size_t STAGE = PLANE_BYTES + sizeof(float) * 5 * kGE;  // + rows 0..4
+  static_assert(NT % QV == 0, "a thread's staged vectors share one coordinate quad (its centre)");
   static constexpr size_t RED = R > 1 ? sizeof(double) * W * 768 : 0;               // the splits' sums
   static constexpr size_t LDS = STAGE > RED ? STAGE : RED;
 };
 
 __device__ __forceinline__ float bf_f(__bf16 b) { return (float)b; }
 
-template <int KB, bool VEC>
-__global__ void __launch_bounds__(Gram3Cfg<KB>::NT) __attribute__((amdgpu_waves_per_eu(KB >= 3 ? 3 : 4)))
+template <int KB, bool VEC, int L = 0>
+__global__ void __launch_bounds__((Gram3Cfg<KB, L>::NT)) __attribute__((amdgpu_waves_per_eu(KB >= 3 && !L ? 3 : 4)))
 k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restrict__ ptrs, int k,
              int64_t nchunks, double* __restrict__ partial, unsigned* __restrict__ ctr) {
-  using C = Gram3Cfg<KB>;
+  using C = Gram3Cfg<KB, L>;
   constexpr int QV = C::QV;
   if (blockIdx.x == 0 && threadIdx.x == 0) *ctr = 0u;  // k_gram_reduce's arrival counter
   extern __shared__ __attribute__((aligned(16))) char g3[];
@@ -1612,7 +1616,6 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
   float* const c5 = (float*)(g3 + C::PLANE_BYTES);  // [5][kGE] raw rows 0..4
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  float* const crow = c5 + 5 * kGE + w * kGE;  // this wave's centre row (wave-private)
   const int li = lane & 15, kk = lane >> 4;
   // the wave's tile set (the S16 forms' tables): type 0 a diagonal pair (b0,b0), (b0,b1), (b1,b1);
   // 1 a triangle (b0,b1), (b0,b2), (b1,b2); 2 a cross pair (b0,b1), (b0,b2) -- and its coordinate split
@@ -1675,26 +1678,26 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
     // A) rows 0..4 (staged by threads 0..159 in their first vector) to LDS
     if (t < 5 * QV) *(gf4*)&c5[(t / QV) * kGE + 4 * (t % QV)] = v[0];
     __syncthreads();  // also: every wave is done reading the planes of chunk ch - 1
-    // B) this wave's copy of the chunk's centre: the median of clients 0..4 (k > 32 here)
-    if (lane < QV) {
-      const gf4 a = *(const gf4*)&c5[4 * lane], b = *(const gf4*)&c5[kGE + 4 * lane],
-                 c = *(const gf4*)&c5[2 * kGE + 4 * lane], d = *(const gf4*)&c5[3 * kGE + 4 * lane],
-                 f = *(const gf4*)&c5[4 * kGE + 4 * lane];
-      gf4 m;
+    // B) the chunk's centre at this thread's coordinate quad (every staged vector of the thread is at
+    // quad t % QV): the median of clients 0..4 (k > 32 here)
+    const int q = t % QV;
+    gf4 cq;
+    {
+      const gf4 a = *(const gf4*)&c5[4 * q], b = *(const gf4*)&c5[kGE + 4 * q],
+                 c = *(const gf4*)&c5[2 * kGE + 4 * q], d = *(const gf4*)&c5[3 * kGE + 4 * q],
+                 f = *(const gf4*)&c5[4 * kGE + 4 * q];
 #pragma unroll
       for (int z = 0; z < 4; ++z)
-        m[z] = __builtin_amdgcn_fmed3f(f[z], fmaxf(fminf(a[z], b[z]), fminf(c[z], d[z])),
-                                       fminf(fmaxf(a[z], b[z]), fmaxf(c[z], d[z])));
-      *(gf4*)&crow[4 * lane] = m;
+        cq[z] = __builtin_amdgcn_fmed3f(f[z], fmaxf(fminf(a[z], b[z]), fminf(c[z], d[z])),
+                                        fminf(fmaxf(a[z], b[z]), fmaxf(c[z], d[z])));
     }
-    __builtin_amdgcn_wave_barrier();
     // C) y = x - c split into h + m + l, written to the three planes
 #pragma unroll
     for (int u = 0; u < C::NLD; ++u) {
       const int idx = t + u * C::NT;
       if (C::NLD * C::NT == C::KP * QV || idx < C::KP * QV) {
-        const int cl = idx / QV, q = idx % QV;
-        const gf4 y = v[u] - *(const gf4*)&crow[4 * q];
+        const int cl = idx / QV;
+        const gf4 y = v[u] - cq;
         gbf4 h, m, l;
 #pragma unroll
         for (int z = 0; z < 4; ++z) {
@@ -2076,6 +2079,14 @@ bool gram3() {  // K in (32, 128]: the bf16x3 split form (FA_GRAM3=0: the f32-in
   return on;
 }
 
+bool gram3_l2() {  // K in (32, 64]: the two-workgroup bf16x3 layout (Gram3Cfg<2, 1>; FA_GRAM3_L2=0: one, A/B)
+  static const bool on = [] {
+    const char* e = getenv("FA_GRAM3_L2");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int gram_glds() {  // K <= 32: the LDS-DMA ring kernel (FA_GRAM_GLDS=0: the register-staged k_pair_gram<1>, A/B)
   static const int d = [] {
     const char* e = getenv("FA_GRAM_GLDS");
@@ -2090,7 +2101,8 @@ int gram_nblocks(int64_t nchunks, int kb) {
     const char* e = getenv("FA_GRAM_BLOCKS");
     return e ? atoi(e) : 0;
   }();
-  const int64_t cap = ov >= 64 && ov <= 8192 ? ov : kb >= 2 ? 256 : 1024;
+  const bool two = kb == 2 && gram3() && gram3_l2();  // two workgroups per CU
+  const int64_t cap = ov >= 64 && ov <= 8192 ? ov : two ? 512 : kb >= 2 ? 256 : 1024;
   return (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, cap));
 }
 
@@ -2144,7 +2156,7 @@ GramRun gram_run(int kb, bool glds) {
   const bool g3 = kb >= 2 && gram3();
   switch (kb) {
     case 1: return {128, 0.0};                        // R = 4, FL = 4
-    case 2: return {64, g3 ? 1.2e-8 : 0.0};           // R = 4, FL = 2 (bf16x3: one 32-coordinate group per split)
+    case 2: return {64, g3 ? 1.2e-8 : 0.0};           // f32: R = 4, FL = 2; bf16x3: R = 2, FL = 1 -- 64 either way
     case 3: return {128, g3 ? 4e-8 : 0.0};            // f32: R = 2, FL = 2; bf16x3: R = 1, FL = 1 (as K > 96)
     default: return g3 ? GramRun{128, 4e-8} : GramRun{256, 0.0};  // bf16x3: FL = 1; f32: R = 1, FL = 2
   }
@@ -2392,14 +2404,14 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
     hipLaunchKernelGGL((k_gram_reduce<KB>), dim3((unsigned)ntr), dim3(64 * kGRW), 0, st, (const double*)part,    \
                        nblocks, gm, k, (double*)d_dist, (double*)d_kappa_max, ctr);                           \
   } while (0)
-#define FA_GR3(KB)                                                                                             \
+#define FA_GR3(KB, L)                                                                                          \
   do {                                                                                                         \
     if (vec)                                                                                                   \
-      hipLaunchKernelGGL((k_pair_gram3<KB, true>), dim3((unsigned)nblocks), dim3(Gram3Cfg<KB>::NT),             \
-                         Gram3Cfg<KB>::LDS, st, sg, nseg, pp, k, nchunks, part, ctr);                           \
+      hipLaunchKernelGGL((k_pair_gram3<KB, true, L>), dim3((unsigned)nblocks), dim3(Gram3Cfg<KB, L>::NT),       \
+                         (Gram3Cfg<KB, L>::LDS), st, sg, nseg, pp, k, nchunks, part, ctr);                      \
     else                                                                                                       \
-      hipLaunchKernelGGL((k_pair_gram3<KB, false>), dim3((unsigned)nblocks), dim3(Gram3Cfg<KB>::NT),            \
-                         Gram3Cfg<KB>::LDS, st, sg, nseg, pp, k, nchunks, part, ctr);                           \
+      hipLaunchKernelGGL((k_pair_gram3<KB, false, L>), dim3((unsigned)nblocks), dim3(Gram3Cfg<KB, L>::NT),      \
+                         (Gram3Cfg<KB, L>::LDS), st, sg, nseg, pp, k, nchunks, part, ctr);                      \
     hipLaunchKernelGGL((k_gram_reduce<KB>), dim3((unsigned)ntr), dim3(64 * kGRW), 0, st, (const double*)part,    \
                        nblocks, gm, k, (double*)d_dist, (double*)d_kappa_max, ctr);                           \
   } while (0)
@@ -2414,17 +2426,19 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
   } else switch (kb) {
     case 1: FA_GR(1, false); break;
     case 2:
-      if (gram3()) FA_GR3(2);  // the bf16x3 split form (K in (32, 64])
+      if (gram3() && gram3_l2()) FA_GR3(2, 1);  // the bf16x3 split form (K in (32, 64])
+      else if (gram3()) FA_GR3(2, 0);
       else if (gram_s16()) FA_GR(2, true);
       else FA_GR(2, false);
       break;
     case 3:
-      if (gram3()) FA_GR3(3);  // the bf16x3 split form (K in (64, 96])
+      if (gram3()) FA_GR3(3, 0);  // the bf16x3 split form (K in (64, 96]; two workgroups per CU at
+                                  // 128 VGPRs spilled 76-88 bytes, not built)
       else FA_GR(3, false);
       break;
     default:
       if (gram3()) {  // the bf16x3 split form (K in (96, 128])
-        FA_GR3(4);
+        FA_GR3(4, 0);
       } else if (gram_s16()) {
         FA_GR(4, true);
       } else {
