@@ -1587,7 +1587,7 @@ typedef __bf16 gbf4 __attribute__((ext_vector_type(4)));
 template <int KB, int L = 0>
 struct Gram3Cfg {
   static_assert(KB >= 2 && KB <= 4, "16x16 wave tables for 4, 6 or 8 client blocks of 16");
-  static_assert(L == 0 || KB == 2, "the two-workgroup layout is for 4 client blocks of 16");
+  static_assert(L == 0 || KB <= 3, "the two-workgroup layouts are for 4 or 6 client blocks of 16");
   static constexpr int KP = 32 * KB, QV = kGE / 4;
   static constexpr int W = KB == 4 ? 12 : KB == 3 ? 7 : L ? 8 : 16, NT = W * 64;
   static constexpr int R = KB == 2 ? (L ? 2 : 4) : 1;          // coordinate splits (groups of 32 per chunk / R)
@@ -1596,7 +1596,12 @@ struct Gram3Cfg {
   static constexpr bool PRE = KB != 2 && !L;                    // next group's fragments read ahead (VGPRs)
   static constexpr int PLANE = KP * kG3S;                       // bf16 per plane
   static constexpr size_t PLANE_BYTES = (size_t)3 * PLANE * 2;  // h, m, l
-  static constexpr size_t STAGE = PLANE_BYTES + sizeof(float) * 5 * kGE;  // + rows 0..4
+  // L = 1 at K in (64, 96] (the default there): the client pointers in LDS instead of 7 pointer
+  // pairs per thread and two planes live at a time in the MFMA phase -- the registers a second
+  // workgroup per CU needs (124 of 128 per lane; 2 x 81.7 KB of LDS): K = 96 1.45-1.47 -> 1.37-1.39 ms
+  // (profiles/r06y)
+  static constexpr bool PT = L && KB == 3;
+  static constexpr size_t STAGE = PLANE_BYTES + sizeof(float) * 5 * kGE + (PT ? sizeof(void*) * KP : 0);
   static_assert(NT % QV == 0, "a thread's staged vectors share one coordinate quad (its centre)");
   static constexpr size_t RED = R > 1 ? sizeof(double) * W * 768 : 0;               // the splits' sums
   static constexpr size_t LDS = STAGE > RED ? STAGE : RED;
@@ -1637,36 +1642,54 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
 #pragma unroll
   for (int q = 0; q < 12; ++q) accd[q] = 0.0;
   gf4 v[C::NLD];
-  const float* src[C::NLD];
+  const float* src[C::PT ? 1 : C::NLD];
+  const float** const ptab = (const float**)(g3 + C::PLANE_BYTES + sizeof(float) * 5 * kGE);  // [KP] if PT
   int cseg = -1;
   auto load = [&](int64_t ch) {  // as k_pair_gram: client rows, coalesced 16-byte loads
     const int si = nseg > 1 ? find_seg(segs, nseg, ch) : 0;
     const PSeg sg = segs[si];
     if (si != cseg) {
       cseg = si;
+      if constexpr (C::PT) {  // (a uniform branch: every thread reaches both barriers)
+        __syncthreads();      // every thread's loads from the previous segment's table are issued
+        if (t < C::KP) ptab[t] = t < k ? (const float*)ptrs[sg.ptr_base + t] : nullptr;
+        __syncthreads();
+      } else {
 #pragma unroll
-      for (int u = 0; u < C::NLD; ++u) {
-        const int idx = t + u * C::NT;
-        const int cl = idx / QV;
-        src[u] = idx < C::KP * QV && cl < k ? (const float*)ptrs[sg.ptr_base + cl] + 4 * (idx % QV) : nullptr;
+        for (int u = 0; u < C::NLD; ++u) {
+          const int idx = t + u * C::NT;
+          const int cl = idx / QV;
+          src[u] = idx < C::KP * QV && cl < k ? (const float*)ptrs[sg.ptr_base + cl] + 4 * (idx % QV) : nullptr;
+        }
       }
     }
+    auto srcp = [&](int u) -> const float* {
+      if constexpr (C::PT) {
+        const int idx = t + u * C::NT;
+        const float* b = idx < C::KP * QV ? ptab[idx / QV] : nullptr;
+        return b ? b + 4 * (idx % QV) : nullptr;
+      } else {
+        return src[u];
+      }
+    };
     const int64_t b0 = (ch - sg.tile_start) * kGE;
     if (VEC && b0 + kGE <= sg.numel) {
 #pragma unroll
       for (int u = 0; u < C::NLD; ++u) {
         const gf4 z = {0.f, 0.f, 0.f, 0.f};
-        v[u] = src[u] ? *(const __attribute__((address_space(1))) gf4*)(src[u] + b0) : z;
+        const float* sp = srcp(u);
+        v[u] = sp ? *(const __attribute__((address_space(1))) gf4*)(sp + b0) : z;
       }
     } else {
 #pragma unroll
       for (int u = 0; u < C::NLD; ++u) {
         const int idx = t + u * C::NT;
         gf4 x = {0.f, 0.f, 0.f, 0.f};
-        if (src[u]) {
+        const float* sp = srcp(u);
+        if (sp) {
           const int64_t left = sg.numel - (b0 + 4 * (idx % QV));
 #pragma unroll
-          for (int z = 0; z < 4; ++z) if (z < left) x[z] = gld<float>(src[u] + b0, z);
+          for (int z = 0; z < 4; ++z) if (z < left) x[z] = gld<float>(sp + b0, z);
         }
         v[u] = x;
       }
@@ -1721,6 +1744,41 @@ k_pair_gram3(const PSeg* __restrict__ segs, int nseg, const void* const* __restr
       constexpr int TYP = decltype(typc)::value;
       constexpr int NB = TYP == 0 ? 2 : 3, NT3 = TYP == 2 ? 2 : 3;
       constexpr int NG = kGE / 32 / C::R;
+      if constexpr (C::PT) {
+        // (the two-workgroup layout at K in (64, 96]: 128 registers per lane) two planes live at a
+        // time -- H and M for M M, H M, M H, then L in M's registers for H L, L H and H H
+#pragma unroll
+        for (int gi = 0; gi < NG; ++gi) {
+          const int G = r16 + gi * C::R;
+          gbf8 fh[NB], fx[NB];
+#pragma unroll
+          for (int x = 0; x < NB; ++x) {
+            fh[x] = *(const gbf8*)&planes[ro[x] + 32 * G];
+            fx[x] = *(const gbf8*)&planes[C::PLANE + ro[x] + 32 * G];
+          }
+#pragma unroll
+          for (int x = 0; x < NT3; ++x) {
+            const int pa = x == 2 ? 1 : 0, pb = TYP == 0 ? (x == 0 ? 0 : 1) : (x == 0 ? 1 : 2);
+            gf4 acc = a16[x];
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fx[pa], fx[pb], acc, 0, 0, 0);  // M M
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[pa], fx[pb], acc, 0, 0, 0);  // H M
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fx[pa], fh[pb], acc, 0, 0, 0);  // M H
+            a16[x] = acc;
+          }
+#pragma unroll
+          for (int x = 0; x < NB; ++x) fx[x] = *(const gbf8*)&planes[2 * C::PLANE + ro[x] + 32 * G];
+#pragma unroll
+          for (int x = 0; x < NT3; ++x) {
+            const int pa = x == 2 ? 1 : 0, pb = TYP == 0 ? (x == 0 ? 0 : 1) : (x == 0 ? 1 : 2);
+            gf4 acc = a16[x];
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[pa], fx[pb], acc, 0, 0, 0);  // H L
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fx[pa], fh[pb], acc, 0, 0, 0);  // L H
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[pa], fh[pb], acc, 0, 0, 0);  // H H
+            a16[x] = acc;
+          }
+        }
+        return;
+      }
       gbf8 f[NB][3], fn[NB][3];
       auto rd = [&](gbf8 (&d)[NB][3], int G) {
 #pragma unroll
@@ -2087,6 +2145,14 @@ bool gram3_l2() {  // K in (32, 64]: the two-workgroup bf16x3 layout (Gram3Cfg<2
   return on;
 }
 
+bool gram3_l3() {  // K in (64, 96]: the two-workgroup bf16x3 layout (Gram3Cfg<3, 1>; FA_GRAM3_L3=0: one, A/B)
+  static const bool on = [] {
+    const char* e = getenv("FA_GRAM3_L3");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 int gram_glds() {  // K <= 32: the LDS-DMA ring kernel (FA_GRAM_GLDS=0: the register-staged k_pair_gram<1>, A/B)
   static const int d = [] {
     const char* e = getenv("FA_GRAM_GLDS");
@@ -2101,7 +2167,7 @@ int gram_nblocks(int64_t nchunks, int kb) {
     const char* e = getenv("FA_GRAM_BLOCKS");
     return e ? atoi(e) : 0;
   }();
-  const bool two = kb == 2 && gram3() && gram3_l2();  // two workgroups per CU
+  const bool two = (kb == 2 && gram3() && gram3_l2()) || (kb == 3 && gram3() && gram3_l3());  // 2 WGs / CU
   const int64_t cap = ov >= 64 && ov <= 8192 ? ov : two ? 512 : kb >= 2 ? 256 : 1024;
   return (int)std::max<int64_t>(1, std::min<int64_t>(nchunks, cap));
 }
@@ -2432,8 +2498,8 @@ int fa_pairwise_sqdist_gram(fa_ctx* ctx, int32_t num_segments, const int64_t* se
       else FA_GR(2, false);
       break;
     case 3:
-      if (gram3()) FA_GR3(3, 0);  // the bf16x3 split form (K in (64, 96]; two workgroups per CU at
-                                  // 128 VGPRs spilled 76-88 bytes, not built)
+      if (gram3() && gram3_l3()) FA_GR3(3, 1);  // the bf16x3 split form (K in (64, 96])
+      else if (gram3()) FA_GR3(3, 0);
       else FA_GR(3, false);
       break;
     default:
