@@ -365,6 +365,7 @@ def make_arena_rows(idx, P, dtype=torch.float32):
 
 
 ARENA_ALLOC = set()  # how the tiled arenas of this run were allocated (ClientArena.alloc_kind)
+ARENA_PLACEMENT = []  # their placement checks (ClientArena.placement)
 
 
 def make_tiled_arena(idx, P, dtype=torch.float32):
@@ -383,6 +384,8 @@ def make_tiled_arena(idx, P, dtype=torch.float32):
     from fedml_amd.arena import ArenaLayout, ClientArena
     arena = ClientArena(ArenaLayout([("w", (P,), dtype)]), capacity=len(idx), zero=False, tiled=True)
     ARENA_ALLOC.add(arena.alloc_kind[dtype])
+    if dtype in arena.placement:
+        ARENA_PLACEMENT.append(arena.placement[dtype])
     for j, i in enumerate(idx):
         g = torch.Generator(device=DEV).manual_seed(1000 + i)
         arena.write(j, {"w": torch.randn(P, generator=g, device=DEV, dtype=torch.float32).to(dtype)})
@@ -2210,7 +2213,8 @@ def main():
                                           else "")
                                        if world > 1 or args.loopback else ""),
                        "kernel_variant": args.variant, "layout": args.layout,
-                       "arena_alloc": "/".join(sorted(ARENA_ALLOC)) or None},
+                       "arena_alloc": "/".join(sorted(ARENA_ALLOC)) or None,
+                       "arena_placement": ARENA_PLACEMENT or None},
             "roofline": roofline_block(wl, world, value, unit, achieved, kernel_ms, launch_bytes),
             "cpu_baseline": cpu,
             "parity": parity,

@@ -12,6 +12,7 @@ import pytest
 import torch
 
 from fedml_amd.arena import ArenaLayout, ClientArena
+from fedml_amd.engine import SUM
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -64,3 +65,24 @@ def test_contiguous_blocks_are_freed():
 def test_small_groups_stay_on_the_caching_allocator():
     a = ClientArena(ArenaLayout([("w", (1000,), torch.float32)]), capacity=3, device=DEV, tiled=True)
     assert a.alloc_kind[torch.float32] == "torch"
+
+
+def test_placement_check_keeps_the_best_block(monkeypatch):
+    """The placement check (ClientArena._place) on a 16 GiB tiled group: the ratio of every block it
+    measured is recorded, at most PLACEMENT_TRIES blocks, the kept one has the smallest ratio; forcing
+    a threshold of 0 makes it try all of them; the kept block still aggregates bit-exactly."""
+    monkeypatch.setattr(ClientArena, "PLACEMENT_RATIO", 0.0)  # every block "slow": all tries happen
+    P = 1 << 25
+    lay = ArenaLayout([("w", (P,), torch.float32)])  # 128 MiB per client x 128 clients = 16 GiB
+    a = ClientArena(lay, capacity=128, device=DEV, zero=True, tiled=True)
+    pl = a.placement[torch.float32]
+    assert len(pl["ratios"]) == ClientArena.PLACEMENT_TRIES
+    assert pl["ratios"][pl["kept"]] == min(pl["ratios"]) and all(r > 0.5 for r in pl["ratios"])
+    for i in (0, 1, 127):
+        a.write(i, {"w": torch.full((P,), float(i + 1), device=DEV)})
+    got = a.aggregate(SUM, clients=[0, 1, 127])["w"]  # 1 + 2 + 128
+    assert float(got.min()) == 131.0 and float(got.max()) == 131.0
+    del a, got
+    monkeypatch.setenv("FEDML_AMD_ARENA_PLACEMENT", "0")
+    b = ClientArena(lay, capacity=128, device=DEV, zero=False, tiled=True)
+    assert torch.float32 not in b.placement
