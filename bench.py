@@ -1982,6 +1982,16 @@ class ClockSampler:
             self.th.join(1.0)
         return False
 
+    def sample_now(self) -> dict:
+        """One reading, synchronously (outside any timed region)."""
+        if self.h is None:
+            return {"error": self.err or "no handle"}
+        try:
+            r = self._one()
+        except Exception as e:
+            return {"error": f"{type(e).__name__}: {e}"[:200]}
+        return {k: (round(v, 1) if isinstance(v, float) else v) for k, v in r.items() if v is not None}
+
     @staticmethod
     def maybe(s):
         """``s`` as a context manager, or a no-op one yielding None."""
@@ -2141,17 +2151,21 @@ def main():
     stage("barrier before the timed steps")
     barrier(world)
     sync()
+    # one clock sample on each side of the timed steps, none inside: a sampler thread's Python work
+    # holds the GIL for ~1-2 ms per sample and slowed host-bound short lines by up to 17 % (r06ah)
+    clk_edges = [clk.sample_now()] if clk is not None else None
     timer.start()
     stage("timed steps")
     t0 = time.perf_counter()
     lat = []
-    with ClockSampler.maybe(clk) as cs_timed:
-        for _ in range(args.steps):
-            lat.append(wl["step"]())
-        timer.end()
-        sync()
+    for _ in range(args.steps):
+        lat.append(wl["step"]())
+    timer.end()
+    sync()
     barrier(world)
     sync()
+    if clk_edges is not None:
+        clk_edges.append(clk.sample_now())
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
     timer.stop()
     sustained = None
@@ -2239,8 +2253,10 @@ def main():
                 rl["frac_of_ceiling"] = round(rl["achieved"] / ceiling["value"], 4)
         if cold is not None:
             line["cold"] = cold
-        if cs_timed is not None:
-            line["clock"] = dict(cs_timed.summary(), region="the timed steps (rank 0's GPU)")
+        if clk_edges is not None:
+            line["clock"] = {"before_timed_steps": clk_edges[0], "after_timed_steps": clk_edges[1],
+                             "source": "amdsmi gpu_metrics (rank 0's GPU); the read probe's own samples are "
+                                       "under roofline.measured_read_ceiling.clock"}
         line.update(wl.get("extra_line", {}))
         mf = wl.get("mfma_flops_per_launch")
         if mf and world == 1 and kernel_ms and line.get("pair_form") == "gram" and wl.get("mfma_bound"):

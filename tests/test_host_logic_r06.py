@@ -86,3 +86,4 @@ def test_clock_summary_and_missing_table():
     assert "hbm_c" not in s and s["throttle_frac"] == 0.4
     with bench.ClockSampler.maybe(None) as z:
         assert z is None
+    assert cs.sample_now() == {"error": "RuntimeError: no table"}
