@@ -2139,6 +2139,10 @@ def main():
             ceiling = read_ceiling(eng, wl)
         if cs is not None:
             ceiling["clock"] = cs.summary()
+    # one clock sample on each side of the timed steps, none inside them: a sampler thread's Python
+    # work holds the GIL for ~1-2 ms per sample and slowed host-bound short lines (r06ah), and a sample
+    # takes ~1-5 ms -- this one goes before the re-warm, the other after the wall clock stops (r06aj)
+    clk_edges = [clk.sample_now()] if clk is not None else None
     if auto_warmup and world == 1 and not wl.get("latency"):
         # ~0.2 s of the workload's own steps, each waited for, right before the timed ones: the timed
         # steps then start on a busy GPU (r06ae / r06af / r06ag: after the probe or any idle gap,
@@ -2151,9 +2155,6 @@ def main():
     stage("barrier before the timed steps")
     barrier(world)
     sync()
-    # one clock sample on each side of the timed steps, none inside: a sampler thread's Python work
-    # holds the GIL for ~1-2 ms per sample and slowed host-bound short lines by up to 17 % (r06ah)
-    clk_edges = [clk.sample_now()] if clk is not None else None
     timer.start()
     stage("timed steps")
     t0 = time.perf_counter()
@@ -2164,9 +2165,9 @@ def main():
     sync()
     barrier(world)
     sync()
-    if clk_edges is not None:
-        clk_edges.append(clk.sample_now())
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    if clk_edges is not None:  # (after the clock stops: a sample takes ~1-5 ms, r06aj)
+        clk_edges.append(clk.sample_now())
     timer.stop()
     sustained = None
     if args.soak_seconds > 0 and world == 1 and not wl.get("latency") and wl.get("bytes_total"):
@@ -2255,6 +2256,7 @@ def main():
             line["cold"] = cold
         if clk_edges is not None:
             line["clock"] = {"before_timed_steps": clk_edges[0], "after_timed_steps": clk_edges[1],
+                             "note": "before: ahead of the 0.2 s re-warm; after: once the wall clock stopped",
                              "source": "amdsmi gpu_metrics (rank 0's GPU); the read probe's own samples are "
                                        "under roofline.measured_read_ceiling.clock"}
         line.update(wl.get("extra_line", {}))
